@@ -1,0 +1,121 @@
+"""ctypes binding of libargus_hip.so (include/argus_hip.h).
+
+The product path has exactly one compute backend: these HIP kernels. If the library is missing or
+fails to load, every op raises — there is no CPU or PyTorch fallback.
+
+torch is imported before the library is opened: torch's bundled ``libamdhip64.so`` carries the same
+SONAME (``libamdhip64.so.7``) as ROCm's, so the dynamic linker binds libargus_hip.so to the HIP
+runtime torch already loaded — one runtime per process, and torch's streams/pointers are valid here.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import torch  # noqa: F401  (must precede the CDLL, see module docstring)
+
+LIB_PATH = Path(os.environ.get("ARGUS_HIP_LIB", Path(__file__).resolve().parent / "libargus_hip.so"))
+
+F32, BF16 = 0, 1
+ABI_VERSION = 1
+
+
+class ConvDesc(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("n", "h", "w", "c", "k", "r", "s", "stride", "pad", "ho", "wo", "stem")]
+
+
+_P = C.c_void_p
+_I = C.c_int
+_I64 = C.c_int64
+_F = C.c_float
+_SZ = C.c_size_t
+_DESC = C.POINTER(ConvDesc)
+
+# name -> (restype, argtypes); must mirror include/argus_hip.h exactly (tests check the export list)
+SIGNATURES = {
+    "argus_abi_version": (_I, []),
+    "argus_last_error": (C.c_char_p, []),
+    "argus_images_to_nhwc4": (_I, [_I, _I64, _I, _I, _P, _P, _P]),
+    "argus_conv_weight_prep": (_I, [_DESC, _I, _P, _P, _P, _P, _P]),
+    "argus_conv_fwd": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "argus_conv_fwd_stat_rows": (_I, [_DESC, _I]),
+    "argus_conv_fwd_stat_tile": (_I, [_DESC, _I]),
+    "argus_conv_dgrad": (_I, [_DESC, _I, _P, _P, _P, _I, _P]),
+    "argus_conv_wgrad_workspace_bytes": (_SZ, [_DESC, _I]),
+    "argus_conv_wgrad": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P, _SZ, _P]),
+    "argus_bn_workspace_bytes": (_SZ, [_I]),
+    "argus_bn_finalize": (_I, [_I, _I, _I, _P, _I64, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "argus_bn_eval_coeffs": (_I, [_I, _P, _P, _P, _P, _F, _P, _P, _P]),
+    "argus_bn_apply": (_I, [_I, _I64, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P]),
+    "argus_bn_bwd_rows": (_I, [_I64, _I]),
+    "argus_bn_bwd_reduce": (_I, [_I, _I64, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "argus_bn_bwd_finalize": (_I, [_I, _I, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "argus_bn_bwd_apply": (_I, [_I, _I64, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "argus_maxpool_fwd": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
+    "argus_maxpool_bwd": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P]),
+    "argus_avgpool_fwd": (_I, [_I, _I, _I, _I, _P, _P, _P]),
+    "argus_avgpool_bwd": (_I, [_I, _I, _I, _I, _P, _P, _P]),
+    "argus_gemm_f32": (_I, [_I, _I, _I, _P, _I, _I, _P, _I, _I, _P, _I, _P, _I, _P, _P]),
+    "argus_colsum_f32": (_I, [_I, _I, _P, _I, _P, _P]),
+    "argus_gelu_f32": (_I, [_I64, _P, _P, _P]),
+    "argus_gelu_bwd_f32": (_I, [_I64, _P, _P, _P, _P]),
+    "argus_se3_loss": (_I, [_I, _P, _P, _P, _P, _F, _P]),
+    "argus_sumsq_workspace_bytes": (_SZ, [_I64]),
+    "argus_global_norm": (_I, [_I64, _P, _P, _P, _P]),
+    "argus_adam_step": (_I, [_I64, _P, _P, _P, _P, _P, _F, _F, _F, _F, _F, _F, _F, _F, _P]),
+}
+
+
+class ArgusHipError(RuntimeError):
+    pass
+
+
+class _Lib:
+    def __init__(self) -> None:
+        if not LIB_PATH.exists():
+            raise ArgusHipError(
+                f"{LIB_PATH} not found: build it with `python -m argus_amd.build` "
+                "(the argus_amd GPU path has no fallback)"
+            )
+        self.dll = C.CDLL(str(LIB_PATH))
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(self.dll, name)
+            fn.restype = res
+            fn.argtypes = args
+        v = self.dll.argus_abi_version()
+        if v != ABI_VERSION:
+            raise ArgusHipError(f"libargus_hip ABI {v} != expected {ABI_VERSION}")
+
+    def __getattr__(self, name: str):
+        fn = getattr(self.dll, "argus_" + name)
+        if fn.restype is _I and not name.endswith(("rows", "tile", "version")):
+            def call(*args, _fn=fn, _name=name):
+                rc = _fn(*args)
+                if rc != 0:
+                    msg = self.dll.argus_last_error().decode(errors="replace")
+                    raise ArgusHipError(f"argus_{_name} failed ({rc}): {msg}")
+                return rc
+            setattr(self, name, call)
+            return call
+        setattr(self, name, fn)
+        return fn
+
+
+_LIB: _Lib | None = None
+
+
+def lib() -> _Lib:
+    global _LIB
+    if _LIB is None:
+        _LIB = _Lib()
+    return _LIB
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a tensor (None -> NULL)."""
+    return None if t is None else t.data_ptr()
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream

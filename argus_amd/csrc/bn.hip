@@ -1,0 +1,551 @@
+// BatchNorm2d (train/eval), residual add, ReLU, MaxPool2d(3,2,1), AdaptiveAvgPool2d(1) for the
+// ResNet-50 backbone (torchvision, argus/models.py:43,55), NHWC, fp32 statistics.
+//
+// Train-mode BN is a two-phase dependency: the conv epilogue (conv.hip) emits per-row-tile
+// {sum, sumsq} partials; bn_colreduce + bn_finalize turn them into mean / invstd and the fused
+// coefficients scale/shift that the *consumer* applies (next conv's staging prologue, or
+// bn_apply_kernel for block outputs). Backward: bn_bwd_reduce_kernel emits {sum dm, sum dm*xhat}
+// partials, bn_bwd_finalize gives dgamma/dbeta and dy = ca*dm + cb*y + cc coefficients,
+// bn_bwd_apply_kernel materialises dy. Every cross-workgroup reduction is a fixed-order two-level
+// reduction (deterministic, run-to-run bitwise reproducible).
+#include "common.h"
+#include "internal.h"
+
+namespace argus {
+
+// ---- forward statistics: Chan/Welford merge of per-tile {sum, M2} partials ----------------------
+// part float2[rows][C], tile t covers n_t = min(tile_rows, count - t*tile_rows) elements.
+// Level 1 merges groups of tiles into {n, mean, M2} (double), level 2 merges the groups.
+struct Welf {
+  double n, mean, m2;
+};
+ARGUS_DEV void welf_merge(Welf& a, double nb, double meanb, double m2b) {
+  if (nb <= 0.0) return;
+  const double n = a.n + nb;
+  const double d = meanb - a.mean;
+  a.mean += d * (nb / n);
+  a.m2 += m2b + d * d * (a.n * nb / n);
+  a.n = n;
+}
+
+__global__ __launch_bounds__(256) void stats_reduce_kernel(const float2* __restrict__ part, int rows, int C,
+                                                           int rows_per_group, int64_t count, int tile_rows,
+                                                           double* __restrict__ out) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int lane_r = threadIdx.x >> 6;
+  const int g = blockIdx.y;
+  const int r0 = g * rows_per_group, r1 = min(rows, r0 + rows_per_group);
+  Welf w = {0.0, 0.0, 0.0};
+  if (c < C)
+    for (int r = r0 + lane_r; r < r1; r += 4) {
+      const float2 v = part[(size_t)r * C + c];
+      const int64_t left = count - (int64_t)r * tile_rows;
+      const double nt = (double)(left < tile_rows ? left : tile_rows);
+      welf_merge(w, nt, nt > 0.0 ? (double)v.x / nt : 0.0, (double)v.y);
+    }
+  __shared__ double red[4][64][3];
+  red[lane_r][threadIdx.x & 63][0] = w.n;
+  red[lane_r][threadIdx.x & 63][1] = w.mean;
+  red[lane_r][threadIdx.x & 63][2] = w.m2;
+  __syncthreads();
+  if (lane_r == 0 && c < C) {
+    for (int i = 1; i < 4; ++i) welf_merge(w, red[i][threadIdx.x][0], red[i][threadIdx.x][1], red[i][threadIdx.x][2]);
+    double* o = out + ((size_t)g * C + c) * 3;
+    o[0] = w.n; o[1] = w.mean; o[2] = w.m2;
+  }
+}
+
+// ---- backward partial sums: plain two-level column reduction float2 -> double2 -------------------
+__global__ __launch_bounds__(256) void colreduce_kernel(const float2* __restrict__ part, int rows, int C,
+                                                        int rows_per_group, double2* __restrict__ out) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int lane_r = threadIdx.x >> 6;  // 4 row lanes
+  const int g = blockIdx.y;
+  const int r0 = g * rows_per_group, r1 = min(rows, r0 + rows_per_group);
+  double s = 0.0, q = 0.0;
+  if (c < C)
+    for (int r = r0 + lane_r; r < r1; r += 4) {
+      const float2 v = part[(size_t)r * C + c];
+      s += v.x;
+      q += v.y;
+    }
+  __shared__ double2 red[4][64];
+  red[lane_r][threadIdx.x & 63] = make_double2(s, q);
+  __syncthreads();
+  if (lane_r == 0 && c < C) {
+    double2 a = red[0][threadIdx.x];
+    for (int i = 1; i < 4; ++i) { a.x += red[i][threadIdx.x].x; a.y += red[i][threadIdx.x].y; }
+    out[(size_t)g * C + c] = a;
+  }
+}
+
+static int reduce_groups(int rows) { return rows < 128 ? 1 : (rows < 4096 ? 32 : 128); }
+
+static int colreduce(const float* part, int rows, int C, void* ws, int& G, hipStream_t st) {
+  G = reduce_groups(rows);
+  const int rpg = (rows + G - 1) / G;
+  hipLaunchKernelGGL(colreduce_kernel, dim3((C + 63) / 64, G), dim3(256), 0, st,
+                     reinterpret_cast<const float2*>(part), rows, C, rpg, reinterpret_cast<double2*>(ws));
+  return check_launch("colreduce_kernel");
+}
+
+__global__ void bn_finalize_kernel(const double* __restrict__ red, int G, int C, const float* gamma,
+                                   const float* beta, float eps, float momentum, float* running_mean,
+                                   float* running_var, int64_t* nbt, float* mean_o, float* invstd_o,
+                                   float* scale_o, float* shift_o) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == 0 && nbt) nbt[0] += 1;
+  if (c >= C) return;
+  Welf w = {0.0, 0.0, 0.0};
+  for (int g = 0; g < G; ++g) {
+    const double* r = red + ((size_t)g * C + c) * 3;
+    welf_merge(w, r[0], r[1], r[2]);
+  }
+  const double count = w.n;
+  const double mean = w.mean;
+  const double var = count > 0.0 ? w.m2 / count : 0.0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float sc = gamma[c] * invstd;
+  if (mean_o) mean_o[c] = (float)mean;
+  if (invstd_o) invstd_o[c] = invstd;
+  if (scale_o) scale_o[c] = sc;
+  if (shift_o) shift_o[c] = beta[c] - (float)mean * sc;
+  if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+  if (running_var) {
+    const double unbiased = count > 1.0 ? w.m2 / (count - 1.0) : var;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unbiased;
+  }
+}
+
+__global__ void bn_eval_kernel(int C, const float* gamma, const float* beta, const float* rm, const float* rv,
+                               float eps, float* scale, float* shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float inv = 1.f / sqrtf(rv[c] + eps);
+  const float sc = gamma[c] * inv;
+  scale[c] = sc;
+  shift[c] = beta[c] - rm[c] * sc;
+}
+
+// ---- elementwise apply ------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void bn_apply_kernel(int64_t nchunks, int C, const T* __restrict__ y,
+                                                       const float* __restrict__ sc, const float* __restrict__ sh,
+                                                       const T* __restrict__ res, const float* __restrict__ rsc,
+                                                       const float* __restrict__ rsh, int relu, T* out) {
+  constexpr int E = Chunk<T>::E;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < nchunks; i += (int64_t)gridDim.x * 256) {
+    const int c0 = (int)((i * E) % C);
+    float f[E];
+    unpack(ld16(y + i * E), f);
+    float r[E];
+    if (res) {
+      unpack(ld16(res + i * E), r);
+      if (rsc) {
+#pragma unroll
+        for (int j = 0; j < E; ++j) r[j] = fmaf(r[j], rsc[c0 + j], rsh[c0 + j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      float v = fmaf(f[j], sc[c0 + j], sh[c0 + j]);
+      if (res) v += r[j];
+      if (relu) v = fmaxf(v, 0.f);
+      f[j] = v;
+    }
+    st16(out + i * E, pack(f));
+  }
+}
+
+// ---- backward reduce ----------------------------------------------------------------------------
+// Grid: x = channel groups of CC chunks, y = pixel blocks. Block: CC chunk-columns x PL pixel lanes.
+static int bwd_rows(int64_t pixels) {
+  int64_t r = (pixels + 63) / 64;  // >= 64 pixels per block
+  return (int)(r > 1024 ? 1024 : (r < 1 ? 1 : r));
+}
+static void bwd_geometry(int C, int E, int64_t pixels, int& CC, int& PL, int& cgroups, int& rows, int64_t& ppb) {
+  const int chunks = C / E;
+  CC = chunks < 256 ? chunks : 256;
+  PL = 256 / CC;
+  cgroups = chunks / CC;
+  rows = bwd_rows(pixels);
+  ppb = (pixels + rows - 1) / rows;
+  rows = (int)((pixels + ppb - 1) / ppb);
+}
+
+template <typename T>
+ARGUS_DEV void load_mask(int mode, const T* mask_src, const T* y, const float* sc, const float* sh, int64_t off,
+                         int c0, const float (&yv)[Chunk<T>::E], float (&m)[Chunk<T>::E]) {
+  constexpr int E = Chunk<T>::E;
+  if (mode == 1) {
+    float s[E];
+    unpack(ld16(mask_src + off), s);
+#pragma unroll
+    for (int j = 0; j < E; ++j) m[j] = s[j] > 0.f ? 1.f : 0.f;
+  } else if (mode == 2) {
+#pragma unroll
+    for (int j = 0; j < E; ++j) m[j] = fmaf(yv[j], sc[c0 + j], sh[c0 + j]) > 0.f ? 1.f : 0.f;
+  } else {
+#pragma unroll
+    for (int j = 0; j < E; ++j) m[j] = 1.f;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(int64_t pixels, int C, int CC, int PL, int64_t ppb,
+                                                            const T* __restrict__ dz, int mode,
+                                                            const T* __restrict__ mask_src, const T* __restrict__ y,
+                                                            const float* __restrict__ sc, const float* __restrict__ sh,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ invstd, float2* __restrict__ part) {
+  constexpr int E = Chunk<T>::E;
+  const int cc = threadIdx.x % CC, pl = threadIdx.x / CC;
+  const int c0 = (blockIdx.x * CC + cc) * E;
+  const int64_t p0 = blockIdx.y * ppb, p1 = min(pixels, p0 + ppb);
+  float mu[E], is[E], s[E], t[E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) { mu[j] = mean[c0 + j]; is[j] = invstd[c0 + j]; s[j] = 0.f; t[j] = 0.f; }
+  if (pl < PL)
+    for (int64_t px = p0 + pl; px < p1; px += PL) {
+      const int64_t off = px * C + c0;
+      float d[E], yv[E], m[E];
+      unpack(ld16(dz + off), d);
+      unpack(ld16(y + off), yv);
+      load_mask<T>(mode, mask_src, y, sc, sh, off, c0, yv, m);
+#pragma unroll
+      for (int j = 0; j < E; ++j) {
+        const float dm = d[j] * m[j];
+        s[j] += dm;
+        t[j] = fmaf(dm, (yv[j] - mu[j]) * is[j], t[j]);
+      }
+    }
+  __shared__ float2 red[256 * 8];
+  // reduce over pixel lanes: layout red[pl][cc*E + j]
+  const int W = CC * E;
+#pragma unroll
+  for (int j = 0; j < E; ++j) red[pl * W + cc * E + j] = make_float2(s[j], t[j]);
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < W; idx += 256) {
+    float2 a = red[idx];
+    for (int l = 1; l < PL; ++l) { a.x += red[l * W + idx].x; a.y += red[l * W + idx].y; }
+    part[(size_t)blockIdx.y * C + blockIdx.x * W + idx] = a;
+  }
+}
+
+__global__ void bn_bwd_finalize_kernel(const double2* __restrict__ red, int G, int C, double count,
+                                       const float* gamma, const float* mean, const float* invstd, float* dgamma,
+                                       float* dbeta, float* ca, float* cb, float* cc) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double S = 0.0, Tt = 0.0;
+  for (int g = 0; g < G; ++g) { S += red[(size_t)g * C + c].x; Tt += red[(size_t)g * C + c].y; }
+  if (dgamma) dgamma[c] = (float)Tt;
+  if (dbeta) dbeta[c] = (float)S;
+  const double gi = (double)gamma[c] * invstd[c];
+  const double gi2 = gi * invstd[c];
+  ca[c] = (float)gi;
+  cb[c] = (float)(-gi2 * Tt / count);
+  cc[c] = (float)(-gi * S / count + gi2 * Tt / count * mean[c]);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(int64_t nchunks, int C, const T* __restrict__ dz, int mode,
+                                                           const T* __restrict__ mask_src, const T* __restrict__ y,
+                                                           const float* __restrict__ sc, const float* __restrict__ sh,
+                                                           const float* __restrict__ ca, const float* __restrict__ cb,
+                                                           const float* __restrict__ cc, T* __restrict__ dy,
+                                                           T* __restrict__ dm_out) {
+  constexpr int E = Chunk<T>::E;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < nchunks; i += (int64_t)gridDim.x * 256) {
+    const int c0 = (int)((i * E) % C);
+    const int64_t off = i * E;
+    float d[E], yv[E], m[E];
+    unpack(ld16(dz + off), d);
+    unpack(ld16(y + off), yv);
+    load_mask<T>(mode, mask_src, y, sc, sh, off, c0, yv, m);
+    float o[E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      d[j] *= m[j];
+      o[j] = fmaf(ca[c0 + j], d[j], fmaf(cb[c0 + j], yv[j], cc[c0 + j]));
+    }
+    st16(dy + off, pack(o));
+    if (dm_out) st16(dm_out + off, pack(d));
+  }
+}
+
+// ---- max pool 3x3/2 p1 fused with the stem BN + ReLU ---------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool_fwd_kernel(int n, int H, int W, int C, int Ho, int Wo,
+                                                          const T* __restrict__ y, const float* __restrict__ sc,
+                                                          const float* __restrict__ sh, T* __restrict__ out,
+                                                          uint8_t* __restrict__ amax) {
+  constexpr int E = Chunk<T>::E;
+  const int CH = C / E;
+  const int64_t total = (int64_t)n * Ho * Wo * CH;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int ch = (int)(i % CH);
+    const int64_t pix = i / CH;
+    const int ow = (int)(pix % Wo);
+    const int oh = (int)((pix / Wo) % Ho);
+    const int img = (int)(pix / ((int64_t)Wo * Ho));
+    const int c0 = ch * E;
+    float best[E];
+    uint8_t idx[E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) { best[j] = -INFINITY; idx[j] = 0; }
+    for (int r = 0; r < 3; ++r) {
+      const int ih = 2 * oh - 1 + r;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      for (int s = 0; s < 3; ++s) {
+        const int iw = 2 * ow - 1 + s;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        float v[E];
+        unpack(ld16(y + (((int64_t)img * H + ih) * W + iw) * C + c0), v);
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+          const float z = fmaxf(fmaf(v[j], sc[c0 + j], sh[c0 + j]), 0.f);
+          if (z > best[j]) { best[j] = z; idx[j] = (uint8_t)(r * 3 + s); }
+        }
+      }
+    }
+    st16(out + pix * C + c0, pack(best));
+#pragma unroll
+    for (int j = 0; j < E; ++j) amax[pix * C + c0 + j] = idx[j];
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(int n, int H, int W, int C, int Ho, int Wo,
+                                                          const T* __restrict__ dout, const uint8_t* __restrict__ amax,
+                                                          T* __restrict__ dz) {
+  constexpr int E = Chunk<T>::E;
+  const int CH = C / E;
+  const int64_t total = (int64_t)n * H * W * CH;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int ch = (int)(i % CH);
+    const int64_t pix = i / CH;
+    const int iw = (int)(pix % W);
+    const int ih = (int)((pix / W) % H);
+    const int img = (int)(pix / ((int64_t)W * H));
+    const int c0 = ch * E;
+    float acc[E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) acc[j] = 0.f;
+    const int oh_lo = max(0, ih / 2), oh_hi = min(Ho - 1, (ih + 1) / 2);
+    const int ow_lo = max(0, iw / 2), ow_hi = min(Wo - 1, (iw + 1) / 2);
+    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+      const int r = ih - (2 * oh - 1);
+      if (r < 0 || r > 2) continue;
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        const int s = iw - (2 * ow - 1);
+        if (s < 0 || s > 2) continue;
+        const int64_t o = (((int64_t)img * Ho + oh) * Wo + ow) * C + c0;
+        float g[E];
+        unpack(ld16(dout + o), g);
+        const uint8_t want = (uint8_t)(r * 3 + s);
+#pragma unroll
+        for (int j = 0; j < E; ++j)
+          if (amax[o + j] == want) acc[j] += g[j];
+      }
+    }
+    st16(dz + pix * C + c0, pack(acc));
+  }
+}
+
+// ---- global average pool ------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void avgpool_fwd_kernel(int n, int hw, int C, const T* __restrict__ x,
+                                                          float* __restrict__ feat) {
+  const int64_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)n * C) return;
+  const int img = (int)(i / C), c = (int)(i % C);
+  float s = 0.f;
+  for (int p = 0; p < hw; ++p) s += to_f32(x[((int64_t)img * hw + p) * C + c]);
+  feat[i] = s / (float)hw;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void avgpool_bwd_kernel(int64_t nchunks, int hw, int C, const float* __restrict__ dfeat,
+                                                          T* __restrict__ dx) {
+  constexpr int E = Chunk<T>::E;
+  const float inv = 1.f / (float)hw;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < nchunks; i += (int64_t)gridDim.x * 256) {
+    const int64_t e = i * E;
+    const int c0 = (int)(e % C);
+    const int64_t img = e / ((int64_t)hw * C);
+    float f[E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) f[j] = dfeat[img * C + c0 + j] * inv;
+    st16(dx + e, pack(f));
+  }
+}
+
+static int grid_for(int64_t work) {
+  int64_t b = (work + 255) / 256;
+  if (b > 8192) b = 8192;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+}  // namespace argus
+
+using namespace argus;
+
+extern "C" {
+
+size_t argus_bn_workspace_bytes(int channels) { return (size_t)128 * channels * 3 * sizeof(double); }
+
+int argus_bn_finalize(int C, int rows, int tile_rows, const float* part, int64_t count, const float* gamma,
+                      const float* beta, float eps, float momentum, float* rm, float* rv, int64_t* nbt, float* mean,
+                      float* invstd, float* scale, float* shift, void* ws, argus_stream_t stream) {
+  if (C <= 0 || rows <= 0 || tile_rows <= 0 || count <= 0 || !part || !gamma || !beta || !ws ||
+      (int64_t)rows * tile_rows < count) {
+    set_error("bn_finalize: bad arguments");
+    return ARGUS_ERR_ARG;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const int G = reduce_groups(rows);
+  const int rpg = (rows + G - 1) / G;
+  hipLaunchKernelGGL(stats_reduce_kernel, dim3((C + 63) / 64, G), dim3(256), 0, st,
+                     reinterpret_cast<const float2*>(part), rows, C, rpg, count, tile_rows, reinterpret_cast<double*>(ws));
+  if (int e = check_launch("stats_reduce_kernel")) return e;
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st,
+                     reinterpret_cast<const double*>(ws), G, C, gamma, beta, eps, momentum, rm, rv,
+                     nbt, mean, invstd, scale, shift);
+  return check_launch("bn_finalize_kernel");
+}
+
+int argus_bn_eval_coeffs(int C, const float* gamma, const float* beta, const float* rm, const float* rv, float eps,
+                         float* scale, float* shift, argus_stream_t stream) {
+  hipLaunchKernelGGL(bn_eval_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, C, gamma, beta, rm,
+                     rv, eps, scale, shift);
+  return check_launch("bn_eval_kernel");
+}
+
+int argus_bn_apply(int dtype, int64_t pixels, int C, const void* y, const float* scale, const float* shift,
+                   const void* res, const float* rsc, const float* rsh, int relu, void* out, argus_stream_t stream) {
+  const int E = dtype == ARGUS_BF16 ? 8 : 4;
+  if (C % E || pixels <= 0) { set_error("bn_apply: channels must be a multiple of the chunk"); return ARGUS_ERR_SHAPE; }
+  const int64_t nch = pixels * C / E;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == ARGUS_BF16)
+    hipLaunchKernelGGL(bn_apply_kernel<bf16>, dim3(grid_for(nch)), dim3(256), 0, st, nch, C, (const bf16*)y, scale,
+                       shift, (const bf16*)res, rsc, rsh, relu, (bf16*)out);
+  else
+    hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(grid_for(nch)), dim3(256), 0, st, nch, C, (const float*)y, scale,
+                       shift, (const float*)res, rsc, rsh, relu, (float*)out);
+  return check_launch("bn_apply_kernel");
+}
+
+int argus_bn_bwd_rows(int64_t pixels, int C) {
+  (void)C;
+  const int r = bwd_rows(pixels);
+  const int64_t ppb = (pixels + r - 1) / r;
+  return (int)((pixels + ppb - 1) / ppb);
+}
+
+int argus_bn_bwd_reduce(int dtype, int64_t pixels, int C, const void* dz, int mode, const void* mask_src,
+                        const void* y, const float* scale, const float* shift, const float* mean,
+                        const float* invstd, float* part, argus_stream_t stream) {
+  const int E = dtype == ARGUS_BF16 ? 8 : 4;
+  if (C % E || pixels <= 0) { set_error("bn_bwd_reduce: bad shape"); return ARGUS_ERR_SHAPE; }
+  int CC, PL, cg, rows;
+  int64_t ppb;
+  bwd_geometry(C, E, pixels, CC, PL, cg, rows, ppb);
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid(cg, rows);
+  if (dtype == ARGUS_BF16)
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<bf16>, grid, dim3(256), 0, st, pixels, C, CC, PL, ppb, (const bf16*)dz,
+                       mode, (const bf16*)mask_src, (const bf16*)y, scale, shift, mean, invstd, (float2*)part);
+  else
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<float>, grid, dim3(256), 0, st, pixels, C, CC, PL, ppb, (const float*)dz,
+                       mode, (const float*)mask_src, (const float*)y, scale, shift, mean, invstd, (float2*)part);
+  return check_launch("bn_bwd_reduce_kernel");
+}
+
+int argus_bn_bwd_finalize(int C, int rows, const float* part, int64_t count, const float* gamma, const float* mean,
+                          const float* invstd, float* dgamma, float* dbeta, float* ca, float* cb, float* cc, void* ws,
+                          argus_stream_t stream) {
+  hipStream_t st = (hipStream_t)stream;
+  int G;
+  if (int e = colreduce(part, rows, C, ws, G, st)) return e;
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st,
+                     reinterpret_cast<const double2*>(ws), G, C, (double)count, gamma, mean, invstd, dgamma, dbeta,
+                     ca, cb, cc);
+  return check_launch("bn_bwd_finalize_kernel");
+}
+
+int argus_bn_bwd_apply(int dtype, int64_t pixels, int C, const void* dz, int mode, const void* mask_src, const void* y,
+                       const float* scale, const float* shift, const float* ca, const float* cb, const float* cc,
+                       void* dy, void* dm_out, argus_stream_t stream) {
+  const int E = dtype == ARGUS_BF16 ? 8 : 4;
+  if (C % E || pixels <= 0) { set_error("bn_bwd_apply: bad shape"); return ARGUS_ERR_SHAPE; }
+  const int64_t nch = pixels * C / E;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == ARGUS_BF16)
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16>, dim3(grid_for(nch)), dim3(256), 0, st, nch, C, (const bf16*)dz, mode,
+                       (const bf16*)mask_src, (const bf16*)y, scale, shift, ca, cb, cc, (bf16*)dy, (bf16*)dm_out);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, dim3(grid_for(nch)), dim3(256), 0, st, nch, C, (const float*)dz,
+                       mode, (const float*)mask_src, (const float*)y, scale, shift, ca, cb, cc, (float*)dy,
+                       (float*)dm_out);
+  return check_launch("bn_bwd_apply_kernel");
+}
+
+int argus_maxpool_fwd(int dtype, int n, int h, int w, int c, const void* y, const float* scale, const float* shift,
+                      void* out, uint8_t* amax, argus_stream_t stream) {
+  const int E = dtype == ARGUS_BF16 ? 8 : 4;
+  if (c % E) { set_error("maxpool_fwd: bad channels"); return ARGUS_ERR_SHAPE; }
+  const int ho = (h + 2 - 3) / 2 + 1, wo = (w + 2 - 3) / 2 + 1;
+  const int64_t work = (int64_t)n * ho * wo * (c / E);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == ARGUS_BF16)
+    hipLaunchKernelGGL(maxpool_fwd_kernel<bf16>, dim3(grid_for(work)), dim3(256), 0, st, n, h, w, c, ho, wo,
+                       (const bf16*)y, scale, shift, (bf16*)out, amax);
+  else
+    hipLaunchKernelGGL(maxpool_fwd_kernel<float>, dim3(grid_for(work)), dim3(256), 0, st, n, h, w, c, ho, wo,
+                       (const float*)y, scale, shift, (float*)out, amax);
+  return check_launch("maxpool_fwd_kernel");
+}
+
+int argus_maxpool_bwd(int dtype, int n, int h, int w, int c, const void* dout, const uint8_t* amax, void* dz,
+                      argus_stream_t stream) {
+  const int E = dtype == ARGUS_BF16 ? 8 : 4;
+  if (c % E) { set_error("maxpool_bwd: bad channels"); return ARGUS_ERR_SHAPE; }
+  const int ho = (h + 2 - 3) / 2 + 1, wo = (w + 2 - 3) / 2 + 1;
+  const int64_t work = (int64_t)n * h * w * (c / E);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == ARGUS_BF16)
+    hipLaunchKernelGGL(maxpool_bwd_kernel<bf16>, dim3(grid_for(work)), dim3(256), 0, st, n, h, w, c, ho, wo,
+                       (const bf16*)dout, amax, (bf16*)dz);
+  else
+    hipLaunchKernelGGL(maxpool_bwd_kernel<float>, dim3(grid_for(work)), dim3(256), 0, st, n, h, w, c, ho, wo,
+                       (const float*)dout, amax, (float*)dz);
+  return check_launch("maxpool_bwd_kernel");
+}
+
+int argus_avgpool_fwd(int dtype, int n, int hw, int c, const void* x, float* feat, argus_stream_t stream) {
+  const int64_t work = (int64_t)n * c;
+  hipStream_t st = (hipStream_t)stream;
+  const int blocks = (int)((work + 255) / 256);
+  if (dtype == ARGUS_BF16)
+    hipLaunchKernelGGL(avgpool_fwd_kernel<bf16>, dim3(blocks), dim3(256), 0, st, n, hw, c, (const bf16*)x, feat);
+  else
+    hipLaunchKernelGGL(avgpool_fwd_kernel<float>, dim3(blocks), dim3(256), 0, st, n, hw, c, (const float*)x, feat);
+  return check_launch("avgpool_fwd_kernel");
+}
+
+int argus_avgpool_bwd(int dtype, int n, int hw, int c, const float* dfeat, void* dx, argus_stream_t stream) {
+  const int E = dtype == ARGUS_BF16 ? 8 : 4;
+  if (c % E) { set_error("avgpool_bwd: bad channels"); return ARGUS_ERR_SHAPE; }
+  const int64_t nch = (int64_t)n * hw * c / E;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == ARGUS_BF16)
+    hipLaunchKernelGGL(avgpool_bwd_kernel<bf16>, dim3(grid_for(nch)), dim3(256), 0, st, nch, hw, c, dfeat, (bf16*)dx);
+  else
+    hipLaunchKernelGGL(avgpool_bwd_kernel<float>, dim3(grid_for(nch)), dim3(256), 0, st, nch, hw, c, dfeat, (float*)dx);
+  return check_launch("avgpool_bwd_kernel");
+}
+
+}  // extern "C"

@@ -1,0 +1,75 @@
+// extern "C" surface of libargus_hip.so (include/argus_hip.h) + error reporting.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <string>
+
+#include "internal.h"
+
+namespace argus {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+int check_launch(const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error(std::string(what) + ": " + hipGetErrorString(e));
+    return ARGUS_ERR_HIP;
+  }
+  return ARGUS_OK;
+}
+
+}  // namespace argus
+
+using namespace argus;
+
+extern "C" {
+
+int argus_abi_version(void) { return 1; }
+
+const char* argus_last_error(void) { return g_last_error.c_str(); }
+
+int argus_images_to_nhwc4(int dtype, int64_t nimg, int h, int w, const float* x, void* out, argus_stream_t stream) {
+  if (nimg <= 0 || h <= 0 || w <= 0 || !x || !out) { set_error("images_to_nhwc4: bad arguments"); return ARGUS_ERR_ARG; }
+  return images_to_nhwc4(dtype, nimg, h, w, x, out, (hipStream_t)stream);
+}
+
+int argus_conv_weight_prep(const argus_conv_desc* d, int dtype, const float* w, const int64_t* strides, void* wf,
+                           void* wd, argus_stream_t stream) {
+  if (!d || !w) { set_error("conv_weight_prep: null argument"); return ARGUS_ERR_ARG; }
+  return conv_weight_prep(*d, dtype, w, strides, wf, wd, (hipStream_t)stream);
+}
+
+int argus_conv_fwd(const argus_conv_desc* d, int dtype, const void* x, const void* w, void* y, const float* sc,
+                   const float* sh, float* stats, argus_stream_t stream) {
+  if (!d || !x || !w || !y || (sc == nullptr) != (sh == nullptr)) {
+    set_error("conv_fwd: bad arguments");
+    return ARGUS_ERR_ARG;
+  }
+  return conv_fwd(*d, dtype, x, w, y, sc, sh, stats, (hipStream_t)stream);
+}
+
+int argus_conv_fwd_stat_rows(const argus_conv_desc* d, int dtype) { return d ? conv_fwd_stat_rows(*d, dtype) : 0; }
+
+int argus_conv_fwd_stat_tile(const argus_conv_desc* d, int dtype) { return d ? conv_fwd_stat_tile(*d, dtype) : 0; }
+
+int argus_conv_dgrad(const argus_conv_desc* d, int dtype, const void* dy, const void* wt, void* dx, int accumulate,
+                     argus_stream_t stream) {
+  if (!d || !dy || !wt || !dx) { set_error("conv_dgrad: bad arguments"); return ARGUS_ERR_ARG; }
+  return conv_dgrad(*d, dtype, dy, wt, dx, accumulate, (hipStream_t)stream);
+}
+
+size_t argus_conv_wgrad_workspace_bytes(const argus_conv_desc* d, int dtype) { return d ? conv_wgrad_ws(*d, dtype) : 0; }
+
+int argus_conv_wgrad(const argus_conv_desc* d, int dtype, const void* x, const float* sc, const float* sh,
+                     const void* dy, float* dw, void* ws, size_t ws_bytes, argus_stream_t stream) {
+  if (!d || !x || !dy || !dw || !ws || (sc == nullptr) != (sh == nullptr)) {
+    set_error("conv_wgrad: bad arguments");
+    return ARGUS_ERR_ARG;
+  }
+  return conv_wgrad(*d, dtype, x, sc, sh, dy, dw, ws, ws_bytes, (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,82 @@
+// Shared device helpers for the argus MI355X (gfx950 / CDNA4) kernels.
+//
+// Storage types: activations/weights are either fp32 (`float`, the parity path) or bf16
+// (`__bf16`, the throughput path). Every reduction, BN statistic, loss and optimizer value is fp32
+// (doubles where a reduction crosses many workgroups).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define ARGUS_DEV __device__ __forceinline__
+
+typedef __bf16 bf16;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+namespace argus {
+
+constexpr int kWave = 64;
+
+ARGUS_DEV float to_f32(float x) { return x; }
+ARGUS_DEV float to_f32(bf16 x) { return (float)x; }
+template <typename T> ARGUS_DEV T from_f32(float x);
+template <> ARGUS_DEV float from_f32<float>(float x) { return x; }
+template <> ARGUS_DEV bf16 from_f32<bf16>(float x) { return (bf16)x; }
+
+// A 16-byte "chunk": 8 bf16 or 4 fp32 elements. All activation and weight traffic moves in chunks.
+template <typename T> struct Chunk;
+template <> struct Chunk<float> { static constexpr int E = 4; };
+template <> struct Chunk<bf16> { static constexpr int E = 8; };
+
+ARGUS_DEV u32x4 ld16(const void* p) { return *reinterpret_cast<const u32x4*>(p); }
+ARGUS_DEV void st16(void* p, u32x4 v) { *reinterpret_cast<u32x4*>(p) = v; }
+
+// unpack / pack a chunk to fp32 lanes
+ARGUS_DEV void unpack(u32x4 v, float (&f)[4]) {
+  f[0] = __uint_as_float(v.x); f[1] = __uint_as_float(v.y);
+  f[2] = __uint_as_float(v.z); f[3] = __uint_as_float(v.w);
+}
+ARGUS_DEV void unpack(u32x4 v, float (&f)[8]) {
+  unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+ARGUS_DEV u32x4 pack(const float (&f)[4]) {
+  u32x4 v; v.x = __float_as_uint(f[0]); v.y = __float_as_uint(f[1]);
+  v.z = __float_as_uint(f[2]); v.w = __float_as_uint(f[3]); return v;
+}
+ARGUS_DEV unsigned pack2_bf16(float a, float b) {
+  bf16 x = (bf16)a, y = (bf16)b;
+  unsigned short ux = __builtin_bit_cast(unsigned short, x), uy = __builtin_bit_cast(unsigned short, y);
+  return (unsigned)ux | ((unsigned)uy << 16);
+}
+ARGUS_DEV u32x4 pack(const float (&f)[8]) {
+  u32x4 v; v.x = pack2_bf16(f[0], f[1]); v.y = pack2_bf16(f[2], f[3]);
+  v.z = pack2_bf16(f[4], f[5]); v.w = pack2_bf16(f[6], f[7]); return v;
+}
+
+// wave-level sum (64 lanes)
+ARGUS_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+ARGUS_DEV double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Bijective XCD-aware remap of a 1-D block id (MI355X: 8 XCDs, blocks dealt round-robin).
+// Consecutive remapped ids land on the same XCD so neighbouring tiles share that XCD's L2.
+ARGUS_DEV int xcd_remap(int bid, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+}
+
+}  // namespace argus

@@ -1,0 +1,824 @@
+// Convolution kernels for the ResNet-50 backbone (torchvision Conv2d, bias=False; the 53 convs of
+// argus/models.py:43 — SURVEY.md Appendix B), NHWC activations, OHWI weights, MFMA on gfx950.
+//
+//  igemm_kernel  : implicit GEMM  C[m][n] = sum_k A[m][k] * B[n][k]
+//                  forward:  m = output pixel, n = output channel, k = (tap, input channel);
+//                            A = im2col(x) gathered on the fly (optionally BN+ReLU applied while
+//                            staging), B = w[k][r][s][c]; epilogue stores y and per-tile BN stats.
+//                  dgrad:    the same kernel on dy with the transposed weights w_t[c][r][s][k],
+//                            one grid.z slice per output phase (ph, pw) of a strided conv so every
+//                            tile sees a dense, uniform tap set (no zero-insertion).
+//  wgrad_kernel  : dW[k][(r,s,c)] = sum_pixels dy[p][k] * im2col(x)[p][(r,s,c)], split over pixel
+//                  ranges; both operands are pixel-major in LDS and are read transposed with
+//                  ds_read_b64_tr_b16 (bf16) — fp32 partial slabs, then a deterministic reduce.
+//
+// Tiles: 256 threads = 4 waves (2 x 2), wave tile (BM/2) x (BN/2) of 16x16 MFMA blocks.
+// bf16: v_mfma_f32_16x16x32_bf16, K-step 64; fp32 (parity path): v_mfma_f32_16x16x4_f32, K-step 32.
+// LDS rows are 8 x 16-byte chunks, XOR-swizzled (chunk ^ ((row>>1)&7)) so the ds_read_b128
+// fragment reads are bank-conflict free. Register-staged double buffering: the global loads of
+// k-step t+1 are issued before the MFMAs of step t and written to the other LDS buffer after.
+#include "common.h"
+#include "internal.h"
+
+namespace argus {
+
+// ------------------------------------------------------------------------------------------------
+// implicit GEMM (forward / dgrad)
+// ------------------------------------------------------------------------------------------------
+struct IgPhase {
+  int M;          // GEMM rows of this phase = images * Hq * Wq
+  int Hq, Wq;     // output grid of this phase
+  int oh0, ow0;   // output pixel = (qh*osh + oh0, qw*osw + ow0)
+  int K;          // ntaps * Cin (0: this phase has no taps -> zeros / nothing to accumulate)
+  int dh[9], dw[9], boff[9];  // per tap: input offset (input = q*is + d) and B-row element offset
+};
+
+struct IgParams {
+  const void* a;
+  const void* b;
+  void* c;
+  const float* pro_scale;
+  const float* pro_shift;
+  float2* stats;
+  int N, Cin, lda, H, W, ish, isw, Ho, Wo, osh, osw, ldc, ldb;
+  int accumulate, stem, nphase;
+  IgPhase ph[4];
+};
+
+template <typename T> struct Mma;
+template <> struct Mma<bf16> {
+  static ARGUS_DEV void run(f32x4& acc, u32x4 a, u32x4 b) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                  __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
+  }
+};
+template <> struct Mma<float> {
+  // lane group g supplies k = 4g + j at sub-step j (same mapping for A and B)
+  static ARGUS_DEV void run(f32x4& acc, u32x4 a, u32x4 b) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.x), __uint_as_float(b.x), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.y), __uint_as_float(b.y), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.z), __uint_as_float(b.z), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), acc, 0, 0, 0);
+  }
+};
+
+template <typename T>
+ARGUS_DEV u32x4 bn_relu_chunk(u32x4 v, const float* __restrict__ sc, const float* __restrict__ sh, int ch) {
+  constexpr int E = Chunk<T>::E;
+  float f[E];
+  unpack(v, f);
+#pragma unroll
+  for (int j = 0; j < E; ++j) f[j] = fmaxf(fmaf(f[j], sc[ch + j], sh[ch + j]), 0.f);
+  return pack(f);
+}
+
+ARGUS_DEV int swz8(int row) { return (row >> 1) & 7; }
+
+template <typename T, int BM, int BN>
+__global__ __launch_bounds__(256) void igemm_kernel(const IgParams p) {
+  constexpr int E = Chunk<T>::E;
+  constexpr int BKE = 8 * E;  // K elements per k-step (8 chunks of 16 B per LDS row)
+  constexpr int MI = BM / 32, NI = BN / 32;
+  constexpr int AR = BM / 32, BR = BN / 32;
+  __shared__ __attribute__((aligned(16))) u32x4 lds[2][(BM + BN) * 8];
+
+  const IgPhase& ph = p.ph[blockIdx.z];
+  const int mtiles = (ph.M + BM - 1) / BM;
+  const int ntiles = p.N / BN;
+  const int nwg = mtiles * ntiles;
+  if ((int)blockIdx.x >= nwg) return;
+  if (ph.K == 0 && p.accumulate) return;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int mt = bid / ntiles, nt = bid - mt * ntiles;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int cidx = tid & 7;
+  const T* __restrict__ A = reinterpret_cast<const T*>(p.a);
+  const T* __restrict__ B = reinterpret_cast<const T*>(p.b);
+
+  // per-thread A rows (output pixels) and B rows (output channels)
+  int a_n[AR], a_ih[AR], a_iw[AR];
+  bool a_ok[AR];
+  const int HWq = ph.Hq * ph.Wq;
+#pragma unroll
+  for (int i = 0; i < AR; ++i) {
+    const int m = mt * BM + (tid >> 3) + 32 * i;
+    a_ok[i] = m < ph.M;
+    const int mm = a_ok[i] ? m : 0;
+    const int nimg = mm / HWq, rem = mm - nimg * HWq;
+    const int qh = rem / ph.Wq, qw = rem - qh * ph.Wq;
+    a_n[i] = nimg;
+    a_ih[i] = qh * p.ish;
+    a_iw[i] = qw * p.isw;
+  }
+  const T* b_row[BR];
+#pragma unroll
+  for (int i = 0; i < BR; ++i)
+    b_row[i] = B + (size_t)(nt * BN + (tid >> 3) + 32 * i) * p.ldb + cidx * E;
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  u32x4 ra[AR], rb[BR];
+  const u32x4 zero = {0u, 0u, 0u, 0u};
+
+  auto load = [&](int kt) {
+    const int k0 = kt * BKE;
+    if (p.stem) {
+      const int k = k0 + cidx * E;
+      const int r = k >> 5, s0 = (k & 31) >> 2;
+#pragma unroll
+      for (int i = 0; i < AR; ++i) {
+        const int ih = a_ih[i] + r - 3;
+        const bool rok = a_ok[i] && (unsigned)ih < (unsigned)p.H;
+        const T* rowp = A + ((size_t)a_n[i] * p.H + (rok ? ih : 0)) * p.W * 4;
+        if constexpr (E == 8) {
+          unsigned w4[4];
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const int iw = a_iw[i] + s0 + u - 3;
+            if (rok && (unsigned)iw < (unsigned)p.W) {
+              const uint2 v = *reinterpret_cast<const uint2*>(rowp + (size_t)iw * 4);
+              w4[2 * u] = v.x; w4[2 * u + 1] = v.y;
+            } else {
+              w4[2 * u] = 0u; w4[2 * u + 1] = 0u;
+            }
+          }
+          ra[i] = u32x4{w4[0], w4[1], w4[2], w4[3]};
+        } else {
+          const int iw = a_iw[i] + s0 - 3;
+          ra[i] = (rok && (unsigned)iw < (unsigned)p.W) ? ld16(rowp + (size_t)iw * 4) : zero;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < BR; ++i) rb[i] = ld16(b_row[i] + k0);
+      return;
+    }
+    const int t = k0 / p.Cin;
+    const int ci0 = k0 - t * p.Cin;
+    const int dh = ph.dh[t], dw = ph.dw[t], boff = ph.boff[t];
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int ih = a_ih[i] + dh, iw = a_iw[i] + dw;
+      const bool ok = a_ok[i] && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+      if (ok) {
+        u32x4 v = ld16(A + (((size_t)a_n[i] * p.H + ih) * p.W + iw) * p.lda + ci0 + cidx * E);
+        if (p.pro_scale) v = bn_relu_chunk<T>(v, p.pro_scale, p.pro_shift, ci0 + cidx * E);
+        ra[i] = v;
+      } else {
+        ra[i] = zero;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) rb[i] = ld16(b_row[i] + boff + ci0);
+  };
+
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int row = (tid >> 3) + 32 * i;
+      lds[buf][row * 8 + (cidx ^ swz8(row))] = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int row = (tid >> 3) + 32 * i;
+      lds[buf][BM * 8 + row * 8 + (cidx ^ swz8(row))] = rb[i];
+    }
+  };
+
+  const int g = lane >> 4, i16 = lane & 15;
+  auto compute = [&](int buf) {
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      u32x4 fa[MI], fb[NI];
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) {
+        const int row = wm * (BM / 2) + mi * 16 + i16;
+        fa[mi] = lds[buf][row * 8 + ((4 * s2 + g) ^ swz8(row))];
+      }
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) {
+        const int row = wn * (BN / 2) + ni * 16 + i16;
+        fb[ni] = lds[buf][BM * 8 + row * 8 + ((4 * s2 + g) ^ swz8(row))];
+      }
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) Mma<T>::run(acc[mi][ni], fa[mi], fb[ni]);
+    }
+  };
+
+  const int nk = ph.K / BKE;
+  if (nk > 0) {
+    load(0);
+    store(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) load(kt + 1);
+      compute(cur);
+      if (kt + 1 < nk) store(cur ^ 1);
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue: y (+)= acc ----
+  T* __restrict__ C = reinterpret_cast<T*>(p.c);
+  size_t obase[MI][4];
+  bool ook[MI][4];
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = mt * BM + wm * (BM / 2) + mi * 16 + g * 4 + r;
+      ook[mi][r] = m < ph.M;
+      const int mm = ook[mi][r] ? m : 0;
+      const int nimg = mm / HWq, rem = mm - nimg * HWq;
+      const int qh = rem / ph.Wq, qw = rem - qh * ph.Wq;
+      const int oh = qh * p.osh + ph.oh0, ow = qw * p.osw + ph.ow0;
+      obase[mi][r] = (((size_t)nimg * p.Ho + oh) * p.Wo + ow) * p.ldc;
+    }
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni) {
+    const int n = nt * BN + wn * (BN / 2) + ni * 16 + i16;
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (!ook[mi][r]) continue;
+        float v = acc[mi][ni][r];
+        T* dst = C + obase[mi][r] + n;
+        if (p.accumulate) v += to_f32(*dst);
+        *dst = from_f32<T>(v);
+      }
+  }
+
+  if (p.stats) {
+    // Per-tile {sum, M2} of the tile's valid rows (M2 = sum of squared deviations from the tile
+    // mean): each wave centres its own half-tile, the two halves merge with Chan's formula.
+    float2* red = reinterpret_cast<float2*>(&lds[0][0]);  // [2][BN]
+    int nvalid_w = ph.M - (mt * BM + wm * (BM / 2));
+    nvalid_w = nvalid_w < 0 ? 0 : (nvalid_w > BM / 2 ? BM / 2 : nvalid_w);
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+      float s = 0.f;
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s += ook[mi][r] ? acc[mi][ni][r] : 0.f;
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      const float mean_w = nvalid_w > 0 ? s / (float)nvalid_w : 0.f;
+      float q = 0.f;
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float d = acc[mi][ni][r] - mean_w;
+          q = ook[mi][r] ? fmaf(d, d, q) : q;
+        }
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      if (lane < 16) red[wm * BN + wn * (BN / 2) + ni * 16 + lane] = make_float2(s, q);
+    }
+    __syncthreads();
+    if (tid < BN) {
+      int na = ph.M - mt * BM;
+      na = na < 0 ? 0 : (na > BM / 2 ? BM / 2 : na);
+      int nb = ph.M - (mt * BM + BM / 2);
+      nb = nb < 0 ? 0 : (nb > BM / 2 ? BM / 2 : nb);
+      const float2 a0 = red[tid], a1 = red[BN + tid];
+      float m2 = a0.y + a1.y;
+      if (na > 0 && nb > 0) {
+        const float d = a0.x / (float)na - a1.x / (float)nb;
+        m2 += d * d * ((float)na * (float)nb / (float)(na + nb));
+      }
+      p.stats[(size_t)mt * p.N + nt * BN + tid] = make_float2(a0.x + a1.x, m2);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// weight gradient (split over pixel ranges)
+// ------------------------------------------------------------------------------------------------
+struct WgParams {
+  const void* x;
+  const void* dy;
+  const float* pro_scale;
+  const float* pro_shift;
+  float* part;  // [splits][M][N]
+  int M, N, Cin, lda, H, W, Ho, Wo, stride, pad, S;
+  int P;
+  int pps;  // pixels per split (multiple of the k-step)
+  int stem;
+};
+
+// bf16 LDS image: rows of 256 B = 8 slots of 32 B; slot XOR swz32(row) makes the 8 rows a
+// ds_read_b64_tr_b16 half-wave touches land on 8 distinct slots.
+ARGUS_DEV int swz32(int row) { return (row & 3) | (((row >> 3) & 1) << 2); }
+
+template <typename T, int BM, int BN>
+__global__ __launch_bounds__(256) void wgrad_kernel(const WgParams p) {
+  constexpr int E = Chunk<T>::E;
+  constexpr bool BF = (E == 8);
+  constexpr int BKP = BF ? 64 : 32;               // pixels per k-step
+  constexpr int CA = BM * (int)sizeof(T) / 16;    // chunks per A row
+  constexpr int CB = BN * (int)sizeof(T) / 16;
+  constexpr int RSA = BF ? 16 : CA;               // LDS row stride (chunks)
+  constexpr int RSB = BF ? 16 : CB;
+  constexpr int RPA = 256 / CA, RPB = 256 / CB;   // rows per staging pass
+  constexpr int PA = BKP / RPA, PB = BKP / RPB;   // passes
+  constexpr int MI = BM / 32, NI = BN / 32;
+  __shared__ __attribute__((aligned(16))) u32x4 lds[2][BKP * (RSA + RSB)];
+
+  const int mtiles = p.M / BM, ntiles = p.N / BN;
+  const int nwg = mtiles * ntiles;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int mt = bid / ntiles, nt = bid - mt * ntiles;
+  const int split = blockIdx.y;
+  const int pbeg = split * p.pps;
+  const int pend = min(p.P, pbeg + p.pps);
+  if (pbeg >= pend) {
+    // still must zero the partial slab of this split
+  }
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const T* __restrict__ X = reinterpret_cast<const T*>(p.x);
+  const T* __restrict__ DY = reinterpret_cast<const T*>(p.dy);
+
+  // A staging: dy[p][mt*BM + ca*E .. +E)
+  const int ca = tid % CA, ra0 = tid / CA;
+  const T* a_col = DY + mt * BM + ca * E;
+  // B staging: column chunk fixed per thread -> tap / channel fixed
+  const int cb = tid % CB, rb0 = tid / CB;
+  const int kcol = nt * BN + cb * E;
+  int tap_r, tap_s, ci;
+  if (p.stem) {
+    tap_r = kcol >> 5; tap_s = (kcol & 31) >> 2; ci = 0;
+  } else {
+    const int t = kcol / p.Cin;
+    ci = kcol - t * p.Cin;
+    tap_r = t / p.S; tap_s = t - tap_r * p.S;
+  }
+  const int HWo = p.Ho * p.Wo;
+  const u32x4 zero = {0u, 0u, 0u, 0u};
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  u32x4 ra[PA], rb[PB];
+  auto load = [&](int p0) {
+#pragma unroll
+    for (int i = 0; i < PA; ++i) {
+      const int pix = p0 + ra0 + RPA * i;
+      ra[i] = pix < pend ? ld16(a_col + (size_t)pix * p.M) : zero;
+    }
+#pragma unroll
+    for (int i = 0; i < PB; ++i) {
+      const int pix = p0 + rb0 + RPB * i;
+      u32x4 v = zero;
+      if (pix < pend) {
+        const int nimg = pix / HWo, rem = pix - nimg * HWo;
+        const int oh = rem / p.Wo, ow = rem - oh * p.Wo;
+        const int ih = oh * p.stride - p.pad + tap_r;
+        const int iw0 = ow * p.stride - p.pad + tap_s;
+        if ((unsigned)ih < (unsigned)p.H) {
+          const T* rowp = X + ((size_t)nimg * p.H + ih) * p.W * p.lda;
+          if (p.stem) {
+            if constexpr (BF) {
+              unsigned w4[4];
+#pragma unroll
+              for (int u = 0; u < 2; ++u) {
+                const int iw = iw0 + u;
+                if ((unsigned)iw < (unsigned)p.W) {
+                  const uint2 q = *reinterpret_cast<const uint2*>(rowp + (size_t)iw * 4);
+                  w4[2 * u] = q.x; w4[2 * u + 1] = q.y;
+                } else {
+                  w4[2 * u] = 0u; w4[2 * u + 1] = 0u;
+                }
+              }
+              v = u32x4{w4[0], w4[1], w4[2], w4[3]};
+            } else {
+              if ((unsigned)iw0 < (unsigned)p.W) v = ld16(rowp + (size_t)iw0 * 4);
+            }
+          } else if ((unsigned)iw0 < (unsigned)p.W) {
+            v = ld16(rowp + (size_t)iw0 * p.lda + ci);
+            if (p.pro_scale) v = bn_relu_chunk<T>(v, p.pro_scale, p.pro_shift, ci);
+          }
+        }
+      }
+      rb[i] = v;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < PA; ++i) {
+      const int row = ra0 + RPA * i;
+      int c = ca;
+      if constexpr (BF) c = (((ca >> 1) ^ swz32(row)) << 1) | (ca & 1);
+      lds[buf][row * RSA + c] = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < PB; ++i) {
+      const int row = rb0 + RPB * i;
+      int c = cb;
+      if constexpr (BF) c = (((cb >> 1) ^ swz32(row)) << 1) | (cb & 1);
+      lds[buf][BKP * RSA + row * RSB + c] = rb[i];
+    }
+  };
+
+  const int g = lane >> 4, i16 = lane & 15;
+  auto compute = [&](int buf) {
+    if constexpr (BF) {
+      const char* base = reinterpret_cast<const char*>(&lds[buf][0]);
+      const int q = i16 >> 2, pq = i16 & 3;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        u32x4 fa[MI], fb[NI];
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi) {
+          const int slot = (wm * (BM / 2) + mi * 16) >> 4;
+          unsigned w[4];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int row = 32 * s2 + 8 * g + 4 * h + q;
+            const char* addr = base + row * 256 + ((slot ^ swz32(row)) << 5) + pq * 8;
+            const s16x4 t = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (s16x4 __attribute__((address_space(3)))*)(uintptr_t)(uint32_t)(uintptr_t)addr);
+            const uint2 u = __builtin_bit_cast(uint2, t);
+            w[2 * h] = u.x; w[2 * h + 1] = u.y;
+          }
+          fa[mi] = u32x4{w[0], w[1], w[2], w[3]};
+        }
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) {
+          const int slot = (wn * (BN / 2) + ni * 16) >> 4;
+          unsigned w[4];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int row = 32 * s2 + 8 * g + 4 * h + q;
+            const char* addr = base + BKP * RSA * 16 + row * 256 + ((slot ^ swz32(row)) << 5) + pq * 8;
+            const s16x4 t = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (s16x4 __attribute__((address_space(3)))*)(uintptr_t)(uint32_t)(uintptr_t)addr);
+            const uint2 u = __builtin_bit_cast(uint2, t);
+            w[2 * h] = u.x; w[2 * h + 1] = u.y;
+          }
+          fb[ni] = u32x4{w[0], w[1], w[2], w[3]};
+        }
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni) Mma<bf16>::run(acc[mi][ni], fa[mi], fb[ni]);
+      }
+    } else {
+      const float* fa = reinterpret_cast<const float*>(&lds[buf][0]);
+      const float* fb = reinterpret_cast<const float*>(&lds[buf][BKP * RSA]);
+#pragma unroll
+      for (int sub = 0; sub < BKP / 4; ++sub) {
+        const int row = 4 * sub + g;
+        float av[MI], bv[NI];
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi) av[mi] = fa[row * RSA * 4 + wm * (BM / 2) + mi * 16 + i16];
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) bv[ni] = fb[row * RSB * 4 + wn * (BN / 2) + ni * 16 + i16];
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[mi], bv[ni], acc[mi][ni], 0, 0, 0);
+      }
+    }
+  };
+
+  const int nk = pend > pbeg ? (pend - pbeg + BKP - 1) / BKP : 0;
+  if (nk > 0) {
+    load(pbeg);
+    store(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) load(pbeg + (kt + 1) * BKP);
+      compute(cur);
+      if (kt + 1 < nk) store(cur ^ 1);
+      __syncthreads();
+    }
+  }
+
+  float* out = p.part + (size_t)split * p.M * p.N;
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+      const int n = nt * BN + wn * (BN / 2) + ni * 16 + i16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = mt * BM + wm * (BM / 2) + mi * 16 + g * 4 + r;
+        out[(size_t)m * p.N + n] = acc[mi][ni][r];
+      }
+    }
+}
+
+// dw[e] = sum_s part[s][e]; for the stem scatter the padded (r8, s8, c4) columns to OHWI 7x7x3.
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int splits,
+                                                           int M, int N, int stem, float* __restrict__ dw) {
+  const size_t total4 = (size_t)M * N / 4;
+  const size_t stride = (size_t)M * N;
+  for (size_t e4 = blockIdx.x * 256 + threadIdx.x; e4 < total4; e4 += (size_t)gridDim.x * 256) {
+    f32x4 s = *reinterpret_cast<const f32x4*>(part + e4 * 4);
+    for (int k = 1; k < splits; ++k) s += *reinterpret_cast<const f32x4*>(part + k * stride + e4 * 4);
+    if (!stem) {
+      *reinterpret_cast<f32x4*>(dw + e4 * 4) = s;
+    } else {
+      const size_t e = e4 * 4;
+      const int m = (int)(e / N), col = (int)(e - (size_t)m * N);
+      const int r = col >> 5, sp = (col & 31) >> 2;  // 4 consecutive cols = c 0..3 of one (r, s)
+      if (r < 7 && sp < 7) {
+        float* o = dw + (size_t)m * 147 + (r * 7 + sp) * 3;
+        o[0] = s.x; o[1] = s.y; o[2] = s.z;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// layout kernels
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void images_to_nhwc4_kernel(const float* __restrict__ x, T* __restrict__ out,
+                                                              int64_t nimg, int hw) {
+  const int64_t total = nimg * hw;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t img = i / hw, pix = i - img * hw;
+    const float* src = x + img * 3 * hw + pix;
+    T* dst = out + i * 4;
+    dst[0] = from_f32<T>(src[0]);
+    dst[1] = from_f32<T>(src[hw]);
+    dst[2] = from_f32<T>(src[2 * hw]);
+    dst[3] = from_f32<T>(0.f);
+  }
+}
+
+// fp32 master weight (any strides: element (k, c, r, s) at k*sk + c*sc + r*sr + s*ss) -> forward
+// copy w_fwd[k][r][s][c] (dtype; stem padded [k][8][8][4]) and dgrad copy w_dgrad[c][r][s][k].
+struct WStrides { long long sk, sc, sr, ss; };
+
+template <typename T>
+__global__ __launch_bounds__(256) void weight_prep_kernel(const float* __restrict__ w, WStrides st,
+                                                          T* __restrict__ wf, T* __restrict__ wd, int K, int R,
+                                                          int S, int C, int stem) {
+  if (stem) {
+    const int total = K * 256;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+      const int k = i >> 8, col = i & 255;
+      const int r = col >> 5, s = (col & 31) >> 2, c = col & 3;
+      float v = 0.f;
+      if (r < 7 && s < 7 && c < 3) v = w[k * st.sk + c * st.sc + r * st.sr + s * st.ss];
+      wf[i] = from_f32<T>(v);
+    }
+    return;
+  }
+  const int RSC = R * S * C;
+  const int total = K * RSC;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int k = i / RSC, rem = i - k * RSC;
+    const int rs = rem / C, c = rem - rs * C;
+    const int r = rs / S, s = rs - r * S;
+    const float v = w[k * st.sk + c * st.sc + r * st.sr + s * st.ss];
+    if (wf) wf[i] = from_f32<T>(v);
+    if (wd) wd[((size_t)c * R * S + rs) * K + k] = from_f32<T>(v);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// host launchers
+// ------------------------------------------------------------------------------------------------
+static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+static int check_desc(const argus_conv_desc& d) {
+  if (d.n <= 0 || d.h <= 0 || d.w <= 0 || d.k <= 0 || d.r <= 0 || d.s <= 0 || d.stride <= 0) {
+    set_error("conv: non-positive dimension in descriptor");
+    return ARGUS_ERR_ARG;
+  }
+  if (d.ho != (d.h + 2 * d.pad - d.r) / d.stride + 1 || d.wo != (d.w + 2 * d.pad - d.s) / d.stride + 1) {
+    set_error("conv: ho/wo inconsistent with h/w/r/s/stride/pad");
+    return ARGUS_ERR_SHAPE;
+  }
+  if (d.stem) {
+    if (d.c != 3 || d.r != 7 || d.s != 7 || d.stride != 2 || d.pad != 3 || d.k % 64) {
+      set_error("conv: stem must be 3->k (k%64==0) 7x7/2 p3");
+      return ARGUS_ERR_SHAPE;
+    }
+  } else if (d.c % 64 || d.k % 64 || d.r > 3 || d.s > 3 || d.stride > 2) {
+    set_error("conv: channels must be multiples of 64, filters <= 3x3, stride <= 2");
+    return ARGUS_ERR_SHAPE;
+  }
+  return ARGUS_OK;
+}
+
+template <typename T, int BM, int BN>
+static void launch_ig(const IgParams& p, int maxM, hipStream_t st) {
+  const int ntiles = p.N / BN;
+  dim3 grid(cdiv(maxM, BM) * ntiles, 1, p.nphase);
+  hipLaunchKernelGGL((igemm_kernel<T, BM, BN>), grid, dim3(256), 0, st, p);
+}
+
+template <typename T>
+static int run_ig(const IgParams& p, hipStream_t st, int bm_pref) {
+  int maxM = 0;
+  for (int i = 0; i < p.nphase; ++i) maxM = p.ph[i].M > maxM ? p.ph[i].M : maxM;
+  const bool bn128 = (p.N % 128) == 0;
+  if (bm_pref == 128) {
+    if (bn128) launch_ig<T, 128, 128>(p, maxM, st);
+    else launch_ig<T, 128, 64>(p, maxM, st);
+  } else {
+    if (bn128) launch_ig<T, 64, 128>(p, maxM, st);
+    else launch_ig<T, 64, 64>(p, maxM, st);
+  }
+  return check_launch("igemm_kernel");
+}
+
+// row-tile size of the forward GEMM (drives the BN-statistics partial count)
+static int fwd_bm(const argus_conv_desc& d) {
+  const long M = (long)d.n * d.ho * d.wo;
+  return M >= 64L * 1024 ? 128 : 64;
+}
+
+int conv_fwd_stat_rows(const argus_conv_desc& d, int) {
+  return cdiv(d.n * d.ho * d.wo, fwd_bm(d));
+}
+
+int conv_fwd_stat_tile(const argus_conv_desc& d, int) { return fwd_bm(d); }
+
+int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, void* y,
+             const float* sc, const float* sh, float* stats, hipStream_t st) {
+  if (int e = check_desc(d)) return e;
+  IgParams p = {};
+  p.a = x; p.b = w; p.c = y; p.pro_scale = sc; p.pro_shift = sh;
+  p.stats = reinterpret_cast<float2*>(stats);
+  p.N = d.k; p.H = d.h; p.W = d.w; p.ish = d.stride; p.isw = d.stride;
+  p.Ho = d.ho; p.Wo = d.wo; p.osh = 1; p.osw = 1; p.ldc = d.k;
+  p.accumulate = 0; p.stem = d.stem; p.nphase = 1;
+  IgPhase& ph = p.ph[0];
+  ph.M = d.n * d.ho * d.wo; ph.Hq = d.ho; ph.Wq = d.wo; ph.oh0 = 0; ph.ow0 = 0;
+  if (d.stem) {
+    if (sc) { set_error("conv_fwd: stem has no prologue"); return ARGUS_ERR_ARG; }
+    p.Cin = 256; p.lda = 4; p.ldb = 256; ph.K = 256;
+    ph.dh[0] = 0; ph.dw[0] = 0; ph.boff[0] = 0;
+  } else {
+    p.Cin = d.c; p.lda = d.c; p.ldb = d.r * d.s * d.c; ph.K = d.r * d.s * d.c;
+    for (int r = 0; r < d.r; ++r)
+      for (int s = 0; s < d.s; ++s) {
+        const int t = r * d.s + s;
+        ph.dh[t] = r - d.pad; ph.dw[t] = s - d.pad; ph.boff[t] = t * d.c;
+      }
+  }
+  const int bm = fwd_bm(d);
+  return dtype == ARGUS_BF16 ? run_ig<bf16>(p, st, bm) : run_ig<float>(p, st, bm);
+}
+
+int conv_dgrad(const argus_conv_desc& d, int dtype, const void* dy, const void* wt, void* dx,
+               int accumulate, hipStream_t st) {
+  if (int e = check_desc(d)) return e;
+  if (d.stem) { set_error("conv_dgrad: the stem input has no gradient"); return ARGUS_ERR_ARG; }
+  IgParams p = {};
+  p.a = dy; p.b = wt; p.c = dx;
+  p.N = d.c; p.Cin = d.k; p.lda = d.k; p.H = d.ho; p.W = d.wo; p.ish = 1; p.isw = 1;
+  p.Ho = d.h; p.Wo = d.w; p.osh = d.stride; p.osw = d.stride; p.ldc = d.c; p.ldb = d.r * d.s * d.k;
+  p.accumulate = accumulate; p.stem = 0;
+  const int s = d.stride;
+  int np = 0;
+  for (int phh = 0; phh < s; ++phh)
+    for (int pww = 0; pww < s; ++pww) {
+      IgPhase& ph = p.ph[np++];
+      ph.Hq = cdiv(d.h - phh, s); ph.Wq = cdiv(d.w - pww, s);
+      ph.oh0 = phh; ph.ow0 = pww; ph.M = d.n * ph.Hq * ph.Wq;
+      int t = 0;
+      for (int r = 0; r < d.r; ++r) {
+        const int a = phh + d.pad - r;
+        if (((a % s) + s) % s) continue;
+        for (int c = 0; c < d.s; ++c) {
+          const int b = pww + d.pad - c;
+          if (((b % s) + s) % s) continue;
+          ph.dh[t] = a / s; ph.dw[t] = b / s;  // exact division (a, b divisible by s)
+          ph.boff[t] = (r * d.s + c) * d.k;
+          ++t;
+        }
+      }
+      ph.K = t * d.k;
+    }
+  p.nphase = np;
+  const long M = (long)d.n * d.h * d.w / (s * s);
+  const int bm = M >= 64L * 1024 ? 128 : 64;
+  return dtype == ARGUS_BF16 ? run_ig<bf16>(p, st, bm) : run_ig<float>(p, st, bm);
+}
+
+struct WgPlan {
+  int bm, bn, mt, nt, splits, pps, kstep;
+  int N;
+};
+
+static WgPlan wgrad_plan(const argus_conv_desc& d, int dtype) {
+  WgPlan pl;
+  pl.N = d.stem ? 256 : d.r * d.s * d.c;
+  pl.bm = d.k % 128 == 0 ? 128 : 64;
+  pl.bn = pl.N % 128 == 0 ? 128 : 64;
+  pl.mt = d.k / pl.bm;
+  pl.nt = pl.N / pl.bn;
+  pl.kstep = dtype == ARGUS_BF16 ? 64 : 32;
+  const long P = (long)d.n * d.ho * d.wo;
+  const long tiles = (long)pl.mt * pl.nt;
+  long splits = (1024 + tiles - 1) / tiles;
+  const long max_splits = (P + pl.kstep * 4 - 1) / (pl.kstep * 4);  // >= 4 k-steps per split
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  long pps = (P + splits - 1) / splits;
+  pps = (pps + pl.kstep - 1) / pl.kstep * pl.kstep;
+  splits = (P + pps - 1) / pps;
+  pl.splits = (int)splits;
+  pl.pps = (int)pps;
+  return pl;
+}
+
+size_t conv_wgrad_ws(const argus_conv_desc& d, int dtype) {
+  if (check_desc(d)) return 0;
+  const WgPlan pl = wgrad_plan(d, dtype);
+  return (size_t)pl.splits * d.k * pl.N * sizeof(float);
+}
+
+template <typename T, int BM, int BN>
+static void launch_wg(const WgParams& p, const WgPlan& pl, hipStream_t st) {
+  dim3 grid(pl.mt * pl.nt, pl.splits);
+  hipLaunchKernelGGL((wgrad_kernel<T, BM, BN>), grid, dim3(256), 0, st, p);
+}
+
+template <typename T>
+static void dispatch_wg(const WgParams& p, const WgPlan& pl, hipStream_t st) {
+  if (pl.bm == 128 && pl.bn == 128) launch_wg<T, 128, 128>(p, pl, st);
+  else if (pl.bm == 128) launch_wg<T, 128, 64>(p, pl, st);
+  else if (pl.bn == 128) launch_wg<T, 64, 128>(p, pl, st);
+  else launch_wg<T, 64, 64>(p, pl, st);
+}
+
+int conv_wgrad(const argus_conv_desc& d, int dtype, const void* x, const float* sc, const float* sh,
+               const void* dy, float* dw, void* ws, size_t ws_bytes, hipStream_t st) {
+  if (int e = check_desc(d)) return e;
+  const WgPlan pl = wgrad_plan(d, dtype);
+  if (ws_bytes < (size_t)pl.splits * d.k * pl.N * sizeof(float)) {
+    set_error("conv_wgrad: workspace too small");
+    return ARGUS_ERR_ARG;
+  }
+  WgParams p = {};
+  p.x = x; p.dy = dy; p.pro_scale = sc; p.pro_shift = sh; p.part = reinterpret_cast<float*>(ws);
+  p.M = d.k; p.N = pl.N; p.Cin = d.stem ? 4 : d.c; p.lda = d.stem ? 4 : d.c;
+  p.H = d.h; p.W = d.w; p.Ho = d.ho; p.Wo = d.wo; p.stride = d.stride; p.pad = d.pad; p.S = d.s;
+  p.P = d.n * d.ho * d.wo; p.pps = pl.pps; p.stem = d.stem;
+  if (d.stem && sc) { set_error("conv_wgrad: stem has no prologue"); return ARGUS_ERR_ARG; }
+  if (dtype == ARGUS_BF16) dispatch_wg<bf16>(p, pl, st);
+  else dispatch_wg<float>(p, pl, st);
+  if (int e = check_launch("wgrad_kernel")) return e;
+  const size_t total4 = (size_t)d.k * pl.N / 4;
+  const int blocks = (int)std::min<size_t>((total4 + 255) / 256, 2048);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st,
+                     reinterpret_cast<const float*>(ws), pl.splits, d.k, pl.N, d.stem, dw);
+  return check_launch("wgrad_reduce_kernel");
+}
+
+int conv_weight_prep(const argus_conv_desc& d, int dtype, const float* w, const int64_t* strides, void* wf,
+                     void* wd, hipStream_t st) {
+  if (int e = check_desc(d)) return e;
+  WStrides ws;
+  if (strides) {
+    ws = {strides[0], strides[1], strides[2], strides[3]};
+  } else {  // OHWI contiguous
+    ws = {(long long)d.r * d.s * d.c, 1, (long long)d.s * d.c, d.c};
+  }
+  if (d.stem && !wf) { set_error("weight_prep: stem needs w_fwd"); return ARGUS_ERR_ARG; }
+  const int total = d.stem ? d.k * 256 : d.k * d.r * d.s * d.c;
+  const int blocks = std::min(cdiv(total, 256), 4096);
+  if (dtype == ARGUS_BF16)
+    hipLaunchKernelGGL(weight_prep_kernel<bf16>, dim3(blocks), dim3(256), 0, st, w, ws, (bf16*)wf,
+                       (bf16*)(d.stem ? nullptr : wd), d.k, d.r, d.s, d.c, d.stem);
+  else
+    hipLaunchKernelGGL(weight_prep_kernel<float>, dim3(blocks), dim3(256), 0, st, w, ws, (float*)wf,
+                       (float*)(d.stem ? nullptr : wd), d.k, d.r, d.s, d.c, d.stem);
+  return check_launch("weight_prep_kernel");
+}
+
+int images_to_nhwc4(int dtype, int64_t nimg, int h, int w, const float* x, void* out, hipStream_t st) {
+  const int64_t total = nimg * h * w;
+  const int blocks = (int)std::min<int64_t>((total + 255) / 256, 8192);
+  if (dtype == ARGUS_BF16)
+    hipLaunchKernelGGL(images_to_nhwc4_kernel<bf16>, dim3(blocks), dim3(256), 0, st, x, (bf16*)out, nimg, h * w);
+  else
+    hipLaunchKernelGGL(images_to_nhwc4_kernel<float>, dim3(blocks), dim3(256), 0, st, x, (float*)out, nimg, h * w);
+  return check_launch("images_to_nhwc4_kernel");
+}
+
+}  // namespace argus

@@ -1,0 +1,141 @@
+// FC / MLP head (nn.Linear + exact-erf GELU): resnet.fc 2048->1024 (argus/models.py:56) and the
+// output MLP 2048->128->128->6 (models.py:58-64, GELU at :88). fp32 throughout: these GEMMs are
+// < 0.03 GFLOP/sample and latency-bound, so a simple LDS-tiled kernel on the exact
+// f32 MFMA (v_mfma_f32_16x16x4_f32) keeps the head at fp32 accuracy in every precision mode.
+#include "common.h"
+#include "internal.h"
+
+namespace argus {
+
+ARGUS_DEV float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+ARGUS_DEV float gelu_grad(float x) {
+  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+// 64x64 output tile, 256 threads (4 waves, 2x2, each 32x32 = 2x2 MFMA blocks), K-step 16.
+__global__ __launch_bounds__(256) void gemm_f32_kernel(int M, int N, int K, const float* __restrict__ A, int lda,
+                                                       int ta, const float* __restrict__ B, int ldb, int tb,
+                                                       float* __restrict__ C, int ldc, const float* __restrict__ bias,
+                                                       int epi, float* __restrict__ aux) {
+  __shared__ float As[16][65];  // [k][m]
+  __shared__ float Bs[16][65];  // [k][n]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < K; k0 += 16) {
+    // stage 16 x 64 of A (as [k][m]) and B (as [k][n]): 1024 elements each, 4 per thread
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int idx = tid + 256 * e;
+      int kk, mm;
+      if (ta) { kk = idx >> 6; mm = idx & 63; } else { mm = idx >> 4; kk = idx & 15; }
+      const int gm = m0 + mm, gk = k0 + kk;
+      float v = 0.f;
+      if (gm < M && gk < K) v = ta ? A[(size_t)gk * lda + gm] : A[(size_t)gm * lda + gk];
+      As[kk][mm] = v;
+      int kb, nn;
+      if (tb) { nn = idx >> 4; kb = idx & 15; } else { kb = idx >> 6; nn = idx & 63; }
+      const int gn = n0 + nn, gk2 = k0 + kb;
+      float w = 0.f;
+      if (gn < N && gk2 < K) w = tb ? B[(size_t)gn * ldb + gk2] : B[(size_t)gk2 * ldb + gn];
+      Bs[kb][nn] = w;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int kk = 4 * s + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const float a = As[kk][wm * 32 + i * 16 + (lane & 15)];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const float b = Bs[kk][wn * 32 + j * 16 + (lane & 15)];
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[i][j], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wn * 32 + j * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
+        if (m >= M || n >= N) continue;
+        float v = acc[i][j][r];
+        float* dst = C + (size_t)m * ldc + n;
+        switch (epi) {
+          case 0: *dst = v; break;
+          case 1: *dst = v + bias[n]; break;
+          case 2: v += bias[n]; aux[(size_t)m * ldc + n] = v; *dst = gelu_f(v); break;
+          case 3: *dst = v * gelu_grad(aux[(size_t)m * ldc + n]); break;
+          default: *dst += v; break;
+        }
+      }
+    }
+}
+
+__global__ void colsum_kernel(int M, int N, const float* __restrict__ x, int ld, float* __restrict__ out) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int m = 0; m < M; ++m) s += x[(size_t)m * ld + n];
+  out[n] = s;
+}
+
+__global__ void gelu_kernel(int64_t n, const float* __restrict__ x, float* __restrict__ y) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) y[i] = gelu_f(x[i]);
+}
+__global__ void gelu_bwd_kernel(int64_t n, const float* __restrict__ x, const float* __restrict__ dy,
+                                float* __restrict__ dx) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    dx[i] = dy[i] * gelu_grad(x[i]);
+}
+
+}  // namespace argus
+
+using namespace argus;
+
+extern "C" {
+
+int argus_gemm_f32(int m, int n, int k, const float* a, int lda, int ta, const float* b, int ldb, int tb, float* c,
+                   int ldc, const float* bias, int epi, float* aux, argus_stream_t stream) {
+  if (m <= 0 || n <= 0 || k <= 0 || !a || !b || !c || epi < 0 || epi > 4 || ((epi == 1 || epi == 2) && !bias) ||
+      ((epi == 2 || epi == 3) && !aux)) {
+    set_error("gemm_f32: bad arguments");
+    return ARGUS_ERR_ARG;
+  }
+  dim3 grid((n + 63) / 64, (m + 63) / 64);
+  hipLaunchKernelGGL(gemm_f32_kernel, grid, dim3(256), 0, (hipStream_t)stream, m, n, k, a, lda, ta, b, ldb, tb, c, ldc,
+                     bias, epi, aux);
+  return check_launch("gemm_f32_kernel");
+}
+
+int argus_colsum_f32(int m, int n, const float* x, int ld, float* out, argus_stream_t stream) {
+  hipLaunchKernelGGL(colsum_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, m, n, x, ld, out);
+  return check_launch("colsum_kernel");
+}
+
+int argus_gelu_f32(int64_t count, const float* x, float* y, argus_stream_t stream) {
+  const int blocks = (int)std::min<int64_t>((count + 255) / 256, 4096);
+  hipLaunchKernelGGL(gelu_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, count, x, y);
+  return check_launch("gelu_kernel");
+}
+
+int argus_gelu_bwd_f32(int64_t count, const float* x, const float* dy, float* dx, argus_stream_t stream) {
+  const int blocks = (int)std::min<int64_t>((count + 255) / 256, 4096);
+  hipLaunchKernelGGL(gelu_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, count, x, dy, dx);
+  return check_launch("gelu_bwd_kernel");
+}
+
+}  // extern "C"

@@ -1,0 +1,30 @@
+// Internal (C++) launcher declarations shared by the .hip translation units and capi.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/argus_hip.h"
+
+namespace argus {
+
+void set_error(const std::string& msg);
+int check_launch(const char* what);
+
+int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, void* y,
+             const float* sc, const float* sh, float* stats, hipStream_t st);
+int conv_fwd_stat_rows(const argus_conv_desc& d, int dtype);
+int conv_fwd_stat_tile(const argus_conv_desc& d, int dtype);
+int conv_dgrad(const argus_conv_desc& d, int dtype, const void* dy, const void* wt, void* dx,
+               int accumulate, hipStream_t st);
+size_t conv_wgrad_ws(const argus_conv_desc& d, int dtype);
+int conv_wgrad(const argus_conv_desc& d, int dtype, const void* x, const float* sc,
+               const float* sh, const void* dy, float* dw, void* ws, size_t ws_bytes,
+               hipStream_t st);
+int conv_weight_prep(const argus_conv_desc& d, int dtype, const float* w, const int64_t* strides,
+                     void* wf, void* wd, hipStream_t st);
+int images_to_nhwc4(int dtype, int64_t nimg, int h, int w, const float* x, void* out,
+                    hipStream_t st);
+
+}  // namespace argus

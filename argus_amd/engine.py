@@ -1,0 +1,394 @@
+"""Native ResNet-50 x N-camera forward/backward schedule over libargus_hip (MI355X / gfx950).
+
+Replaces the implicit ATen/cuDNN work behind ``NCameraCNN.forward`` (argus/models.py:66-90, the
+torchvision ResNet-50 at :43) and its autograd backward (argus/train.py:316). The schedule is
+fixed for the architecture, so it is written out explicitly instead of being traced:
+
+forward (train mode), per Bottleneck (stride on the 3x3, torchvision v1.5):
+    y1 = conv1(h)                      + BN1 stats   (epilogue)        -> finalize -> (sc1, sh1)
+    y2 = conv2(relu(bn1(y1)))          + BN2 stats   (BN1+ReLU applied while staging y1)
+    y3 = conv3(relu(bn2(y2)))          + BN3 stats
+    yd = downsample(h)                 + BNd stats   (first block of a stage)
+    out = relu(bn3(y3) + (bnd(yd) | h))                                  (one fused pass)
+stem: y0 = conv7x7/2(x) + stats; p0 = maxpool3x3/2(relu(bn1(y0))) (fused, argmax kept)
+head (fp32): feat = avgpool(out) -> fc 2048->1024 -> reshape (B, n_cams*1024) -> GELU -> MLP -> (B,6)
+
+Saved for backward: y1, y2, y3, yd, out per block (compute dtype), BN mean/invstd/scale/shift,
+stem y0 + maxpool argmax, head pre-activations. ReLU masks and normalised activations are
+recomputed from the raw conv outputs (no x_hat tensors are stored).
+
+Eval mode uses running statistics (bn_eval_coeffs) and skips all statistics / running updates.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import torch
+
+from argus_amd._lib import BF16, F32, ConvDesc, lib, ptr, stream
+
+
+@dataclass(frozen=True)
+class Block:
+    prefix: str  # "resnet.layer{L}.{i}"
+    cin: int
+    width: int
+    cout: int
+    stride: int
+    has_ds: bool
+
+
+def resnet50_blocks() -> list[Block]:
+    blocks, inplanes = [], 64
+    for L, (planes, n, stride) in enumerate([(64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2)], start=1):
+        for i in range(n):
+            blocks.append(Block(f"resnet.layer{L}.{i}", inplanes, planes, planes * 4, stride if i == 0 else 1, i == 0))
+            inplanes = planes * 4
+    return blocks
+
+
+def _out(h: int, k: int, s: int, p: int) -> int:
+    return (h + 2 * p - k) // s + 1
+
+
+@dataclass
+class _Conv:
+    name: str
+    desc: ConvDesc
+    wf: torch.Tensor
+    wd: torch.Tensor | None
+    stat_rows: int
+    stat_tile: int
+
+
+class ResNetEngine:
+    """Workspace + launch schedule for one (batch, H, W, dtype) configuration on one device."""
+
+    def __init__(self, n_cams: int, resnet_output_dim: int, dtype: str, device: torch.device):
+        if dtype not in ("fp32", "bf16"):
+            raise ValueError(f"compute dtype must be 'fp32' or 'bf16', got {dtype!r}")
+        self.L = lib()
+        self.n_cams = n_cams
+        self.rdim = resnet_output_dim
+        self.dtype = dtype
+        self.dt = BF16 if dtype == "bf16" else F32
+        self.tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
+        self.device = torch.device(device)
+        self.blocks = resnet50_blocks()
+        self.shape = None
+        self.saved = False
+        self.debug: dict | None = None  # when a dict: clones of block outputs / block-input grads
+
+    # ------------------------------------------------------------------ allocation
+    def _t(self, *shape, dtype=None):
+        return torch.empty(shape, dtype=dtype or self.tdt, device=self.device)
+
+    def _f(self, *shape):
+        return torch.empty(shape, dtype=torch.float32, device=self.device)
+
+    def ensure(self, B: int, H: int, W: int) -> None:
+        if self.shape == (B, H, W):
+            return
+        self.shape = (B, H, W)
+        N = B * self.n_cams
+        self.N = N
+        L = self.L
+        dt = self.dt
+        convs: dict[str, _Conv] = {}
+
+        def add(name, n, h, w, c, k, ks, s, p, stem=False):
+            d = ConvDesc(n, h, w, c, k, ks, ks, s, p, _out(h, ks, s, p), _out(w, ks, s, p), int(stem))
+            if stem:
+                wf = self._t(k, 256)
+                wd = None
+            else:
+                wf = self._t(k, ks * ks * c)
+                wd = self._t(c, ks * ks * k)
+            rows = L.dll.argus_conv_fwd_stat_rows(C.byref(d), dt)
+            tile = L.dll.argus_conv_fwd_stat_tile(C.byref(d), dt)
+            convs[name] = _Conv(name, d, wf, wd, rows, tile)
+            return d.ho, d.wo
+
+        H1, W1 = add("resnet.conv1", N, H, W, 3, 64, 7, 2, 3, stem=True)
+        H2, W2 = _out(H1, 3, 2, 1), _out(W1, 3, 2, 1)
+        self.stem_hw = (H1, W1)
+        self.pool_hw = (H2, W2)
+        self.x0 = self._t(N, H, W, 4)
+        self.y0 = self._t(N, H1, W1, 64)
+        self.p0 = self._t(N, H2, W2, 64)
+        self.amax = torch.empty((N, H2, W2, 64), dtype=torch.uint8, device=self.device)
+        act = []
+        h, w = H2, W2
+        max_elems = N * H1 * W1 * 64
+        for b in self.blocks:
+            add(b.prefix + ".conv1", N, h, w, b.cin, b.width, 1, 1, 0)
+            ho, wo = add(b.prefix + ".conv2", N, h, w, b.width, b.width, 3, b.stride, 1)
+            add(b.prefix + ".conv3", N, ho, wo, b.width, b.cout, 1, 1, 0)
+            if b.has_ds:
+                add(b.prefix + ".downsample.0", N, h, w, b.cin, b.cout, 1, b.stride, 0)
+            a = {
+                "hw_in": (h, w), "hw": (ho, wo),
+                "y1": self._t(N, h, w, b.width), "y2": self._t(N, ho, wo, b.width),
+                "y3": self._t(N, ho, wo, b.cout), "out": self._t(N, ho, wo, b.cout),
+                "yd": self._t(N, ho, wo, b.cout) if b.has_ds else None,
+            }
+            max_elems = max(max_elems, N * h * w * b.cin, N * h * w * b.width, N * ho * wo * b.cout)
+            act.append(a)
+            h, w = ho, wo
+        self.act = act
+        self.final_hw = (h, w)
+        self.convs = convs
+
+        # BN state: rows of [mean, invstd, scale, shift] and backward coefficients [ca, cb, cc]
+        self.bn_names = ["resnet.bn1"]
+        for b in self.blocks:
+            self.bn_names += [b.prefix + ".bn1", b.prefix + ".bn2", b.prefix + ".bn3"]
+            if b.has_ds:
+                self.bn_names.append(b.prefix + ".downsample.1")
+        chans = {"resnet.bn1": 64}
+        for b in self.blocks:
+            chans[b.prefix + ".bn1"] = b.width
+            chans[b.prefix + ".bn2"] = b.width
+            chans[b.prefix + ".bn3"] = b.cout
+            if b.has_ds:
+                chans[b.prefix + ".downsample.1"] = b.cout
+        self.bn_ch = chans
+        self.bn_state = {n: self._f(4, c) for n, c in chans.items()}
+        self.bn_coef = {n: self._f(3, c) for n, c in chans.items()}
+
+        max_stat = max(cv.stat_rows * cv.desc.k for cv in convs.values())
+        self.stat_part = self._f(max_stat * 2)
+        self.bn_ws = torch.empty(L.dll.argus_bn_workspace_bytes(2048), dtype=torch.uint8, device=self.device)
+        max_bwd = 0
+        for b, a in zip(self.blocks, act):
+            for hw, c in ((a["hw_in"], b.width), (a["hw"], b.width), (a["hw"], b.cout)):
+                px = N * hw[0] * hw[1]
+                max_bwd = max(max_bwd, L.dll.argus_bn_bwd_rows(px, c) * c)
+        max_bwd = max(max_bwd, L.dll.argus_bn_bwd_rows(N * H1 * W1, 64) * 64)
+        self.bwd_part = self._f(max_bwd * 2)
+        ws = max(L.dll.argus_conv_wgrad_workspace_bytes(C.byref(cv.desc), dt) for cv in convs.values())
+        self.wg_ws = torch.empty(ws, dtype=torch.uint8, device=self.device)
+        self.wg_ws_bytes = ws
+        self.gbuf = [self._t(max_elems) for _ in range(6)]
+
+        Fd = 512 * 4
+        self.feat = self._f(N, Fd)
+        self.h0 = self._f(N, self.rdim)
+        self.g0 = self._f(B, self.n_cams * self.rdim)
+        self.h1, self.g1 = self._f(B, 128), self._f(B, 128)
+        self.h2, self.g2 = self._f(B, 128), self._f(B, 128)
+        self.pred = self._f(B, 6)
+        self.dh2, self.dh1 = self._f(B, 128), self._f(B, 128)
+        self.dh0 = self._f(B, self.n_cams * self.rdim)
+        self.dfeat = self._f(N, Fd)
+
+    # ------------------------------------------------------------------ helpers
+    def _bn_train(self, P, Bf, name, rows, tile, count):
+        st = self.bn_state[name]
+        mom = Bf.get(name + ".momentum", 0.1)
+        self.L.bn_finalize(self.bn_ch[name], rows, tile, ptr(self.stat_part), count, ptr(P[name + ".weight"]),
+                           ptr(P[name + ".bias"]), C.c_float(Bf.get(name + ".eps", 1e-5)), C.c_float(mom),
+                           ptr(Bf[name + ".running_mean"]), ptr(Bf[name + ".running_var"]),
+                           ptr(Bf[name + ".num_batches_tracked"]), ptr(st[0]), ptr(st[1]), ptr(st[2]), ptr(st[3]),
+                           ptr(self.bn_ws), stream())
+
+    def _bn_eval(self, P, Bf, name):
+        st = self.bn_state[name]
+        self.L.bn_eval_coeffs(self.bn_ch[name], ptr(P[name + ".weight"]), ptr(P[name + ".bias"]),
+                              ptr(Bf[name + ".running_mean"]), ptr(Bf[name + ".running_var"]),
+                              C.c_float(Bf.get(name + ".eps", 1e-5)), ptr(st[2]), ptr(st[3]), stream())
+
+    def _conv_bn(self, P, Bf, conv, bn, x, y, pro, training):
+        cv = self.convs[conv]
+        sc = sh = None
+        if pro is not None:
+            sc, sh = self.bn_state[pro][2], self.bn_state[pro][3]
+        self.L.conv_fwd(C.byref(cv.desc), self.dt, ptr(x), ptr(cv.wf), ptr(y), ptr(sc), ptr(sh),
+                        ptr(self.stat_part) if training else None, stream())
+        if training:
+            count = cv.desc.n * cv.desc.ho * cv.desc.wo
+            self._bn_train(P, Bf, bn, cv.stat_rows, cv.stat_tile, count)
+        else:
+            self._bn_eval(P, Bf, bn)
+
+    def prepare_weights(self, P) -> None:
+        s = stream()
+        for name, cv in self.convs.items():
+            w = P[name + ".weight"]
+            if w.dtype != torch.float32 or w.device != self.device:
+                raise TypeError(f"{name}.weight must be fp32 on {self.device}")
+            strides = (C.c_int64 * 4)(*w.stride())
+            self.L.conv_weight_prep(C.byref(cv.desc), self.dt, ptr(w), strides, ptr(cv.wf), ptr(cv.wd), s)
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, x: torch.Tensor, P: dict, Bf: dict, training: bool) -> torch.Tensor:
+        B, Cn, H, W = x.shape
+        if Cn != 3 * self.n_cams:
+            raise ValueError(f"expected {3 * self.n_cams} input channels, got {Cn}")
+        self.ensure(B, H, W)
+        x = x.contiguous()
+        if x.dtype != torch.float32:
+            x = x.float()
+        L, dt, s = self.L, self.dt, stream()
+        N = self.N
+        self.prepare_weights(P)
+        L.images_to_nhwc4(dt, N, H, W, ptr(x), ptr(self.x0), s)
+        # stem
+        self._conv_bn(P, Bf, "resnet.conv1", "resnet.bn1", self.x0, self.y0, None, training)
+        st = self.bn_state["resnet.bn1"]
+        H1, W1 = self.stem_hw
+        L.maxpool_fwd(dt, N, H1, W1, 64, ptr(self.y0), ptr(st[2]), ptr(st[3]), ptr(self.p0), ptr(self.amax), s)
+        h = self.p0
+        for b, a in zip(self.blocks, self.act):
+            pf = b.prefix
+            self._conv_bn(P, Bf, pf + ".conv1", pf + ".bn1", h, a["y1"], None, training)
+            self._conv_bn(P, Bf, pf + ".conv2", pf + ".bn2", a["y1"], a["y2"], pf + ".bn1", training)
+            self._conv_bn(P, Bf, pf + ".conv3", pf + ".bn3", a["y2"], a["y3"], pf + ".bn2", training)
+            s3 = self.bn_state[pf + ".bn3"]
+            px = N * a["hw"][0] * a["hw"][1]
+            if b.has_ds:
+                self._conv_bn(P, Bf, pf + ".downsample.0", pf + ".downsample.1", h, a["yd"], None, training)
+                sd = self.bn_state[pf + ".downsample.1"]
+                L.bn_apply(dt, px, b.cout, ptr(a["y3"]), ptr(s3[2]), ptr(s3[3]), ptr(a["yd"]), ptr(sd[2]),
+                           ptr(sd[3]), 1, ptr(a["out"]), s)
+            else:
+                L.bn_apply(dt, px, b.cout, ptr(a["y3"]), ptr(s3[2]), ptr(s3[3]), ptr(h), None, None, 1,
+                           ptr(a["out"]), s)
+            h = a["out"]
+            if self.debug is not None:
+                self.debug["fwd." + pf] = a["out"].clone()
+        hf, wf = self.final_hw
+        L.avgpool_fwd(dt, N, hf * wf, 2048, ptr(h), ptr(self.feat), s)
+        # head (fp32)
+        fcw, fcb = P["resnet.fc.weight"], P["resnet.fc.bias"]
+        L.gemm_f32(N, self.rdim, 2048, ptr(self.feat), 2048, 0, ptr(fcw), 2048, 1, ptr(self.h0), self.rdim,
+                   ptr(fcb), 1, None, s)
+        D = self.n_cams * self.rdim
+        L.gelu_f32(B * D, ptr(self.h0), ptr(self.g0), s)
+        w0, b0 = P["output_mlp.0.weight"], P["output_mlp.0.bias"]
+        w2, b2 = P["output_mlp.2.weight"], P["output_mlp.2.bias"]
+        w4, b4 = P["output_mlp.4.weight"], P["output_mlp.4.bias"]
+        L.gemm_f32(B, 128, D, ptr(self.g0), D, 0, ptr(w0), D, 1, ptr(self.g1), 128, ptr(b0), 2, ptr(self.h1), s)
+        L.gemm_f32(B, 128, 128, ptr(self.g1), 128, 0, ptr(w2), 128, 1, ptr(self.g2), 128, ptr(b2), 2, ptr(self.h2), s)
+        L.gemm_f32(B, 6, 128, ptr(self.g2), 128, 0, ptr(w4), 128, 1, ptr(self.pred), 6, ptr(b4), 1, None, s)
+        self.saved = training
+        return self.pred
+
+    # ------------------------------------------------------------------ backward
+    def backward(self, dpred: torch.Tensor, P: dict, G: dict) -> None:
+        """Write every parameter gradient into G[name] (fp32; conv weights OHWI-contiguous)."""
+        if not self.saved:
+            raise RuntimeError("backward without a saved train-mode forward")
+        L, dt, s = self.L, self.dt, stream()
+        B = self.shape[0]
+        N = self.N
+        D = self.n_cams * self.rdim
+        dpred = dpred.contiguous().float()
+        w0, w2, w4 = P["output_mlp.0.weight"], P["output_mlp.2.weight"], P["output_mlp.4.weight"]
+        # MLP
+        L.gemm_f32(6, 128, B, ptr(dpred), 6, 1, ptr(self.g2), 128, 0, ptr(G["output_mlp.4.weight"]), 128, None, 0, None, s)
+        L.colsum_f32(B, 6, ptr(dpred), 6, ptr(G["output_mlp.4.bias"]), s)
+        L.gemm_f32(B, 128, 6, ptr(dpred), 6, 0, ptr(w4), 128, 0, ptr(self.dh2), 128, None, 3, ptr(self.h2), s)
+        L.gemm_f32(128, 128, B, ptr(self.dh2), 128, 1, ptr(self.g1), 128, 0, ptr(G["output_mlp.2.weight"]), 128, None, 0, None, s)
+        L.colsum_f32(B, 128, ptr(self.dh2), 128, ptr(G["output_mlp.2.bias"]), s)
+        L.gemm_f32(B, 128, 128, ptr(self.dh2), 128, 0, ptr(w2), 128, 0, ptr(self.dh1), 128, None, 3, ptr(self.h1), s)
+        L.gemm_f32(128, D, B, ptr(self.dh1), 128, 1, ptr(self.g0), D, 0, ptr(G["output_mlp.0.weight"]), D, None, 0, None, s)
+        L.colsum_f32(B, 128, ptr(self.dh1), 128, ptr(G["output_mlp.0.bias"]), s)
+        L.gemm_f32(B, D, 128, ptr(self.dh1), 128, 0, ptr(w0), D, 0, ptr(self.dh0), D, None, 3, ptr(self.h0), s)
+        # fc (rows = images)
+        fcw = P["resnet.fc.weight"]
+        R = self.rdim
+        L.gemm_f32(R, 2048, N, ptr(self.dh0), R, 1, ptr(self.feat), 2048, 0, ptr(G["resnet.fc.weight"]), 2048, None, 0, None, s)
+        L.colsum_f32(N, R, ptr(self.dh0), R, ptr(G["resnet.fc.bias"]), s)
+        L.gemm_f32(N, 2048, R, ptr(self.dh0), R, 0, ptr(fcw), 2048, 0, ptr(self.dfeat), 2048, None, 0, None, s)
+        hf, wf = self.final_hw
+        g = self.gbuf
+        dh, dx = g[0], g[3]
+        L.avgpool_bwd(dt, N, hf * wf, 2048, ptr(self.dfeat), ptr(dh), s)
+
+        for idx in range(len(self.blocks) - 1, -1, -1):
+            b, a = self.blocks[idx], self.act[idx]
+            pf = b.prefix
+            h_in = self.act[idx - 1]["out"] if idx > 0 else self.p0
+            hi, wi = a["hw_in"]
+            ho, wo = a["hw"]
+            px_o = N * ho * wo
+            px_i = N * hi * wi
+            dy3, dyd, dz, dyw = g[1], g[2], g[4], g[5]
+            dbg = self.debug
+
+            def cap(key, t, n, shape):
+                if dbg is not None:
+                    dbg[key + "." + pf] = t[:n].view(*shape).clone()
+
+            cap("b_dout", dh, px_o * b.cout, (N, ho, wo, b.cout))
+            # bn3 (+ bnd) backward, relu mask from the block output
+            self._bn_bwd(P, G, pf + ".bn3", px_o, b.cout, dh, 1, a["out"], a["y3"], dy3,
+                         None if b.has_ds else dx)
+            if b.has_ds:
+                self._bn_bwd(P, G, pf + ".downsample.1", px_o, b.cout, dh, 1, a["out"], a["yd"], dyd, None)
+            cap("b_dy3", dy3, px_o * b.cout, (N, ho, wo, b.cout))
+            # conv3
+            s2 = self.bn_state[pf + ".bn2"]
+            self._wgrad(pf + ".conv3", a["y2"], s2, dy3, G)
+            self._dgrad(pf + ".conv3", dy3, dz, 0)
+            cap("b_dz2", dz, px_o * b.width, (N, ho, wo, b.width))
+            self._bn_bwd(P, G, pf + ".bn2", px_o, b.width, dz, 2, None, a["y2"], dyw, None)
+            cap("b_dy2", dyw, px_o * b.width, (N, ho, wo, b.width))
+            # conv2
+            s1 = self.bn_state[pf + ".bn1"]
+            self._wgrad(pf + ".conv2", a["y1"], s1, dyw, G)
+            self._dgrad(pf + ".conv2", dyw, dz, 0)
+            cap("b_dz1", dz, px_i * b.width, (N, hi, wi, b.width))
+            self._bn_bwd(P, G, pf + ".bn1", px_i, b.width, dz, 2, None, a["y1"], dyw, None)
+            cap("b_dy1", dyw, px_i * b.width, (N, hi, wi, b.width))
+            # conv1 (+ downsample)
+            self._wgrad(pf + ".conv1", h_in, None, dyw, G)
+            if b.has_ds:
+                self._dgrad(pf + ".conv1", dyw, dx, 0)
+                self._wgrad(pf + ".downsample.0", h_in, None, dyd, G)
+                self._dgrad(pf + ".downsample.0", dyd, dx, 1)
+            else:
+                self._dgrad(pf + ".conv1", dyw, dx, 1)
+            dh, dx = dx, dh
+            if self.debug is not None:
+                n_in = N * hi * wi * b.cin
+                self.debug["bwd." + pf] = dh[:n_in].view(N, hi, wi, b.cin).clone()
+                self.debug["bwd_dh." + pf] = dy3[:px_o * b.cout].view(N, ho, wo, b.cout).clone()
+        # stem: maxpool -> relu/bn1 -> conv1 wgrad
+        H1, W1 = self.stem_hw
+        dz0, dy0 = g[4], g[5]
+        L.maxpool_bwd(dt, N, H1, W1, 64, ptr(dh), ptr(self.amax), ptr(dz0), s)
+        self._bn_bwd(P, G, "resnet.bn1", N * H1 * W1, 64, dz0, 2, None, self.y0, dy0, None)
+        self._wgrad("resnet.conv1", self.x0, None, dy0, G)
+
+    def _bn_bwd(self, P, G, name, px, ch, dz, mode, mask_src, y, dy_out, dm_out):
+        L, dt, s = self.L, self.dt, stream()
+        st, cf = self.bn_state[name], self.bn_coef[name]
+        L.bn_bwd_reduce(dt, px, ch, ptr(dz), mode, ptr(mask_src), ptr(y), ptr(st[2]), ptr(st[3]), ptr(st[0]),
+                        ptr(st[1]), ptr(self.bwd_part), s)
+        rows = L.dll.argus_bn_bwd_rows(px, ch)
+        L.bn_bwd_finalize(ch, rows, ptr(self.bwd_part), px, ptr(P[name + ".weight"]), ptr(st[0]), ptr(st[1]),
+                          ptr(G[name + ".weight"]), ptr(G[name + ".bias"]), ptr(cf[0]), ptr(cf[1]), ptr(cf[2]),
+                          ptr(self.bn_ws), s)
+        L.bn_bwd_apply(dt, px, ch, ptr(dz), mode, ptr(mask_src), ptr(y), ptr(st[2]), ptr(st[3]), ptr(cf[0]),
+                       ptr(cf[1]), ptr(cf[2]), ptr(dy_out), ptr(dm_out), s)
+
+    def _wgrad(self, conv, x, pro_state, dy, G):
+        cv = self.convs[conv]
+        sc = sh = None
+        if pro_state is not None:
+            sc, sh = pro_state[2], pro_state[3]
+        self.L.conv_wgrad(C.byref(cv.desc), self.dt, ptr(x), ptr(sc), ptr(sh), ptr(dy), ptr(G[conv + ".weight"]),
+                          ptr(self.wg_ws), self.wg_ws_bytes, stream())
+
+    def _dgrad(self, conv, dy, dx, accumulate):
+        cv = self.convs[conv]
+        self.L.conv_dgrad(C.byref(cv.desc), self.dt, ptr(dy), ptr(cv.wd), ptr(dx), accumulate, stream())
+
+
+def conv_grad_shape(shape_oihw) -> tuple:
+    """OHWI buffer shape for an OIHW conv weight (the layout conv_wgrad writes)."""
+    k, c, r, s = shape_oihw
+    return (k, r, s, c)

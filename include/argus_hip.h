@@ -1,0 +1,165 @@
+/*
+ * argus_hip.h — C ABI of libargus_hip.so, the MI355X (gfx950) kernels behind the argus training
+ * hot path. Plain C: raw device pointers, sizes, an opaque HIP stream; no torch types.
+ *
+ * The reference (pculbertson/argus) has no FFI; its device work is dispatched implicitly through
+ * torchvision / pypose / torch.optim / DDP. Each entry point below replaces one of
+ * those implicit kernels and names the reference call site it stands in for. The Python host layer
+ * (argus_amd/_lib.py, ctypes) binds exactly these symbols; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *  - Activations are NHWC, channel-contiguous, dtype ARGUS_F32 or ARGUS_BF16.
+ *  - Conv weights are OHWI ("KRSC"): w[k][r][s][c]. The stem (7x7, C=3) uses a padded compute layout
+ *    w[k][r(8)][s(8)][c(4)] (r=7, s=7, c=3 zero) and an NHWC4 input (channel 3 zero).
+ *  - Statistics, losses, gradients of parameters and optimizer state are fp32.
+ *  - Every call enqueues on `stream` (hipStream_t; NULL = legacy default) and returns 0 on success or
+ *    a nonzero code; argus_last_error() then describes it. The library never allocates device memory:
+ *    callers pass workspaces sized by the *_bytes() queries. No call synchronises the device.
+ */
+#ifndef ARGUS_HIP_H
+#define ARGUS_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* argus_stream_t; /* hipStream_t */
+
+enum { ARGUS_F32 = 0, ARGUS_BF16 = 1 };
+enum { ARGUS_OK = 0, ARGUS_ERR_ARG = 1, ARGUS_ERR_SHAPE = 2, ARGUS_ERR_HIP = 3 };
+
+typedef struct {
+  int32_t n, h, w; /* images, input spatial */
+  int32_t c;       /* input channels (3 for the stem) */
+  int32_t k;       /* output channels */
+  int32_t r, s;    /* filter size */
+  int32_t stride, pad;
+  int32_t ho, wo; /* output spatial */
+  int32_t stem;   /* 1: the 7x7/2 stem (NHWC4 input, padded weights) */
+} argus_conv_desc;
+
+int argus_abi_version(void);
+const char* argus_last_error(void);
+
+/* ---- input / weight layout ------------------------------------------------------------------ */
+/* (B,3*ncam,H,W) fp32 NCHW -> (B*ncam,H,W,4) NHWC4 of dtype; replaces the reshape at
+ * argus/models.py:81 plus the layout change cuDNN does internally. */
+int argus_images_to_nhwc4(int dtype, int64_t nimg, int h, int w, const float* x, void* out,
+                          argus_stream_t stream);
+/* fp32 master weight -> compute copies: w_fwd[k][r][s][c] (dtype; padded [k][8][8][4] for the
+ * stem) and w_dgrad[c][r][s][k] (dtype; ignored for the stem). The master is read with element
+ * strides {sk, sc, sr, ss} (so an OIHW nn.Parameter or a channels-last view both work);
+ * strides == NULL means OHWI contiguous. */
+int argus_conv_weight_prep(const argus_conv_desc* d, int dtype, const float* w_master,
+                           const int64_t* strides, void* w_fwd, void* w_dgrad,
+                           argus_stream_t stream);
+
+/* ---- convolution (torchvision Conv2d, bias=False; models.py:43) ------------------------------ */
+/* y = conv(x', w) where x' = relu(x*pro_scale+pro_shift) per input channel when pro_scale != NULL
+ * (the producer's BatchNorm+ReLU applied while staging; zero padding stays zero), else x.
+ * If stat_part != NULL, per-(row-tile, channel) {sum, M2} of y (fp32 accumulators, before
+ * rounding; M2 about the tile mean) are written: float2[argus_conv_fwd_stat_rows(d)][k], each row
+ * tile covering argus_conv_fwd_stat_tile(d) output pixels (the last one possibly fewer). */
+int argus_conv_fwd(const argus_conv_desc* d, int dtype, const void* x, const void* w_fwd, void* y,
+                   const float* pro_scale, const float* pro_shift, float* stat_part,
+                   argus_stream_t stream);
+int argus_conv_fwd_stat_rows(const argus_conv_desc* d, int dtype);
+int argus_conv_fwd_stat_tile(const argus_conv_desc* d, int dtype);
+/* dx (+)= dgrad(dy, w_dgrad); accumulate != 0 adds into dx. */
+int argus_conv_dgrad(const argus_conv_desc* d, int dtype, const void* dy, const void* w_dgrad,
+                     void* dx, int accumulate, argus_stream_t stream);
+/* dw (fp32, OHWI 7x7x3 for the stem) = sum over pixels of dy x im2col(x'), x' as in conv_fwd. */
+size_t argus_conv_wgrad_workspace_bytes(const argus_conv_desc* d, int dtype);
+int argus_conv_wgrad(const argus_conv_desc* d, int dtype, const void* x, const float* pro_scale,
+                     const float* pro_shift, const void* dy, float* dw, void* workspace,
+                     size_t workspace_bytes, argus_stream_t stream);
+
+/* ---- BatchNorm2d (train: batch stats, eps, momentum; eval: running stats) --------------------- */
+size_t argus_bn_workspace_bytes(int channels);
+/* From tile partials float2[rows][C] = {sum, M2 (sum of squared deviations from the tile mean)},
+ * tile t holding min(tile_rows, count - t*tile_rows) elements per channel (as argus_conv_fwd
+ * writes them): merged in fp64 (Chan), gives mean, invstd, the fused apply coefficients
+ * scale = gamma*invstd, shift = beta - mean*scale; updates running stats (momentum, unbiased
+ * variance) and num_batches_tracked when those pointers are non-NULL. */
+int argus_bn_finalize(int channels, int rows, int tile_rows, const float* part, int64_t count,
+                      const float* gamma,
+                      const float* beta, float eps, float momentum, float* running_mean,
+                      float* running_var, int64_t* num_batches_tracked, float* mean, float* invstd,
+                      float* scale, float* shift, void* workspace, argus_stream_t stream);
+int argus_bn_eval_coeffs(int channels, const float* gamma, const float* beta,
+                         const float* running_mean, const float* running_var, float eps,
+                         float* scale, float* shift, argus_stream_t stream);
+/* out = [relu]( y*scale+shift + residual' ), residual' = res*res_scale+res_shift (if res_scale),
+ * res (if res), else 0. out may alias y. */
+int argus_bn_apply(int dtype, int64_t pixels, int channels, const void* y, const float* scale,
+                   const float* shift, const void* res, const float* res_scale,
+                   const float* res_shift, int relu, void* out, argus_stream_t stream);
+/* Backward. mask_mode: 0 none; 1 relu mask from `mask_src` (>0, e.g. a block output);
+ * 2 relu mask recomputed from y as (y*scale+shift > 0). dm = dz*mask.
+ * reduce: part float2[rows][C] = {sum dm, sum dm*(y-mean)*invstd}; rows = argus_bn_bwd_rows(). */
+int argus_bn_bwd_rows(int64_t pixels, int channels);
+int argus_bn_bwd_reduce(int dtype, int64_t pixels, int channels, const void* dz, int mask_mode,
+                        const void* mask_src, const void* y, const float* scale,
+                        const float* shift, const float* mean, const float* invstd, float* part,
+                        argus_stream_t stream);
+/* dgamma/dbeta (fp32, written) and coefficients so that dy = ca*dm + cb*y + cc. */
+int argus_bn_bwd_finalize(int channels, int rows, const float* part, int64_t count,
+                          const float* gamma, const float* mean, const float* invstd,
+                          float* dgamma, float* dbeta, float* ca, float* cb, float* cc,
+                          void* workspace, argus_stream_t stream);
+/* dy = ca*dm + cb*y + cc (dtype); if dm_out != NULL also writes dm (the masked dz). */
+int argus_bn_bwd_apply(int dtype, int64_t pixels, int channels, const void* dz, int mask_mode,
+                       const void* mask_src, const void* y, const float* scale, const float* shift,
+                       const float* ca, const float* cb, const float* cc, void* dy, void* dm_out,
+                       argus_stream_t stream);
+
+/* ---- pooling (MaxPool2d(3,2,1) fused with the stem's BN+ReLU; AdaptiveAvgPool2d(1)) ----------- */
+int argus_maxpool_fwd(int dtype, int n, int h, int w, int c, const void* y, const float* scale,
+                      const float* shift, void* out, uint8_t* argmax, argus_stream_t stream);
+int argus_maxpool_bwd(int dtype, int n, int h, int w, int c, const void* dout,
+                      const uint8_t* argmax, void* dz, argus_stream_t stream);
+int argus_avgpool_fwd(int dtype, int n, int hw, int c, const void* x, float* feat,
+                      argus_stream_t stream);
+int argus_avgpool_bwd(int dtype, int n, int hw, int c, const float* dfeat, void* dx,
+                      argus_stream_t stream);
+
+/* ---- FC / MLP head (nn.Linear + exact GELU; models.py:56-64,88), fp32 ------------------------ */
+/* C[m][n] = sum_k opA(A)[m][k] * opB(B)[k][n]; opA(A)[m][k] = trans_a ? A[k*lda+m] : A[m*lda+k],
+ * opB(B)[k][n] = trans_b ? B[n*ldb+k] : B[k*ldb+n].
+ * epilogue 0: C = acc; 1: C = acc + bias[n]; 2: aux = acc + bias[n], C = gelu(aux);
+ * 3: C = acc * gelu'(aux[m][n]) (backward through a GELU whose pre-activation is aux, ld = ldc);
+ * 4: C += acc. */
+int argus_gemm_f32(int m, int n, int k, const float* a, int lda, int trans_a, const float* b,
+                   int ldb, int trans_b, float* c, int ldc, const float* bias, int epilogue,
+                   float* aux, argus_stream_t stream);
+/* out[n] = sum_m x[m*ld + n] (bias gradients). */
+int argus_colsum_f32(int m, int n, const float* x, int ld, float* out, argus_stream_t stream);
+int argus_gelu_f32(int64_t count, const float* x, float* y, argus_stream_t stream);
+int argus_gelu_bwd_f32(int64_t count, const float* x, const float* dy, float* dx,
+                       argus_stream_t stream);
+
+/* ---- SE(3) geodesic loss (geometric_loss_fn, argus/train.py:105-119; pypose Exp/Inv/@/Log) ---- */
+/* loss[b] = |Log(Exp(pred_b) @ target_b^-1)|^2 ; dpred[b] = grad_scale * d loss[b] / d pred[b]
+ * (dpred may be NULL). pred (B,6) [rho, phi]; target (B,7) [t, qx, qy, qz, qw]. */
+int argus_se3_loss(int batch, const float* pred, const float* target, float* loss, float* dpred,
+                   float grad_scale, argus_stream_t stream);
+
+/* ---- optimizer step (clip_grad_norm_ + Adam, argus/train.py:232,317-320) --------------------- */
+size_t argus_sumsq_workspace_bytes(int64_t count);
+/* out[0] = sqrt(sum x^2) (fp32, deterministic two-level reduction). */
+int argus_global_norm(int64_t count, const float* x, float* out, void* workspace,
+                      argus_stream_t stream);
+/* g' = g * min(1, max_norm/(norm[0]+1e-6)) (if norm != NULL); Adam (torch semantics, bias
+ * corrections bc1 = 1-beta1^t, bc2 = 1-beta2^t); writes param, m, v. */
+int argus_adam_step(int64_t count, float* param, const float* grad, float* exp_avg,
+                    float* exp_avg_sq, const float* norm, float max_norm, float lr, float beta1,
+                    float beta2, float eps, float weight_decay, float bc1, float bc2,
+                    argus_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ARGUS_HIP_H */

@@ -1,0 +1,378 @@
+"""Per-kernel parity of libargus_hip on the MI355X against torch fp64 CPU references.
+
+Every call goes through the C ABI (argus_amd._lib). fp32 path: relative error <= 2e-5 (exact-f32
+MFMA, fp32 accumulation). bf16 path: inputs are rounded to bf16 first and the reference is computed
+in fp64 on those rounded inputs; tolerance 1.5e-2 of the reference's max magnitude (one bf16 output
+rounding + fp32 accumulation order).
+"""
+import ctypes as C
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from argus_amd._lib import BF16, F32, ConvDesc, lib, ptr, stream
+
+pytestmark = pytest.mark.gpu
+
+TOL = {"fp32": 2e-5, "bf16": 1.5e-2}
+TDT = {"fp32": torch.float32, "bf16": torch.bfloat16}
+DT = {"fp32": F32, "bf16": BF16}
+
+# (cin, cout, k, stride, input size) — every distinct conv shape of SURVEY.md Appendix B at small
+# spatial sizes (odd sizes exercise partial tiles and the 376x672 rounding).
+CONV_SHAPES = [
+    (64, 64, 1, 1, 12), (64, 64, 3, 1, 12), (64, 256, 1, 1, 12), (256, 64, 1, 1, 12), (256, 128, 1, 1, 12),
+    (128, 128, 3, 2, 12), (128, 512, 1, 1, 8), (256, 512, 1, 2, 12), (512, 128, 1, 1, 8), (128, 128, 3, 1, 8),
+    (512, 256, 1, 1, 8), (256, 256, 3, 2, 9), (256, 1024, 1, 1, 6), (512, 1024, 1, 2, 9), (1024, 256, 1, 1, 6),
+    (256, 256, 3, 1, 6), (1024, 512, 1, 1, 6), (512, 512, 3, 2, 7), (512, 2048, 1, 1, 4), (1024, 2048, 1, 2, 7),
+    (2048, 512, 1, 1, 4), (512, 512, 3, 1, 4),
+]
+
+
+def _rel(a, b):
+    a = a.double().cpu()
+    b = b.double().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+def _desc(n, h, w, cin, cout, k, s, stem=False):
+    p = 3 if stem else (1 if k == 3 else 0)
+    ho, wo = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
+    return ConvDesc(n, h, w, cin, cout, k, k, s, p, ho, wo, int(stem)), p
+
+
+def _prep(d, dt, w_ohwi, cuda):
+    """weight_prep from an fp32 OHWI master; returns (w_fwd, w_dgrad)."""
+    k, r, s, c = w_ohwi.shape
+    if d.stem:
+        wf = torch.empty(k, 256, dtype=TDT[dt], device=cuda)
+        wd = None
+    else:
+        wf = torch.empty(k, r * s * c, dtype=TDT[dt], device=cuda)
+        wd = torch.empty(c, r * s * k, dtype=TDT[dt], device=cuda)
+    lib().conv_weight_prep(C.byref(d), DT[dt], ptr(w_ohwi), None, ptr(wf), ptr(wd), stream())
+    return wf, wd
+
+
+def _q(t, dt):  # round to the compute dtype (reference inputs)
+    return t.to(TDT[dt]).to(torch.float64)
+
+
+def _merge_stats(part, tile, count):
+    """Chan-merge per-tile {sum, M2} partials (rows, C, 2) -> per-channel (mean, biased var)."""
+    n = torch.tensor([min(tile, count - t * tile) for t in range(part.shape[0])], dtype=torch.float64)
+    mean_t = part[..., 0] / n[:, None]
+    mean = part[..., 0].sum(0) / count
+    m2 = part[..., 1].sum(0) + (n[:, None] * (mean_t - mean) ** 2).sum(0)
+    return mean, m2 / count
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+def test_conv_fwd_dgrad_wgrad_all_shapes(cuda, dt):
+    torch.manual_seed(0)
+    L = lib()
+    for cin, cout, k, s, hin in CONV_SHAPES:
+        n = 2
+        d, p = _desc(n, hin, hin, cin, cout, k, s)
+        x = torch.randn(n, hin, hin, cin)
+        w = torch.randn(cout, k, k, cin) * (2.0 / (k * k * cin)) ** 0.5
+        dy = torch.randn(n, d.ho, d.wo, cout)
+        xd, wd_, dyd = x.to(cuda, TDT[dt]), w.to(cuda), dy.to(cuda, TDT[dt])
+        wf, wt = _prep(d, dt, wd_, cuda)
+        # forward (+ BN statistics partials)
+        y = torch.empty(n, d.ho, d.wo, cout, dtype=TDT[dt], device=cuda)
+        rows = L.dll.argus_conv_fwd_stat_rows(C.byref(d), DT[dt])
+        stats = torch.empty(rows, cout, 2, device=cuda)
+        L.conv_fwd(C.byref(d), DT[dt], ptr(xd), ptr(wf), ptr(y), None, None, ptr(stats), stream())
+        xr, wr, dyr = _q(x, dt).permute(0, 3, 1, 2), _q(w, dt).permute(0, 3, 1, 2), _q(dy, dt).permute(0, 3, 1, 2)
+        ref = F.conv2d(xr, wr, stride=s, padding=p)
+        e = _rel(y.permute(0, 3, 1, 2), ref)
+        assert e < TOL[dt], f"fwd {cin}->{cout} k{k} s{s} {dt}: {e}"
+        tile = L.dll.argus_conv_fwd_stat_tile(C.byref(d), DT[dt])
+        mean, var = _merge_stats(stats.double().cpu(), tile, n * d.ho * d.wo)
+        yr = y.double().cpu().reshape(-1, cout) if dt == "fp32" else ref.permute(0, 2, 3, 1).reshape(-1, cout)
+        assert _rel(mean, yr.mean(0)) < 1e-4 or (mean - yr.mean(0)).abs().max() < 1e-5 * yr.std(0).max()
+        assert _rel(var, yr.var(0, unbiased=False)) < (1e-5 if dt == "fp32" else 1e-2), f"stats {cin}->{cout}"
+        # dgrad (accumulate onto a non-zero buffer to check both modes)
+        dx0 = torch.randn(n, hin, hin, cin)
+        dx = dx0.to(cuda, TDT[dt])
+        L.conv_dgrad(C.byref(d), DT[dt], ptr(dyd), ptr(wt), ptr(dx), 1, stream())
+        refd = torch.nn.grad.conv2d_input(xr.shape, wr, dyr, stride=s, padding=p) + _q(dx0, dt).permute(0, 3, 1, 2)
+        e = _rel(dx.permute(0, 3, 1, 2), refd)
+        assert e < TOL[dt], f"dgrad {cin}->{cout} k{k} s{s} {dt}: {e}"
+        # wgrad
+        ws = torch.empty(L.dll.argus_conv_wgrad_workspace_bytes(C.byref(d), DT[dt]), dtype=torch.uint8, device=cuda)
+        dw = torch.empty(cout, k, k, cin, device=cuda)
+        L.conv_wgrad(C.byref(d), DT[dt], ptr(xd), None, None, ptr(dyd), ptr(dw), ptr(ws), ws.numel(), stream())
+        refw = torch.nn.grad.conv2d_weight(xr, wr.shape, dyr, stride=s, padding=p)
+        e = _rel(dw.permute(0, 3, 1, 2), refw)
+        assert e < (TOL[dt] if dt == "fp32" else 2e-3), f"wgrad {cin}->{cout} k{k} s{s} {dt}: {e}"
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+def test_conv_bn_relu_prologue(cuda, dt):
+    """conv(relu(x*scale+shift)) with the BN+ReLU applied while staging; padding stays zero."""
+    torch.manual_seed(1)
+    L = lib()
+    for cin, cout, k, s, hin in [(64, 64, 3, 1, 10), (128, 128, 3, 2, 11), (256, 64, 1, 1, 6)]:
+        n = 2
+        d, p = _desc(n, hin, hin, cin, cout, k, s)
+        x = torch.randn(n, hin, hin, cin)
+        sc, sh = torch.rand(cin) + 0.5, torch.randn(cin) * 0.5
+        w = torch.randn(cout, k, k, cin) * 0.05
+        wf, _ = _prep(d, dt, w.to(cuda), cuda)
+        y = torch.empty(n, d.ho, d.wo, cout, dtype=TDT[dt], device=cuda)
+        scd, shd = sc.to(cuda), sh.to(cuda)
+        xg = x.to(cuda, TDT[dt])
+        L.conv_fwd(C.byref(d), DT[dt], ptr(xg), ptr(wf), ptr(y), ptr(scd), ptr(shd), None, stream())
+        xa = torch.relu(_q(x, dt) * sc.double() + sh.double())
+        xa = xa.to(TDT[dt]).double() if dt == "bf16" else xa
+        ref = F.conv2d(xa.permute(0, 3, 1, 2), _q(w, dt).permute(0, 3, 1, 2), stride=s, padding=p)
+        e = _rel(y.permute(0, 3, 1, 2), ref)
+        assert e < TOL[dt] * (2 if dt == "bf16" else 1), f"prologue fwd {cin}->{cout}: {e}"
+        # wgrad with the same prologue
+        dy = torch.randn(n, d.ho, d.wo, cout)
+        ws = torch.empty(L.dll.argus_conv_wgrad_workspace_bytes(C.byref(d), DT[dt]), dtype=torch.uint8, device=cuda)
+        dw = torch.empty(cout, k, k, cin, device=cuda)
+        dyg = dy.to(cuda, TDT[dt])
+        L.conv_wgrad(C.byref(d), DT[dt], ptr(xg), ptr(scd), ptr(shd), ptr(dyg), ptr(dw), ptr(ws), ws.numel(), stream())
+        refw = torch.nn.grad.conv2d_weight(xa.permute(0, 3, 1, 2), (cout, cin, k, k), _q(dy, dt).permute(0, 3, 1, 2),
+                                           stride=s, padding=p)
+        e = _rel(dw.permute(0, 3, 1, 2), refw)
+        assert e < (TOL[dt] if dt == "fp32" else 3e-3), f"prologue wgrad {cin}->{cout}: {e}"
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+def test_stem_fwd_wgrad(cuda, dt):
+    torch.manual_seed(2)
+    L = lib()
+    for hw in [(32, 32), (38, 30)]:
+        n, H, W = 3, *hw
+        d, p = _desc(n, H, W, 3, 64, 7, 2, stem=True)
+        img = torch.rand(n, 3, H, W)
+        x4 = torch.empty(n, H, W, 4, dtype=TDT[dt], device=cuda)
+        imgg = img.to(cuda)
+        L.images_to_nhwc4(DT[dt], n, H, W, ptr(imgg), ptr(x4), stream())
+        assert torch.equal(x4[..., :3].permute(0, 3, 1, 2).cpu().float(), _q(img, dt).float())
+        assert (x4[..., 3] == 0).all()
+        w = torch.randn(64, 7, 7, 3) * 0.1
+        wmaster = w.permute(0, 3, 1, 2).contiguous().to(cuda)  # OIHW nn.Parameter layout
+        wf = torch.empty(64, 256, dtype=TDT[dt], device=cuda)
+        strides = (C.c_int64 * 4)(*wmaster.stride())
+        L.conv_weight_prep(C.byref(d), DT[dt], ptr(wmaster), strides, ptr(wf), None, stream())
+        y = torch.empty(n, d.ho, d.wo, 64, dtype=TDT[dt], device=cuda)
+        L.conv_fwd(C.byref(d), DT[dt], ptr(x4), ptr(wf), ptr(y), None, None, None, stream())
+        ref = F.conv2d(_q(img, dt), _q(w, dt).permute(0, 3, 1, 2), stride=2, padding=3)
+        e = _rel(y.permute(0, 3, 1, 2), ref)
+        assert e < TOL[dt], f"stem fwd {hw} {dt}: {e}"
+        dy = torch.randn(n, d.ho, d.wo, 64)
+        ws = torch.empty(L.dll.argus_conv_wgrad_workspace_bytes(C.byref(d), DT[dt]), dtype=torch.uint8, device=cuda)
+        dw = torch.empty(64, 7, 7, 3, device=cuda)
+        dyg = dy.to(cuda, TDT[dt])
+        L.conv_wgrad(C.byref(d), DT[dt], ptr(x4), None, None, ptr(dyg), ptr(dw), ptr(ws), ws.numel(), stream())
+        refw = torch.nn.grad.conv2d_weight(_q(img, dt), (64, 3, 7, 7), _q(dy, dt).permute(0, 3, 1, 2), stride=2,
+                                           padding=3)
+        e = _rel(dw.permute(0, 3, 1, 2), refw)
+        assert e < (TOL[dt] if dt == "fp32" else 2e-3), f"stem wgrad {hw} {dt}: {e}"
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+def test_bn_train_forward_backward(cuda, dt):
+    """finalize + apply(+residual, relu) + backward reduce/finalize/apply vs autograd BatchNorm2d."""
+    torch.manual_seed(3)
+    L = lib()
+    n, h, w, c = 4, 7, 5, 64
+    px = n * h * w
+    y = torch.randn(n, h, w, c) * 2 + 0.5
+    res = torch.randn(n, h, w, c)
+    gamma, beta = torch.rand(c) + 0.5, torch.randn(c)
+    yq, resq = _q(y, dt), _q(res, dt)
+    # partials: one row per pixel block of 5 pixels
+    yy = yq.reshape(px, c).reshape(-1, 5, c)
+    part = torch.stack([yy.sum(1), ((yy - yy.mean(1, keepdim=True)) ** 2).sum(1)], -1).float()
+    rows = part.shape[0]
+    rm, rv = torch.zeros(c, device=cuda), torch.ones(c, device=cuda)
+    nbt = torch.zeros((), dtype=torch.int64, device=cuda)
+    stt = torch.empty(4, c, device=cuda)
+    ws = torch.empty(L.dll.argus_bn_workspace_bytes(c), dtype=torch.uint8, device=cuda)
+    gd, bd = gamma.to(cuda), beta.to(cuda)
+    partg = part.to(cuda)
+    L.bn_finalize(c, rows, 5, ptr(partg), px, ptr(gd), ptr(bd), C.c_float(1e-5), C.c_float(0.1), ptr(rm), ptr(rv),
+                  ptr(nbt), ptr(stt[0]), ptr(stt[1]), ptr(stt[2]), ptr(stt[3]), ptr(ws), stream())
+    bn = torch.nn.BatchNorm2d(c).double()
+    with torch.no_grad():
+        bn.weight.copy_(gamma)
+        bn.bias.copy_(beta)
+    xin = yq.permute(0, 3, 1, 2).clone().requires_grad_(True)
+    z = bn(xin)
+    out = torch.relu(z + resq.permute(0, 3, 1, 2))
+    assert _rel(rm, bn.running_mean) < 1e-5 and _rel(rv, bn.running_var) < 1e-5 and int(nbt) == 1
+    yd = y.to(cuda, TDT[dt])
+    o = torch.empty_like(yd)
+    resg = res.to(cuda, TDT[dt])
+    L.bn_apply(DT[dt], px, c, ptr(yd), ptr(stt[2]), ptr(stt[3]), ptr(resg), None, None, 1, ptr(o), stream())
+    assert _rel(o.permute(0, 3, 1, 2), out) < TOL[dt]
+    # backward: mask from the block output (mode 1), dm_out = masked grad
+    dout = torch.randn(n, h, w, c)
+    doutq = _q(dout, dt)
+    out.backward(doutq.permute(0, 3, 1, 2))
+    bpart = torch.empty(L.dll.argus_bn_bwd_rows(px, c), c, 2, device=cuda)
+    doutg = dout.to(cuda, TDT[dt])
+    L.bn_bwd_reduce(DT[dt], px, c, ptr(doutg), 1, ptr(o), ptr(yd), ptr(stt[2]), ptr(stt[3]),
+                    ptr(stt[0]), ptr(stt[1]), ptr(bpart), stream())
+    dg, db = torch.empty(c, device=cuda), torch.empty(c, device=cuda)
+    cf = torch.empty(3, c, device=cuda)
+    L.bn_bwd_finalize(c, bpart.shape[0], ptr(bpart), px, ptr(gd), ptr(stt[0]), ptr(stt[1]), ptr(dg), ptr(db),
+                      ptr(cf[0]), ptr(cf[1]), ptr(cf[2]), ptr(ws), stream())
+    dyo, dmo = torch.empty_like(yd), torch.empty_like(yd)
+    L.bn_bwd_apply(DT[dt], px, c, ptr(doutg), 1, ptr(o), ptr(yd), ptr(stt[2]), ptr(stt[3]), ptr(cf[0]),
+                   ptr(cf[1]), ptr(cf[2]), ptr(dyo), ptr(dmo), stream())
+    tol = TOL[dt] * (3 if dt == "bf16" else 1)
+    assert _rel(dg, bn.weight.grad) < tol, "dgamma"
+    assert _rel(db, bn.bias.grad) < tol, "dbeta"
+    assert _rel(dyo.permute(0, 3, 1, 2), xin.grad) < tol * 2, "dx"
+    # mode 2 (relu mask recomputed from y via scale/shift)
+    xin2 = yq.permute(0, 3, 1, 2).clone().requires_grad_(True)
+    bn2 = torch.nn.BatchNorm2d(c).double()
+    with torch.no_grad():
+        bn2.weight.copy_(gamma)
+        bn2.bias.copy_(beta)
+    torch.relu(bn2(xin2)).backward(doutq.permute(0, 3, 1, 2))
+    L.bn_bwd_reduce(DT[dt], px, c, ptr(doutg), 2, None, ptr(yd), ptr(stt[2]), ptr(stt[3]),
+                    ptr(stt[0]), ptr(stt[1]), ptr(bpart), stream())
+    L.bn_bwd_finalize(c, bpart.shape[0], ptr(bpart), px, ptr(gd), ptr(stt[0]), ptr(stt[1]), ptr(dg), ptr(db),
+                      ptr(cf[0]), ptr(cf[1]), ptr(cf[2]), ptr(ws), stream())
+    L.bn_bwd_apply(DT[dt], px, c, ptr(doutg), 2, None, ptr(yd), ptr(stt[2]), ptr(stt[3]), ptr(cf[0]),
+                   ptr(cf[1]), ptr(cf[2]), ptr(dyo), None, stream())
+    assert _rel(dyo.permute(0, 3, 1, 2), xin2.grad) < tol * 2, "dx mode 2"
+    assert _rel(dg, bn2.weight.grad) < tol, "dgamma mode 2"
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+def test_maxpool_avgpool(cuda, dt):
+    torch.manual_seed(4)
+    L = lib()
+    n, h, w, c = 2, 13, 10, 64
+    y = torch.randn(n, h, w, c)
+    sc, sh = torch.rand(c) + 0.5, torch.randn(c) * 0.3
+    yq = _q(y, dt)
+    # the kernel pools the exact fp32 z = relu(y*scale+shift) and rounds only the max
+    z = torch.relu(yq.float() * sc + sh).double()
+    zin = z.permute(0, 3, 1, 2).clone().requires_grad_(True)
+    ref = F.max_pool2d(zin, 3, 2, 1)
+    ho, wo = ref.shape[2], ref.shape[3]
+    out = torch.empty(n, ho, wo, c, dtype=TDT[dt], device=cuda)
+    am = torch.empty(n, ho, wo, c, dtype=torch.uint8, device=cuda)
+    yg, scg, shg = y.to(cuda, TDT[dt]), sc.to(cuda), sh.to(cuda)
+    L.maxpool_fwd(DT[dt], n, h, w, c, ptr(yg), ptr(scg), ptr(shg), ptr(out), ptr(am), stream())
+    assert _rel(out.permute(0, 3, 1, 2), ref) < TOL[dt] / 2
+    g = torch.randn(n, ho, wo, c)
+    ref.backward(_q(g, dt).permute(0, 3, 1, 2))
+    dz = torch.empty(n, h, w, c, dtype=TDT[dt], device=cuda)
+    gg = g.to(cuda, TDT[dt])
+    L.maxpool_bwd(DT[dt], n, h, w, c, ptr(gg), ptr(am), ptr(dz), stream())
+    assert _rel(dz.permute(0, 3, 1, 2), zin.grad) < TOL[dt]
+    # global average pool
+    x = torch.randn(n, 8, 8, 2048)
+    feat = torch.empty(n, 2048, device=cuda)
+    xg = x.to(cuda, TDT[dt])
+    L.avgpool_fwd(DT[dt], n, 64, 2048, ptr(xg), ptr(feat), stream())
+    assert _rel(feat, _q(x, dt).mean((1, 2))) < (1e-5 if dt == "fp32" else 2e-3)
+    df = torch.randn(n, 2048)
+    dx = torch.empty(n, 8, 8, 2048, dtype=TDT[dt], device=cuda)
+    dfg = df.to(cuda)
+    L.avgpool_bwd(DT[dt], n, 64, 2048, ptr(dfg), ptr(dx), stream())
+    assert _rel(dx, (df / 64)[:, None, None, :].expand(n, 8, 8, 2048)) < TOL[dt] / 2
+
+
+def test_gemm_f32_epilogues(cuda):
+    torch.manual_seed(5)
+    L = lib()
+    for (m, n, k) in [(128, 1024, 2048), (5, 128, 2048), (6, 128, 7), (1024, 2048, 130), (70, 6, 128)]:
+        for ta in (0, 1):
+            for tb in (0, 1):
+                a = torch.randn(k, m) if ta else torch.randn(m, k)
+                b = torch.randn(n, k) if tb else torch.randn(k, n)
+                ref = (a.double().T if ta else a.double()) @ (b.double().T if tb else b.double())
+                c = torch.empty(m, n, device=cuda)
+                ag, bg = a.to(cuda), b.to(cuda)
+                L.gemm_f32(m, n, k, ptr(ag), a.shape[1], ta, ptr(bg), b.shape[1], tb, ptr(c), n, None, 0, None, stream())
+                assert _rel(c, ref) < 1e-5, (m, n, k, ta, tb)
+    m, n, k = 9, 33, 40
+    a, b, bias = torch.randn(m, k), torch.randn(n, k), torch.randn(n)
+    aux = torch.empty(m, n, device=cuda)
+    c = torch.empty(m, n, device=cuda)
+    ag, bg, biasg = a.to(cuda), b.to(cuda), bias.to(cuda)
+    L.gemm_f32(m, n, k, ptr(ag), k, 0, ptr(bg), k, 1, ptr(c), n, ptr(biasg), 2, ptr(aux), stream())
+    pre = a.double() @ b.double().T + bias.double()
+    assert _rel(aux, pre) < 1e-5 and _rel(c, F.gelu(pre)) < 1e-5
+    g = torch.randn(m, n)
+    pre_t = pre.clone().requires_grad_(True)
+    F.gelu(pre_t).backward(g.double())
+    # epilogue 3: C = (A @ B) * gelu'(aux): use A = g, B = I
+    eye = torch.eye(n)
+    gg, eyeg = g.to(cuda), eye.to(cuda)
+    L.gemm_f32(m, n, n, ptr(gg), n, 0, ptr(eyeg), n, 0, ptr(c), n, None, 3, ptr(aux), stream())
+    assert _rel(c, pre_t.grad) < 1e-5
+    cs = torch.empty(n, device=cuda)
+    L.colsum_f32(m, n, ptr(gg), n, ptr(cs), stream())
+    assert _rel(cs, g.double().sum(0)) < 1e-6
+
+
+def test_se3_loss_kernel(cuda, golden):
+    from oracle import se3
+
+    L = lib()
+    for kat in golden["loss_kats"]:
+        p = torch.tensor([kat["pred"]], dtype=torch.float32)
+        t = torch.tensor([kat["target"]], dtype=torch.float32)
+        loss = torch.empty(1, device=cuda)
+        pg, tg = p.to(cuda), t.to(cuda)
+        L.se3_loss(1, ptr(pg), ptr(tg), ptr(loss), None, C.c_float(1.0), stream())
+        assert abs(loss.item() - kat["loss"]) < 1e-5 * max(1.0, kat["loss"]), kat
+    g = torch.Generator().manual_seed(6)
+    for B, scale in [(64, 0.3), (257, 1.5), (5, 1e-6)]:
+        pred = (torch.randn(B, 6, generator=g) * scale).float()
+        T = se3.random_targets(B, generator=g)
+        ref_l, ref_g = se3.loss_and_grad(pred, T, mean=True)
+        loss = torch.empty(B, device=cuda)
+        dpred = torch.empty(B, 6, device=cuda)
+        pg, tg = pred.to(cuda), T.to(cuda)
+        L.se3_loss(B, ptr(pg), ptr(tg), ptr(loss), ptr(dpred), C.c_float(1.0 / B), stream())
+        assert (loss.cpu().double() - ref_l).abs().max() < 1e-5 * max(1.0, ref_l.abs().max().item())
+        assert (dpred.cpu().double() - ref_g).abs().max() < 1e-6 + 1e-5 * ref_g.abs().max().item()
+    # identity: loss(p, Exp(p)) == 0 (tests/test_train.py:32-36)
+    pred = torch.randn(32, 6, generator=g).float()
+    T = se3.se3_exp(pred.double()).float()
+    loss = torch.empty(32, device=cuda)
+    pg, tg = pred.to(cuda), T.to(cuda)
+    L.se3_loss(32, ptr(pg), ptr(tg), ptr(loss), None, C.c_float(1.0), stream())
+    assert loss.abs().max().item() < 1e-8 + 1e-5
+
+
+def test_norm_and_adam(cuda):
+    torch.manual_seed(7)
+    L = lib()
+    n = 1_000_003
+    p0, g0 = torch.randn(n), torch.randn(n) * 1e-3
+    ws = torch.empty(L.dll.argus_sumsq_workspace_bytes(n), dtype=torch.uint8, device=cuda)
+    # pad to a 16-byte-aligned length (as the flat buffers are)
+    pd, gd = p0.to(cuda), g0.to(cuda)
+    norm = torch.empty(1, device=cuda)
+    L.global_norm(n, ptr(gd), ptr(norm), ptr(ws), stream())
+    assert abs(norm.item() - g0.double().norm().item()) < 1e-6 * g0.double().norm().item()
+    m, v = torch.zeros(n, device=cuda), torch.zeros(n, device=cuda)
+    ref_p = p0.clone().requires_grad_(True)
+    opt = torch.optim.Adam([ref_p], lr=1e-4)
+    for step in range(1, 4):
+        gs = g0 * (1.0 + 0.5 * step) * 100  # norm >> 1 -> clipping active
+        ref_p.grad = gs.clone()
+        torch.nn.utils.clip_grad_norm_([ref_p], 1.0)
+        opt.step()
+        gd = gs.to(cuda)
+        L.global_norm(n, ptr(gd), ptr(norm), ptr(ws), stream())
+        L.adam_step(n, ptr(pd), ptr(gd), ptr(m), ptr(v), ptr(norm), C.c_float(1.0), C.c_float(1e-4), C.c_float(0.9),
+                    C.c_float(0.999), C.c_float(1e-8), C.c_float(0.0), C.c_float(1 - 0.9**step),
+                    C.c_float(1 - 0.999**step), stream())
+    assert (pd.cpu() - ref_p.detach()).abs().max().item() < 2e-6

@@ -1,0 +1,167 @@
+"""Whole-model parity: argus_amd.NCameraCNN (HIP engine) vs the CPU oracle (reference models.py
+semantics, pinned by tests/golden/golden_b2.json) on identical seeded weights and batches.
+
+Tolerances
+- fp32 path, forward (north_star): pose 6-vector and per-sample loss within 1e-4 absolute, train
+  and eval mode; BN running statistics within 1e-4 relative.
+- fp32 path, gradients: the train-mode gradient of this network at batch 2 is ill-conditioned —
+  the reference's OWN fp32 gradients differ from its fp64 gradients by up to ~18 % (median ~2 %,
+  BatchNorm over 256 values per channel at layer4 + ReLU masks). Parity is therefore stated against
+  the fp64 oracle relative to that intrinsic fp32 noise: the global relative error of our gradient
+  vector must be <= 3x the reference-fp32 one, and no parameter's error may exceed 3x the
+  reference's worst parameter. Kernel exactness at full-model shapes is checked separately by
+  re-deriving every backward stage of every block in fp64 from the engine's own saved tensors
+  (relative error <= 2e-5).
+- bf16 path: pose within 2e-2 absolute of the fp32 reference (stated tolerance).
+"""
+import pytest
+import torch
+
+from oracle import se3
+from oracle.ncamera import build_reference_model
+
+pytestmark = pytest.mark.gpu
+
+
+def _inputs(golden):
+    import tests.golden.make_golden as mg
+
+    x = mg.synthetic_images(2, 256, 256, seed=1234)
+    T = torch.tensor(golden["inputs"]["targets"], dtype=torch.float32)
+    assert abs(float(x.double().sum()) - golden["inputs"]["images_sum"]) < 1e-3
+    return x, T
+
+
+def _product(cuda, dtype="fp32", seed=42):
+    from argus_amd.models import NCameraCNN
+
+    torch.manual_seed(seed)
+    return NCameraCNN(compute_dtype=dtype).to(cuda)
+
+
+def _rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+def test_forward_train_eval_matches_golden(cuda, golden):
+    x, T = _inputs(golden)
+    m = _product(cuda)
+    with torch.no_grad():
+        m.train()
+        pt = m(x.to(cuda)).cpu()
+        m.eval()
+        pe = m(x.to(cuda)).cpu()
+    ref_t = torch.tensor(golden["pred_train"])
+    ref_e = torch.tensor(golden["pred_eval"])
+    assert (pt - ref_t).abs().max().item() < 1e-4, (pt, ref_t)
+    assert (pe - ref_e).abs().max().item() < 1e-4, (pe, ref_e)
+    losses = se3.geometric_loss(pt.double(), T.double())
+    assert (losses - torch.tensor(golden["loss_train"], dtype=torch.float64)).abs().max().item() < 1e-4
+
+
+def test_gradients_match_fp64_oracle(cuda, golden):
+    from argus_amd.losses import geometric_loss_fn
+
+    x, T = _inputs(golden)
+    m = _product(cuda)
+    m.train()
+    pred = m(x.to(cuda))
+    losses = geometric_loss_fn(pred, T.to(cuda))
+    losses.mean().backward()
+    assert (losses.detach().cpu() - torch.tensor(golden["loss_train"])).abs().max().item() < 1e-4
+
+    grads = {}
+    for dt in (torch.float32, torch.float64):
+        ref = build_reference_model(42).to(dt)
+        ref.train()
+        se3.geometric_loss(ref(x.to(dt)), T.to(dt)).mean().backward()
+        grads[dt] = {n: p.grad.double() for n, p in ref.named_parameters()}
+        if dt == torch.float32:
+            sd_ref = ref.state_dict()
+    g64, g32 = grads[torch.float64], grads[torch.float32]
+    ours = {n: p.grad.double().cpu() for n, p in m.named_parameters()}
+    assert list(ours) == list(g64)
+    flat = lambda d: torch.cat([v.flatten() for v in d.values()])  # noqa: E731
+    e_ours = ((flat(ours) - flat(g64)).norm() / flat(g64).norm()).item()
+    e_ref = ((flat(g32) - flat(g64)).norm() / flat(g64).norm()).item()
+    per_ours = {n: _rel(ours[n], g64[n]) for n in g64}
+    per_ref = {n: _rel(g32[n], g64[n]) for n in g64}
+    assert e_ours <= 3 * e_ref + 1e-4, (e_ours, e_ref)
+    worst = max(per_ours.items(), key=lambda kv: kv[1])
+    assert worst[1] <= 3 * max(per_ref.values()) + 1e-4, (worst, max(per_ref.values()))
+    # the head (no BatchNorm behind it) is well conditioned: tight bound
+    for n in ("output_mlp.4.weight", "output_mlp.4.bias", "output_mlp.2.weight", "output_mlp.0.weight",
+              "resnet.fc.weight", "resnet.fc.bias"):
+        assert per_ours[n] < 1e-3, (n, per_ours[n])
+    # BN running statistics after one train-mode forward
+    sd = m.state_dict()
+    for k in sd:
+        if k.endswith(("running_mean", "running_var")):
+            assert _rel(sd[k], sd_ref[k]) < 1e-4, k
+        if k.endswith("num_batches_tracked"):
+            assert int(sd[k]) == 1
+
+
+def test_block_backward_stages_exact(cuda, golden):
+    """Every backward stage of every Bottleneck, re-derived in fp64 from the engine's own tensors."""
+    from argus_amd.losses import geometric_loss_fn
+
+    x, T = _inputs(golden)
+    m = _product(cuda)
+    eng = m._engine(cuda)
+    eng.debug = {}
+    m.train()
+    geometric_loss_fn(m(x.to(cuda)), T.to(cuda)).mean().backward()
+    eng_debug, eng.debug = eng.debug, None
+    P = dict(m.named_parameters())
+    nchw = lambda t: t.detach().double().cpu().permute(0, 3, 1, 2)  # noqa: E731
+    col = lambda v: v[None, :, None, None]  # noqa: E731
+
+    def bn_bwd(dm, y, mean, invstd, gamma):
+        xh = (y - col(mean)) * col(invstd)
+        n = dm.shape[0] * dm.shape[2] * dm.shape[3]
+        S, Tt = dm.sum((0, 2, 3)), (dm * xh).sum((0, 2, 3))
+        return col(gamma * invstd) * (dm - col(S) / n - xh * col(Tt) / n)
+
+    for idx, (b, a) in enumerate(zip(eng.blocks, eng.act)):
+        pf = b.prefix
+        st = {k: eng.bn_state[pf + k].double().cpu() for k in (".bn1", ".bn2", ".bn3")}
+        gm = {k: P[pf + k + ".weight"].double().cpu() for k in (".bn1", ".bn2", ".bn3")}
+        D = {k: nchw(eng_debug[k + "." + pf]) for k in ("b_dout", "b_dy3", "b_dz2", "b_dy2", "b_dz1", "b_dy1")}
+        out, y3, y2, y1 = nchw(a["out"]), nchw(a["y3"]), nchw(a["y2"]), nchw(a["y1"])
+        checks = {}
+        checks["dy3"] = (D["b_dy3"], bn_bwd(D["b_dout"] * (out > 0), y3, st[".bn3"][0], st[".bn3"][1], gm[".bn3"]))
+        w3 = P[pf + ".conv3.weight"].double().cpu()
+        checks["dz2"] = (D["b_dz2"], torch.nn.grad.conv2d_input(y2.shape, w3, D["b_dy3"]))
+        mask2 = (y2 * col(st[".bn2"][2]) + col(st[".bn2"][3])) > 0
+        checks["dy2"] = (D["b_dy2"], bn_bwd(D["b_dz2"] * mask2, y2, st[".bn2"][0], st[".bn2"][1], gm[".bn2"]))
+        w2 = P[pf + ".conv2.weight"].double().cpu()
+        checks["dz1"] = (D["b_dz1"], torch.nn.grad.conv2d_input(y1.shape, w2, D["b_dy2"], stride=b.stride, padding=1))
+        mask1 = (y1 * col(st[".bn1"][2]) + col(st[".bn1"][3])) > 0
+        checks["dy1"] = (D["b_dy1"], bn_bwd(D["b_dz1"] * mask1, y1, st[".bn1"][0], st[".bn1"][1], gm[".bn1"]))
+        z1 = torch.relu(y1 * col(st[".bn1"][2]) + col(st[".bn1"][3]))
+        z2 = torch.relu(y2 * col(st[".bn2"][2]) + col(st[".bn2"][3]))
+        checks["dW3"] = (P[pf + ".conv3.weight"].grad, torch.nn.grad.conv2d_weight(z2, w3.shape, D["b_dy3"]))
+        checks["dW2"] = (P[pf + ".conv2.weight"].grad,
+                         torch.nn.grad.conv2d_weight(z1, w2.shape, D["b_dy2"], stride=b.stride, padding=1))
+        for k, (got, want) in checks.items():
+            assert _rel(got, want) < 2e-5, (pf, k, _rel(got, want))
+
+
+def test_bf16_forward_tolerance(cuda, golden):
+    x, _ = _inputs(golden)
+    m = _product(cuda, "bf16")
+    with torch.no_grad():
+        m.train()
+        pt = m(x.to(cuda)).cpu()
+    ref_t = torch.tensor(golden["pred_train"])
+    assert (pt - ref_t).abs().max().item() < 2e-2, (pt, ref_t)
+
+
+def test_non_4d_input_asserts(cuda):
+    m = _product(cuda)
+    with pytest.raises(AssertionError):
+        m(torch.randn(6, 64, 64, device=cuda))
+    out = m(torch.rand(2, 6, 64, 64, device=cuda))
+    assert out.shape == (2, 6)
