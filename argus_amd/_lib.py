@@ -41,6 +41,7 @@ SIGNATURES = {
     "argus_conv_fwd": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P, _P]),
     "argus_conv_fwd_stat_rows": (_I, [_DESC, _I]),
     "argus_conv_fwd_stat_tile": (_I, [_DESC, _I]),
+    "argus_conv_launch_info": (_I, [_DESC, _I, _I, C.POINTER(C.c_int64)]),
     "argus_conv_dgrad": (_I, [_DESC, _I, _P, _P, _P, _I, _P]),
     "argus_conv_wgrad_workspace_bytes": (_SZ, [_DESC, _I]),
     "argus_conv_wgrad": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P, _SZ, _P]),
@@ -61,9 +62,10 @@ SIGNATURES = {
     "argus_gelu_f32": (_I, [_I64, _P, _P, _P]),
     "argus_gelu_bwd_f32": (_I, [_I64, _P, _P, _P, _P]),
     "argus_se3_loss": (_I, [_I, _P, _P, _P, _P, _F, _P]),
+    "argus_se3_exp": (_I, [_I, _P, _P, _I, _P]),
     "argus_sumsq_workspace_bytes": (_SZ, [_I64]),
     "argus_global_norm": (_I, [_I64, _P, _P, _P, _P]),
-    "argus_adam_step": (_I, [_I64, _P, _P, _P, _P, _P, _F, _F, _F, _F, _F, _F, _F, _F, _P]),
+    "argus_adam_step": (_I, [_I64, _P, _P, _P, _P, _P, _F, _F, _F, _F, _F, _F, _F, _F, _F, _P]),
 }
 
 
@@ -89,7 +91,7 @@ class _Lib:
 
     def __getattr__(self, name: str):
         fn = getattr(self.dll, "argus_" + name)
-        if fn.restype is _I and not name.endswith(("rows", "tile", "version")):
+        if fn.restype is _I and not name.endswith(("rows", "tile", "version", "info")):
             def call(*args, _fn=fn, _name=name):
                 rc = _fn(*args)
                 if rc != 0:

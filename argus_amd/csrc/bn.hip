@@ -79,7 +79,7 @@ __global__ __launch_bounds__(256) void colreduce_kernel(const float2* __restrict
   }
 }
 
-static int reduce_groups(int rows) { return rows < 128 ? 1 : (rows < 4096 ? 32 : 128); }
+static int reduce_groups(int rows) { return rows < 64 ? 1 : (rows < 1024 ? 8 : 16); }
 
 static int colreduce(const float* part, int rows, int C, void* ws, int& G, hipStream_t st) {
   G = reduce_groups(rows);
@@ -127,33 +127,60 @@ __global__ void bn_eval_kernel(int C, const float* gamma, const float* beta, con
   shift[c] = beta[c] - rm[c] * sc;
 }
 
-// ---- elementwise apply ------------------------------------------------------------------------
+// ---- elementwise kernels: channel-chunk-stationary threads ---------------------------------------
+// Grid x = channel groups of CC chunks, y = pixel blocks; a thread owns one 16-byte channel chunk,
+// keeps its per-channel coefficients in registers and walks pixels with stride PL (consecutive
+// threads read consecutive chunks of a pixel row: fully coalesced 16-byte accesses).
+struct EwGeom {
+  int CC, PL, cgroups, rows;
+  int64_t ppb;
+};
+static EwGeom ew_geom(int C, int E, int64_t pixels, int target_blocks) {
+  EwGeom g;
+  const int chunks = C / E;
+  g.CC = chunks < 256 ? chunks : 256;
+  g.PL = 256 / g.CC;
+  g.cgroups = chunks / g.CC;
+  int64_t rows = target_blocks / g.cgroups;
+  const int64_t maxrows = (pixels + 4 * g.PL - 1) / (4 * g.PL);  // >= 4 pixels per thread
+  if (rows > maxrows) rows = maxrows;
+  if (rows < 1) rows = 1;
+  g.ppb = (pixels + rows - 1) / rows;
+  g.rows = (int)((pixels + g.ppb - 1) / g.ppb);
+  return g;
+}
+
 template <typename T>
-__global__ __launch_bounds__(256) void bn_apply_kernel(int64_t nchunks, int C, const T* __restrict__ y,
-                                                       const float* __restrict__ sc, const float* __restrict__ sh,
-                                                       const T* __restrict__ res, const float* __restrict__ rsc,
-                                                       const float* __restrict__ rsh, int relu, T* out) {
+__global__ __launch_bounds__(256) void bn_apply_kernel(int64_t pixels, int C, int CC, int PL, int64_t ppb,
+                                                       const T* __restrict__ y, const float* __restrict__ sc,
+                                                       const float* __restrict__ sh, const T* __restrict__ res,
+                                                       const float* __restrict__ rsc, const float* __restrict__ rsh,
+                                                       int relu, T* out) {
   constexpr int E = Chunk<T>::E;
-  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < nchunks; i += (int64_t)gridDim.x * 256) {
-    const int c0 = (int)((i * E) % C);
-    float f[E];
-    unpack(ld16(y + i * E), f);
-    float r[E];
-    if (res) {
-      unpack(ld16(res + i * E), r);
-      if (rsc) {
+  const int cc = threadIdx.x % CC, pl = threadIdx.x / CC;
+  const int c0 = (blockIdx.x * CC + cc) * E;
+  const int64_t p0 = blockIdx.y * ppb, p1 = min(pixels, p0 + ppb);
+  float a[E], b[E], ra[E], rb[E];
 #pragma unroll
-        for (int j = 0; j < E; ++j) r[j] = fmaf(r[j], rsc[c0 + j], rsh[c0 + j]);
-      }
-    }
+  for (int j = 0; j < E; ++j) {
+    a[j] = sc[c0 + j];
+    b[j] = sh[c0 + j];
+    ra[j] = rsc ? rsc[c0 + j] : 1.f;
+    rb[j] = rsc ? rsh[c0 + j] : 0.f;
+  }
+  for (int64_t px = p0 + pl; px < p1; px += PL) {
+    const int64_t off = px * C + c0;
+    float f[E], r[E];
+    unpack(ld16(y + off), f);
+    if (res) unpack(ld16(res + off), r);
 #pragma unroll
     for (int j = 0; j < E; ++j) {
-      float v = fmaf(f[j], sc[c0 + j], sh[c0 + j]);
-      if (res) v += r[j];
+      float v = fmaf(f[j], a[j], b[j]);
+      if (res) v += fmaf(r[j], ra[j], rb[j]);
       if (relu) v = fmaxf(v, 0.f);
       f[j] = v;
     }
-    st16(out + i * E, pack(f));
+    st16(out + off, pack(f));
   }
 }
 
@@ -174,24 +201,6 @@ static void bwd_geometry(int C, int E, int64_t pixels, int& CC, int& PL, int& cg
 }
 
 template <typename T>
-ARGUS_DEV void load_mask(int mode, const T* mask_src, const T* y, const float* sc, const float* sh, int64_t off,
-                         int c0, const float (&yv)[Chunk<T>::E], float (&m)[Chunk<T>::E]) {
-  constexpr int E = Chunk<T>::E;
-  if (mode == 1) {
-    float s[E];
-    unpack(ld16(mask_src + off), s);
-#pragma unroll
-    for (int j = 0; j < E; ++j) m[j] = s[j] > 0.f ? 1.f : 0.f;
-  } else if (mode == 2) {
-#pragma unroll
-    for (int j = 0; j < E; ++j) m[j] = fmaf(yv[j], sc[c0 + j], sh[c0 + j]) > 0.f ? 1.f : 0.f;
-  } else {
-#pragma unroll
-    for (int j = 0; j < E; ++j) m[j] = 1.f;
-  }
-}
-
-template <typename T>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(int64_t pixels, int C, int CC, int PL, int64_t ppb,
                                                             const T* __restrict__ dz, int mode,
                                                             const T* __restrict__ mask_src, const T* __restrict__ y,
@@ -202,23 +211,35 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(int64_t pixels, int 
   const int cc = threadIdx.x % CC, pl = threadIdx.x / CC;
   const int c0 = (blockIdx.x * CC + cc) * E;
   const int64_t p0 = blockIdx.y * ppb, p1 = min(pixels, p0 + ppb);
-  float mu[E], is[E], s[E], t[E];
+  float mu[E], is[E], S[E], H[E], s[E], t[E];
 #pragma unroll
-  for (int j = 0; j < E; ++j) { mu[j] = mean[c0 + j]; is[j] = invstd[c0 + j]; s[j] = 0.f; t[j] = 0.f; }
-  if (pl < PL)
-    for (int64_t px = p0 + pl; px < p1; px += PL) {
-      const int64_t off = px * C + c0;
-      float d[E], yv[E], m[E];
-      unpack(ld16(dz + off), d);
-      unpack(ld16(y + off), yv);
-      load_mask<T>(mode, mask_src, y, sc, sh, off, c0, yv, m);
+  for (int j = 0; j < E; ++j) {
+    mu[j] = mean[c0 + j];
+    is[j] = invstd[c0 + j];
+    S[j] = mode == 2 ? sc[c0 + j] : 0.f;
+    H[j] = mode == 2 ? sh[c0 + j] : 0.f;
+    s[j] = 0.f;
+    t[j] = 0.f;
+  }
+  for (int64_t px = p0 + pl; px < p1; px += PL) {
+    const int64_t off = px * C + c0;
+    float d[E], yv[E], m[E];
+    unpack(ld16(dz + off), d);
+    unpack(ld16(y + off), yv);
+    if (mode == 1) {
+      unpack(ld16(mask_src + off), m);
 #pragma unroll
-      for (int j = 0; j < E; ++j) {
-        const float dm = d[j] * m[j];
-        s[j] += dm;
-        t[j] = fmaf(dm, (yv[j] - mu[j]) * is[j], t[j]);
-      }
+      for (int j = 0; j < E; ++j) d[j] = m[j] > 0.f ? d[j] : 0.f;
+    } else if (mode == 2) {
+#pragma unroll
+      for (int j = 0; j < E; ++j) d[j] = fmaf(yv[j], S[j], H[j]) > 0.f ? d[j] : 0.f;
     }
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      s[j] += d[j];
+      t[j] = fmaf(d[j], (yv[j] - mu[j]) * is[j], t[j]);
+    }
+  }
   __shared__ float2 red[256 * 8];
   // reduce over pixel lanes: layout red[pl][cc*E + j]
   const int W = CC * E;
@@ -249,26 +270,42 @@ __global__ void bn_bwd_finalize_kernel(const double2* __restrict__ red, int G, i
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(int64_t nchunks, int C, const T* __restrict__ dz, int mode,
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(int64_t pixels, int C, int CC, int PL, int64_t ppb,
+                                                           const T* __restrict__ dz, int mode,
                                                            const T* __restrict__ mask_src, const T* __restrict__ y,
                                                            const float* __restrict__ sc, const float* __restrict__ sh,
                                                            const float* __restrict__ ca, const float* __restrict__ cb,
-                                                           const float* __restrict__ cc, T* __restrict__ dy,
+                                                           const float* __restrict__ cc_, T* __restrict__ dy,
                                                            T* __restrict__ dm_out) {
   constexpr int E = Chunk<T>::E;
-  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < nchunks; i += (int64_t)gridDim.x * 256) {
-    const int c0 = (int)((i * E) % C);
-    const int64_t off = i * E;
+  const int cc = threadIdx.x % CC, pl = threadIdx.x / CC;
+  const int c0 = (blockIdx.x * CC + cc) * E;
+  const int64_t p0 = blockIdx.y * ppb, p1 = min(pixels, p0 + ppb);
+  float A[E], Bc[E], Cc[E], S[E], H[E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    A[j] = ca[c0 + j];
+    Bc[j] = cb[c0 + j];
+    Cc[j] = cc_[c0 + j];
+    S[j] = mode == 2 ? sc[c0 + j] : 0.f;
+    H[j] = mode == 2 ? sh[c0 + j] : 0.f;
+  }
+  for (int64_t px = p0 + pl; px < p1; px += PL) {
+    const int64_t off = px * C + c0;
     float d[E], yv[E], m[E];
     unpack(ld16(dz + off), d);
     unpack(ld16(y + off), yv);
-    load_mask<T>(mode, mask_src, y, sc, sh, off, c0, yv, m);
+    if (mode == 1) {
+      unpack(ld16(mask_src + off), m);
+#pragma unroll
+      for (int j = 0; j < E; ++j) d[j] = m[j] > 0.f ? d[j] : 0.f;
+    } else if (mode == 2) {
+#pragma unroll
+      for (int j = 0; j < E; ++j) d[j] = fmaf(yv[j], S[j], H[j]) > 0.f ? d[j] : 0.f;
+    }
     float o[E];
 #pragma unroll
-    for (int j = 0; j < E; ++j) {
-      d[j] *= m[j];
-      o[j] = fmaf(ca[c0 + j], d[j], fmaf(cb[c0 + j], yv[j], cc[c0 + j]));
-    }
+    for (int j = 0; j < E; ++j) o[j] = fmaf(A[j], d[j], fmaf(Bc[j], yv[j], Cc[j]));
     st16(dy + off, pack(o));
     if (dm_out) st16(dm_out + off, pack(d));
   }
@@ -394,7 +431,7 @@ using namespace argus;
 
 extern "C" {
 
-size_t argus_bn_workspace_bytes(int channels) { return (size_t)128 * channels * 3 * sizeof(double); }
+size_t argus_bn_workspace_bytes(int channels) { return (size_t)16 * channels * 3 * sizeof(double); }
 
 int argus_bn_finalize(int C, int rows, int tile_rows, const float* part, int64_t count, const float* gamma,
                       const float* beta, float eps, float momentum, float* rm, float* rv, int64_t* nbt, float* mean,
@@ -426,15 +463,20 @@ int argus_bn_eval_coeffs(int C, const float* gamma, const float* beta, const flo
 int argus_bn_apply(int dtype, int64_t pixels, int C, const void* y, const float* scale, const float* shift,
                    const void* res, const float* rsc, const float* rsh, int relu, void* out, argus_stream_t stream) {
   const int E = dtype == ARGUS_BF16 ? 8 : 4;
-  if (C % E || pixels <= 0) { set_error("bn_apply: channels must be a multiple of the chunk"); return ARGUS_ERR_SHAPE; }
-  const int64_t nch = pixels * C / E;
+  if (C % E || pixels <= 0 || !y || !scale || !shift || !out || ((rsc == nullptr) != (rsh == nullptr)) ||
+      (rsc && !res)) {
+    set_error("bn_apply: bad arguments");
+    return ARGUS_ERR_ARG;
+  }
+  const EwGeom g = ew_geom(C, E, pixels, 2048);
   hipStream_t st = (hipStream_t)stream;
+  dim3 grid(g.cgroups, g.rows);
   if (dtype == ARGUS_BF16)
-    hipLaunchKernelGGL(bn_apply_kernel<bf16>, dim3(grid_for(nch)), dim3(256), 0, st, nch, C, (const bf16*)y, scale,
-                       shift, (const bf16*)res, rsc, rsh, relu, (bf16*)out);
+    hipLaunchKernelGGL(bn_apply_kernel<bf16>, grid, dim3(256), 0, st, pixels, C, g.CC, g.PL, g.ppb, (const bf16*)y,
+                       scale, shift, (const bf16*)res, rsc, rsh, relu, (bf16*)out);
   else
-    hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(grid_for(nch)), dim3(256), 0, st, nch, C, (const float*)y, scale,
-                       shift, (const float*)res, rsc, rsh, relu, (float*)out);
+    hipLaunchKernelGGL(bn_apply_kernel<float>, grid, dim3(256), 0, st, pixels, C, g.CC, g.PL, g.ppb, (const float*)y,
+                       scale, shift, (const float*)res, rsc, rsh, relu, (float*)out);
   return check_launch("bn_apply_kernel");
 }
 
@@ -480,16 +522,22 @@ int argus_bn_bwd_apply(int dtype, int64_t pixels, int C, const void* dz, int mod
                        const float* scale, const float* shift, const float* ca, const float* cb, const float* cc,
                        void* dy, void* dm_out, argus_stream_t stream) {
   const int E = dtype == ARGUS_BF16 ? 8 : 4;
-  if (C % E || pixels <= 0) { set_error("bn_bwd_apply: bad shape"); return ARGUS_ERR_SHAPE; }
-  const int64_t nch = pixels * C / E;
+  if (C % E || pixels <= 0 || !dz || !y || !ca || !cb || !cc || !dy || (mode == 1 && !mask_src) ||
+      (mode == 2 && (!scale || !shift))) {
+    set_error("bn_bwd_apply: bad arguments");
+    return ARGUS_ERR_ARG;
+  }
+  const EwGeom g = ew_geom(C, E, pixels, 2048);
   hipStream_t st = (hipStream_t)stream;
+  dim3 grid(g.cgroups, g.rows);
   if (dtype == ARGUS_BF16)
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16>, dim3(grid_for(nch)), dim3(256), 0, st, nch, C, (const bf16*)dz, mode,
-                       (const bf16*)mask_src, (const bf16*)y, scale, shift, ca, cb, cc, (bf16*)dy, (bf16*)dm_out);
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16>, grid, dim3(256), 0, st, pixels, C, g.CC, g.PL, g.ppb,
+                       (const bf16*)dz, mode, (const bf16*)mask_src, (const bf16*)y, scale, shift, ca, cb, cc,
+                       (bf16*)dy, (bf16*)dm_out);
   else
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, dim3(grid_for(nch)), dim3(256), 0, st, nch, C, (const float*)dz,
-                       mode, (const float*)mask_src, (const float*)y, scale, shift, ca, cb, cc, (float*)dy,
-                       (float*)dm_out);
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, grid, dim3(256), 0, st, pixels, C, g.CC, g.PL, g.ppb,
+                       (const float*)dz, mode, (const float*)mask_src, (const float*)y, scale, shift, ca, cb, cc,
+                       (float*)dy, (float*)dm_out);
   return check_launch("bn_bwd_apply_kernel");
 }
 

@@ -53,6 +53,10 @@ int argus_conv_fwd(const argus_conv_desc* d, int dtype, const void* x, const voi
 
 int argus_conv_fwd_stat_rows(const argus_conv_desc* d, int dtype) { return d ? conv_fwd_stat_rows(*d, dtype) : 0; }
 
+int argus_conv_launch_info(const argus_conv_desc* d, int dtype, int pass, int64_t* flops) {
+  return d ? conv_launch_info(*d, dtype, pass, flops) : -1;
+}
+
 int argus_conv_fwd_stat_tile(const argus_conv_desc* d, int dtype) { return d ? conv_fwd_stat_tile(*d, dtype) : 0; }
 
 int argus_conv_dgrad(const argus_conv_desc* d, int dtype, const void* dy, const void* wt, void* dx, int accumulate,

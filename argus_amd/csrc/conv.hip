@@ -656,6 +656,11 @@ int conv_fwd_stat_rows(const argus_conv_desc& d, int) {
 
 int conv_fwd_stat_tile(const argus_conv_desc& d, int) { return fwd_bm(d); }
 
+static int dgrad_bm(const argus_conv_desc& d) {
+  const long M = (long)d.n * d.h * d.w / (d.stride * d.stride);
+  return M >= 64L * 1024 ? 128 : 64;
+}
+
 int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, void* y,
              const float* sc, const float* sh, float* stats, hipStream_t st) {
   if (int e = check_desc(d)) return e;
@@ -714,8 +719,7 @@ int conv_dgrad(const argus_conv_desc& d, int dtype, const void* dy, const void* 
       ph.K = t * d.k;
     }
   p.nphase = np;
-  const long M = (long)d.n * d.h * d.w / (s * s);
-  const int bm = M >= 64L * 1024 ? 128 : 64;
+  const int bm = dgrad_bm(d);
   return dtype == ARGUS_BF16 ? run_ig<bf16>(p, st, bm) : run_ig<float>(p, st, bm);
 }
 
@@ -734,7 +738,7 @@ static WgPlan wgrad_plan(const argus_conv_desc& d, int dtype) {
   pl.kstep = dtype == ARGUS_BF16 ? 64 : 32;
   const long P = (long)d.n * d.ho * d.wo;
   const long tiles = (long)pl.mt * pl.nt;
-  long splits = (1024 + tiles - 1) / tiles;
+  long splits = (512 + tiles - 1) / tiles;
   const long max_splits = (P + pl.kstep * 4 - 1) / (pl.kstep * 4);  // >= 4 k-steps per split
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
@@ -788,6 +792,16 @@ int conv_wgrad(const argus_conv_desc& d, int dtype, const void* x, const float* 
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st,
                      reinterpret_cast<const float*>(ws), pl.splits, d.k, pl.N, d.stem, dw);
   return check_launch("wgrad_reduce_kernel");
+}
+
+int conv_launch_info(const argus_conv_desc& d, int dtype, int pass, int64_t* flops) {
+  if (check_desc(d)) return -1;
+  if (flops) *flops = 2LL * d.n * d.ho * d.wo * d.k * d.r * d.s * d.c;
+  const int dtag = dtype == ARGUS_BF16 ? 1 : 0;
+  if (pass == 0) return 10000000 + dtag * 1000000 + fwd_bm(d) * 1000 + (d.k % 128 == 0 ? 128 : 64);
+  if (pass == 1) return 10000000 + dtag * 1000000 + dgrad_bm(d) * 1000 + (d.c % 128 == 0 ? 128 : 64);
+  const WgPlan pl = wgrad_plan(d, dtype);
+  return 20000000 + dtag * 1000000 + pl.bm * 1000 + pl.bn;
 }
 
 int conv_weight_prep(const argus_conv_desc& d, int dtype, const float* w, const int64_t* strides, void* wf,

@@ -137,9 +137,46 @@ __global__ void se3_loss_kernel(int B, const float* __restrict__ pred, const flo
     for (int i = 0; i < 6; ++i) dpred[b * 6 + i] = (float)(gscale * L.d[i]);
 }
 
+// se(3) -> SE(3) exponential map (pypose se3.Exp): out[b] = [t (3), q xyzw (4)], w >= 0 canonical
+// when `canon` (the data pipeline's quaternion convention).
+__global__ void se3_exp_kernel(int B, const float* __restrict__ xi, float* __restrict__ out, int canon) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  D6 x[6];
+  for (int i = 0; i < 6; ++i) x[i] = cst((double)xi[b * 6 + i]);
+  const V3 rho = {x[0], x[1], x[2]};
+  const V3 phi = {x[3], x[4], x[5]};
+  const D6 th2 = dot(phi, phi);
+  const D6 th = dsqrt(th2);
+  D6 imag, real;
+  if (th.v < kSmall) {
+    imag = cst(0.5) - (1.0 / 48) * th2 + (1.0 / 3840) * (th2 * th2);
+    real = cst(1.0) - (1.0 / 8) * th2 + (1.0 / 384) * (th2 * th2);
+  } else {
+    imag = dsin(0.5 * th) / th;
+    real = dcos(0.5 * th);
+  }
+  const V3 t = jl_apply(phi, rho, false);
+  const double sg = (canon && real.v < 0.0) ? -1.0 : 1.0;
+  float* o = out + b * 7;
+  o[0] = (float)t.x.v; o[1] = (float)t.y.v; o[2] = (float)t.z.v;
+  o[3] = (float)(sg * imag.v * phi.x.v); o[4] = (float)(sg * imag.v * phi.y.v);
+  o[5] = (float)(sg * imag.v * phi.z.v); o[6] = (float)(sg * real.v);
+}
+
 }  // namespace argus
 
 using namespace argus;
+
+extern "C" int argus_se3_exp(int batch, const float* xi, float* out, int canonical_w, argus_stream_t stream) {
+  if (batch <= 0 || !xi || !out) {
+    set_error("se3_exp: bad arguments");
+    return ARGUS_ERR_ARG;
+  }
+  hipLaunchKernelGGL(se3_exp_kernel, dim3((batch + 63) / 64), dim3(64), 0, (hipStream_t)stream, batch, xi, out,
+                     canonical_w);
+  return check_launch("se3_exp_kernel");
+}
 
 extern "C" int argus_se3_loss(int batch, const float* pred, const float* target, float* loss, float* dpred,
                               float grad_scale, argus_stream_t stream) {

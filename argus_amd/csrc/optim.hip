@@ -38,10 +38,11 @@ __global__ __launch_bounds__(256) void norm_finalize_kernel(int nparts, const do
 
 __global__ __launch_bounds__(256) void adam_kernel(int64_t n, float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v,
-                                                   const float* __restrict__ norm, float max_norm, float lr, float b1,
-                                                   float b2, float eps, float wd, float bc1, float bc2) {
-  float coef = 1.f;
-  if (norm) coef = fminf(1.f, max_norm / (norm[0] + 1e-6f));
+                                                   const float* __restrict__ norm, float gscale, float max_norm, float lr,
+                                                   float b1, float b2, float eps, float wd, float bc1, float bc2) {
+  // g' = gscale * g (e.g. 1/world after a SUM all-reduce), then clip_grad_norm_ on g'
+  float coef = gscale;
+  if (norm) coef = gscale * fminf(1.f, max_norm / (norm[0] * gscale + 1e-6f));
   const float step = lr / bc1;
   const float bc2s = sqrtf(bc2);
   const int64_t n4 = n / 4;
@@ -90,16 +91,17 @@ int argus_global_norm(int64_t count, const float* x, float* out, void* ws, argus
   return check_launch("norm_finalize_kernel");
 }
 
-int argus_adam_step(int64_t count, float* p, const float* g, float* m, float* v, const float* norm, float max_norm,
-                    float lr, float b1, float b2, float eps, float wd, float bc1, float bc2, argus_stream_t stream) {
+int argus_adam_step(int64_t count, float* p, const float* g, float* m, float* v, const float* norm, float gscale,
+                    float max_norm, float lr, float b1, float b2, float eps, float wd, float bc1, float bc2,
+                    argus_stream_t stream) {
   if (count <= 0 || !p || !g || !m || !v) { set_error("adam_step: bad arguments"); return ARGUS_ERR_ARG; }
   if ((((uintptr_t)p) | ((uintptr_t)g) | ((uintptr_t)m) | ((uintptr_t)v)) & 15) {
     set_error("adam_step: buffers must be 16-byte aligned");
     return ARGUS_ERR_ARG;
   }
   const int blocks = (int)std::min<int64_t>((count / 4 + 255) / 256 + 1, 4096);
-  hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, count, p, g, m, v, norm, max_norm,
-                     lr, b1, b2, eps, wd, bc1, bc2);
+  hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, count, p, g, m, v, norm, gscale,
+                     max_norm, lr, b1, b2, eps, wd, bc1, bc2);
   return check_launch("adam_kernel");
 }
 

@@ -60,6 +60,8 @@ class _Conv:
     wd: torch.Tensor | None
     stat_rows: int
     stat_tile: int
+    tags: tuple  # kernel instantiation per pass (fwd, dgrad, wgrad)
+    flops: int  # algorithmic flops of one pass
 
 
 class ResNetEngine:
@@ -79,6 +81,7 @@ class ResNetEngine:
         self.shape = None
         self.saved = False
         self.debug: dict | None = None  # when a dict: clones of block outputs / block-input grads
+        self.timer = None  # optional argus_amd.profiling.KernelTimer (events around conv launches)
 
     # ------------------------------------------------------------------ allocation
     def _t(self, *shape, dtype=None):
@@ -107,7 +110,9 @@ class ResNetEngine:
                 wd = self._t(c, ks * ks * k)
             rows = L.dll.argus_conv_fwd_stat_rows(C.byref(d), dt)
             tile = L.dll.argus_conv_fwd_stat_tile(C.byref(d), dt)
-            convs[name] = _Conv(name, d, wf, wd, rows, tile)
+            fl = C.c_int64(0)
+            tags = tuple(L.dll.argus_conv_launch_info(C.byref(d), dt, ps, C.byref(fl)) for ps in range(3))
+            convs[name] = _Conv(name, d, wf, wd, rows, tile, tags, fl.value)
             return d.ho, d.wo
 
         H1, W1 = add("resnet.conv1", N, H, W, 3, 64, 7, 2, 3, stem=True)
@@ -204,8 +209,8 @@ class ResNetEngine:
         sc = sh = None
         if pro is not None:
             sc, sh = self.bn_state[pro][2], self.bn_state[pro][3]
-        self.L.conv_fwd(C.byref(cv.desc), self.dt, ptr(x), ptr(cv.wf), ptr(y), ptr(sc), ptr(sh),
-                        ptr(self.stat_part) if training else None, stream())
+        self._launch(cv, 0, lambda: self.L.conv_fwd(C.byref(cv.desc), self.dt, ptr(x), ptr(cv.wf), ptr(y), ptr(sc),
+                                                     ptr(sh), ptr(self.stat_part) if training else None, stream()))
         if training:
             count = cv.desc.n * cv.desc.ho * cv.desc.wo
             self._bn_train(P, Bf, bn, cv.stat_rows, cv.stat_tile, count)
@@ -276,8 +281,13 @@ class ResNetEngine:
         return self.pred
 
     # ------------------------------------------------------------------ backward
-    def backward(self, dpred: torch.Tensor, P: dict, G: dict) -> None:
-        """Write every parameter gradient into G[name] (fp32; conv weights OHWI-contiguous)."""
+    def backward(self, dpred: torch.Tensor, P: dict, G: dict, on_ready=None) -> None:
+        """Write every parameter gradient into G[name] (fp32; conv weights OHWI-contiguous).
+
+        ``on_ready(name)`` (optional) is called, in stream order, as soon as the gradients of parameter
+        ``name`` and of every parameter registered after it are complete: after the head
+        ("resnet.fc.weight"), after each block ("<block>.conv1.weight"), after the stem
+        ("resnet.conv1.weight"). The trainer uses it to start bucketed all-reduces during backward."""
         if not self.saved:
             raise RuntimeError("backward without a saved train-mode forward")
         L, dt, s = self.L, self.dt, stream()
@@ -306,6 +316,8 @@ class ResNetEngine:
         g = self.gbuf
         dh, dx = g[0], g[3]
         L.avgpool_bwd(dt, N, hf * wf, 2048, ptr(self.dfeat), ptr(dh), s)
+        if on_ready is not None:
+            on_ready("resnet.fc.weight")
 
         for idx in range(len(self.blocks) - 1, -1, -1):
             b, a = self.blocks[idx], self.act[idx]
@@ -352,6 +364,8 @@ class ResNetEngine:
             else:
                 self._dgrad(pf + ".conv1", dyw, dx, 1)
             dh, dx = dx, dh
+            if on_ready is not None:
+                on_ready(pf + ".conv1.weight")
             if self.debug is not None:
                 n_in = N * hi * wi * b.cin
                 self.debug["bwd." + pf] = dh[:n_in].view(N, hi, wi, b.cin).clone()
@@ -362,6 +376,8 @@ class ResNetEngine:
         L.maxpool_bwd(dt, N, H1, W1, 64, ptr(dh), ptr(self.amax), ptr(dz0), s)
         self._bn_bwd(P, G, "resnet.bn1", N * H1 * W1, 64, dz0, 2, None, self.y0, dy0, None)
         self._wgrad("resnet.conv1", self.x0, None, dy0, G)
+        if on_ready is not None:
+            on_ready("resnet.conv1.weight")
 
     def _bn_bwd(self, P, G, name, px, ch, dz, mode, mask_src, y, dy_out, dm_out):
         L, dt, s = self.L, self.dt, stream()
@@ -380,12 +396,20 @@ class ResNetEngine:
         sc = sh = None
         if pro_state is not None:
             sc, sh = pro_state[2], pro_state[3]
-        self.L.conv_wgrad(C.byref(cv.desc), self.dt, ptr(x), ptr(sc), ptr(sh), ptr(dy), ptr(G[conv + ".weight"]),
-                          ptr(self.wg_ws), self.wg_ws_bytes, stream())
+        self._launch(cv, 2, lambda: self.L.conv_wgrad(C.byref(cv.desc), self.dt, ptr(x), ptr(sc), ptr(sh), ptr(dy),
+                                                       ptr(G[conv + ".weight"]), ptr(self.wg_ws), self.wg_ws_bytes,
+                                                       stream()))
 
     def _dgrad(self, conv, dy, dx, accumulate):
         cv = self.convs[conv]
-        self.L.conv_dgrad(C.byref(cv.desc), self.dt, ptr(dy), ptr(cv.wd), ptr(dx), accumulate, stream())
+        self._launch(cv, 1, lambda: self.L.conv_dgrad(C.byref(cv.desc), self.dt, ptr(dy), ptr(cv.wd), ptr(dx),
+                                                       accumulate, stream()))
+
+    def _launch(self, cv, pass_, fn):
+        if self.timer is None:
+            fn()
+        else:
+            self.timer.wrap(cv.tags[pass_], cv.flops, fn)
 
 
 def conv_grad_shape(shape_oihw) -> tuple:

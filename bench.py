@@ -1,0 +1,201 @@
+#!/usr/bin/env python
+"""Benchmark of the argus training hot path on MI355X (BASELINE.json metric / configs[1]).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 64] [--hw 256 256] [--dtype bf16]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+A step = one fused native train step (argus/train.py:298-320) on a device-resident synthetic batch:
+images (B, 6, H, W) fp32 in [0,1] (uint8-uniform pixels / 255, seed 1000+rank) and SE(3) targets
+Exp(xi), xi ~ N(0, 0.5^2) (seed 2000+rank) -> NCameraCNN forward (bf16 HIP kernels) -> SE(3) loss ->
+backward -> [RCCL SUM all-reduce, bucketed, overlapped] -> clip_grad_norm_(1.0) -> Adam(1e-4).
+Weights: seeded random init (torch.manual_seed(42)) of the reference architecture.
+value = images/s over all ranks (one sample = 2 camera images); weak scaling (B per rank fixed).
+
+Also reported:
+  roofline     - the dominant conv kernel instantiation (largest total time in the step), timed
+                 live with HIP events around each of its launches in the timed region; achieved =
+                 algorithmic FLOPs per launch / average launch time; peak = dense bf16 MFMA.
+  cpu_baseline - the CPU oracle (the reference's torch.nn ops on CPU, fp32, B=8) train step timed on
+                 this host (rank 0, N=1), a bounded sample of ~15 s.
+  val_loss     - mean SE(3) loss (argus/train.py:342) of the trained model in eval mode on a
+                 synthetic validation batch, and its sqrt (geodesic error).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import time
+
+import torch
+import torch.distributed as dist
+
+BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 MFMA
+F32_MFMA_PEAK_TFLOPS = 157.3
+HBM_PEAK_GBS = 8000.0
+
+
+def synthetic_batch(B, H, W, seed, device):
+    from argus_amd.utils import se3_exp
+
+    g = torch.Generator(device=device).manual_seed(seed)
+    images = torch.randint(0, 256, (B, 6, H, W), generator=g, device=device, dtype=torch.uint8).float() / 255.0
+    xi = torch.randn(B, 6, generator=g, device=device) * 0.5
+    targets = se3_exp(xi, canonical_w=True)
+    return images, targets
+
+
+def cpu_baseline(batch: int, H: int, W: int, budget_s: float = 15.0) -> dict:
+    """Oracle (CPU restatement of the reference model, same torch CPU ops) fwd+loss+bwd+clip+Adam."""
+    from oracle import se3
+    from oracle.ncamera import build_reference_model
+
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    model = build_reference_model(42)
+    model.train()
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+    g = torch.Generator().manual_seed(1000)
+    x = torch.randint(0, 256, (batch, 6, H, W), generator=g, dtype=torch.uint8).float() / 255.0
+    T = se3.random_targets(batch, generator=g)
+
+    def step():
+        losses = se3.geometric_loss(model(x), T)
+        opt.zero_grad()
+        losses.mean().backward()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+        opt.step()
+
+    step()  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while n < 2 or (time.perf_counter() - t0 < budget_s and n < 12):
+        step()
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(2 * batch * n / dt, 3), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"oracle (reference torch.nn ops on CPU) fp32 train step, batch {batch} samples "
+                      f"({2 * batch} images) of {H}x{W}, {n} timed steps after 1 warm-up, {dt:.1f} s"}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=64, help="samples (camera pairs) per rank")
+    ap.add_argument("--hw", type=int, nargs=2, default=(256, 256))
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from argus_amd.models import NCameraCNN
+    from argus_amd.profiling import KernelTimer
+    from argus_amd.step import FusedTrainer
+    from argus_amd.losses import geometric_loss_fn
+
+    B, (H, W) = args.batch, args.hw
+    torch.manual_seed(42)
+    model = NCameraCNN(compute_dtype=args.dtype).to(dev)
+    model.train()
+    trainer = FusedTrainer(model, lr=1e-4, max_grad_norm=1.0)
+    images, targets = synthetic_batch(B, H, W, 1000 + rank, dev)
+
+    for _ in range(args.warmup):
+        trainer.step(images, targets)
+    # find the dominant conv kernel instantiation over one instrumented step
+    eng = model._engine(dev)
+    probe = KernelTimer()
+    probe.enabled = True
+    eng.timer = probe
+    trainer.step(images, targets)
+    summ = probe.summary()
+    dom_tag = max(summ, key=lambda t: summ[t]["total_ms"])
+    timer = KernelTimer(tags=[dom_tag])
+    eng.timer = timer
+
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    timer.enabled = True
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        losses = trainer.step(images, targets)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    timer.enabled = False
+    eng.timer = None
+    el = torch.tensor([elapsed], device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = el.item()
+    train_loss = losses.mean().item()
+
+    # validation SE(3) error (eval mode, running BN statistics), synthetic held-out batch
+    model.eval()
+    vimg, vtgt = synthetic_batch(B, H, W, 5000 + rank, dev)
+    with torch.no_grad():
+        vloss = geometric_loss_fn(model(vimg), vtgt)
+    vsum = torch.stack([vloss.sum(), torch.tensor(float(vloss.numel()), device=dev)])
+    if world > 1:
+        dist.all_reduce(vsum)
+    val_loss = (vsum[0] / vsum[1]).item()
+
+    ks = timer.summary()[dom_tag]
+    achieved = ks["flops_per_launch"] / (ks["avg_us"] * 1e-6) / 1e12
+    peak = BF16_DENSE_PEAK_TFLOPS if args.dtype == "bf16" else F32_MFMA_PEAK_TFLOPS
+    ms = 1e3 * elapsed / args.steps
+    images_per_s = world * B * 2 * args.steps / elapsed
+    # algorithmic conv FLOPs per step: fwd + dgrad + wgrad (the stem has no dgrad)
+    step_flops = sum((2 if n == "resnet.conv1" else 3) * c.flops for n, c in eng.convs.items())
+    out = {
+        "metric": "train images/sec + val SE(3) geodesic err, 2x256x256 RGB",
+        "value": round(images_per_s, 2),
+        "unit": "images/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic (uint8-uniform images, Exp(N(0,0.5^2)) SE(3) targets, seeded random-init weights)",
+        "config": {
+            "workload": f"configs[1] cube_unity_data_small-shaped: fused train step, {B} samples "
+                        f"({2 * B} images) of {H}x{W} per rank, 2 cams, ResNet-50 + MLP head, {args.dtype}",
+            "batch_per_rank": B, "global_batch": B * world, "image_hw": [H, W], "parallelism": f"dp{world}",
+        },
+        "roofline": {
+            "bound": "mfma", "kernel": ks["name"], "launches": ks["launches"],
+            "flops_per_launch": ks["flops_per_launch"], "avg_launch_us": round(ks["avg_us"], 3),
+            "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+            "traffic": None,
+        },
+        "step_conv_tflops_per_gpu": round(step_flops / (ms * 1e-3) / 1e12, 2),
+        "step_conv_frac_of_bf16_peak": round(step_flops / (ms * 1e-3) / 1e12 / BF16_DENSE_PEAK_TFLOPS, 4),
+        "train_loss": round(train_loss, 6),
+        "val_loss": round(val_loss, 6),
+        "val_geodesic_err": round(math.sqrt(max(val_loss, 0.0)), 6),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(8, H, W, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -71,6 +71,11 @@ int argus_conv_fwd_stat_tile(const argus_conv_desc* d, int dtype);
 /* dx (+)= dgrad(dy, w_dgrad); accumulate != 0 adds into dx. */
 int argus_conv_dgrad(const argus_conv_desc* d, int dtype, const void* dy, const void* w_dgrad,
                      void* dx, int accumulate, argus_stream_t stream);
+/* Which kernel instantiation a pass launches and its algorithmic work: pass 0 fwd, 1 dgrad,
+ * 2 wgrad. Returns a tag (kind*10^7 + dtype*10^6 + tile_m*1000 + tile_n; kind 1 igemm,
+ * 2 wgrad) and writes 2*P*K*R*S*C flops (P = n*ho*wo output pixels). Used to time exactly the
+ * launches rocprof groups under one kernel name. */
+int argus_conv_launch_info(const argus_conv_desc* d, int dtype, int pass, int64_t* flops);
 /* dw (fp32, OHWI 7x7x3 for the stem) = sum over pixels of dy x im2col(x'), x' as in conv_fwd. */
 size_t argus_conv_wgrad_workspace_bytes(const argus_conv_desc* d, int dtype);
 int argus_conv_wgrad(const argus_conv_desc* d, int dtype, const void* x, const float* pro_scale,
@@ -147,17 +152,22 @@ int argus_gelu_bwd_f32(int64_t count, const float* x, const float* dy, float* dx
 int argus_se3_loss(int batch, const float* pred, const float* target, float* loss, float* dpred,
                    float grad_scale, argus_stream_t stream);
 
+/* se(3) -> SE(3) exponential (pypose se3.Exp; get_pose, argus/utils.py:179-189): out (B,7) =
+ * [t, qx, qy, qz, qw]; canonical_w != 0 flips q to w >= 0. */
+int argus_se3_exp(int batch, const float* xi, float* out, int canonical_w, argus_stream_t stream);
+
 /* ---- optimizer step (clip_grad_norm_ + Adam, argus/train.py:232,317-320) --------------------- */
 size_t argus_sumsq_workspace_bytes(int64_t count);
 /* out[0] = sqrt(sum x^2) (fp32, deterministic two-level reduction). */
 int argus_global_norm(int64_t count, const float* x, float* out, void* workspace,
                       argus_stream_t stream);
-/* g' = g * min(1, max_norm/(norm[0]+1e-6)) (if norm != NULL); Adam (torch semantics, bias
- * corrections bc1 = 1-beta1^t, bc2 = 1-beta2^t); writes param, m, v. */
+/* g' = grad_scale*g (e.g. 1/world after a SUM all-reduce); if norm != NULL (norm[0] = |g|),
+ * g' *= min(1, max_norm/(grad_scale*norm[0]+1e-6)) (clip_grad_norm_); then Adam (torch
+ * semantics, bias corrections bc1 = 1-beta1^t, bc2 = 1-beta2^t); writes param, m, v. */
 int argus_adam_step(int64_t count, float* param, const float* grad, float* exp_avg,
-                    float* exp_avg_sq, const float* norm, float max_norm, float lr, float beta1,
-                    float beta2, float eps, float weight_decay, float bc1, float bc2,
-                    argus_stream_t stream);
+                    float* exp_avg_sq, const float* norm, float grad_scale, float max_norm,
+                    float lr, float beta1, float beta2, float eps, float weight_decay, float bc1,
+                    float bc2, argus_stream_t stream);
 
 #ifdef __cplusplus
 }

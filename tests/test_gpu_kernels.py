@@ -372,7 +372,8 @@ def test_norm_and_adam(cuda):
         opt.step()
         gd = gs.to(cuda)
         L.global_norm(n, ptr(gd), ptr(norm), ptr(ws), stream())
-        L.adam_step(n, ptr(pd), ptr(gd), ptr(m), ptr(v), ptr(norm), C.c_float(1.0), C.c_float(1e-4), C.c_float(0.9),
+        L.adam_step(n, ptr(pd), ptr(gd), ptr(m), ptr(v), ptr(norm), C.c_float(1.0), C.c_float(1.0), C.c_float(1e-4),
+                    C.c_float(0.9),
                     C.c_float(0.999), C.c_float(1e-8), C.c_float(0.0), C.c_float(1 - 0.9**step),
                     C.c_float(1 - 0.999**step), stream())
     assert (pd.cpu() - ref_p.detach()).abs().max().item() < 2e-6
