@@ -74,13 +74,45 @@ ARGUS_DEV u32x4 bn_relu_chunk(u32x4 v, const float* __restrict__ sc, const float
 
 ARGUS_DEV int swz8(int row) { return (row >> 1) & 7; }
 
-template <typename T, int BM, int BN>
+ARGUS_DEV u32x4 sel(bool ok, u32x4 v) {
+  const u32x4 z = {0u, 0u, 0u, 0u};
+  return ok ? v : z;
+}
+
+// Per-thread BN+ReLU coefficients for one 16-byte chunk of channels.
+template <typename T> struct ProCoef {
+  float s[Chunk<T>::E], h[Chunk<T>::E];
+  ARGUS_DEV void load(const float* __restrict__ sc, const float* __restrict__ sh, int ch) {
+#pragma unroll
+    for (int j = 0; j < Chunk<T>::E; j += 4) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(sc + ch + j);
+      const f32x4 b = *reinterpret_cast<const f32x4*>(sh + ch + j);
+      s[j] = a.x; s[j + 1] = a.y; s[j + 2] = a.z; s[j + 3] = a.w;
+      h[j] = b.x; h[j + 1] = b.y; h[j + 2] = b.z; h[j + 3] = b.w;
+    }
+  }
+  ARGUS_DEV u32x4 apply(u32x4 v) const {
+    constexpr int E = Chunk<T>::E;
+    float f[E];
+    unpack(v, f);
+#pragma unroll
+    for (int j = 0; j < E; ++j) f[j] = fmaxf(fmaf(f[j], s[j], h[j]), 0.f);
+    return pack(f);
+  }
+};
+
+// C tile of the implicit GEMM, staged through LDS for 16-byte coalesced global stores.
+// Returns the LDS element stride of a staged row.
+template <typename T, int BN> constexpr int epi_ld() { return BN + 16 / (int)sizeof(T); }
+
+template <typename T, int BM, int BN, bool STEM, bool PRO>
 __global__ __launch_bounds__(256) void igemm_kernel(const IgParams p) {
   constexpr int E = Chunk<T>::E;
   constexpr int BKE = 8 * E;  // K elements per k-step (8 chunks of 16 B per LDS row)
   constexpr int MI = BM / 32, NI = BN / 32;
   constexpr int AR = BM / 32, BR = BN / 32;
-  __shared__ __attribute__((aligned(16))) u32x4 lds[2][(BM + BN) * 8];
+  constexpr int LDS_BYTES = 2 * (BM + BN) * 128;
+  __shared__ __attribute__((aligned(16))) u32x4 lds[LDS_BYTES / 16];
 
   const IgPhase& ph = p.ph[blockIdx.z];
   const int mtiles = (ph.M + BM - 1) / BM;
@@ -108,7 +140,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(const IgParams p) {
     const int mm = a_ok[i] ? m : 0;
     const int nimg = mm / HWq, rem = mm - nimg * HWq;
     const int qh = rem / ph.Wq, qw = rem - qh * ph.Wq;
-    a_n[i] = nimg;
+    a_n[i] = nimg * p.H;
     a_ih[i] = qh * p.ish;
     a_iw[i] = qw * p.isw;
   }
@@ -124,86 +156,89 @@ __global__ __launch_bounds__(256) void igemm_kernel(const IgParams p) {
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   u32x4 ra[AR], rb[BR];
-  const u32x4 zero = {0u, 0u, 0u, 0u};
+  bool a_ok_k[AR];
+  int pro_ch = 0;
 
   auto load = [&](int kt) {
     const int k0 = kt * BKE;
-    if (p.stem) {
+    if constexpr (STEM) {
+      // K = (r, s(8), c(4)); a chunk is 2 pixels x 4 channels (bf16) or 1 pixel x 4 channels (fp32)
       const int k = k0 + cidx * E;
       const int r = k >> 5, s0 = (k & 31) >> 2;
 #pragma unroll
       for (int i = 0; i < AR; ++i) {
         const int ih = a_ih[i] + r - 3;
         const bool rok = a_ok[i] && (unsigned)ih < (unsigned)p.H;
-        const T* rowp = A + ((size_t)a_n[i] * p.H + (rok ? ih : 0)) * p.W * 4;
+        const T* rowp = A + ((size_t)a_n[i] + (rok ? ih : 0)) * p.W * 4;
         if constexpr (E == 8) {
-          unsigned w4[4];
-#pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            const int iw = a_iw[i] + s0 + u - 3;
-            if (rok && (unsigned)iw < (unsigned)p.W) {
-              const uint2 v = *reinterpret_cast<const uint2*>(rowp + (size_t)iw * 4);
-              w4[2 * u] = v.x; w4[2 * u + 1] = v.y;
-            } else {
-              w4[2 * u] = 0u; w4[2 * u + 1] = 0u;
-            }
-          }
-          ra[i] = u32x4{w4[0], w4[1], w4[2], w4[3]};
+          const int iw0 = a_iw[i] + s0 - 3, iw1 = iw0 + 1;
+          const bool ok0 = rok && (unsigned)iw0 < (unsigned)p.W, ok1 = rok && (unsigned)iw1 < (unsigned)p.W;
+          const uint2 v0 = *reinterpret_cast<const uint2*>(rowp + (size_t)(ok0 ? iw0 : 0) * 4);
+          const uint2 v1 = *reinterpret_cast<const uint2*>(rowp + (size_t)(ok1 ? iw1 : 0) * 4);
+          ra[i] = u32x4{ok0 ? v0.x : 0u, ok0 ? v0.y : 0u, ok1 ? v1.x : 0u, ok1 ? v1.y : 0u};
         } else {
           const int iw = a_iw[i] + s0 - 3;
-          ra[i] = (rok && (unsigned)iw < (unsigned)p.W) ? ld16(rowp + (size_t)iw * 4) : zero;
+          const bool ok = rok && (unsigned)iw < (unsigned)p.W;
+          ra[i] = sel(ok, ld16(rowp + (size_t)(ok ? iw : 0) * 4));
         }
       }
 #pragma unroll
       for (int i = 0; i < BR; ++i) rb[i] = ld16(b_row[i] + k0);
-      return;
-    }
-    const int t = k0 / p.Cin;
-    const int ci0 = k0 - t * p.Cin;
-    const int dh = ph.dh[t], dw = ph.dw[t], boff = ph.boff[t];
+    } else {
+      const int t = k0 / p.Cin;
+      const int ci0 = k0 - t * p.Cin;
+      const int dh = ph.dh[t], dw = ph.dw[t], boff = ph.boff[t];
+      const int ch = ci0 + cidx * E;
 #pragma unroll
-    for (int i = 0; i < AR; ++i) {
-      const int ih = a_ih[i] + dh, iw = a_iw[i] + dw;
-      const bool ok = a_ok[i] && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-      if (ok) {
-        u32x4 v = ld16(A + (((size_t)a_n[i] * p.H + ih) * p.W + iw) * p.lda + ci0 + cidx * E);
-        if (p.pro_scale) v = bn_relu_chunk<T>(v, p.pro_scale, p.pro_shift, ci0 + cidx * E);
-        ra[i] = v;
-      } else {
-        ra[i] = zero;
+      for (int i = 0; i < AR; ++i) {
+        const int ih = a_ih[i] + dh, iw = a_iw[i] + dw;
+        const bool ok = a_ok[i] && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+        const size_t off = ok ? ((size_t)(a_n[i] + ih) * p.W + iw) * p.lda + ch : (size_t)ch;
+        ra[i] = ld16(A + off);
+        if constexpr (!PRO) ra[i] = sel(ok, ra[i]);
+        a_ok_k[i] = ok;
       }
-    }
 #pragma unroll
-    for (int i = 0; i < BR; ++i) rb[i] = ld16(b_row[i] + boff + ci0);
+      for (int i = 0; i < BR; ++i) rb[i] = ld16(b_row[i] + boff + ci0);
+      if constexpr (PRO) pro_ch = ch;
+    }
   };
 
   auto store = [&](int buf) {
+    u32x4* L = lds + buf * (BM + BN) * 8;
+    if constexpr (PRO && !STEM) {
+      ProCoef<T> pc;
+      pc.load(p.pro_scale, p.pro_shift, pro_ch);
+#pragma unroll
+      for (int i = 0; i < AR; ++i) ra[i] = sel(a_ok_k[i], pc.apply(ra[i]));
+    }
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
       const int row = (tid >> 3) + 32 * i;
-      lds[buf][row * 8 + (cidx ^ swz8(row))] = ra[i];
+      L[row * 8 + (cidx ^ swz8(row))] = ra[i];
     }
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
       const int row = (tid >> 3) + 32 * i;
-      lds[buf][BM * 8 + row * 8 + (cidx ^ swz8(row))] = rb[i];
+      L[BM * 8 + row * 8 + (cidx ^ swz8(row))] = rb[i];
     }
   };
 
   const int g = lane >> 4, i16 = lane & 15;
   auto compute = [&](int buf) {
+    const u32x4* L = lds + buf * (BM + BN) * 8;
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       u32x4 fa[MI], fb[NI];
 #pragma unroll
       for (int mi = 0; mi < MI; ++mi) {
         const int row = wm * (BM / 2) + mi * 16 + i16;
-        fa[mi] = lds[buf][row * 8 + ((4 * s2 + g) ^ swz8(row))];
+        fa[mi] = L[row * 8 + ((4 * s2 + g) ^ swz8(row))];
       }
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni) {
         const int row = wn * (BN / 2) + ni * 16 + i16;
-        fb[ni] = lds[buf][BM * 8 + row * 8 + ((4 * s2 + g) ^ swz8(row))];
+        fb[ni] = L[BM * 8 + row * 8 + ((4 * s2 + g) ^ swz8(row))];
       }
 #pragma unroll
       for (int mi = 0; mi < MI; ++mi)
@@ -226,41 +261,9 @@ __global__ __launch_bounds__(256) void igemm_kernel(const IgParams p) {
     }
   }
 
-  // ---- epilogue: y (+)= acc ----
-  T* __restrict__ C = reinterpret_cast<T*>(p.c);
-  size_t obase[MI][4];
-  bool ook[MI][4];
-#pragma unroll
-  for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = mt * BM + wm * (BM / 2) + mi * 16 + g * 4 + r;
-      ook[mi][r] = m < ph.M;
-      const int mm = ook[mi][r] ? m : 0;
-      const int nimg = mm / HWq, rem = mm - nimg * HWq;
-      const int qh = rem / ph.Wq, qw = rem - qh * ph.Wq;
-      const int oh = qh * p.osh + ph.oh0, ow = qw * p.osw + ph.ow0;
-      obase[mi][r] = (((size_t)nimg * p.Ho + oh) * p.Wo + ow) * p.ldc;
-    }
-#pragma unroll
-  for (int ni = 0; ni < NI; ++ni) {
-    const int n = nt * BN + wn * (BN / 2) + ni * 16 + i16;
-#pragma unroll
-    for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (!ook[mi][r]) continue;
-        float v = acc[mi][ni][r];
-        T* dst = C + obase[mi][r] + n;
-        if (p.accumulate) v += to_f32(*dst);
-        *dst = from_f32<T>(v);
-      }
-  }
-
+  // ---- BN statistics of this tile: {sum, M2} per column (fp32 accumulators) ----
   if (p.stats) {
-    // Per-tile {sum, M2} of the tile's valid rows (M2 = sum of squared deviations from the tile
-    // mean): each wave centres its own half-tile, the two halves merge with Chan's formula.
-    float2* red = reinterpret_cast<float2*>(&lds[0][0]);  // [2][BN]
+    float2* red = reinterpret_cast<float2*>(lds);  // [2][BN]
     int nvalid_w = ph.M - (mt * BM + wm * (BM / 2));
     nvalid_w = nvalid_w < 0 ? 0 : (nvalid_w > BM / 2 ? BM / 2 : nvalid_w);
 #pragma unroll
@@ -269,7 +272,10 @@ __global__ __launch_bounds__(256) void igemm_kernel(const IgParams p) {
 #pragma unroll
       for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) s += ook[mi][r] ? acc[mi][ni][r] : 0.f;
+        for (int r = 0; r < 4; ++r) {
+          const bool ok = mi * 16 + g * 4 + r < nvalid_w;
+          s += ok ? acc[mi][ni][r] : 0.f;
+        }
       s += __shfl_xor(s, 16, 64);
       s += __shfl_xor(s, 32, 64);
       const float mean_w = nvalid_w > 0 ? s / (float)nvalid_w : 0.f;
@@ -279,7 +285,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(const IgParams p) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float d = acc[mi][ni][r] - mean_w;
-          q = ook[mi][r] ? fmaf(d, d, q) : q;
+          q = mi * 16 + g * 4 + r < nvalid_w ? fmaf(d, d, q) : q;
         }
       q += __shfl_xor(q, 16, 64);
       q += __shfl_xor(q, 32, 64);
@@ -299,6 +305,54 @@ __global__ __launch_bounds__(256) void igemm_kernel(const IgParams p) {
       }
       p.stats[(size_t)mt * p.N + nt * BN + tid] = make_float2(a0.x + a1.x, m2);
     }
+    __syncthreads();
+  }
+
+  // ---- epilogue: stage the C tile in LDS, then 16-byte coalesced (+accumulating) stores ----
+  constexpr int LD = epi_ld<T, BN>();
+  constexpr int EPASS = (BM * LD * (int)sizeof(T) > LDS_BYTES) ? 2 : 1;
+  constexpr int ROWS = BM / EPASS;
+  constexpr int CPR = BN * (int)sizeof(T) / 16;  // 16-byte chunks per row
+  constexpr int RPP = 256 / CPR;                  // rows per store pass
+  T* Cs = reinterpret_cast<T*>(lds);
+  T* __restrict__ Cg = reinterpret_cast<T*>(p.c);
+#pragma unroll
+  for (int q = 0; q < EPASS; ++q) {
+    if (EPASS == 1 || wm == q) {
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = (EPASS == 1 ? wm * (BM / 2) : 0) + mi * 16 + g * 4 + r;
+            const int col = wn * (BN / 2) + ni * 16 + i16;
+            Cs[row * LD + col] = from_f32<T>(acc[mi][ni][r]);
+          }
+    }
+    __syncthreads();
+    const int c = tid % CPR;
+#pragma unroll
+    for (int rr = tid / CPR; rr < ROWS; rr += RPP) {
+      const int m = mt * BM + q * ROWS + rr;
+      if (m < ph.M) {
+        const int nimg = m / HWq, rem = m - nimg * HWq;
+        const int qh = rem / ph.Wq, qw = rem - qh * ph.Wq;
+        const int oh = qh * p.osh + ph.oh0, ow = qw * p.osw + ph.ow0;
+        T* dst = Cg + (((size_t)nimg * p.Ho + oh) * p.Wo + ow) * p.ldc + nt * BN + c * E;
+        u32x4 v = *reinterpret_cast<const u32x4*>(Cs + rr * LD + c * E);
+        if (p.accumulate) {
+          float f[E], o[E];
+          unpack(v, f);
+          unpack(ld16(dst), o);
+#pragma unroll
+          for (int j = 0; j < E; ++j) f[j] += o[j];
+          v = pack(f);
+        }
+        st16(dst, v);
+      }
+    }
+    if (EPASS > 1) __syncthreads();
   }
 }
 
@@ -321,7 +375,7 @@ struct WgParams {
 // ds_read_b64_tr_b16 half-wave touches land on 8 distinct slots.
 ARGUS_DEV int swz32(int row) { return (row & 3) | (((row >> 3) & 1) << 2); }
 
-template <typename T, int BM, int BN>
+template <typename T, int BM, int BN, bool STEM, bool PRO>
 __global__ __launch_bounds__(256) void wgrad_kernel(const WgParams p) {
   constexpr int E = Chunk<T>::E;
   constexpr bool BF = (E == 8);
@@ -342,9 +396,6 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgParams p) {
   const int split = blockIdx.y;
   const int pbeg = split * p.pps;
   const int pend = min(p.P, pbeg + p.pps);
-  if (pbeg >= pend) {
-    // still must zero the partial slab of this split
-  }
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const T* __restrict__ X = reinterpret_cast<const T*>(p.x);
@@ -357,7 +408,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgParams p) {
   const int cb = tid % CB, rb0 = tid / CB;
   const int kcol = nt * BN + cb * E;
   int tap_r, tap_s, ci;
-  if (p.stem) {
+  if constexpr (STEM) {
     tap_r = kcol >> 5; tap_s = (kcol & 31) >> 2; ci = 0;
   } else {
     const int t = kcol / p.Cin;
@@ -373,48 +424,44 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgParams p) {
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  ProCoef<T> pc;
+  if constexpr (PRO) pc.load(p.pro_scale, p.pro_shift, ci);
   u32x4 ra[PA], rb[PB];
   auto load = [&](int p0) {
 #pragma unroll
     for (int i = 0; i < PA; ++i) {
       const int pix = p0 + ra0 + RPA * i;
-      ra[i] = pix < pend ? ld16(a_col + (size_t)pix * p.M) : zero;
+      const bool ok = pix < pend;
+      ra[i] = sel(ok, ld16(a_col + (size_t)(ok ? pix : pbeg) * p.M));
     }
 #pragma unroll
     for (int i = 0; i < PB; ++i) {
       const int pix = p0 + rb0 + RPB * i;
-      u32x4 v = zero;
-      if (pix < pend) {
-        const int nimg = pix / HWo, rem = pix - nimg * HWo;
-        const int oh = rem / p.Wo, ow = rem - oh * p.Wo;
-        const int ih = oh * p.stride - p.pad + tap_r;
-        const int iw0 = ow * p.stride - p.pad + tap_s;
-        if ((unsigned)ih < (unsigned)p.H) {
-          const T* rowp = X + ((size_t)nimg * p.H + ih) * p.W * p.lda;
-          if (p.stem) {
-            if constexpr (BF) {
-              unsigned w4[4];
-#pragma unroll
-              for (int u = 0; u < 2; ++u) {
-                const int iw = iw0 + u;
-                if ((unsigned)iw < (unsigned)p.W) {
-                  const uint2 q = *reinterpret_cast<const uint2*>(rowp + (size_t)iw * 4);
-                  w4[2 * u] = q.x; w4[2 * u + 1] = q.y;
-                } else {
-                  w4[2 * u] = 0u; w4[2 * u + 1] = 0u;
-                }
-              }
-              v = u32x4{w4[0], w4[1], w4[2], w4[3]};
-            } else {
-              if ((unsigned)iw0 < (unsigned)p.W) v = ld16(rowp + (size_t)iw0 * 4);
-            }
-          } else if ((unsigned)iw0 < (unsigned)p.W) {
-            v = ld16(rowp + (size_t)iw0 * p.lda + ci);
-            if (p.pro_scale) v = bn_relu_chunk<T>(v, p.pro_scale, p.pro_shift, ci);
-          }
+      const bool pok = pix < pend;
+      const int pp = pok ? pix : pbeg;
+      const int nimg = pp / HWo, rem = pp - nimg * HWo;
+      const int oh = rem / p.Wo, ow = rem - oh * p.Wo;
+      const int ih = oh * p.stride - p.pad + tap_r;
+      const int iw0 = ow * p.stride - p.pad + tap_s;
+      const bool hok = pok && (unsigned)ih < (unsigned)p.H;
+      const T* rowp = X + ((size_t)nimg * p.H + (hok ? ih : 0)) * p.W * p.lda;
+      if constexpr (STEM) {
+        if constexpr (BF) {
+          const int iw1 = iw0 + 1;
+          const bool ok0 = hok && (unsigned)iw0 < (unsigned)p.W, ok1 = hok && (unsigned)iw1 < (unsigned)p.W;
+          const uint2 v0 = *reinterpret_cast<const uint2*>(rowp + (size_t)(ok0 ? iw0 : 0) * 4);
+          const uint2 v1 = *reinterpret_cast<const uint2*>(rowp + (size_t)(ok1 ? iw1 : 0) * 4);
+          rb[i] = u32x4{ok0 ? v0.x : 0u, ok0 ? v0.y : 0u, ok1 ? v1.x : 0u, ok1 ? v1.y : 0u};
+        } else {
+          const bool ok = hok && (unsigned)iw0 < (unsigned)p.W;
+          rb[i] = sel(ok, ld16(rowp + (size_t)(ok ? iw0 : 0) * 4));
         }
+      } else {
+        const bool ok = hok && (unsigned)iw0 < (unsigned)p.W;
+        u32x4 v = ld16(rowp + (size_t)(ok ? iw0 : 0) * p.lda + ci);
+        if constexpr (PRO) v = pc.apply(v);
+        rb[i] = sel(ok, v);
       }
-      rb[i] = v;
     }
   };
   auto store = [&](int buf) {
@@ -622,30 +669,43 @@ static int check_desc(const argus_conv_desc& d) {
   return ARGUS_OK;
 }
 
-template <typename T, int BM, int BN>
+template <typename T, int BM, int BN, bool STEM, bool PRO>
 static void launch_ig(const IgParams& p, int maxM, hipStream_t st) {
   const int ntiles = p.N / BN;
   dim3 grid(cdiv(maxM, BM) * ntiles, 1, p.nphase);
-  hipLaunchKernelGGL((igemm_kernel<T, BM, BN>), grid, dim3(256), 0, st, p);
+  hipLaunchKernelGGL((igemm_kernel<T, BM, BN, STEM, PRO>), grid, dim3(256), 0, st, p);
+}
+
+template <typename T, bool PRO>
+static void dispatch_ig(const IgParams& p, int maxM, int bm, hipStream_t st) {
+  const bool bn128 = (p.N % 128) == 0;
+  if (bm == 128) {
+    if (bn128) launch_ig<T, 128, 128, false, PRO>(p, maxM, st);
+    else launch_ig<T, 128, 64, false, PRO>(p, maxM, st);
+  } else {
+    if (bn128) launch_ig<T, 64, 128, false, PRO>(p, maxM, st);
+    else launch_ig<T, 64, 64, false, PRO>(p, maxM, st);
+  }
 }
 
 template <typename T>
-static int run_ig(const IgParams& p, hipStream_t st, int bm_pref) {
+static int run_ig(const IgParams& p, hipStream_t st, int bm) {
   int maxM = 0;
   for (int i = 0; i < p.nphase; ++i) maxM = p.ph[i].M > maxM ? p.ph[i].M : maxM;
-  const bool bn128 = (p.N % 128) == 0;
-  if (bm_pref == 128) {
-    if (bn128) launch_ig<T, 128, 128>(p, maxM, st);
-    else launch_ig<T, 128, 64>(p, maxM, st);
+  if (p.stem) {
+    if (p.N != 64 || bm != 128) { set_error("igemm: stem expects 64 output channels"); return ARGUS_ERR_SHAPE; }
+    launch_ig<T, 128, 64, true, false>(p, maxM, st);
+  } else if (p.pro_scale) {
+    dispatch_ig<T, true>(p, maxM, bm, st);
   } else {
-    if (bn128) launch_ig<T, 64, 128>(p, maxM, st);
-    else launch_ig<T, 64, 64>(p, maxM, st);
+    dispatch_ig<T, false>(p, maxM, bm, st);
   }
   return check_launch("igemm_kernel");
 }
 
 // row-tile size of the forward GEMM (drives the BN-statistics partial count)
 static int fwd_bm(const argus_conv_desc& d) {
+  if (d.stem) return 128;
   const long M = (long)d.n * d.ho * d.wo;
   return M >= 64L * 1024 ? 128 : 64;
 }
@@ -756,18 +816,25 @@ size_t conv_wgrad_ws(const argus_conv_desc& d, int dtype) {
   return (size_t)pl.splits * d.k * pl.N * sizeof(float);
 }
 
-template <typename T, int BM, int BN>
+template <typename T, int BM, int BN, bool STEM, bool PRO>
 static void launch_wg(const WgParams& p, const WgPlan& pl, hipStream_t st) {
   dim3 grid(pl.mt * pl.nt, pl.splits);
-  hipLaunchKernelGGL((wgrad_kernel<T, BM, BN>), grid, dim3(256), 0, st, p);
+  hipLaunchKernelGGL((wgrad_kernel<T, BM, BN, STEM, PRO>), grid, dim3(256), 0, st, p);
+}
+
+template <typename T, bool PRO>
+static void dispatch_wg_tiles(const WgParams& p, const WgPlan& pl, hipStream_t st) {
+  if (pl.bm == 128 && pl.bn == 128) launch_wg<T, 128, 128, false, PRO>(p, pl, st);
+  else if (pl.bm == 128) launch_wg<T, 128, 64, false, PRO>(p, pl, st);
+  else if (pl.bn == 128) launch_wg<T, 64, 128, false, PRO>(p, pl, st);
+  else launch_wg<T, 64, 64, false, PRO>(p, pl, st);
 }
 
 template <typename T>
 static void dispatch_wg(const WgParams& p, const WgPlan& pl, hipStream_t st) {
-  if (pl.bm == 128 && pl.bn == 128) launch_wg<T, 128, 128>(p, pl, st);
-  else if (pl.bm == 128) launch_wg<T, 128, 64>(p, pl, st);
-  else if (pl.bn == 128) launch_wg<T, 64, 128>(p, pl, st);
-  else launch_wg<T, 64, 64>(p, pl, st);
+  if (p.stem) launch_wg<T, 64, 128, true, false>(p, pl, st);  // stem: M = 64 channels, N = 256
+  else if (p.pro_scale) dispatch_wg_tiles<T, true>(p, pl, st);
+  else dispatch_wg_tiles<T, false>(p, pl, st);
 }
 
 int conv_wgrad(const argus_conv_desc& d, int dtype, const void* x, const float* sc, const float* sh,
