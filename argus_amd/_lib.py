@@ -57,7 +57,8 @@ SIGNATURES = {
     "argus_maxpool_bwd": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "argus_avgpool_fwd": (_I, [_I, _I, _I, _I, _P, _P, _P]),
     "argus_avgpool_bwd": (_I, [_I, _I, _I, _I, _P, _P, _P]),
-    "argus_gemm_f32": (_I, [_I, _I, _I, _P, _I, _I, _P, _I, _I, _P, _I, _P, _I, _P, _P]),
+    "argus_gemm_f32_workspace_bytes": (_SZ, [_I, _I, _I]),
+    "argus_gemm_f32": (_I, [_I, _I, _I, _P, _I, _I, _P, _I, _I, _P, _I, _P, _I, _P, _P, _SZ, _P]),
     "argus_colsum_f32": (_I, [_I, _I, _P, _I, _P, _P]),
     "argus_gelu_f32": (_I, [_I64, _P, _P, _P]),
     "argus_gelu_bwd_f32": (_I, [_I64, _P, _P, _P, _P]),

@@ -13,45 +13,35 @@
 
 namespace argus {
 
-// ---- forward statistics: Chan/Welford merge of per-tile {sum, M2} partials ----------------------
-// part float2[rows][C], tile t covers n_t = min(tile_rows, count - t*tile_rows) elements.
-// Level 1 merges groups of tiles into {n, mean, M2} (double), level 2 merges the groups.
-struct Welf {
-  double n, mean, m2;
-};
-ARGUS_DEV void welf_merge(Welf& a, double nb, double meanb, double m2b) {
-  if (nb <= 0.0) return;
-  const double n = a.n + nb;
-  const double d = meanb - a.mean;
-  a.mean += d * (nb / n);
-  a.m2 += m2b + d * d * (a.n * nb / n);
-  a.n = n;
-}
-
+// ---- forward statistics: merge of per-tile {sum, M2} partials ------------------------------------
+// part float2[rows][C], tile t covers n_t = min(tile_rows, count - t*tile_rows) elements. In fp64:
+// S = sum_t sum_t, Q = sum_t (M2_t + sum_t^2 / n_t)  ->  mean = S/n, M2 = Q - S^2/n
+// (= sum_t M2_t + sum_t n_t (mean_t - mean)^2, the exact parallel-variance merge; the within-tile
+// M2_t carry the large part, so fp64 leaves no cancellation problem).
 __global__ __launch_bounds__(256) void stats_reduce_kernel(const float2* __restrict__ part, int rows, int C,
                                                            int rows_per_group, int64_t count, int tile_rows,
-                                                           double* __restrict__ out) {
+                                                           double2* __restrict__ out) {
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int lane_r = threadIdx.x >> 6;
   const int g = blockIdx.y;
   const int r0 = g * rows_per_group, r1 = min(rows, r0 + rows_per_group);
-  Welf w = {0.0, 0.0, 0.0};
+  const double inv_full = 1.0 / (double)tile_rows;
+  double S = 0.0, Q = 0.0;
   if (c < C)
     for (int r = r0 + lane_r; r < r1; r += 4) {
       const float2 v = part[(size_t)r * C + c];
       const int64_t left = count - (int64_t)r * tile_rows;
-      const double nt = (double)(left < tile_rows ? left : tile_rows);
-      welf_merge(w, nt, nt > 0.0 ? (double)v.x / nt : 0.0, (double)v.y);
+      const double inv = left >= tile_rows ? inv_full : 1.0 / (double)left;
+      S += (double)v.x;
+      Q += (double)v.y + (double)v.x * (double)v.x * inv;
     }
-  __shared__ double red[4][64][3];
-  red[lane_r][threadIdx.x & 63][0] = w.n;
-  red[lane_r][threadIdx.x & 63][1] = w.mean;
-  red[lane_r][threadIdx.x & 63][2] = w.m2;
+  __shared__ double2 red[4][64];
+  red[lane_r][threadIdx.x & 63] = make_double2(S, Q);
   __syncthreads();
   if (lane_r == 0 && c < C) {
-    for (int i = 1; i < 4; ++i) welf_merge(w, red[i][threadIdx.x][0], red[i][threadIdx.x][1], red[i][threadIdx.x][2]);
-    double* o = out + ((size_t)g * C + c) * 3;
-    o[0] = w.n; o[1] = w.mean; o[2] = w.m2;
+    double2 a = red[0][threadIdx.x];
+    for (int i = 1; i < 4; ++i) { a.x += red[i][threadIdx.x].x; a.y += red[i][threadIdx.x].y; }
+    out[(size_t)g * C + c] = a;
   }
 }
 
@@ -79,7 +69,7 @@ __global__ __launch_bounds__(256) void colreduce_kernel(const float2* __restrict
   }
 }
 
-static int reduce_groups(int rows) { return rows < 64 ? 1 : (rows < 1024 ? 8 : 16); }
+static int reduce_groups(int rows) { return rows < 64 ? 1 : (rows < 512 ? 8 : (rows < 4096 ? 32 : 64)); }
 
 static int colreduce(const float* part, int rows, int C, void* ws, int& G, hipStream_t st) {
   G = reduce_groups(rows);
@@ -89,21 +79,23 @@ static int colreduce(const float* part, int rows, int C, void* ws, int& G, hipSt
   return check_launch("colreduce_kernel");
 }
 
-__global__ void bn_finalize_kernel(const double* __restrict__ red, int G, int C, const float* gamma,
+__global__ void bn_finalize_kernel(const double2* __restrict__ red, int G, int C, double count, const float* gamma,
                                    const float* beta, float eps, float momentum, float* running_mean,
                                    float* running_var, int64_t* nbt, float* mean_o, float* invstd_o,
                                    float* scale_o, float* shift_o) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c == 0 && nbt) nbt[0] += 1;
   if (c >= C) return;
-  Welf w = {0.0, 0.0, 0.0};
+  double S = 0.0, Q = 0.0;
   for (int g = 0; g < G; ++g) {
-    const double* r = red + ((size_t)g * C + c) * 3;
-    welf_merge(w, r[0], r[1], r[2]);
+    const double2 v = red[(size_t)g * C + c];
+    S += v.x;
+    Q += v.y;
   }
-  const double count = w.n;
-  const double mean = w.mean;
-  const double var = count > 0.0 ? w.m2 / count : 0.0;
+  const double mean = S / count;
+  double m2 = Q - S * mean;
+  if (m2 < 0.0) m2 = 0.0;
+  const double var = m2 / count;
   const float invstd = (float)(1.0 / sqrt(var + (double)eps));
   const float sc = gamma[c] * invstd;
   if (mean_o) mean_o[c] = (float)mean;
@@ -112,7 +104,7 @@ __global__ void bn_finalize_kernel(const double* __restrict__ red, int G, int C,
   if (shift_o) shift_o[c] = beta[c] - (float)mean * sc;
   if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
   if (running_var) {
-    const double unbiased = count > 1.0 ? w.m2 / (count - 1.0) : var;
+    const double unbiased = count > 1.0 ? m2 / (count - 1.0) : var;
     running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unbiased;
   }
 }
@@ -431,7 +423,7 @@ using namespace argus;
 
 extern "C" {
 
-size_t argus_bn_workspace_bytes(int channels) { return (size_t)16 * channels * 3 * sizeof(double); }
+size_t argus_bn_workspace_bytes(int channels) { return (size_t)64 * channels * sizeof(double2); }
 
 int argus_bn_finalize(int C, int rows, int tile_rows, const float* part, int64_t count, const float* gamma,
                       const float* beta, float eps, float momentum, float* rm, float* rv, int64_t* nbt, float* mean,
@@ -445,10 +437,10 @@ int argus_bn_finalize(int C, int rows, int tile_rows, const float* part, int64_t
   const int G = reduce_groups(rows);
   const int rpg = (rows + G - 1) / G;
   hipLaunchKernelGGL(stats_reduce_kernel, dim3((C + 63) / 64, G), dim3(256), 0, st,
-                     reinterpret_cast<const float2*>(part), rows, C, rpg, count, tile_rows, reinterpret_cast<double*>(ws));
+                     reinterpret_cast<const float2*>(part), rows, C, rpg, count, tile_rows, reinterpret_cast<double2*>(ws));
   if (int e = check_launch("stats_reduce_kernel")) return e;
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st,
-                     reinterpret_cast<const double*>(ws), G, C, gamma, beta, eps, momentum, rm, rv,
+                     reinterpret_cast<const double2*>(ws), G, C, (double)count, gamma, beta, eps, momentum, rm, rv,
                      nbt, mean, invstd, scale, shift);
   return check_launch("bn_finalize_kernel");
 }

@@ -15,10 +15,25 @@ ARGUS_DEV float gelu_grad(float x) {
 }
 
 // 64x64 output tile, 256 threads (4 waves, 2x2, each 32x32 = 2x2 MFMA blocks), K-step 16.
+ARGUS_DEV void epilogue_store(float v, int m, int n, float* __restrict__ C, int ldc, const float* __restrict__ bias,
+                               int epi, float* __restrict__ aux) {
+  float* dst = C + (size_t)m * ldc + n;
+  switch (epi) {
+    case 0: *dst = v; break;
+    case 1: *dst = v + bias[n]; break;
+    case 2: v += bias[n]; aux[(size_t)m * ldc + n] = v; *dst = gelu_f(v); break;
+    case 3: *dst = v * gelu_grad(aux[(size_t)m * ldc + n]); break;
+    default: *dst += v; break;
+  }
+}
+
+// split-K slice z covers k in [z*kc, min(K, (z+1)*kc)); with splits > 1 the raw partial tile goes to
+// ws[z][M][N] and gemm_reduce_kernel applies the epilogue after a fixed-order sum.
 __global__ __launch_bounds__(256) void gemm_f32_kernel(int M, int N, int K, const float* __restrict__ A, int lda,
                                                        int ta, const float* __restrict__ B, int ldb, int tb,
                                                        float* __restrict__ C, int ldc, const float* __restrict__ bias,
-                                                       int epi, float* __restrict__ aux) {
+                                                       int epi, float* __restrict__ aux, int kc,
+                                                       float* __restrict__ ws) {
   __shared__ float As[16][65];  // [k][m]
   __shared__ float Bs[16][65];  // [k][n]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -29,7 +44,8 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(int M, int N, int K, cons
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int k0 = 0; k0 < K; k0 += 16) {
+  const int kbeg = blockIdx.z * kc, kend = min(K, kbeg + kc);
+  for (int k0 = kbeg; k0 < kend; k0 += 16) {
     // stage 16 x 64 of A (as [k][m]) and B (as [k][n]): 1024 elements each, 4 per thread
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -38,13 +54,13 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(int M, int N, int K, cons
       if (ta) { kk = idx >> 6; mm = idx & 63; } else { mm = idx >> 4; kk = idx & 15; }
       const int gm = m0 + mm, gk = k0 + kk;
       float v = 0.f;
-      if (gm < M && gk < K) v = ta ? A[(size_t)gk * lda + gm] : A[(size_t)gm * lda + gk];
+      if (gm < M && gk < kend) v = ta ? A[(size_t)gk * lda + gm] : A[(size_t)gm * lda + gk];
       As[kk][mm] = v;
       int kb, nn;
       if (tb) { nn = idx >> 4; kb = idx & 15; } else { kb = idx >> 6; nn = idx & 63; }
       const int gn = n0 + nn, gk2 = k0 + kb;
       float w = 0.f;
-      if (gn < N && gk2 < K) w = tb ? B[(size_t)gn * ldb + gk2] : B[(size_t)gk2 * ldb + gn];
+      if (gn < N && gk2 < kend) w = tb ? B[(size_t)gn * ldb + gk2] : B[(size_t)gk2 * ldb + gn];
       Bs[kb][nn] = w;
     }
     __syncthreads();
@@ -72,17 +88,21 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(int M, int N, int K, cons
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
         if (m >= M || n >= N) continue;
-        float v = acc[i][j][r];
-        float* dst = C + (size_t)m * ldc + n;
-        switch (epi) {
-          case 0: *dst = v; break;
-          case 1: *dst = v + bias[n]; break;
-          case 2: v += bias[n]; aux[(size_t)m * ldc + n] = v; *dst = gelu_f(v); break;
-          case 3: *dst = v * gelu_grad(aux[(size_t)m * ldc + n]); break;
-          default: *dst += v; break;
-        }
+        if (ws) ws[((size_t)blockIdx.z * M + m) * N + n] = acc[i][j][r];
+        else epilogue_store(acc[i][j][r], m, n, C, ldc, bias, epi, aux);
       }
     }
+}
+
+__global__ __launch_bounds__(256) void gemm_reduce_kernel(int M, int N, int splits, const float* __restrict__ ws,
+                                                          float* __restrict__ C, int ldc, const float* __restrict__ bias,
+                                                          int epi, float* __restrict__ aux) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)M * N) return;
+  float v = 0.f;
+  for (int z = 0; z < splits; ++z) v += ws[(size_t)z * M * N + e];
+  const int m = (int)(e / N), n = (int)(e - (int64_t)m * N);
+  epilogue_store(v, m, n, C, ldc, bias, epi, aux);
 }
 
 __global__ void colsum_kernel(int M, int N, const float* __restrict__ x, int ld, float* __restrict__ out) {
@@ -108,17 +128,36 @@ using namespace argus;
 
 extern "C" {
 
+size_t argus_gemm_f32_workspace_bytes(int m, int n, int k) {
+  const int tiles = ((m + 63) / 64) * ((n + 63) / 64);
+  int splits = 1;
+  while (tiles * splits < 256 && k / (splits * 2) >= 128) splits *= 2;
+  return splits > 1 ? (size_t)splits * m * n * sizeof(float) : 0;
+}
+
 int argus_gemm_f32(int m, int n, int k, const float* a, int lda, int ta, const float* b, int ldb, int tb, float* c,
-                   int ldc, const float* bias, int epi, float* aux, argus_stream_t stream) {
+                   int ldc, const float* bias, int epi, float* aux, void* ws, size_t ws_bytes, argus_stream_t stream) {
   if (m <= 0 || n <= 0 || k <= 0 || !a || !b || !c || epi < 0 || epi > 4 || ((epi == 1 || epi == 2) && !bias) ||
       ((epi == 2 || epi == 3) && !aux)) {
     set_error("gemm_f32: bad arguments");
     return ARGUS_ERR_ARG;
   }
-  dim3 grid((n + 63) / 64, (m + 63) / 64);
-  hipLaunchKernelGGL(gemm_f32_kernel, grid, dim3(256), 0, (hipStream_t)stream, m, n, k, a, lda, ta, b, ldb, tb, c, ldc,
-                     bias, epi, aux);
-  return check_launch("gemm_f32_kernel");
+  const int tiles = ((m + 63) / 64) * ((n + 63) / 64);
+  int splits = 1;
+  while (tiles * splits < 256 && k / (splits * 2) >= 128) splits *= 2;
+  if (splits > 1 && (!ws || ws_bytes < (size_t)splits * m * n * sizeof(float))) splits = 1;  // no workspace
+  const int kc = ((k + splits - 1) / splits + 15) / 16 * 16;
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid((n + 63) / 64, (m + 63) / 64, splits);
+  hipLaunchKernelGGL(gemm_f32_kernel, grid, dim3(256), 0, st, m, n, k, a, lda, ta, b, ldb, tb, c, ldc, bias, epi, aux,
+                     kc, splits > 1 ? (float*)ws : (float*)nullptr);
+  if (int e = check_launch("gemm_f32_kernel")) return e;
+  if (splits > 1) {
+    hipLaunchKernelGGL(gemm_reduce_kernel, dim3((unsigned)(((int64_t)m * n + 255) / 256)), dim3(256), 0, st, m, n,
+                       splits, (const float*)ws, c, ldc, bias, epi, aux);
+    return check_launch("gemm_reduce_kernel");
+  }
+  return ARGUS_OK;
 }
 
 int argus_colsum_f32(int m, int n, const float* x, int ld, float* out, argus_stream_t stream) {

@@ -187,6 +187,11 @@ class ResNetEngine:
         self.dh2, self.dh1 = self._f(B, 128), self._f(B, 128)
         self.dh0 = self._f(B, self.n_cams * self.rdim)
         self.dfeat = self._f(N, Fd)
+        D = self.n_cams * self.rdim
+        shapes = [(N, self.rdim, Fd), (B, 128, D), (B, 128, 128), (B, 6, 128), (6, 128, B), (B, 128, 6),
+                  (128, 128, B), (128, D, B), (B, D, 128), (self.rdim, Fd, N), (N, Fd, self.rdim)]
+        hws = max(L.dll.argus_gemm_f32_workspace_bytes(*sh) for sh in shapes)
+        self.gemm_ws = torch.empty(max(hws, 16), dtype=torch.uint8, device=self.device)
 
     # ------------------------------------------------------------------ helpers
     def _bn_train(self, P, Bf, name, rows, tile, count):
@@ -268,15 +273,15 @@ class ResNetEngine:
         # head (fp32)
         fcw, fcb = P["resnet.fc.weight"], P["resnet.fc.bias"]
         L.gemm_f32(N, self.rdim, 2048, ptr(self.feat), 2048, 0, ptr(fcw), 2048, 1, ptr(self.h0), self.rdim,
-                   ptr(fcb), 1, None, s)
+                   ptr(fcb), 1, None, ptr(self.gemm_ws), self.gemm_ws.numel(), s)
         D = self.n_cams * self.rdim
         L.gelu_f32(B * D, ptr(self.h0), ptr(self.g0), s)
         w0, b0 = P["output_mlp.0.weight"], P["output_mlp.0.bias"]
         w2, b2 = P["output_mlp.2.weight"], P["output_mlp.2.bias"]
         w4, b4 = P["output_mlp.4.weight"], P["output_mlp.4.bias"]
-        L.gemm_f32(B, 128, D, ptr(self.g0), D, 0, ptr(w0), D, 1, ptr(self.g1), 128, ptr(b0), 2, ptr(self.h1), s)
-        L.gemm_f32(B, 128, 128, ptr(self.g1), 128, 0, ptr(w2), 128, 1, ptr(self.g2), 128, ptr(b2), 2, ptr(self.h2), s)
-        L.gemm_f32(B, 6, 128, ptr(self.g2), 128, 0, ptr(w4), 128, 1, ptr(self.pred), 6, ptr(b4), 1, None, s)
+        L.gemm_f32(B, 128, D, ptr(self.g0), D, 0, ptr(w0), D, 1, ptr(self.g1), 128, ptr(b0), 2, ptr(self.h1), ptr(self.gemm_ws), self.gemm_ws.numel(), s)
+        L.gemm_f32(B, 128, 128, ptr(self.g1), 128, 0, ptr(w2), 128, 1, ptr(self.g2), 128, ptr(b2), 2, ptr(self.h2), ptr(self.gemm_ws), self.gemm_ws.numel(), s)
+        L.gemm_f32(B, 6, 128, ptr(self.g2), 128, 0, ptr(w4), 128, 1, ptr(self.pred), 6, ptr(b4), 1, None, ptr(self.gemm_ws), self.gemm_ws.numel(), s)
         self.saved = training
         return self.pred
 
@@ -297,21 +302,21 @@ class ResNetEngine:
         dpred = dpred.contiguous().float()
         w0, w2, w4 = P["output_mlp.0.weight"], P["output_mlp.2.weight"], P["output_mlp.4.weight"]
         # MLP
-        L.gemm_f32(6, 128, B, ptr(dpred), 6, 1, ptr(self.g2), 128, 0, ptr(G["output_mlp.4.weight"]), 128, None, 0, None, s)
+        L.gemm_f32(6, 128, B, ptr(dpred), 6, 1, ptr(self.g2), 128, 0, ptr(G["output_mlp.4.weight"]), 128, None, 0, None, ptr(self.gemm_ws), self.gemm_ws.numel(), s)
         L.colsum_f32(B, 6, ptr(dpred), 6, ptr(G["output_mlp.4.bias"]), s)
-        L.gemm_f32(B, 128, 6, ptr(dpred), 6, 0, ptr(w4), 128, 0, ptr(self.dh2), 128, None, 3, ptr(self.h2), s)
-        L.gemm_f32(128, 128, B, ptr(self.dh2), 128, 1, ptr(self.g1), 128, 0, ptr(G["output_mlp.2.weight"]), 128, None, 0, None, s)
+        L.gemm_f32(B, 128, 6, ptr(dpred), 6, 0, ptr(w4), 128, 0, ptr(self.dh2), 128, None, 3, ptr(self.h2), ptr(self.gemm_ws), self.gemm_ws.numel(), s)
+        L.gemm_f32(128, 128, B, ptr(self.dh2), 128, 1, ptr(self.g1), 128, 0, ptr(G["output_mlp.2.weight"]), 128, None, 0, None, ptr(self.gemm_ws), self.gemm_ws.numel(), s)
         L.colsum_f32(B, 128, ptr(self.dh2), 128, ptr(G["output_mlp.2.bias"]), s)
-        L.gemm_f32(B, 128, 128, ptr(self.dh2), 128, 0, ptr(w2), 128, 0, ptr(self.dh1), 128, None, 3, ptr(self.h1), s)
-        L.gemm_f32(128, D, B, ptr(self.dh1), 128, 1, ptr(self.g0), D, 0, ptr(G["output_mlp.0.weight"]), D, None, 0, None, s)
+        L.gemm_f32(B, 128, 128, ptr(self.dh2), 128, 0, ptr(w2), 128, 0, ptr(self.dh1), 128, None, 3, ptr(self.h1), ptr(self.gemm_ws), self.gemm_ws.numel(), s)
+        L.gemm_f32(128, D, B, ptr(self.dh1), 128, 1, ptr(self.g0), D, 0, ptr(G["output_mlp.0.weight"]), D, None, 0, None, ptr(self.gemm_ws), self.gemm_ws.numel(), s)
         L.colsum_f32(B, 128, ptr(self.dh1), 128, ptr(G["output_mlp.0.bias"]), s)
-        L.gemm_f32(B, D, 128, ptr(self.dh1), 128, 0, ptr(w0), D, 0, ptr(self.dh0), D, None, 3, ptr(self.h0), s)
+        L.gemm_f32(B, D, 128, ptr(self.dh1), 128, 0, ptr(w0), D, 0, ptr(self.dh0), D, None, 3, ptr(self.h0), ptr(self.gemm_ws), self.gemm_ws.numel(), s)
         # fc (rows = images)
         fcw = P["resnet.fc.weight"]
         R = self.rdim
-        L.gemm_f32(R, 2048, N, ptr(self.dh0), R, 1, ptr(self.feat), 2048, 0, ptr(G["resnet.fc.weight"]), 2048, None, 0, None, s)
+        L.gemm_f32(R, 2048, N, ptr(self.dh0), R, 1, ptr(self.feat), 2048, 0, ptr(G["resnet.fc.weight"]), 2048, None, 0, None, ptr(self.gemm_ws), self.gemm_ws.numel(), s)
         L.colsum_f32(N, R, ptr(self.dh0), R, ptr(G["resnet.fc.bias"]), s)
-        L.gemm_f32(N, 2048, R, ptr(self.dh0), R, 0, ptr(fcw), 2048, 0, ptr(self.dfeat), 2048, None, 0, None, s)
+        L.gemm_f32(N, 2048, R, ptr(self.dh0), R, 0, ptr(fcw), 2048, 0, ptr(self.dfeat), 2048, None, 0, None, ptr(self.gemm_ws), self.gemm_ws.numel(), s)
         hf, wf = self.final_hw
         g = self.gbuf
         dh, dx = g[0], g[3]

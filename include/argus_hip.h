@@ -136,10 +136,12 @@ int argus_avgpool_bwd(int dtype, int n, int hw, int c, const float* dfeat, void*
  * opB(B)[k][n] = trans_b ? B[n*ldb+k] : B[k*ldb+n].
  * epilogue 0: C = acc; 1: C = acc + bias[n]; 2: aux = acc + bias[n], C = gelu(aux);
  * 3: C = acc * gelu'(aux[m][n]) (backward through a GELU whose pre-activation is aux, ld = ldc);
- * 4: C += acc. */
+ * 4: C += acc. Small-output / long-K products split K over workgroups (deterministic fixed-order
+ * reduce) when a workspace of argus_gemm_f32_workspace_bytes() is given (NULL: no split). */
+size_t argus_gemm_f32_workspace_bytes(int m, int n, int k);
 int argus_gemm_f32(int m, int n, int k, const float* a, int lda, int trans_a, const float* b,
                    int ldb, int trans_b, float* c, int ldc, const float* bias, int epilogue,
-                   float* aux, argus_stream_t stream);
+                   float* aux, void* workspace, size_t workspace_bytes, argus_stream_t stream);
 /* out[n] = sum_m x[m*ld + n] (bias gradients). */
 int argus_colsum_f32(int m, int n, const float* x, int ld, float* out, argus_stream_t stream);
 int argus_gelu_f32(int64_t count, const float* x, float* y, argus_stream_t stream);

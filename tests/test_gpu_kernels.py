@@ -297,14 +297,16 @@ def test_gemm_f32_epilogues(cuda):
                 ref = (a.double().T if ta else a.double()) @ (b.double().T if tb else b.double())
                 c = torch.empty(m, n, device=cuda)
                 ag, bg = a.to(cuda), b.to(cuda)
-                L.gemm_f32(m, n, k, ptr(ag), a.shape[1], ta, ptr(bg), b.shape[1], tb, ptr(c), n, None, 0, None, stream())
+                ws = torch.empty(max(16, L.dll.argus_gemm_f32_workspace_bytes(m, n, k)), dtype=torch.uint8, device=cuda)
+                L.gemm_f32(m, n, k, ptr(ag), a.shape[1], ta, ptr(bg), b.shape[1], tb, ptr(c), n, None, 0, None, ptr(ws),
+                           ws.numel(), stream())
                 assert _rel(c, ref) < 1e-5, (m, n, k, ta, tb)
     m, n, k = 9, 33, 40
     a, b, bias = torch.randn(m, k), torch.randn(n, k), torch.randn(n)
     aux = torch.empty(m, n, device=cuda)
     c = torch.empty(m, n, device=cuda)
     ag, bg, biasg = a.to(cuda), b.to(cuda), bias.to(cuda)
-    L.gemm_f32(m, n, k, ptr(ag), k, 0, ptr(bg), k, 1, ptr(c), n, ptr(biasg), 2, ptr(aux), stream())
+    L.gemm_f32(m, n, k, ptr(ag), k, 0, ptr(bg), k, 1, ptr(c), n, ptr(biasg), 2, ptr(aux), None, 0, stream())
     pre = a.double() @ b.double().T + bias.double()
     assert _rel(aux, pre) < 1e-5 and _rel(c, F.gelu(pre)) < 1e-5
     g = torch.randn(m, n)
@@ -313,7 +315,7 @@ def test_gemm_f32_epilogues(cuda):
     # epilogue 3: C = (A @ B) * gelu'(aux): use A = g, B = I
     eye = torch.eye(n)
     gg, eyeg = g.to(cuda), eye.to(cuda)
-    L.gemm_f32(m, n, n, ptr(gg), n, 0, ptr(eyeg), n, 0, ptr(c), n, None, 3, ptr(aux), stream())
+    L.gemm_f32(m, n, n, ptr(gg), n, 0, ptr(eyeg), n, 0, ptr(c), n, None, 3, ptr(aux), None, 0, stream())
     assert _rel(c, pre_t.grad) < 1e-5
     cs = torch.empty(n, device=cuda)
     L.colsum_f32(m, n, ptr(gg), n, ptr(cs), stream())
