@@ -41,6 +41,7 @@ SIGNATURES = {
     "argus_conv_fwd": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P, _P]),
     "argus_conv_fwd_stat_rows": (_I, [_DESC, _I]),
     "argus_conv_fwd_stat_tile": (_I, [_DESC, _I]),
+    "argus_conv_tuning": (_I, [_I, _I]),
     "argus_conv_launch_info": (_I, [_DESC, _I, _I, C.POINTER(C.c_int64)]),
     "argus_conv_dgrad": (_I, [_DESC, _I, _P, _P, _P, _I, _P]),
     "argus_conv_wgrad_workspace_bytes": (_SZ, [_DESC, _I]),
@@ -92,7 +93,7 @@ class _Lib:
 
     def __getattr__(self, name: str):
         fn = getattr(self.dll, "argus_" + name)
-        if fn.restype is _I and not name.endswith(("rows", "tile", "version", "info")):
+        if fn.restype is _I and not name.endswith(("rows", "tile", "version", "info", "tuning")):
             def call(*args, _fn=fn, _name=name):
                 rc = _fn(*args)
                 if rc != 0:

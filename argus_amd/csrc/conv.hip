@@ -106,7 +106,7 @@ template <typename T> struct ProCoef {
 template <typename T, int BN> constexpr int epi_ld() { return BN + 16 / (int)sizeof(T); }
 
 template <typename T, int BM, int BN, bool STEM, bool PRO>
-__global__ __launch_bounds__(256) void igemm_kernel(const IgParams p) {
+__global__ __launch_bounds__(256, 2) void igemm_kernel(const IgParams p) {
   constexpr int E = Chunk<T>::E;
   constexpr int BKE = 8 * E;  // K elements per k-step (8 chunks of 16 B per LDS row)
   constexpr int MI = BM / 32, NI = BN / 32;
@@ -129,8 +129,9 @@ __global__ __launch_bounds__(256) void igemm_kernel(const IgParams p) {
   const T* __restrict__ A = reinterpret_cast<const T*>(p.a);
   const T* __restrict__ B = reinterpret_cast<const T*>(p.b);
 
-  // per-thread A rows (output pixels) and B rows (output channels)
-  int a_n[AR], a_ih[AR], a_iw[AR];
+  // per-thread A rows (output pixels) and B rows (output channels); element offsets fit int32
+  // (checked on the host)
+  int a_off[AR], a_ih[AR], a_iw[AR];
   bool a_ok[AR];
   const int HWq = ph.Hq * ph.Wq;
 #pragma unroll
@@ -140,9 +141,9 @@ __global__ __launch_bounds__(256) void igemm_kernel(const IgParams p) {
     const int mm = a_ok[i] ? m : 0;
     const int nimg = mm / HWq, rem = mm - nimg * HWq;
     const int qh = rem / ph.Wq, qw = rem - qh * ph.Wq;
-    a_n[i] = nimg * p.H;
     a_ih[i] = qh * p.ish;
     a_iw[i] = qw * p.isw;
+    a_off[i] = ((nimg * p.H + a_ih[i]) * p.W + a_iw[i]) * p.lda;
   }
   const T* b_row[BR];
 #pragma unroll
@@ -155,11 +156,14 @@ __global__ __launch_bounds__(256) void igemm_kernel(const IgParams p) {
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  u32x4 ra[AR], rb[BR];
-  bool a_ok_k[AR];
-  int pro_ch = 0;
+  // one k-step of staged operands (two named copies form the 2-deep prefetch ring)
+  struct Stage {
+    u32x4 a[AR], b[BR];
+    bool ok[AR];
+    int ch;
+  };
 
-  auto load = [&](int kt) {
+  auto load = [&](int kt, Stage& S) {
     const int k0 = kt * BKE;
     if constexpr (STEM) {
       // K = (r, s(8), c(4)); a chunk is 2 pixels x 4 channels (bf16) or 1 pixel x 4 channels (fp32)
@@ -169,58 +173,58 @@ __global__ __launch_bounds__(256) void igemm_kernel(const IgParams p) {
       for (int i = 0; i < AR; ++i) {
         const int ih = a_ih[i] + r - 3;
         const bool rok = a_ok[i] && (unsigned)ih < (unsigned)p.H;
-        const T* rowp = A + ((size_t)a_n[i] + (rok ? ih : 0)) * p.W * 4;
+        const int rowoff = a_off[i] + ((r - 3) * p.W + s0 - 3) * 4;
         if constexpr (E == 8) {
           const int iw0 = a_iw[i] + s0 - 3, iw1 = iw0 + 1;
           const bool ok0 = rok && (unsigned)iw0 < (unsigned)p.W, ok1 = rok && (unsigned)iw1 < (unsigned)p.W;
-          const uint2 v0 = *reinterpret_cast<const uint2*>(rowp + (size_t)(ok0 ? iw0 : 0) * 4);
-          const uint2 v1 = *reinterpret_cast<const uint2*>(rowp + (size_t)(ok1 ? iw1 : 0) * 4);
-          ra[i] = u32x4{ok0 ? v0.x : 0u, ok0 ? v0.y : 0u, ok1 ? v1.x : 0u, ok1 ? v1.y : 0u};
+          const uint2 v0 = *reinterpret_cast<const uint2*>(A + (ok0 ? rowoff : 0));
+          const uint2 v1 = *reinterpret_cast<const uint2*>(A + (ok1 ? rowoff + 4 : 0));
+          S.a[i] = u32x4{ok0 ? v0.x : 0u, ok0 ? v0.y : 0u, ok1 ? v1.x : 0u, ok1 ? v1.y : 0u};
         } else {
           const int iw = a_iw[i] + s0 - 3;
           const bool ok = rok && (unsigned)iw < (unsigned)p.W;
-          ra[i] = sel(ok, ld16(rowp + (size_t)(ok ? iw : 0) * 4));
+          S.a[i] = sel(ok, ld16(A + (ok ? rowoff : 0)));
         }
       }
 #pragma unroll
-      for (int i = 0; i < BR; ++i) rb[i] = ld16(b_row[i] + k0);
+      for (int i = 0; i < BR; ++i) S.b[i] = ld16(b_row[i] + k0);
     } else {
       const int t = k0 / p.Cin;
       const int ci0 = k0 - t * p.Cin;
       const int dh = ph.dh[t], dw = ph.dw[t], boff = ph.boff[t];
       const int ch = ci0 + cidx * E;
+      const int tap = (dh * p.W + dw) * p.lda + ch;
 #pragma unroll
       for (int i = 0; i < AR; ++i) {
         const int ih = a_ih[i] + dh, iw = a_iw[i] + dw;
         const bool ok = a_ok[i] && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-        const size_t off = ok ? ((size_t)(a_n[i] + ih) * p.W + iw) * p.lda + ch : (size_t)ch;
-        ra[i] = ld16(A + off);
-        if constexpr (!PRO) ra[i] = sel(ok, ra[i]);
-        a_ok_k[i] = ok;
+        S.a[i] = ld16(A + (ok ? a_off[i] + tap : ch));
+        if constexpr (!PRO) S.a[i] = sel(ok, S.a[i]);
+        S.ok[i] = ok;
       }
 #pragma unroll
-      for (int i = 0; i < BR; ++i) rb[i] = ld16(b_row[i] + boff + ci0);
-      if constexpr (PRO) pro_ch = ch;
+      for (int i = 0; i < BR; ++i) S.b[i] = ld16(b_row[i] + boff + ci0);
+      S.ch = ch;
     }
   };
 
-  auto store = [&](int buf) {
+  auto store = [&](int buf, Stage& S) {
     u32x4* L = lds + buf * (BM + BN) * 8;
     if constexpr (PRO && !STEM) {
       ProCoef<T> pc;
-      pc.load(p.pro_scale, p.pro_shift, pro_ch);
+      pc.load(p.pro_scale, p.pro_shift, S.ch);
 #pragma unroll
-      for (int i = 0; i < AR; ++i) ra[i] = sel(a_ok_k[i], pc.apply(ra[i]));
+      for (int i = 0; i < AR; ++i) S.a[i] = sel(S.ok[i], pc.apply(S.a[i]));
     }
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
       const int row = (tid >> 3) + 32 * i;
-      L[row * 8 + (cidx ^ swz8(row))] = ra[i];
+      L[row * 8 + (cidx ^ swz8(row))] = S.a[i];
     }
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
       const int row = (tid >> 3) + 32 * i;
-      L[BM * 8 + row * 8 + (cidx ^ swz8(row))] = rb[i];
+      L[BM * 8 + row * 8 + (cidx ^ swz8(row))] = S.b[i];
     }
   };
 
@@ -247,16 +251,31 @@ __global__ __launch_bounds__(256) void igemm_kernel(const IgParams p) {
     }
   };
 
+  // Main loop: LDS double buffer + 2-deep register prefetch ring (S0/S1). At the MFMAs of step kt,
+  // the global loads of steps kt+1 and kt+2 are in flight.
   const int nk = ph.K / BKE;
   if (nk > 0) {
-    load(0);
-    store(0);
+    Stage S0, S1;
+    load(0, S0);
+    store(0, S0);
+    if (nk > 1) load(1, S1);
+    if (nk > 2) load(2, S0);
     __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-      const int cur = kt & 1;
-      if (kt + 1 < nk) load(kt + 1);
-      compute(cur);
-      if (kt + 1 < nk) store(cur ^ 1);
+    int kt = 0;
+    for (; kt + 1 < nk; kt += 2) {
+      compute(0);
+      store(1, S1);
+      if (kt + 3 < nk) load(kt + 3, S1);
+      __syncthreads();
+      compute(1);
+      if (kt + 2 < nk) {
+        store(0, S0);
+        if (kt + 4 < nk) load(kt + 4, S0);
+      }
+      __syncthreads();
+    }
+    if (kt < nk) {
+      compute(0);
       __syncthreads();
     }
   }
@@ -375,8 +394,8 @@ struct WgParams {
 // ds_read_b64_tr_b16 half-wave touches land on 8 distinct slots.
 ARGUS_DEV int swz32(int row) { return (row & 3) | (((row >> 3) & 1) << 2); }
 
-template <typename T, int BM, int BN, bool STEM, bool PRO>
-__global__ __launch_bounds__(256) void wgrad_kernel(const WgParams p) {
+template <typename T, int BM, int BN, bool STEM, bool PRO, bool FAST>
+__global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgParams p) {
   constexpr int E = Chunk<T>::E;
   constexpr bool BF = (E == 8);
   constexpr int BKP = BF ? 64 : 32;               // pixels per k-step
@@ -416,7 +435,14 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgParams p) {
     tap_r = t / p.S; tap_s = t - tap_r * p.S;
   }
   const int HWo = p.Ho * p.Wo;
-  const u32x4 zero = {0u, 0u, 0u, 0u};
+  const int ldrow = p.W * p.lda;  // elements per input row
+  // FAST: per-thread (row, col) offsets of its B rows inside a k-step
+  int dr[PB], dc[PB];
+#pragma unroll
+  for (int i = 0; i < PB; ++i) {
+    const int r = rb0 + RPB * i;
+    if (p.Wo >= BKP) { dr[i] = 0; dc[i] = r; } else { dr[i] = r / p.Wo; dc[i] = r - dr[i] * p.Wo; }
+  }
 
   f32x4 acc[MI][NI];
 #pragma unroll
@@ -426,58 +452,76 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgParams p) {
 
   ProCoef<T> pc;
   if constexpr (PRO) pc.load(p.pro_scale, p.pro_shift, ci);
-  u32x4 ra[PA], rb[PB];
-  auto load = [&](int p0) {
+
+  struct Stage {
+    u32x4 a[PA], b[PB];
+  };
+
+  auto load = [&](int p0, Stage& S) {
 #pragma unroll
     for (int i = 0; i < PA; ++i) {
       const int pix = p0 + ra0 + RPA * i;
       const bool ok = pix < pend;
-      ra[i] = sel(ok, ld16(a_col + (size_t)(ok ? pix : pbeg) * p.M));
+      S.a[i] = sel(ok, ld16(a_col + (size_t)(ok ? pix : pbeg) * p.M));
+    }
+    int n0 = 0, oh0 = 0, ow0 = 0;
+    if constexpr (FAST) {  // uniform: the k-step lies inside one image
+      n0 = p0 / HWo;
+      const int rem0 = p0 - n0 * HWo;
+      oh0 = rem0 / p.Wo;
+      ow0 = rem0 - oh0 * p.Wo;
     }
 #pragma unroll
     for (int i = 0; i < PB; ++i) {
       const int pix = p0 + rb0 + RPB * i;
       const bool pok = pix < pend;
-      const int pp = pok ? pix : pbeg;
-      const int nimg = pp / HWo, rem = pp - nimg * HWo;
-      const int oh = rem / p.Wo, ow = rem - oh * p.Wo;
+      int nimg, oh, ow;
+      if constexpr (FAST) {
+        nimg = n0; oh = oh0 + dr[i]; ow = ow0 + dc[i];
+      } else {
+        const int pp = pok ? pix : pbeg;
+        nimg = pp / HWo;
+        const int rem = pp - nimg * HWo;
+        oh = rem / p.Wo;
+        ow = rem - oh * p.Wo;
+      }
       const int ih = oh * p.stride - p.pad + tap_r;
       const int iw0 = ow * p.stride - p.pad + tap_s;
       const bool hok = pok && (unsigned)ih < (unsigned)p.H;
-      const T* rowp = X + ((size_t)nimg * p.H + (hok ? ih : 0)) * p.W * p.lda;
+      const int rowoff = (nimg * p.H + ih) * ldrow;
       if constexpr (STEM) {
         if constexpr (BF) {
           const int iw1 = iw0 + 1;
           const bool ok0 = hok && (unsigned)iw0 < (unsigned)p.W, ok1 = hok && (unsigned)iw1 < (unsigned)p.W;
-          const uint2 v0 = *reinterpret_cast<const uint2*>(rowp + (size_t)(ok0 ? iw0 : 0) * 4);
-          const uint2 v1 = *reinterpret_cast<const uint2*>(rowp + (size_t)(ok1 ? iw1 : 0) * 4);
-          rb[i] = u32x4{ok0 ? v0.x : 0u, ok0 ? v0.y : 0u, ok1 ? v1.x : 0u, ok1 ? v1.y : 0u};
+          const uint2 v0 = *reinterpret_cast<const uint2*>(X + (ok0 ? rowoff + iw0 * 4 : 0));
+          const uint2 v1 = *reinterpret_cast<const uint2*>(X + (ok1 ? rowoff + iw1 * 4 : 0));
+          S.b[i] = u32x4{ok0 ? v0.x : 0u, ok0 ? v0.y : 0u, ok1 ? v1.x : 0u, ok1 ? v1.y : 0u};
         } else {
           const bool ok = hok && (unsigned)iw0 < (unsigned)p.W;
-          rb[i] = sel(ok, ld16(rowp + (size_t)(ok ? iw0 : 0) * 4));
+          S.b[i] = sel(ok, ld16(X + (ok ? rowoff + iw0 * 4 : 0)));
         }
       } else {
         const bool ok = hok && (unsigned)iw0 < (unsigned)p.W;
-        u32x4 v = ld16(rowp + (size_t)(ok ? iw0 : 0) * p.lda + ci);
+        u32x4 v = ld16(X + (ok ? rowoff + iw0 * p.lda + ci : 0));
         if constexpr (PRO) v = pc.apply(v);
-        rb[i] = sel(ok, v);
+        S.b[i] = sel(ok, v);
       }
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&](int buf, const Stage& S) {
 #pragma unroll
     for (int i = 0; i < PA; ++i) {
       const int row = ra0 + RPA * i;
       int c = ca;
       if constexpr (BF) c = (((ca >> 1) ^ swz32(row)) << 1) | (ca & 1);
-      lds[buf][row * RSA + c] = ra[i];
+      lds[buf][row * RSA + c] = S.a[i];
     }
 #pragma unroll
     for (int i = 0; i < PB; ++i) {
       const int row = rb0 + RPB * i;
       int c = cb;
       if constexpr (BF) c = (((cb >> 1) ^ swz32(row)) << 1) | (cb & 1);
-      lds[buf][BKP * RSA + row * RSB + c] = rb[i];
+      lds[buf][BKP * RSA + row * RSB + c] = S.b[i];
     }
   };
 
@@ -544,18 +588,43 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgParams p) {
     }
   };
 
+  // LDS double buffer + 2-deep register prefetch ring (as igemm_kernel); the 128x128 tile keeps a
+  // single staged k-step (the ring would not fit two waves per SIMD without spilling)
+  constexpr bool RING = !(BM == 128 && BN == 128);
   const int nk = pend > pbeg ? (pend - pbeg + BKP - 1) / BKP : 0;
-  if (nk > 0) {
-    load(pbeg);
-    store(0);
+  if (!RING && nk > 0) {
+    Stage S0;
+    load(pbeg, S0);
+    store(0, S0);
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
       const int cur = kt & 1;
-      if (kt + 1 < nk) load(pbeg + (kt + 1) * BKP);
+      if (kt + 1 < nk) load(pbeg + (kt + 1) * BKP, S0);
       compute(cur);
-      if (kt + 1 < nk) store(cur ^ 1);
+      if (kt + 1 < nk) store(cur ^ 1, S0);
       __syncthreads();
     }
+  } else if (nk > 0) {
+    Stage S0, S1;
+    load(pbeg, S0);
+    store(0, S0);
+    if (nk > 1) load(pbeg + BKP, S1);
+    if (nk > 2) load(pbeg + 2 * BKP, S0);
+    __syncthreads();
+    int kt = 0;
+    for (; kt + 1 < nk; kt += 2) {
+      compute(0);
+      store(1, S1);
+      if (kt + 3 < nk) load(pbeg + (kt + 3) * BKP, S1);
+      __syncthreads();
+      compute(1);
+      if (kt + 2 < nk) {
+        store(0, S0);
+        if (kt + 4 < nk) load(pbeg + (kt + 4) * BKP, S0);
+      }
+      __syncthreads();
+    }
+    if (kt < nk) compute(0);
   }
 
   float* out = p.part + (size_t)split * p.M * p.N;
@@ -675,6 +744,10 @@ static int check_desc(const argus_conv_desc& d) {
     set_error("conv: channels must be multiples of 64, filters <= 3x3, stride <= 2");
     return ARGUS_ERR_SHAPE;
   }
+  if ((int64_t)d.n * d.h * d.w * (d.stem ? 4 : d.c) >= (1LL << 31) || (int64_t)d.n * d.ho * d.wo * d.k >= (1LL << 31)) {
+    set_error("conv: tensor too large for 32-bit element offsets (split the batch)");
+    return ARGUS_ERR_SHAPE;
+  }
   return ARGUS_OK;
 }
 
@@ -686,8 +759,8 @@ static void launch_ig(const IgParams& p, int maxM, hipStream_t st) {
 }
 
 template <typename T, bool PRO>
-static void dispatch_ig(const IgParams& p, int maxM, int bm, hipStream_t st) {
-  const bool bn128 = (p.N % 128) == 0;
+static void dispatch_ig(const IgParams& p, int maxM, int bm, int bn, hipStream_t st) {
+  const bool bn128 = bn == 128;
   if (bm == 128) {
     if (bn128) launch_ig<T, 128, 128, false, PRO>(p, maxM, st);
     else launch_ig<T, 128, 64, false, PRO>(p, maxM, st);
@@ -698,25 +771,44 @@ static void dispatch_ig(const IgParams& p, int maxM, int bm, hipStream_t st) {
 }
 
 template <typename T>
-static int run_ig(const IgParams& p, hipStream_t st, int bm) {
+static int run_ig(const IgParams& p, hipStream_t st, int bm, int bn) {
   int maxM = 0;
   for (int i = 0; i < p.nphase; ++i) maxM = p.ph[i].M > maxM ? p.ph[i].M : maxM;
   if (p.stem) {
     if (p.N != 64 || bm != 128) { set_error("igemm: stem expects 64 output channels"); return ARGUS_ERR_SHAPE; }
     launch_ig<T, 128, 64, true, false>(p, maxM, st);
   } else if (p.pro_scale) {
-    dispatch_ig<T, true>(p, maxM, bm, st);
+    dispatch_ig<T, true>(p, maxM, bm, bn, st);
   } else {
-    dispatch_ig<T, false>(p, maxM, bm, st);
+    dispatch_ig<T, false>(p, maxM, bm, bn, st);
   }
   return check_launch("igemm_kernel");
+}
+
+// Tile policy (argus_conv_tuning): per pass {0 fwd, 1 dgrad, 2 wgrad}, forced tile_m / tile_n
+// (0 = heuristic) and the wgrad split target.
+static int g_force_bm[3] = {0, 0, 0}, g_force_bn[3] = {0, 0, 0};
+static int g_wgrad_target_blocks = 512;
+
+int conv_tuning(int key, int value) {
+  if (key >= 0 && key < 3) { g_force_bm[key] = value; return 0; }
+  if (key >= 3 && key < 6) { g_force_bn[key - 3] = value; return 0; }
+  if (key == 6) { g_wgrad_target_blocks = value; return 0; }
+  return -1;
+}
+
+static int pick_bn(int pass, int n) {
+  const int f = g_force_bn[pass];
+  if (f == 64 || (f == 128 && n % 128 == 0)) return f;
+  return n % 128 == 0 ? 128 : 64;
 }
 
 // row-tile size of the forward GEMM (drives the BN-statistics partial count)
 static int fwd_bm(const argus_conv_desc& d) {
   if (d.stem) return 128;
+  if (g_force_bm[0]) return g_force_bm[0];
   const long M = (long)d.n * d.ho * d.wo;
-  return M >= 64L * 1024 ? 128 : 64;
+  return M >= 16L * 1024 ? 128 : 64;
 }
 
 int conv_fwd_stat_rows(const argus_conv_desc& d, int) {
@@ -726,8 +818,9 @@ int conv_fwd_stat_rows(const argus_conv_desc& d, int) {
 int conv_fwd_stat_tile(const argus_conv_desc& d, int) { return fwd_bm(d); }
 
 static int dgrad_bm(const argus_conv_desc& d) {
+  if (g_force_bm[1]) return g_force_bm[1];
   const long M = (long)d.n * d.h * d.w / (d.stride * d.stride);
-  return M >= 64L * 1024 ? 128 : 64;
+  return M >= 16L * 1024 ? 128 : 64;
 }
 
 int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, void* y,
@@ -753,8 +846,8 @@ int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, 
         ph.dh[t] = r - d.pad; ph.dw[t] = s - d.pad; ph.boff[t] = t * d.c;
       }
   }
-  const int bm = fwd_bm(d);
-  return dtype == ARGUS_BF16 ? run_ig<bf16>(p, st, bm) : run_ig<float>(p, st, bm);
+  const int bm = fwd_bm(d), bn = d.stem ? 64 : pick_bn(0, d.k);
+  return dtype == ARGUS_BF16 ? run_ig<bf16>(p, st, bm, bn) : run_ig<float>(p, st, bm, bn);
 }
 
 int conv_dgrad(const argus_conv_desc& d, int dtype, const void* dy, const void* wt, void* dx,
@@ -788,8 +881,8 @@ int conv_dgrad(const argus_conv_desc& d, int dtype, const void* dy, const void* 
       ph.K = t * d.k;
     }
   p.nphase = np;
-  const int bm = dgrad_bm(d);
-  return dtype == ARGUS_BF16 ? run_ig<bf16>(p, st, bm) : run_ig<float>(p, st, bm);
+  const int bm = dgrad_bm(d), bn = pick_bn(1, d.c);
+  return dtype == ARGUS_BF16 ? run_ig<bf16>(p, st, bm, bn) : run_ig<float>(p, st, bm, bn);
 }
 
 struct WgPlan {
@@ -800,14 +893,19 @@ struct WgPlan {
 static WgPlan wgrad_plan(const argus_conv_desc& d, int dtype) {
   WgPlan pl;
   pl.N = d.stem ? 256 : d.r * d.s * d.c;
-  pl.bm = d.k % 128 == 0 ? 128 : 64;
-  pl.bn = pl.N % 128 == 0 ? 128 : 64;
+  pl.bm = (g_force_bm[2] == 64 || d.k % 128) ? 64 : 128;
+  pl.bn = pick_bn(2, pl.N);
+  if (d.stem) { pl.bm = 64; pl.bn = 128; }
   pl.mt = d.k / pl.bm;
   pl.nt = pl.N / pl.bn;
   pl.kstep = dtype == ARGUS_BF16 ? 64 : 32;
   const long P = (long)d.n * d.ho * d.wo;
   const long tiles = (long)pl.mt * pl.nt;
-  long splits = (512 + tiles - 1) / tiles;
+  // measured (tools/tilesweep.py, MI355X): 1x1 convs peak near 512 workgroups, 3x3 near 1024
+  // (2048 when Cout = 64: one row tile, 9 column tiles)
+  long target = g_wgrad_target_blocks;
+  if (target == 512 && d.r == 3) target = d.k <= 64 ? 2048 : 1024;
+  long splits = (target + tiles - 1) / tiles;
   const long max_splits = (P + pl.kstep * 4 - 1) / (pl.kstep * 4);  // >= 4 k-steps per split
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
@@ -825,25 +923,35 @@ size_t conv_wgrad_ws(const argus_conv_desc& d, int dtype) {
   return (size_t)pl.splits * d.k * pl.N * sizeof(float);
 }
 
-template <typename T, int BM, int BN, bool STEM, bool PRO>
+template <typename T, int BM, int BN, bool STEM, bool PRO, bool FAST>
 static void launch_wg(const WgParams& p, const WgPlan& pl, hipStream_t st) {
   dim3 grid(pl.mt * pl.nt, pl.splits);
-  hipLaunchKernelGGL((wgrad_kernel<T, BM, BN, STEM, PRO>), grid, dim3(256), 0, st, p);
+  hipLaunchKernelGGL((wgrad_kernel<T, BM, BN, STEM, PRO, FAST>), grid, dim3(256), 0, st, p);
 }
 
-template <typename T, bool PRO>
+template <typename T, bool PRO, bool FAST>
 static void dispatch_wg_tiles(const WgParams& p, const WgPlan& pl, hipStream_t st) {
-  if (pl.bm == 128 && pl.bn == 128) launch_wg<T, 128, 128, false, PRO>(p, pl, st);
-  else if (pl.bm == 128) launch_wg<T, 128, 64, false, PRO>(p, pl, st);
-  else if (pl.bn == 128) launch_wg<T, 64, 128, false, PRO>(p, pl, st);
-  else launch_wg<T, 64, 64, false, PRO>(p, pl, st);
+  if (pl.bm == 128 && pl.bn == 128) launch_wg<T, 128, 128, false, PRO, FAST>(p, pl, st);
+  else if (pl.bm == 128) launch_wg<T, 128, 64, false, PRO, FAST>(p, pl, st);
+  else if (pl.bn == 128) launch_wg<T, 64, 128, false, PRO, FAST>(p, pl, st);
+  else launch_wg<T, 64, 64, false, PRO, FAST>(p, pl, st);
 }
 
 template <typename T>
 static void dispatch_wg(const WgParams& p, const WgPlan& pl, hipStream_t st) {
-  if (p.stem) launch_wg<T, 64, 128, true, false>(p, pl, st);  // stem: M = 64 channels, N = 256
-  else if (p.pro_scale) dispatch_wg_tiles<T, true>(p, pl, st);
-  else dispatch_wg_tiles<T, false>(p, pl, st);
+  // FAST pixel indexing: every k-step lies in one image and rows tile the k-step evenly
+  const int bkp = pl.kstep;
+  const bool fast = (p.Ho * p.Wo) % bkp == 0 && (p.Wo % bkp == 0 || bkp % p.Wo == 0);
+  if (p.stem) {
+    if (fast) launch_wg<T, 64, 128, true, false, true>(p, pl, st);  // stem: M = 64 channels, N = 256
+    else launch_wg<T, 64, 128, true, false, false>(p, pl, st);
+  } else if (p.pro_scale) {
+    if (fast) dispatch_wg_tiles<T, true, true>(p, pl, st);
+    else dispatch_wg_tiles<T, true, false>(p, pl, st);
+  } else {
+    if (fast) dispatch_wg_tiles<T, false, true>(p, pl, st);
+    else dispatch_wg_tiles<T, false, false>(p, pl, st);
+  }
 }
 
 int conv_wgrad(const argus_conv_desc& d, int dtype, const void* x, const float* sc, const float* sh,
@@ -876,8 +984,8 @@ int conv_launch_info(const argus_conv_desc& d, int dtype, int pass, int64_t* flo
   if (check_desc(d)) return -1;
   if (flops) *flops = 2LL * d.n * d.ho * d.wo * d.k * d.r * d.s * d.c;
   const int dtag = dtype == ARGUS_BF16 ? 1 : 0;
-  if (pass == 0) return 10000000 + dtag * 1000000 + fwd_bm(d) * 1000 + (d.k % 128 == 0 ? 128 : 64);
-  if (pass == 1) return 10000000 + dtag * 1000000 + dgrad_bm(d) * 1000 + (d.c % 128 == 0 ? 128 : 64);
+  if (pass == 0) return 10000000 + dtag * 1000000 + fwd_bm(d) * 1000 + (d.stem ? 64 : pick_bn(0, d.k));
+  if (pass == 1) return 10000000 + dtag * 1000000 + dgrad_bm(d) * 1000 + pick_bn(1, d.c);
   const WgPlan pl = wgrad_plan(d, dtype);
   return 20000000 + dtag * 1000000 + pl.bm * 1000 + pl.bn;
 }

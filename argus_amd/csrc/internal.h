@@ -16,6 +16,7 @@ int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, 
              const float* sc, const float* sh, float* stats, hipStream_t st);
 int conv_fwd_stat_rows(const argus_conv_desc& d, int dtype);
 int conv_fwd_stat_tile(const argus_conv_desc& d, int dtype);
+int conv_tuning(int key, int value);
 int conv_launch_info(const argus_conv_desc& d, int dtype, int pass, int64_t* flops);
 int conv_dgrad(const argus_conv_desc& d, int dtype, const void* dy, const void* wt, void* dx,
                int accumulate, hipStream_t st);

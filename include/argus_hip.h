@@ -71,6 +71,10 @@ int argus_conv_fwd_stat_tile(const argus_conv_desc* d, int dtype);
 /* dx (+)= dgrad(dy, w_dgrad); accumulate != 0 adds into dx. */
 int argus_conv_dgrad(const argus_conv_desc* d, int dtype, const void* dy, const void* w_dgrad,
                      void* dx, int accumulate, argus_stream_t stream);
+/* Tuning knobs (process-wide; for autotuning / experiments): key 0..2 force the row tile (64|128,
+ * 0 = heuristic) of pass fwd/dgrad/wgrad, key 3..5 force the column tile, key 6 sets the wgrad
+ * split target (workgroups). Returns 0, or -1 for an unknown key. */
+int argus_conv_tuning(int key, int value);
 /* Which kernel instantiation a pass launches and its algorithmic work: pass 0 fwd, 1 dgrad,
  * 2 wgrad. Returns a tag (kind*10^7 + dtype*10^6 + tile_m*1000 + tile_n; kind 1 igemm,
  * 2 wgrad) and writes 2*P*K*R*S*C flops (P = n*ho*wo output pixels). Used to time exactly the
