@@ -105,6 +105,7 @@ def main() -> None:
     ref = ref_models.NCameraCNN(ref_models.NCameraCNNConfig(n_cams=2))
     orc = oracle_ncamera.build_reference_model(42)
     sd_r, sd_o = ref.state_dict(), orc.state_dict()
+    init_sha = state_sha256(sd_r)  # before any train-mode forward mutates the running stats
     assert list(sd_r.keys()) == list(sd_o.keys()), "state_dict keys differ"
     for k in sd_r:
         assert sd_r[k].shape == sd_o[k].shape and torch.equal(sd_r[k], sd_o[k]), k
@@ -127,7 +128,7 @@ def main() -> None:
         "seed": 42,
         "n_params": sum(v.numel() for k, v in sd_r.items() if not k.endswith(("running_mean", "running_var", "num_batches_tracked"))),
         "state_dict": [[k, list(v.shape), str(v.dtype).replace("torch.", "")] for k, v in sd_r.items()],
-        "state_sha256": state_sha256(sd_r),
+        "state_sha256": init_sha,
         "inputs": {"images": "synthetic_images(2,256,256,seed=1234)", "targets": "synthetic_targets(2,seed=2000)",
                    "images_sum": float(x.double().sum()), "targets": T.tolist()},
     }

@@ -1,0 +1,64 @@
+"""CPU: libargus_hip.so loads, reports its ABI, exports exactly what include/argus_hip.h declares,
+and rejects bad arguments through the error channel (no compute call needs a GPU here)."""
+import ctypes as C
+import re
+import subprocess
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def declared():
+    txt = (ROOT / "include" / "argus_hip.h").read_text()
+    return sorted(set(re.findall(r"^(?:int|size_t|const char\*)\s+(argus_[a-z0-9_]+)\(", txt, re.M)))
+
+
+def test_header_declares_and_library_exports_the_same_symbols():
+    from argus_amd._lib import LIB_PATH, SIGNATURES
+
+    assert declared() == sorted(SIGNATURES)
+    out = subprocess.run(["nm", "-D", "--defined-only", str(LIB_PATH)], capture_output=True, text=True).stdout
+    exported = sorted(set(re.findall(r" T (argus_[a-z0-9_]+)$", out, re.M)))
+    assert exported == declared()
+
+
+def test_library_loads_and_version():
+    from argus_amd._lib import ABI_VERSION, lib
+
+    L = lib()
+    assert L.dll.argus_abi_version() == ABI_VERSION
+
+
+def test_bad_arguments_are_reported():
+    from argus_amd._lib import ArgusHipError, ConvDesc, lib
+
+    L = lib()
+    d = ConvDesc(2, 8, 8, 48, 64, 3, 3, 1, 1, 8, 8, 0)  # 48 channels: unsupported
+    rc = L.dll.argus_conv_fwd(C.byref(d), 1, C.c_void_p(16), C.c_void_p(16), C.c_void_p(16), None, None, None, None)
+    assert rc != 0 and b"multiples of 64" in L.dll.argus_last_error()
+    bad = ConvDesc(2, 8, 8, 64, 64, 3, 3, 1, 1, 7, 8, 0)  # wrong ho
+    with pytest.raises(ArgusHipError, match="ho/wo"):
+        L.conv_fwd(C.byref(bad), 1, 16, 16, 16, None, None, None, None)
+    assert L.dll.argus_conv_tuning(99, 1) == -1
+    fl = C.c_int64(0)
+    good = ConvDesc(2, 8, 8, 64, 128, 3, 3, 2, 1, 4, 4, 0)
+    tag = L.dll.argus_conv_launch_info(C.byref(good), 1, 0, C.byref(fl))
+    assert fl.value == 2 * 2 * 4 * 4 * 128 * 9 * 64 and tag // 10000000 == 1
+    assert L.dll.argus_conv_wgrad_workspace_bytes(C.byref(good), 1) > 0
+
+
+def test_product_path_has_no_cpu_fallback():
+    import torch
+
+    from argus_amd.losses import geometric_loss_fn
+    from argus_amd.models import NCameraCNN
+
+    m = NCameraCNN()
+    with pytest.raises(RuntimeError, match="HIP"):
+        m(torch.rand(1, 6, 32, 32))
+    with pytest.raises(AssertionError):
+        m(torch.rand(6, 32, 32))
+    with pytest.raises(RuntimeError, match="HIP"):
+        geometric_loss_fn(torch.zeros(2, 6), torch.zeros(2, 7))

@@ -1,0 +1,108 @@
+"""GPU: the fused train step against the reference's own step (golden fixture from argus/train.py's
+loop body run on the oracle-backed reference model), and the drop-in train() loop end to end
+(reference tests/test_train.py:39-77: runs, saves a .pth, is seed-reproducible)."""
+import math
+from pathlib import Path
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _golden_inputs():
+    import tests.golden.make_golden as mg
+
+    return mg.synthetic_images(2, 256, 256, seed=1234), mg.synthetic_targets(2, seed=2000)
+
+
+def test_fused_step_matches_reference_step(cuda, golden):
+    from argus_amd.models import NCameraCNN
+    from argus_amd.step import FusedTrainer
+
+    x, T = _golden_inputs()
+    torch.manual_seed(42)
+    m = NCameraCNN().to(cuda)
+    tr = FusedTrainer(m, lr=1e-4, max_grad_norm=1.0)
+    losses = tr.step(x.to(cuda), T.to(cuda))
+    gs = golden["step"]
+    assert torch.allclose(losses.cpu(), torch.tensor(gs["loss"]), atol=1e-4)
+    # the batch-2 train-mode gradient is ill-conditioned (reference fp32 vs fp64: up to 17.5 % per tensor,
+    # DESIGN.md §Parity); its global norm is far better conditioned
+    gn = float(tr.grad_norm())
+    assert abs(gn - gs["grad_norm"]) / gs["grad_norm"] < 0.05, (gn, gs["grad_norm"])
+    sd = m.state_dict()
+    assert int(sd["resnet.bn1.num_batches_tracked"]) == gs["num_batches_tracked"] == 1
+    for k, (s, a) in gs["bn_running_sums"].items():
+        v = sd[k].double().cpu()
+        assert abs(v.sum().item() - s) <= 1e-4 * a + 1e-5, k
+    # one Adam step moves every element by ~lr*sign(g): allow a few % sign flips on near-zero gradients
+    for k, (s, a) in gs["param_sums"].items():
+        v = sd[k].double().cpu()
+        tol = 0.1 * 1e-4 * v.numel() + 1e-4
+        assert abs(v.sum().item() - s) <= tol and abs(v.abs().sum().item() - a) <= tol, k
+    with torch.no_grad():
+        m.train()
+        after = m(x.to(cuda)).cpu()
+    assert torch.allclose(after, torch.tensor(gs["pred_after_step_train"]), atol=2e-3)
+
+
+def test_train_loop_end_to_end_and_reproducible(cuda, dummy_data_path, tmp_path):
+    from argus_amd.data import CameraCubePoseDatasetConfig
+    from argus_amd.models import NCameraCNN, NCameraCNNConfig
+    from argus_amd.train import TrainConfig, train
+
+    save = tmp_path / "ckpt"
+    cfg = TrainConfig(batch_size=10, learning_rate=1e-3, n_epochs=1, device="cuda", max_grad_norm=100.0,
+                      random_seed=42, val_epochs=1, print_epochs=1, save_epochs=1, save_dir=str(save),
+                      model_config=NCameraCNNConfig(n_cams=2),
+                      dataset_config=CameraCubePoseDatasetConfig(dataset_path=dummy_data_path),
+                      compile_model=False, wandb_log=False)
+    train(cfg)
+    pths = list(save.glob("*.pth"))
+    assert len(pths) == 1
+    sd1 = torch.load(pths[0], weights_only=True)
+    model = NCameraCNN().to(cuda).eval()
+    model.load_state_dict(sd1)
+    with torch.no_grad():
+        out1 = model(torch.ones(1, 6, 256, 256, device=cuda))
+    assert torch.isfinite(out1).all()
+    assert int(sd1["resnet.bn1.num_batches_tracked"]) == 1
+    for p in pths:
+        p.unlink()
+    train(cfg)
+    sd2 = torch.load(next(save.glob("*.pth")), weights_only=True)
+    assert all(torch.equal(sd1[k], sd2[k]) for k in sd1)  # deterministic kernels: bit-identical reruns
+    model.load_state_dict(sd2)
+    with torch.no_grad():
+        out2 = model(torch.ones(1, 6, 256, 256, device=cuda))
+    assert torch.equal(out1, out2)
+
+
+def test_loss_fn_api(cuda):
+    """reference tests/test_train.py:18-36 on the HIP loss."""
+    from argus_amd.losses import geometric_loss_fn
+    from argus_amd.utils import se3_exp
+    from oracle import se3
+
+    pred = torch.randn(6, device=cuda)
+    assert geometric_loss_fn(pred, se3.random_targets(1)[0].to(cuda)).shape == torch.Size([])
+    pred = torch.randn(32, 6, device=cuda)
+    targ = se3.random_targets(32).to(cuda)
+    assert geometric_loss_fn(pred, targ).shape == torch.Size([32])
+    assert torch.allclose(geometric_loss_fn(pred, se3_exp(pred)), torch.zeros(32, device=cuda), atol=1e-5)
+
+
+def test_get_pose(cuda):
+    from argus_amd.models import NCameraCNN
+    from argus_amd.utils import get_pose
+    from oracle import se3
+
+    m = NCameraCNN().to(cuda).eval()
+    for b in (1, 3):
+        x = torch.rand(b, 6, 128, 128, device=cuda)
+        with torch.no_grad():
+            pose = get_pose(x, m)
+            want = se3.se3_exp(m(x).cpu().double())  # pp.se3(xi).Exp(), utils.py:179-189
+        assert pose.shape == (b, 7)
+        assert torch.allclose(pose.cpu().double(), want, atol=1e-5)

@@ -1,0 +1,66 @@
+"""CPU: host-side logic — product model init/state_dict vs the golden schema, the train CLI, the
+LR plateau scheduler, the flat parameter layout."""
+import torch
+
+from argus_amd.models import NCameraCNN, NCameraCNNConfig
+
+
+def test_model_state_dict_and_seeded_init_match_reference(golden):
+    from oracle.ncamera import build_reference_model
+
+    torch.manual_seed(42)
+    m = NCameraCNN()
+    sd = m.state_dict()
+    assert [[k, list(v.shape), str(v.dtype).replace("torch.", "")] for k, v in sd.items()] == golden["state_dict"]
+    ref = build_reference_model(42).state_dict()
+    assert all(torch.equal(sd[k], ref[k]) for k in sd)
+    assert NCameraCNN(NCameraCNNConfig(n_cams=3)).output_mlp[0].in_features == 3 * 1024
+
+
+def test_flat_params_keep_reference_views():
+    from argus_amd.step import FlatParams
+
+    torch.manual_seed(0)
+    m = NCameraCNN()
+    before = {k: v.clone() for k, v in m.state_dict().items()}
+    fp = FlatParams(m)
+    after = m.state_dict()
+    assert all(torch.equal(before[k], after[k]) for k in before)
+    w = m.resnet.layer1[0].conv2.weight
+    assert w.shape == (64, 64, 3, 3) and w.data_ptr() >= fp.param.data_ptr()
+    assert fp.G["resnet.layer1.0.conv2.weight"].shape == (64, 3, 3, 64)  # OHWI gradient slot
+    assert all(o % FlatParams.ALIGN == 0 for o in fp.offset.values())
+    m.load_state_dict(before)  # loading into the channels-last views works
+    assert torch.equal(m.resnet.layer1[0].conv2.weight, before["resnet.layer1.0.conv2.weight"])
+
+
+def test_plateau_scheduler_matches_torch():
+    from argus_amd.train import PlateauScheduler
+
+    class T:
+        lr = 1e-4
+
+    t = T()
+    ours = PlateauScheduler(t, patience=5, factor=0.5)
+    p = torch.nn.Parameter(torch.zeros(1))
+    opt = torch.optim.SGD([p], lr=1e-4)
+    ref = torch.optim.lr_scheduler.ReduceLROnPlateau(opt, "min", patience=5, factor=0.5)
+    vals = [1.0, 0.9, 0.95, 0.95, 0.95, 0.95, 0.95, 0.95, 0.95, 0.8, 0.8] + [0.8] * 14
+    for v in vals:
+        ours.step(v)
+        ref.step(v)
+        assert abs(t.lr - opt.param_groups[0]["lr"]) < 1e-15
+
+
+def test_cli_flag_names(tmp_path):
+    from argus_amd.train import parse_args
+
+    d = tmp_path / "ds"
+    (d / "img").mkdir(parents=True)
+    (d / "ds.hdf5").write_bytes(b"")
+    cfg = parse_args(["--dataset-config.dataset-path", str(d), "--batch-size", "10", "--learning-rate", "1e-3",
+                      "--n-epochs", "1", "--amp", "--no-wandb-log", "--model-config.n-cams", "2",
+                      "--dataset-config.center-crop", "128", "128", "--save-dir", str(tmp_path / "out")])
+    assert cfg.batch_size == 10 and cfg.learning_rate == 1e-3 and cfg.amp and not cfg.wandb_log
+    assert cfg.dataset_config.center_crop == (128, 128) and cfg.model_config.n_cams == 2
+    assert cfg.max_grad_norm == 1.0 and cfg.random_seed == 42 and not cfg.multigpu
