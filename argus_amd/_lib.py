@@ -46,6 +46,11 @@ SIGNATURES = {
     "argus_conv_dgrad": (_I, [_DESC, _I, _P, _P, _P, _I, _P]),
     "argus_conv_wgrad_workspace_bytes": (_SZ, [_DESC, _I]),
     "argus_conv_wgrad": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P, _SZ, _P]),
+    "argus_ktimer_enable": (_I, [C.c_char_p]),
+    "argus_ktimer_disable": (_I, []),
+    "argus_ktimer_count": (_I, []),
+    "argus_ktimer_get": (_I, [_I, C.c_char_p, _I, C.POINTER(C.c_int64), C.POINTER(C.c_double),
+                              C.POINTER(C.c_double)]),
     "argus_bn_workspace_bytes": (_SZ, [_I]),
     "argus_bn_finalize": (_I, [_I, _I, _I, _P, _I64, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "argus_bn_eval_coeffs": (_I, [_I, _P, _P, _P, _P, _F, _P, _P, _P]),
@@ -93,7 +98,7 @@ class _Lib:
 
     def __getattr__(self, name: str):
         fn = getattr(self.dll, "argus_" + name)
-        if fn.restype is _I and not name.endswith(("rows", "tile", "version", "info", "tuning")):
+        if fn.restype is _I and not name.endswith(("rows", "tile", "version", "info", "tuning", "count")):
             def call(*args, _fn=fn, _name=name):
                 rc = _fn(*args)
                 if rc != 0:

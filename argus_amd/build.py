@@ -18,7 +18,7 @@ CSRC = HERE / "csrc"
 OUT = HERE / "libargus_hip.so"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
-SOURCES = ["capi.cpp", "conv.hip", "bn.hip", "head.hip", "loss.hip", "optim.hip"]
+SOURCES = ["capi.cpp", "ktimer.cpp", "conv.hip", "bn.hip", "head.hip", "loss.hip", "optim.hip"]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
          "-Wno-unused-variable", "-Wno-unused-but-set-variable"]
 
@@ -27,7 +27,7 @@ def _compile(src: str, verbose: bool) -> Path:
     obj = CSRC / ".build" / (src + ".o")
     obj.parent.mkdir(exist_ok=True)
     srcp = CSRC / src
-    deps = [srcp, CSRC / "common.h", CSRC / "internal.h", HERE.parent / "include" / "argus_hip.h"]
+    deps = [srcp, *CSRC.glob("*.h"), HERE.parent / "include" / "argus_hip.h"]
     if obj.exists() and obj.stat().st_mtime > max(d.stat().st_mtime for d in deps):
         return obj
     cmd = [HIPCC, *FLAGS, "-c", str(srcp), "-o", str(obj)]

@@ -19,6 +19,7 @@
 // k-step t+1 are issued before the MFMAs of step t and written to the other LDS buffer after.
 #include "common.h"
 #include "internal.h"
+#include "ktimer.h"
 
 namespace argus {
 
@@ -752,10 +753,17 @@ static int check_desc(const argus_conv_desc& d) {
 }
 
 template <typename T, int BM, int BN, bool STEM, bool PRO>
+static const char* ig_name() {
+  static const std::string s = std::string("argus::igemm_kernel<") + type_name<T>() + ", " + std::to_string(BM) +
+                               ", " + std::to_string(BN) + ", " + bool_name(STEM) + ", " + bool_name(PRO) + ">";
+  return s.c_str();
+}
+
+template <typename T, int BM, int BN, bool STEM, bool PRO>
 static void launch_ig(const IgParams& p, int maxM, hipStream_t st) {
   const int ntiles = p.N / BN;
   dim3 grid(cdiv(maxM, BM) * ntiles, 1, p.nphase);
-  hipLaunchKernelGGL((igemm_kernel<T, BM, BN, STEM, PRO>), grid, dim3(256), 0, st, p);
+  timed_launch(ig_name<T, BM, BN, STEM, PRO>(), igemm_kernel<T, BM, BN, STEM, PRO>, grid, dim3(256), st, p);
 }
 
 template <typename T, bool PRO>
@@ -826,6 +834,7 @@ static int dgrad_bm(const argus_conv_desc& d) {
 int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, void* y,
              const float* sc, const float* sh, float* stats, hipStream_t st) {
   if (int e = check_desc(d)) return e;
+  g_launch_work = 2.0 * d.n * d.ho * d.wo * d.k * d.r * d.s * d.c;  // algorithmic flops (ktimer)
   IgParams p = {};
   p.a = x; p.b = w; p.c = y; p.pro_scale = sc; p.pro_shift = sh;
   p.stats = reinterpret_cast<float2*>(stats);
@@ -853,6 +862,7 @@ int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, 
 int conv_dgrad(const argus_conv_desc& d, int dtype, const void* dy, const void* wt, void* dx,
                int accumulate, hipStream_t st) {
   if (int e = check_desc(d)) return e;
+  g_launch_work = 2.0 * d.n * d.ho * d.wo * d.k * d.r * d.s * d.c;  // algorithmic flops (ktimer)
   if (d.stem) { set_error("conv_dgrad: the stem input has no gradient"); return ARGUS_ERR_ARG; }
   IgParams p = {};
   p.a = dy; p.b = wt; p.c = dx;
@@ -924,9 +934,18 @@ size_t conv_wgrad_ws(const argus_conv_desc& d, int dtype) {
 }
 
 template <typename T, int BM, int BN, bool STEM, bool PRO, bool FAST>
+static const char* wg_name() {
+  static const std::string s = std::string("argus::wgrad_kernel<") + type_name<T>() + ", " + std::to_string(BM) +
+                               ", " + std::to_string(BN) + ", " + bool_name(STEM) + ", " + bool_name(PRO) + ", " +
+                               bool_name(FAST) + ">";
+  return s.c_str();
+}
+
+template <typename T, int BM, int BN, bool STEM, bool PRO, bool FAST>
 static void launch_wg(const WgParams& p, const WgPlan& pl, hipStream_t st) {
   dim3 grid(pl.mt * pl.nt, pl.splits);
-  hipLaunchKernelGGL((wgrad_kernel<T, BM, BN, STEM, PRO, FAST>), grid, dim3(256), 0, st, p);
+  timed_launch(wg_name<T, BM, BN, STEM, PRO, FAST>(), wgrad_kernel<T, BM, BN, STEM, PRO, FAST>, grid, dim3(256), st,
+               p);
 }
 
 template <typename T, bool PRO, bool FAST>
@@ -957,6 +976,7 @@ static void dispatch_wg(const WgParams& p, const WgPlan& pl, hipStream_t st) {
 int conv_wgrad(const argus_conv_desc& d, int dtype, const void* x, const float* sc, const float* sh,
                const void* dy, float* dw, void* ws, size_t ws_bytes, hipStream_t st) {
   if (int e = check_desc(d)) return e;
+  g_launch_work = 2.0 * d.n * d.ho * d.wo * d.k * d.r * d.s * d.c;  // algorithmic flops (ktimer)
   const WgPlan pl = wgrad_plan(d, dtype);
   if (ws_bytes < (size_t)pl.splits * d.k * pl.N * sizeof(float)) {
     set_error("conv_wgrad: workspace too small");

@@ -81,7 +81,6 @@ class ResNetEngine:
         self.shape = None
         self.saved = False
         self.debug: dict | None = None  # when a dict: clones of block outputs / block-input grads
-        self.timer = None  # optional argus_amd.profiling.KernelTimer (events around conv launches)
 
     # ------------------------------------------------------------------ allocation
     def _t(self, *shape, dtype=None):
@@ -410,11 +409,9 @@ class ResNetEngine:
         self._launch(cv, 1, lambda: self.L.conv_dgrad(C.byref(cv.desc), self.dt, ptr(dy), ptr(cv.wd), ptr(dx),
                                                        accumulate, stream()))
 
-    def _launch(self, cv, pass_, fn):
-        if self.timer is None:
-            fn()
-        else:
-            self.timer.wrap(cv.tags[pass_], cv.flops, fn)
+    @staticmethod
+    def _launch(cv, pass_, fn):
+        fn()
 
 
 def conv_grad_shape(shape_oihw) -> tuple:

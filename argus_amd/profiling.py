@@ -1,53 +1,46 @@
-"""Live kernel timing with HIP events (torch.cuda.Event records on the launching stream)."""
+"""Live per-launch kernel timing through the library's native timer (include/argus_hip.h
+argus_ktimer_*): timed launches carry hipExtLaunchKernelGGL start/stop events in their dispatch
+packet, so durations are the kernels' own execution on the launch stream, as rocprofv3 reports."""
 from __future__ import annotations
 
-import torch
+import ctypes as C
 
-
-def tag_name(tag: int) -> str:
-    """Kernel symbol family for an argus_conv_launch_info tag (matches rocprof's kernel names)."""
-    kind, rest = divmod(tag, 10000000)
-    dt, rest = divmod(rest, 1000000)
-    bm, bn = divmod(rest, 1000)
-    t = "__bf16" if dt == 1 else "float"
-    k = "igemm_kernel" if kind == 1 else "wgrad_kernel"
-    return f"argus::{k}<{t}, {bm}, {bn}>"
+from argus_amd._lib import lib
 
 
 class KernelTimer:
-    """Records (start, end) events around every launch whose instantiation tag is in ``tags``
-    (None = record per tag for all)."""
+    """``with KernelTimer(prefix) as t: ...; t.summary()`` -> per-instantiation timing of conv kernels."""
 
-    def __init__(self, tags=None):
-        self.tags = None if tags is None else set(tags)
-        self.enabled = False
-        self.events: dict[int, list] = {}
-        self.flops: dict[int, int] = {}
+    def __init__(self, prefix: str | None = None):
+        self.prefix = prefix
 
-    def wrap(self, tag: int, flops: int, fn) -> None:
-        if not self.enabled or (self.tags is not None and tag not in self.tags):
-            fn()
-            return
-        s = torch.cuda.Event(enable_timing=True)
-        e = torch.cuda.Event(enable_timing=True)
-        s.record()
-        fn()
-        e.record()
-        self.events.setdefault(tag, []).append((s, e))
-        self.flops[tag] = self.flops.get(tag, 0) + flops
+    def start(self) -> None:
+        lib().ktimer_enable(self.prefix.encode() if self.prefix else None)
 
-    def reset(self) -> None:
-        self.events.clear()
-        self.flops.clear()
+    def stop(self) -> None:
+        lib().ktimer_disable()
+
+    def __enter__(self):
+        self.start()
+        return self
+
+    def __exit__(self, *a):
+        self.stop()
 
     def summary(self) -> dict:
-        """tag -> {launches, total_ms, avg_us, flops_per_launch, tflops}."""
-        torch.cuda.synchronize()
+        """name -> {launches, total_ms, avg_us, flops_per_launch, tflops} (synchronizes)."""
+        L = lib()
+        n = L.ktimer_count()
+        if n < 0:
+            raise RuntimeError(L.dll.argus_last_error().decode())
         out = {}
-        for tag, evs in self.events.items():
-            ms = sum(s.elapsed_time(e) for s, e in evs)
-            n = len(evs)
-            fl = self.flops[tag]
-            out[tag] = {"name": tag_name(tag), "launches": n, "total_ms": ms, "avg_us": 1e3 * ms / n,
-                        "flops_per_launch": fl / n, "tflops": fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0}
+        name = C.create_string_buffer(256)
+        cnt, ms, work = C.c_int64(), C.c_double(), C.c_double()
+        for i in range(n):
+            L.ktimer_get(i, name, 256, C.byref(cnt), C.byref(ms), C.byref(work))
+            k = cnt.value
+            out[name.value.decode()] = {
+                "launches": k, "total_ms": ms.value, "avg_us": 1e3 * ms.value / k,
+                "flops_per_launch": work.value / k,
+                "tflops": work.value / (ms.value * 1e-3) / 1e12 if ms.value > 0 else 0.0}
         return out

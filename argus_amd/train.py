@@ -130,6 +130,8 @@ def initialize_training(cfg: TrainConfig, rank: int = 0, world: int = 1):
     device = torch.device("cuda", rank % max(1, torch.cuda.device_count())) if cfg.multigpu else torch.device(cfg.device)
     if device.type != "cuda":
         raise RuntimeError("argus_amd trains on the MI355X HIP path only (device must be cuda)")
+    if device.index is None:
+        device = torch.device("cuda", torch.cuda.current_device())
     torch.cuda.set_device(device)
 
     train_ds = CameraCubePoseDataset(cfg.dataset_config, cfg_aug=cfg.augmentation_config, train=True)

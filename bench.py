@@ -12,9 +12,11 @@ Weights: seeded random init (torch.manual_seed(42)) of the reference architectur
 value = images/s over all ranks (one sample = 2 camera images); weak scaling (B per rank fixed).
 
 Also reported:
-  roofline     - the dominant conv kernel instantiation (largest total time in the step), timed
-                 live with HIP events around each of its launches in the timed region; achieved =
-                 algorithmic FLOPs per launch / average launch time; peak = dense bf16 MFMA.
+  roofline     - the dominant conv kernel instantiation (largest total time in one probe step),
+                 timed live over the timed region by the library's kernel timer (start/stop HIP
+                 events carried by each of its dispatch packets, on its launch stream); achieved =
+                 algorithmic FLOPs per launch / average launch time; peak = dense bf16 MFMA;
+                 traffic = HBM bytes per launch from the committed PMC summary (tools/pmc_traffic.py).
   cpu_baseline - the CPU oracle (the reference's torch.nn ops on CPU, fp32, B=8) train step timed on
                  this host (rank 0, N=1), a bounded sample of ~15 s.
   val_loss     - mean SE(3) loss (argus/train.py:342) of the trained model in eval mode on a
@@ -27,6 +29,7 @@ import json
 import math
 import os
 import time
+from pathlib import Path
 
 import torch
 import torch.distributed as dist
@@ -44,6 +47,21 @@ def synthetic_batch(B, H, W, seed, device):
     xi = torch.randn(B, 6, generator=g, device=device) * 0.5
     targets = se3_exp(xi, canonical_w=True)
     return images, targets
+
+
+def pmc_traffic(kernel: str, B: int, H: int, W: int, dtype: str):
+    """HBM bytes per launch of ``kernel`` from the committed PMC summary of this exact workload
+    (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from separate FETCH_SIZE and
+    WRITE_SIZE rocprofv3 passes of this bench command). None when no summary matches."""
+    prof = sorted(Path(__file__).resolve().parent.glob("profiles/*_pmc_traffic.json"))
+    for p in reversed(prof):
+        d = json.loads(p.read_text())
+        if d.get("meta", {}).get("workload") != [B, H, W, dtype]:
+            continue
+        for name, v in d["kernels"].items():
+            if name.startswith(kernel):
+                return round(v["traffic_bytes_per_launch"])
+    return None
 
 
 def cpu_baseline(batch: int, H: int, W: int, budget_s: float = 15.0) -> dict:
@@ -69,7 +87,7 @@ def cpu_baseline(batch: int, H: int, W: int, budget_s: float = 15.0) -> dict:
 
     step()  # warm-up
     n, t0 = 0, time.perf_counter()
-    while n < 2 or (time.perf_counter() - t0 < budget_s and n < 12):
+    while n < 2 or (time.perf_counter() - t0 < budget_s and n < 24):
         step()
         n += 1
     dt = time.perf_counter() - t0
@@ -112,21 +130,19 @@ def main() -> None:
 
     for _ in range(args.warmup):
         trainer.step(images, targets)
-    # find the dominant conv kernel instantiation over one instrumented step
-    eng = model._engine(dev)
+    # find the dominant conv kernel instantiation (largest total time) over one instrumented step
     probe = KernelTimer()
-    probe.enabled = True
-    eng.timer = probe
+    probe.start()
     trainer.step(images, targets)
     summ = probe.summary()
-    dom_tag = max(summ, key=lambda t: summ[t]["total_ms"])
-    timer = KernelTimer(tags=[dom_tag])
-    eng.timer = timer
+    probe.stop()
+    dom = max(summ, key=lambda k: summ[k]["total_ms"])
+    timer = KernelTimer(dom)  # exact-name prefix: only this instantiation is timed
 
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    timer.enabled = True
+    timer.start()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         losses = trainer.step(images, targets)
@@ -134,8 +150,7 @@ def main() -> None:
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    timer.enabled = False
-    eng.timer = None
+    timer.stop()
     el = torch.tensor([elapsed], device=dev)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -152,12 +167,13 @@ def main() -> None:
         dist.all_reduce(vsum)
     val_loss = (vsum[0] / vsum[1]).item()
 
-    ks = timer.summary()[dom_tag]
+    ks = timer.summary()[dom]
     achieved = ks["flops_per_launch"] / (ks["avg_us"] * 1e-6) / 1e12
     peak = BF16_DENSE_PEAK_TFLOPS if args.dtype == "bf16" else F32_MFMA_PEAK_TFLOPS
     ms = 1e3 * elapsed / args.steps
     images_per_s = world * B * 2 * args.steps / elapsed
     # algorithmic conv FLOPs per step: fwd + dgrad + wgrad (the stem has no dgrad)
+    eng = model._engine(dev)
     step_flops = sum((2 if n == "resnet.conv1" else 3) * c.flops for n, c in eng.convs.items())
     out = {
         "metric": "train images/sec + val SE(3) geodesic err, 2x256x256 RGB",
@@ -178,10 +194,10 @@ def main() -> None:
             "batch_per_rank": B, "global_batch": B * world, "image_hw": [H, W], "parallelism": f"dp{world}",
         },
         "roofline": {
-            "bound": "mfma", "kernel": ks["name"], "launches": ks["launches"],
+            "bound": "mfma", "kernel": dom, "launches": ks["launches"],
             "flops_per_launch": ks["flops_per_launch"], "avg_launch_us": round(ks["avg_us"], 3),
             "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
-            "traffic": None,
+            "traffic": pmc_traffic(dom, B, H, W, args.dtype),
         },
         "step_conv_tflops_per_gpu": round(step_flops / (ms * 1e-3) / 1e12, 2),
         "step_conv_frac_of_bf16_peak": round(step_flops / (ms * 1e-3) / 1e12 / BF16_DENSE_PEAK_TFLOPS, 4),

@@ -75,16 +75,28 @@ int argus_conv_dgrad(const argus_conv_desc* d, int dtype, const void* dy, const 
  * 0 = heuristic) of pass fwd/dgrad/wgrad, key 3..5 force the column tile, key 6 sets the wgrad
  * split target (workgroups). Returns 0, or -1 for an unknown key. */
 int argus_conv_tuning(int key, int value);
-/* Which kernel instantiation a pass launches and its algorithmic work: pass 0 fwd, 1 dgrad,
- * 2 wgrad. Returns a tag (kind*10^7 + dtype*10^6 + tile_m*1000 + tile_n; kind 1 igemm,
- * 2 wgrad) and writes 2*P*K*R*S*C flops (P = n*ho*wo output pixels). Used to time exactly the
- * launches rocprof groups under one kernel name. */
+/* Which tile a pass launches and its algorithmic work: pass 0 fwd, 1 dgrad, 2 wgrad. Returns a
+ * tag (kind*10^7 + dtype*10^6 + tile_m*1000 + tile_n; kind 1 igemm, 2 wgrad) and writes
+ * 2*P*K*R*S*C flops (P = n*ho*wo output pixels). */
 int argus_conv_launch_info(const argus_conv_desc* d, int dtype, int pass, int64_t* flops);
 /* dw (fp32, OHWI 7x7x3 for the stem) = sum over pixels of dy x im2col(x'), x' as in conv_fwd. */
 size_t argus_conv_wgrad_workspace_bytes(const argus_conv_desc* d, int dtype);
 int argus_conv_wgrad(const argus_conv_desc* d, int dtype, const void* x, const float* pro_scale,
                      const float* pro_shift, const void* dy, float* dw, void* workspace,
                      size_t workspace_bytes, argus_stream_t stream);
+
+/* ---- kernel timer (bench.py roofline) ------------------------------------------------------------
+ * While enabled, conv kernel launches whose demangled instantiation name (e.g.
+ * "argus::igemm_kernel<__bf16, 128, 128, false, true>", as c++filt prints rocprofv3's kernel name)
+ * starts with `filter` (NULL or "" = all) are dispatched with hipExtLaunchKernelGGL start/stop
+ * events, i.e. timed by the dispatch packet on the launch stream. enable() clears old records;
+ * count() synchronizes the recorded events, aggregates per name and returns the number of names;
+ * get(i) returns name, launches, total milliseconds and total algorithmic flops. */
+int argus_ktimer_enable(const char* filter);
+int argus_ktimer_disable(void);
+int argus_ktimer_count(void);
+int argus_ktimer_get(int index, char* name, int name_len, int64_t* launches, double* total_ms,
+                     double* work);
 
 /* ---- BatchNorm2d (train: batch stats, eps, momentum; eval: running stats) --------------------- */
 size_t argus_bn_workspace_bytes(int channels);

@@ -379,3 +379,30 @@ def test_norm_and_adam(cuda):
                     C.c_float(0.999), C.c_float(1e-8), C.c_float(0.0), C.c_float(1 - 0.9**step),
                     C.c_float(1 - 0.999**step), stream())
     assert (pd.cpu() - ref_p.detach()).abs().max().item() < 2e-6
+
+
+def test_kernel_timer_records_exact_instantiations(cuda):
+    from argus_amd.profiling import KernelTimer
+
+    L = lib()
+    d, _ = _desc(4, 32, 32, 64, 128, 3, 1)
+    x = torch.randn(4, 32, 32, 64, device=cuda, dtype=torch.bfloat16)
+    w = torch.randn(128, 3, 3, 64, device=cuda) * 0.05
+    wf, wt = _prep(d, 1, w, cuda)
+    y = torch.empty(4, 32, 32, 128, device=cuda, dtype=torch.bfloat16)
+    with KernelTimer() as t:
+        for _ in range(3):
+            L.conv_fwd(C.byref(d), BF16, ptr(x), ptr(wf), ptr(y), None, None, None, stream())
+    s = t.summary()
+    assert len(s) == 1
+    (name, v), = s.items()
+    fl = C.c_int64()
+    tag = L.dll.argus_conv_launch_info(C.byref(d), BF16, 0, C.byref(fl))
+    bm, bn = divmod(tag % 1000000, 1000)
+    assert name == f"argus::igemm_kernel<__bf16, {bm}, {bn}, false, false>"
+    assert v["launches"] == 3 and v["flops_per_launch"] == fl.value and v["avg_us"] > 0
+    with KernelTimer("argus::wgrad") as t:  # filtered out: nothing recorded
+        L.conv_fwd(C.byref(d), BF16, ptr(x), ptr(wf), ptr(y), None, None, None, stream())
+    assert t.summary() == {}
+    L.conv_fwd(C.byref(d), BF16, ptr(x), ptr(wf), ptr(y), None, None, None, stream())  # disabled: plain launch
+    torch.cuda.synchronize()
