@@ -388,7 +388,7 @@ def test_kernel_timer_records_exact_instantiations(cuda):
     d, _ = _desc(4, 32, 32, 64, 128, 3, 1)
     x = torch.randn(4, 32, 32, 64, device=cuda, dtype=torch.bfloat16)
     w = torch.randn(128, 3, 3, 64, device=cuda) * 0.05
-    wf, wt = _prep(d, 1, w, cuda)
+    wf, wt = _prep(d, "bf16", w, cuda)
     y = torch.empty(4, 32, 32, 128, device=cuda, dtype=torch.bfloat16)
     with KernelTimer() as t:
         for _ in range(3):

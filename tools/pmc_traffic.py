@@ -11,9 +11,44 @@ Output: kernel name -> launches and mean corrected bytes per launch.
 """
 import csv
 import json
+import re
 import sys
 from collections import defaultdict
 from pathlib import Path
+
+
+def demangle(name: str) -> str:
+    """rocprof kernel name -> "argus::igemm_kernel<__bf16, 128, 128, false, false>" (no return type or
+    argument list). Our template kernels are demangled here (binutils' c++filt predates DF16b);
+    names rocprof already prints demangled are cut at their argument list."""
+    m = re.match(r"_ZN5argus(\d+)", name)
+    if m:
+        n = int(m.group(1))
+        p = m.end()
+        base = name[p:p + n]
+        p += n
+        if name[p:p + 1] != "I":
+            return f"argus::{base}"
+        args = []
+        p += 1
+        while name[p] != "E":
+            for pat, fn in ((r"DF16b", lambda g: "__bf16"), (r"f", lambda g: "float"),
+                            (r"Li(-?\d+)E", lambda g: g.group(1)), (r"Lb([01])E", lambda g: "true" if g.group(1) == "1" else "false")):
+                mm = re.match(pat, name[p:])
+                if mm:
+                    args.append(fn(mm))
+                    p += mm.end()
+                    break
+            else:
+                return name
+        return f"argus::{base}<{', '.join(args)}>"
+    depth = 0
+    for i, ch in enumerate(name):
+        depth += ch == "<"
+        depth -= ch == ">"
+        if ch == "(" and depth == 0:
+            return name[:i]
+    return name
 
 
 def per_kernel(d: str, counter: str) -> dict:
@@ -25,7 +60,7 @@ def per_kernel(d: str, counter: str) -> dict:
         for r in csv.DictReader(open(f)):
             if r.get("Counter_Name") != counter:
                 continue
-            acc[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+            acc[demangle(r["Kernel_Name"])].append(float(r["Counter_Value"]))
     return acc
 
 
