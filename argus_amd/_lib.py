@@ -50,7 +50,7 @@ SIGNATURES = {
     "argus_ktimer_disable": (_I, []),
     "argus_ktimer_count": (_I, []),
     "argus_ktimer_get": (_I, [_I, C.c_char_p, _I, C.POINTER(C.c_int64), C.POINTER(C.c_double),
-                              C.POINTER(C.c_double)]),
+                              C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "argus_bn_workspace_bytes": (_SZ, [_I]),
     "argus_bn_finalize": (_I, [_I, _I, _I, _P, _I64, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "argus_bn_eval_coeffs": (_I, [_I, _P, _P, _P, _P, _F, _P, _P, _P]),

@@ -834,7 +834,11 @@ static int dgrad_bm(const argus_conv_desc& d) {
 int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, void* y,
              const float* sc, const float* sh, float* stats, hipStream_t st) {
   if (int e = check_desc(d)) return e;
-  g_launch_work = 2.0 * d.n * d.ho * d.wo * d.k * d.r * d.s * d.c;  // algorithmic flops (ktimer)
+  g_launch_work = 2.0 * d.n * d.ho * d.wo * d.k * d.r * d.s * d.c;  // algorithmic flops / bytes (ktimer)
+  g_launch_bytes = (double)(dtype == ARGUS_BF16 ? 2 : 4) *
+                       ((double)d.n * d.h * d.w * (d.stem ? 4 : d.c) + (double)d.k * d.r * d.s * d.c +
+                        (double)d.n * d.ho * d.wo * d.k) +
+                   (stats ? 8.0 * conv_fwd_stat_rows(d, dtype) * d.k : 0.0);
   IgParams p = {};
   p.a = x; p.b = w; p.c = y; p.pro_scale = sc; p.pro_shift = sh;
   p.stats = reinterpret_cast<float2*>(stats);
@@ -862,7 +866,10 @@ int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, 
 int conv_dgrad(const argus_conv_desc& d, int dtype, const void* dy, const void* wt, void* dx,
                int accumulate, hipStream_t st) {
   if (int e = check_desc(d)) return e;
-  g_launch_work = 2.0 * d.n * d.ho * d.wo * d.k * d.r * d.s * d.c;  // algorithmic flops (ktimer)
+  g_launch_work = 2.0 * d.n * d.ho * d.wo * d.k * d.r * d.s * d.c;  // algorithmic flops / bytes (ktimer)
+  g_launch_bytes = (double)(dtype == ARGUS_BF16 ? 2 : 4) *
+                   ((double)d.n * d.ho * d.wo * d.k + (double)d.k * d.r * d.s * d.c +
+                    (accumulate ? 2.0 : 1.0) * d.n * d.h * d.w * d.c);
   if (d.stem) { set_error("conv_dgrad: the stem input has no gradient"); return ARGUS_ERR_ARG; }
   IgParams p = {};
   p.a = dy; p.b = wt; p.c = dx;
@@ -976,8 +983,11 @@ static void dispatch_wg(const WgParams& p, const WgPlan& pl, hipStream_t st) {
 int conv_wgrad(const argus_conv_desc& d, int dtype, const void* x, const float* sc, const float* sh,
                const void* dy, float* dw, void* ws, size_t ws_bytes, hipStream_t st) {
   if (int e = check_desc(d)) return e;
-  g_launch_work = 2.0 * d.n * d.ho * d.wo * d.k * d.r * d.s * d.c;  // algorithmic flops (ktimer)
+  g_launch_work = 2.0 * d.n * d.ho * d.wo * d.k * d.r * d.s * d.c;  // algorithmic flops / bytes (ktimer)
   const WgPlan pl = wgrad_plan(d, dtype);
+  g_launch_bytes = (double)(dtype == ARGUS_BF16 ? 2 : 4) *
+                       ((double)d.n * d.h * d.w * (d.stem ? 4 : d.c) + (double)d.n * d.ho * d.wo * d.k) +
+                   4.0 * pl.splits * d.k * pl.N;
   if (ws_bytes < (size_t)pl.splits * d.k * pl.N * sizeof(float)) {
     set_error("conv_wgrad: workspace too small");
     return ARGUS_ERR_ARG;

@@ -11,17 +11,17 @@
 
 namespace argus {
 
-thread_local double g_launch_work = 0.0;
+thread_local double g_launch_work = 0.0, g_launch_bytes = 0.0;
 
 namespace {
 struct Rec {
   std::string name;
-  double work;
+  double work, bytes;
   hipEvent_t start, stop;
 };
 struct Agg {
   int64_t launches = 0;
-  double ms = 0.0, work = 0.0;
+  double ms = 0.0, work = 0.0, bytes = 0.0;
 };
 std::mutex g_mu;
 std::atomic<bool> g_on{false};
@@ -55,9 +55,9 @@ bool ktimer_wants(const char* name) {
   return g_filter.empty() || std::strncmp(name, g_filter.c_str(), g_filter.size()) == 0;
 }
 
-void ktimer_slot(const char* name, double work, hipEvent_t* start, hipEvent_t* stop) {
+void ktimer_slot(const char* name, double work, double bytes, hipEvent_t* start, hipEvent_t* stop) {
   std::lock_guard<std::mutex> lk(g_mu);
-  Rec r{name, work, take_event(), take_event()};
+  Rec r{name, work, bytes, take_event(), take_event()};
   *start = r.start;
   *stop = r.stop;
   g_recs.push_back(r);
@@ -101,13 +101,15 @@ int argus_ktimer_count(void) {
     a.launches += 1;
     a.ms += ms;
     a.work += r.work;
+    a.bytes += r.bytes;
   }
   recycle_all();
   g_aggs.assign(m.begin(), m.end());
   return (int)g_aggs.size();
 }
 
-int argus_ktimer_get(int i, char* name, int name_len, int64_t* launches, double* total_ms, double* work) {
+int argus_ktimer_get(int i, char* name, int name_len, int64_t* launches, double* total_ms, double* work,
+                     double* bytes) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (i < 0 || i >= (int)g_aggs.size()) {
     set_error("ktimer_get: index out of range (call argus_ktimer_count first)");
@@ -121,6 +123,7 @@ int argus_ktimer_get(int i, char* name, int name_len, int64_t* launches, double*
   if (launches) *launches = a.second.launches;
   if (total_ms) *total_ms = a.second.ms;
   if (work) *work = a.second.work;
+  if (bytes) *bytes = a.second.bytes;
   return ARGUS_OK;
 }
 

@@ -28,19 +28,19 @@ class KernelTimer:
         self.stop()
 
     def summary(self) -> dict:
-        """name -> {launches, total_ms, avg_us, flops_per_launch, tflops} (synchronizes)."""
+        """name -> {launches, total_ms, avg_us, flops_per_launch, bytes_per_launch, tflops} (synchronizes)."""
         L = lib()
         n = L.ktimer_count()
         if n < 0:
             raise RuntimeError(L.dll.argus_last_error().decode())
         out = {}
         name = C.create_string_buffer(256)
-        cnt, ms, work = C.c_int64(), C.c_double(), C.c_double()
+        cnt, ms, work, nbytes = C.c_int64(), C.c_double(), C.c_double(), C.c_double()
         for i in range(n):
-            L.ktimer_get(i, name, 256, C.byref(cnt), C.byref(ms), C.byref(work))
+            L.ktimer_get(i, name, 256, C.byref(cnt), C.byref(ms), C.byref(work), C.byref(nbytes))
             k = cnt.value
             out[name.value.decode()] = {
                 "launches": k, "total_ms": ms.value, "avg_us": 1e3 * ms.value / k,
-                "flops_per_launch": work.value / k,
+                "flops_per_launch": work.value / k, "bytes_per_launch": nbytes.value / k,
                 "tflops": work.value / (ms.value * 1e-3) / 1e12 if ms.value > 0 else 0.0}
         return out

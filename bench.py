@@ -195,10 +195,12 @@ def main() -> None:
         },
         "roofline": {
             "bound": "mfma", "kernel": dom, "launches": ks["launches"],
-            "flops_per_launch": ks["flops_per_launch"], "avg_launch_us": round(ks["avg_us"], 3),
+            "flops_per_launch": round(ks["flops_per_launch"]), "algorithmic_bytes_per_launch": round(ks["bytes_per_launch"]),
+            "avg_launch_us": round(ks["avg_us"], 3),
             "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
             "traffic": pmc_traffic(dom, B, H, W, args.dtype),
         },
+        "samples_per_s": round(images_per_s / 2, 2),
         "step_conv_tflops_per_gpu": round(step_flops / (ms * 1e-3) / 1e12, 2),
         "step_conv_frac_of_bf16_peak": round(step_flops / (ms * 1e-3) / 1e12 / BF16_DENSE_PEAK_TFLOPS, 4),
         "train_loss": round(train_loss, 6),

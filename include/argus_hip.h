@@ -91,12 +91,14 @@ int argus_conv_wgrad(const argus_conv_desc* d, int dtype, const void* x, const f
  * starts with `filter` (NULL or "" = all) are dispatched with hipExtLaunchKernelGGL start/stop
  * events, i.e. timed by the dispatch packet on the launch stream. enable() clears old records;
  * count() synchronizes the recorded events, aggregates per name and returns the number of names;
- * get(i) returns name, launches, total milliseconds and total algorithmic flops. */
+ * get(i) returns name, launches, total milliseconds, total algorithmic flops and total algorithmic
+ * HBM bytes (each operand read once and each result written once; for wgrad the fp32 split partials
+ * it writes count too). */
 int argus_ktimer_enable(const char* filter);
 int argus_ktimer_disable(void);
 int argus_ktimer_count(void);
 int argus_ktimer_get(int index, char* name, int name_len, int64_t* launches, double* total_ms,
-                     double* work);
+                     double* work, double* bytes);
 
 /* ---- BatchNorm2d (train: batch stats, eps, momentum; eval: running stats) --------------------- */
 size_t argus_bn_workspace_bytes(int channels);

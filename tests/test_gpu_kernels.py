@@ -401,6 +401,7 @@ def test_kernel_timer_records_exact_instantiations(cuda):
     bm, bn = divmod(tag % 1000000, 1000)
     assert name == f"argus::igemm_kernel<__bf16, {bm}, {bn}, false, false>"
     assert v["launches"] == 3 and v["flops_per_launch"] == fl.value and v["avg_us"] > 0
+    assert v["bytes_per_launch"] == 2 * (4 * 32 * 32 * 64 + 128 * 9 * 64 + 4 * 32 * 32 * 128)
     with KernelTimer("argus::wgrad") as t:  # filtered out: nothing recorded
         L.conv_fwd(C.byref(d), BF16, ptr(x), ptr(wf), ptr(y), None, None, None, stream())
     assert t.summary() == {}
