@@ -14,9 +14,11 @@ value = images/s over all ranks (one sample = 2 camera images); weak scaling (B 
 Also reported:
   roofline     - the dominant conv kernel instantiation (largest total time in one probe step),
                  timed live over the timed region by the library's kernel timer (start/stop HIP
-                 events carried by each of its dispatch packets, on its launch stream); achieved =
-                 algorithmic FLOPs per launch / average launch time; peak = dense bf16 MFMA;
-                 traffic = HBM bytes per launch from the committed PMC summary (tools/pmc_traffic.py).
+                 events carried by each of its dispatch packets, on its launch stream). bound =
+                 "mfma" if its algorithmic FLOP/byte is above the ridge (peak FLOP/s / 8 TB/s), else
+                 "hbm"; achieved = algorithmic FLOPs (or bytes) per launch / average launch time;
+                 peak = dense bf16 MFMA (or HBM); traffic = measured HBM bytes per launch from the
+                 committed PMC summary of this workload (tools/pmc_traffic.py).
   cpu_baseline - the CPU oracle (the reference's torch.nn ops on CPU, fp32, B=8) train step timed on
                  this host (rank 0, N=1), a bounded sample of ~15 s.
   val_loss     - mean SE(3) loss (argus/train.py:342) of the trained model in eval mode on a
@@ -168,8 +170,11 @@ def main() -> None:
     val_loss = (vsum[0] / vsum[1]).item()
 
     ks = timer.summary()[dom]
-    achieved = ks["flops_per_launch"] / (ks["avg_us"] * 1e-6) / 1e12
-    peak = BF16_DENSE_PEAK_TFLOPS if args.dtype == "bf16" else F32_MFMA_PEAK_TFLOPS
+    peak_flops = BF16_DENSE_PEAK_TFLOPS if args.dtype == "bf16" else F32_MFMA_PEAK_TFLOPS
+    tflops = ks["flops_per_launch"] / (ks["avg_us"] * 1e-6) / 1e12
+    gbs = ks["bytes_per_launch"] / (ks["avg_us"] * 1e-6) / 1e9
+    # the roof that binds: MFMA if the kernel's algorithmic intensity is above the ridge, else HBM
+    compute_bound = ks["flops_per_launch"] / ks["bytes_per_launch"] > peak_flops * 1e12 / (HBM_PEAK_GBS * 1e9)
     ms = 1e3 * elapsed / args.steps
     images_per_s = world * B * 2 * args.steps / elapsed
     # algorithmic conv FLOPs per step: fwd + dgrad + wgrad (the stem has no dgrad)
@@ -194,10 +199,16 @@ def main() -> None:
             "batch_per_rank": B, "global_batch": B * world, "image_hw": [H, W], "parallelism": f"dp{world}",
         },
         "roofline": {
-            "bound": "mfma", "kernel": dom, "launches": ks["launches"],
+            "bound": "mfma" if compute_bound else "hbm", "kernel": dom, "launches": ks["launches"],
             "flops_per_launch": round(ks["flops_per_launch"]), "algorithmic_bytes_per_launch": round(ks["bytes_per_launch"]),
             "avg_launch_us": round(ks["avg_us"], 3),
-            "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+            "achieved": round(tflops, 2) if compute_bound else round(gbs, 1),
+            "peak": peak_flops if compute_bound else HBM_PEAK_GBS,
+            "unit": "TFLOP/s" if compute_bound else "GB/s",
+            "frac": round(tflops / peak_flops if compute_bound else gbs / HBM_PEAK_GBS, 4),
+            "intensity_flop_per_byte": round(ks["flops_per_launch"] / ks["bytes_per_launch"], 1),
+            "achieved_tflops": round(tflops, 2), "frac_of_mfma_peak": round(tflops / peak_flops, 4),
+            "achieved_gbs": round(gbs, 1), "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4),
             "traffic": pmc_traffic(dom, B, H, W, args.dtype),
         },
         "samples_per_s": round(images_per_s / 2, 2),

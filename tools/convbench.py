@@ -1,5 +1,6 @@
-"""Per-layer conv microbenchmark (dev tool, GPU): fwd / dgrad / wgrad time and TFLOP/s for every
-ResNet-50 conv at a given batch, through the C ABI.  python tools/convbench.py [--batch 64] [--dtype bf16]"""
+"""Per-layer conv microbenchmark (dev tool, GPU): fwd / dgrad / wgrad time, TFLOP/s and fraction of
+the per-launch roofline max(flops / 2.5 PF, algorithmic bytes / 8 TB/s) for every ResNet-50 conv at a
+given batch, through the C ABI.  python tools/convbench.py [--batch 64] [--dtype bf16]"""
 import argparse
 import ctypes as C
 import sys
@@ -9,6 +10,7 @@ import torch
 sys.path.insert(0, ".")
 from argus_amd._lib import BF16, F32, lib, ptr, stream  # noqa: E402
 from argus_amd.engine import ResNetEngine  # noqa: E402
+from argus_amd.profiling import KernelTimer  # noqa: E402
 
 
 def main():
@@ -50,7 +52,10 @@ def main():
             fns[1] = lambda: L.conv_dgrad(C.byref(d), dt, ptr(dy), ptr(wd), ptr(dx), 0, stream())
         row = [name]
         for ps, fn in fns.items():
-            fn()
+            with KernelTimer() as kt:
+                fn()
+            main_k = max(kt.summary().values(), key=lambda v: v["total_ms"])
+            roof_us = max(main_k["flops_per_launch"] / 2.5e15, main_k["bytes_per_launch"] / 8e12) * 1e6
             torch.cuda.synchronize()
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
@@ -60,7 +65,7 @@ def main():
             torch.cuda.synchronize()
             us = s.elapsed_time(e) * 1e3 / a.reps
             tot[ps] += us
-            row.append(f"p{ps}:{us:7.1f}us {cv.flops / us / 1e6:6.1f}TF")
+            row.append(f"p{ps}:{us:7.1f}us {cv.flops / us / 1e6:6.1f}TF {roof_us / us:4.0%}")
         totf += cv.flops * (2 if d.stem else 3)
         print(f"{name:32s} {d.h:3d}x{d.w:<3d} {d.c:4d}->{d.k:4d} k{d.r} s{d.stride}  " + "  ".join(row[1:]))
     allus = sum(tot.values())
