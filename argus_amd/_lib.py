@@ -43,7 +43,7 @@ SIGNATURES = {
     "argus_conv_fwd_stat_tile": (_I, [_DESC, _I]),
     "argus_conv_tuning": (_I, [_I, _I]),
     "argus_conv_launch_info": (_I, [_DESC, _I, _I, C.POINTER(C.c_int64)]),
-    "argus_conv_dgrad": (_I, [_DESC, _I, _P, _P, _P, _I, _P]),
+    "argus_conv_dgrad": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P]),
     "argus_conv_wgrad_workspace_bytes": (_SZ, [_DESC, _I]),
     "argus_conv_wgrad": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     "argus_ktimer_enable": (_I, [C.c_char_p]),
@@ -54,11 +54,11 @@ SIGNATURES = {
     "argus_bn_workspace_bytes": (_SZ, [_I]),
     "argus_bn_finalize": (_I, [_I, _I, _I, _P, _I64, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "argus_bn_eval_coeffs": (_I, [_I, _P, _P, _P, _P, _F, _P, _P, _P]),
-    "argus_bn_apply": (_I, [_I, _I64, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P]),
+    "argus_bn_apply": (_I, [_I, _I64, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P]),
     "argus_bn_bwd_rows": (_I, [_I64, _I]),
-    "argus_bn_bwd_reduce": (_I, [_I, _I64, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "argus_bn_bwd_reduce": (_I, [_I, _I64, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "argus_bn_bwd_finalize": (_I, [_I, _I, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
-    "argus_bn_bwd_apply": (_I, [_I, _I64, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "argus_bn_bwd_apply": (_I, [_I, _I64, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "argus_maxpool_fwd": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
     "argus_maxpool_bwd": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "argus_avgpool_fwd": (_I, [_I, _I, _I, _I, _P, _P, _P]),

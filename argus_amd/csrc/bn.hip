@@ -28,6 +28,7 @@ __global__ __launch_bounds__(256) void stats_reduce_kernel(const float2* __restr
   const double inv_full = 1.0 / (double)tile_rows;
   double S = 0.0, Q = 0.0;
   if (c < C)
+#pragma unroll 8
     for (int r = r0 + lane_r; r < r1; r += 4) {
       const float2 v = part[(size_t)r * C + c];
       const int64_t left = count - (int64_t)r * tile_rows;
@@ -54,6 +55,7 @@ __global__ __launch_bounds__(256) void colreduce_kernel(const float2* __restrict
   const int r0 = g * rows_per_group, r1 = min(rows, r0 + rows_per_group);
   double s = 0.0, q = 0.0;
   if (c < C)
+#pragma unroll 8
     for (int r = r0 + lane_r; r < r1; r += 4) {
       const float2 v = part[(size_t)r * C + c];
       s += v.x;
@@ -87,6 +89,7 @@ __global__ void bn_finalize_kernel(const double2* __restrict__ red, int G, int C
   if (c == 0 && nbt) nbt[0] += 1;
   if (c >= C) return;
   double S = 0.0, Q = 0.0;
+#pragma unroll 8
   for (int g = 0; g < G; ++g) {
     const double2 v = red[(size_t)g * C + c];
     S += v.x;
@@ -147,7 +150,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(int64_t pixels, int C, in
                                                        const T* __restrict__ y, const float* __restrict__ sc,
                                                        const float* __restrict__ sh, const T* __restrict__ res,
                                                        const float* __restrict__ rsc, const float* __restrict__ rsh,
-                                                       int relu, T* out) {
+                                                       int relu, T* out, uint8_t* __restrict__ mask_out) {
   constexpr int E = Chunk<T>::E;
   const int cc = threadIdx.x % CC, pl = threadIdx.x / CC;
   const int c0 = (blockIdx.x * CC + cc) * E;
@@ -172,7 +175,9 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(int64_t pixels, int C, in
       if (relu) v = fmaxf(v, 0.f);
       f[j] = v;
     }
-    st16(out + off, pack(f));
+    const u32x4 o = pack(f);
+    st16(out + off, o);
+    if (mask_out) mask_out[off / E] = chunk_positive_bits<T>(o);
   }
 }
 
@@ -192,18 +197,44 @@ static void bwd_geometry(int C, int E, int64_t pixels, int& CC, int& PL, int& cg
   rows = (int)((pixels + ppb - 1) / ppb);
 }
 
+// Mask of the upstream ReLU for one 16-byte chunk (mode 0 none, 1 src>0, 2 y*S+H>0, 3 mask bits).
 template <typename T>
+ARGUS_DEV void apply_mask(int mode, float (&d)[Chunk<T>::E], const float (&yv)[Chunk<T>::E], const T* __restrict__ msrc,
+                          const uint8_t* __restrict__ mbits, int64_t off, const float* S, const float* H) {
+  constexpr int E = Chunk<T>::E;
+  if (mode == 1) {
+    float m[E];
+    unpack(ld16(msrc + off), m);
+#pragma unroll
+    for (int j = 0; j < E; ++j) d[j] = m[j] > 0.f ? d[j] : 0.f;
+  } else if (mode == 2) {
+#pragma unroll
+    for (int j = 0; j < E; ++j) d[j] = fmaf(yv[j], S[j], H[j]) > 0.f ? d[j] : 0.f;
+  } else if (mode == 3) {
+    const unsigned b = mbits[off / E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) d[j] = (b >> j) & 1u ? d[j] : 0.f;
+  }
+}
+
+// Per-block column partials {sum dm, sum dm*xhat} of one (or, DUAL, two BN branches sharing dm:
+// bn3 and the downsample BN of a bottleneck both see the gradient of the same block output).
+template <typename T, bool DUAL>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(int64_t pixels, int C, int CC, int PL, int64_t ppb,
                                                             const T* __restrict__ dz, int mode,
-                                                            const T* __restrict__ mask_src, const T* __restrict__ y,
+                                                            const T* __restrict__ mask_src,
+                                                            const uint8_t* __restrict__ mbits, const T* __restrict__ y,
                                                             const float* __restrict__ sc, const float* __restrict__ sh,
                                                             const float* __restrict__ mean,
-                                                            const float* __restrict__ invstd, float2* __restrict__ part) {
+                                                            const float* __restrict__ invstd, float2* __restrict__ part,
+                                                            const T* __restrict__ y2, const float* __restrict__ mean2,
+                                                            const float* __restrict__ invstd2,
+                                                            float2* __restrict__ part2) {
   constexpr int E = Chunk<T>::E;
   const int cc = threadIdx.x % CC, pl = threadIdx.x / CC;
   const int c0 = (blockIdx.x * CC + cc) * E;
   const int64_t p0 = blockIdx.y * ppb, p1 = min(pixels, p0 + ppb);
-  float mu[E], is[E], S[E], H[E], s[E], t[E];
+  float mu[E], is[E], S[E], H[E], s[E], t[E], mu2[E], is2[E], t2[E];
 #pragma unroll
   for (int j = 0; j < E; ++j) {
     mu[j] = mean[c0 + j];
@@ -212,36 +243,43 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(int64_t pixels, int 
     H[j] = mode == 2 ? sh[c0 + j] : 0.f;
     s[j] = 0.f;
     t[j] = 0.f;
+    mu2[j] = DUAL ? mean2[c0 + j] : 0.f;
+    is2[j] = DUAL ? invstd2[c0 + j] : 0.f;
+    t2[j] = 0.f;
   }
   for (int64_t px = p0 + pl; px < p1; px += PL) {
     const int64_t off = px * C + c0;
-    float d[E], yv[E], m[E];
+    float d[E], yv[E];
     unpack(ld16(dz + off), d);
     unpack(ld16(y + off), yv);
-    if (mode == 1) {
-      unpack(ld16(mask_src + off), m);
-#pragma unroll
-      for (int j = 0; j < E; ++j) d[j] = m[j] > 0.f ? d[j] : 0.f;
-    } else if (mode == 2) {
-#pragma unroll
-      for (int j = 0; j < E; ++j) d[j] = fmaf(yv[j], S[j], H[j]) > 0.f ? d[j] : 0.f;
-    }
+    apply_mask<T>(mode, d, yv, mask_src, mbits, off, S, H);
 #pragma unroll
     for (int j = 0; j < E; ++j) {
       s[j] += d[j];
       t[j] = fmaf(d[j], (yv[j] - mu[j]) * is[j], t[j]);
+    }
+    if constexpr (DUAL) {
+      float y2v[E];
+      unpack(ld16(y2 + off), y2v);
+#pragma unroll
+      for (int j = 0; j < E; ++j) t2[j] = fmaf(d[j], (y2v[j] - mu2[j]) * is2[j], t2[j]);
     }
   }
   __shared__ float2 red[256 * 8];
   // reduce over pixel lanes: layout red[pl][cc*E + j]
   const int W = CC * E;
 #pragma unroll
-  for (int j = 0; j < E; ++j) red[pl * W + cc * E + j] = make_float2(s[j], t[j]);
-  __syncthreads();
-  for (int idx = threadIdx.x; idx < W; idx += 256) {
-    float2 a = red[idx];
-    for (int l = 1; l < PL; ++l) { a.x += red[l * W + idx].x; a.y += red[l * W + idx].y; }
-    part[(size_t)blockIdx.y * C + blockIdx.x * W + idx] = a;
+  for (int br = 0; br < (DUAL ? 2 : 1); ++br) {
+#pragma unroll
+    for (int j = 0; j < E; ++j) red[pl * W + cc * E + j] = make_float2(s[j], br == 0 ? t[j] : t2[j]);
+    __syncthreads();
+    float2* out = br == 0 ? part : part2;
+    for (int idx = threadIdx.x; idx < W; idx += 256) {
+      float2 a = red[idx];
+      for (int l = 1; l < PL; ++l) { a.x += red[l * W + idx].x; a.y += red[l * W + idx].y; }
+      out[(size_t)blockIdx.y * C + blockIdx.x * W + idx] = a;
+    }
+    __syncthreads();
   }
 }
 
@@ -251,6 +289,7 @@ __global__ void bn_bwd_finalize_kernel(const double2* __restrict__ red, int G, i
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   double S = 0.0, Tt = 0.0;
+#pragma unroll 8
   for (int g = 0; g < G; ++g) { S += red[(size_t)g * C + c].x; Tt += red[(size_t)g * C + c].y; }
   if (dgamma) dgamma[c] = (float)Tt;
   if (dbeta) dbeta[c] = (float)S;
@@ -261,19 +300,22 @@ __global__ void bn_bwd_finalize_kernel(const double2* __restrict__ red, int G, i
   cc[c] = (float)(-gi * S / count + gi2 * Tt / count * mean[c]);
 }
 
-template <typename T>
+template <typename T, bool DUAL>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(int64_t pixels, int C, int CC, int PL, int64_t ppb,
                                                            const T* __restrict__ dz, int mode,
-                                                           const T* __restrict__ mask_src, const T* __restrict__ y,
+                                                           const T* __restrict__ mask_src,
+                                                           const uint8_t* __restrict__ mbits, const T* __restrict__ y,
                                                            const float* __restrict__ sc, const float* __restrict__ sh,
                                                            const float* __restrict__ ca, const float* __restrict__ cb,
                                                            const float* __restrict__ cc_, T* __restrict__ dy,
-                                                           T* __restrict__ dm_out) {
+                                                           T* __restrict__ dm_out, const T* __restrict__ y2,
+                                                           const float* __restrict__ ca2, const float* __restrict__ cb2,
+                                                           const float* __restrict__ cc2, T* __restrict__ dy2) {
   constexpr int E = Chunk<T>::E;
   const int cc = threadIdx.x % CC, pl = threadIdx.x / CC;
   const int c0 = (blockIdx.x * CC + cc) * E;
   const int64_t p0 = blockIdx.y * ppb, p1 = min(pixels, p0 + ppb);
-  float A[E], Bc[E], Cc[E], S[E], H[E];
+  float A[E], Bc[E], Cc[E], S[E], H[E], A2[E], B2[E], C2[E];
 #pragma unroll
   for (int j = 0; j < E; ++j) {
     A[j] = ca[c0 + j];
@@ -281,24 +323,27 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(int64_t pixels, int C
     Cc[j] = cc_[c0 + j];
     S[j] = mode == 2 ? sc[c0 + j] : 0.f;
     H[j] = mode == 2 ? sh[c0 + j] : 0.f;
+    A2[j] = DUAL ? ca2[c0 + j] : 0.f;
+    B2[j] = DUAL ? cb2[c0 + j] : 0.f;
+    C2[j] = DUAL ? cc2[c0 + j] : 0.f;
   }
   for (int64_t px = p0 + pl; px < p1; px += PL) {
     const int64_t off = px * C + c0;
-    float d[E], yv[E], m[E];
+    float d[E], yv[E];
     unpack(ld16(dz + off), d);
     unpack(ld16(y + off), yv);
-    if (mode == 1) {
-      unpack(ld16(mask_src + off), m);
-#pragma unroll
-      for (int j = 0; j < E; ++j) d[j] = m[j] > 0.f ? d[j] : 0.f;
-    } else if (mode == 2) {
-#pragma unroll
-      for (int j = 0; j < E; ++j) d[j] = fmaf(yv[j], S[j], H[j]) > 0.f ? d[j] : 0.f;
-    }
+    apply_mask<T>(mode, d, yv, mask_src, mbits, off, S, H);
     float o[E];
 #pragma unroll
     for (int j = 0; j < E; ++j) o[j] = fmaf(A[j], d[j], fmaf(Bc[j], yv[j], Cc[j]));
     st16(dy + off, pack(o));
+    if constexpr (DUAL) {
+      float y2v[E];
+      unpack(ld16(y2 + off), y2v);
+#pragma unroll
+      for (int j = 0; j < E; ++j) o[j] = fmaf(A2[j], d[j], fmaf(B2[j], y2v[j], C2[j]));
+      st16(dy2 + off, pack(o));
+    }
     if (dm_out) st16(dm_out + off, pack(d));
   }
 }
@@ -453,7 +498,8 @@ int argus_bn_eval_coeffs(int C, const float* gamma, const float* beta, const flo
 }
 
 int argus_bn_apply(int dtype, int64_t pixels, int C, const void* y, const float* scale, const float* shift,
-                   const void* res, const float* rsc, const float* rsh, int relu, void* out, argus_stream_t stream) {
+                   const void* res, const float* rsc, const float* rsh, int relu, void* out, uint8_t* mask_out,
+                   argus_stream_t stream) {
   const int E = dtype == ARGUS_BF16 ? 8 : 4;
   if (C % E || pixels <= 0 || !y || !scale || !shift || !out || ((rsc == nullptr) != (rsh == nullptr)) ||
       (rsc && !res)) {
@@ -465,10 +511,10 @@ int argus_bn_apply(int dtype, int64_t pixels, int C, const void* y, const float*
   dim3 grid(g.cgroups, g.rows);
   if (dtype == ARGUS_BF16)
     hipLaunchKernelGGL(bn_apply_kernel<bf16>, grid, dim3(256), 0, st, pixels, C, g.CC, g.PL, g.ppb, (const bf16*)y,
-                       scale, shift, (const bf16*)res, rsc, rsh, relu, (bf16*)out);
+                       scale, shift, (const bf16*)res, rsc, rsh, relu, (bf16*)out, mask_out);
   else
     hipLaunchKernelGGL(bn_apply_kernel<float>, grid, dim3(256), 0, st, pixels, C, g.CC, g.PL, g.ppb, (const float*)y,
-                       scale, shift, (const float*)res, rsc, rsh, relu, (float*)out);
+                       scale, shift, (const float*)res, rsc, rsh, relu, (float*)out, mask_out);
   return check_launch("bn_apply_kernel");
 }
 
@@ -479,22 +525,34 @@ int argus_bn_bwd_rows(int64_t pixels, int C) {
   return (int)((pixels + ppb - 1) / ppb);
 }
 
-int argus_bn_bwd_reduce(int dtype, int64_t pixels, int C, const void* dz, int mode, const void* mask_src,
+int argus_bn_bwd_reduce(int dtype, int64_t pixels, int C, const void* dz, int mode, const void* mask,
                         const void* y, const float* scale, const float* shift, const float* mean,
-                        const float* invstd, float* part, argus_stream_t stream) {
+                        const float* invstd, float* part, const void* y2, const float* mean2, const float* invstd2,
+                        float* part2, argus_stream_t stream) {
   const int E = dtype == ARGUS_BF16 ? 8 : 4;
   if (C % E || pixels <= 0) { set_error("bn_bwd_reduce: bad shape"); return ARGUS_ERR_SHAPE; }
+  const bool dual = y2 != nullptr;
+  if (!dz || !y || !mean || !invstd || !part || mode < 0 || mode > 3 || ((mode == 1 || mode == 3) && !mask) ||
+      (mode == 2 && (!scale || !shift)) || (dual && (mode == 2 || !mean2 || !invstd2 || !part2))) {
+    set_error("bn_bwd_reduce: bad arguments");
+    return ARGUS_ERR_ARG;
+  }
   int CC, PL, cg, rows;
   int64_t ppb;
   bwd_geometry(C, E, pixels, CC, PL, cg, rows, ppb);
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(cg, rows);
-  if (dtype == ARGUS_BF16)
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<bf16>, grid, dim3(256), 0, st, pixels, C, CC, PL, ppb, (const bf16*)dz,
-                       mode, (const bf16*)mask_src, (const bf16*)y, scale, shift, mean, invstd, (float2*)part);
-  else
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<float>, grid, dim3(256), 0, st, pixels, C, CC, PL, ppb, (const float*)dz,
-                       mode, (const float*)mask_src, (const float*)y, scale, shift, mean, invstd, (float2*)part);
+  const uint8_t* mb = mode == 3 ? (const uint8_t*)mask : nullptr;
+#define ARGUS_BWD_REDUCE(TT, DU)                                                                                  \
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<TT, DU>), grid, dim3(256), 0, st, pixels, C, CC, PL, ppb, (const TT*)dz, \
+                     mode, mode == 1 ? (const TT*)mask : (const TT*)nullptr, mb, (const TT*)y, scale, shift, mean,     \
+                     invstd, (float2*)part, (const TT*)y2, mean2, invstd2, (float2*)part2)
+  if (dtype == ARGUS_BF16) {
+    if (dual) ARGUS_BWD_REDUCE(bf16, true); else ARGUS_BWD_REDUCE(bf16, false);
+  } else {
+    if (dual) ARGUS_BWD_REDUCE(float, true); else ARGUS_BWD_REDUCE(float, false);
+  }
+#undef ARGUS_BWD_REDUCE
   return check_launch("bn_bwd_reduce_kernel");
 }
 
@@ -510,26 +568,32 @@ int argus_bn_bwd_finalize(int C, int rows, const float* part, int64_t count, con
   return check_launch("bn_bwd_finalize_kernel");
 }
 
-int argus_bn_bwd_apply(int dtype, int64_t pixels, int C, const void* dz, int mode, const void* mask_src, const void* y,
+int argus_bn_bwd_apply(int dtype, int64_t pixels, int C, const void* dz, int mode, const void* mask, const void* y,
                        const float* scale, const float* shift, const float* ca, const float* cb, const float* cc,
-                       void* dy, void* dm_out, argus_stream_t stream) {
+                       void* dy, void* dm_out, const void* y2, const float* ca2, const float* cb2, const float* cc2,
+                       void* dy2, argus_stream_t stream) {
   const int E = dtype == ARGUS_BF16 ? 8 : 4;
-  if (C % E || pixels <= 0 || !dz || !y || !ca || !cb || !cc || !dy || (mode == 1 && !mask_src) ||
-      (mode == 2 && (!scale || !shift))) {
+  const bool dual = y2 != nullptr;
+  if (C % E || pixels <= 0 || !dz || !y || !ca || !cb || !cc || !dy || mode < 0 || mode > 3 ||
+      ((mode == 1 || mode == 3) && !mask) || (mode == 2 && (!scale || !shift)) ||
+      (dual && (mode == 2 || !ca2 || !cb2 || !cc2 || !dy2))) {
     set_error("bn_bwd_apply: bad arguments");
     return ARGUS_ERR_ARG;
   }
   const EwGeom g = ew_geom(C, E, pixels, 2048);
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(g.cgroups, g.rows);
-  if (dtype == ARGUS_BF16)
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16>, grid, dim3(256), 0, st, pixels, C, g.CC, g.PL, g.ppb,
-                       (const bf16*)dz, mode, (const bf16*)mask_src, (const bf16*)y, scale, shift, ca, cb, cc,
-                       (bf16*)dy, (bf16*)dm_out);
-  else
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, grid, dim3(256), 0, st, pixels, C, g.CC, g.PL, g.ppb,
-                       (const float*)dz, mode, (const float*)mask_src, (const float*)y, scale, shift, ca, cb, cc,
-                       (float*)dy, (float*)dm_out);
+  const uint8_t* mb = mode == 3 ? (const uint8_t*)mask : nullptr;
+#define ARGUS_BWD_APPLY(TT, DU)                                                                                      \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<TT, DU>), grid, dim3(256), 0, st, pixels, C, g.CC, g.PL, g.ppb,           \
+                     (const TT*)dz, mode, mode == 1 ? (const TT*)mask : (const TT*)nullptr, mb, (const TT*)y, scale,  \
+                     shift, ca, cb, cc, (TT*)dy, (TT*)dm_out, (const TT*)y2, ca2, cb2, cc2, (TT*)dy2)
+  if (dtype == ARGUS_BF16) {
+    if (dual) ARGUS_BWD_APPLY(bf16, true); else ARGUS_BWD_APPLY(bf16, false);
+  } else {
+    if (dual) ARGUS_BWD_APPLY(float, true); else ARGUS_BWD_APPLY(float, false);
+  }
+#undef ARGUS_BWD_APPLY
   return check_launch("bn_bwd_apply_kernel");
 }
 

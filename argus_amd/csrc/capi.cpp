@@ -61,10 +61,11 @@ int argus_conv_launch_info(const argus_conv_desc* d, int dtype, int pass, int64_
 
 int argus_conv_fwd_stat_tile(const argus_conv_desc* d, int dtype) { return d ? conv_fwd_stat_tile(*d, dtype) : 0; }
 
-int argus_conv_dgrad(const argus_conv_desc* d, int dtype, const void* dy, const void* wt, void* dx, int accumulate,
+int argus_conv_dgrad(const argus_conv_desc* d, int dtype, const void* dy, const void* wt, void* dx, const void* addend,
+                     const uint8_t* addend_mask,
                      argus_stream_t stream) {
   if (!d || !dy || !wt || !dx) { set_error("conv_dgrad: bad arguments"); return ARGUS_ERR_ARG; }
-  return conv_dgrad(*d, dtype, dy, wt, dx, accumulate, (hipStream_t)stream);
+  return conv_dgrad(*d, dtype, dy, wt, dx, addend, addend_mask, (hipStream_t)stream);
 }
 
 size_t argus_conv_wgrad_workspace_bytes(const argus_conv_desc* d, int dtype) { return d ? conv_wgrad_ws(*d, dtype) : 0; }

@@ -60,6 +60,17 @@ ARGUS_DEV u32x4 pack(const float (&f)[8]) {
   v.z = pack2_bf16(f[4], f[5]); v.w = pack2_bf16(f[6], f[7]); return v;
 }
 
+// ReLU mask of a stored chunk: bit j set <=> element j > 0 (one byte per 16-byte chunk).
+template <typename T>
+ARGUS_DEV uint8_t chunk_positive_bits(u32x4 v) {
+  float f[Chunk<T>::E];
+  unpack(v, f);
+  unsigned b = 0;
+#pragma unroll
+  for (int j = 0; j < Chunk<T>::E; ++j) b |= (f[j] > 0.f ? 1u : 0u) << j;
+  return (uint8_t)b;
+}
+
 // wave-level sum (64 lanes)
 ARGUS_DEV float wave_sum(float v) {
 #pragma unroll

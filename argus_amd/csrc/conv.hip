@@ -30,7 +30,7 @@ struct IgPhase {
   int M;          // GEMM rows of this phase = images * Hq * Wq
   int Hq, Wq;     // output grid of this phase
   int oh0, ow0;   // output pixel = (qh*osh + oh0, qw*osw + ow0)
-  int K;          // ntaps * Cin (0: this phase has no taps -> zeros / nothing to accumulate)
+  int K;          // ntaps * Cin (0: this phase has no taps -> output = addend or zeros)
   int dh[9], dw[9], boff[9];  // per tap: input offset (input = q*is + d) and B-row element offset
 };
 
@@ -41,8 +41,10 @@ struct IgParams {
   const float* pro_scale;
   const float* pro_shift;
   float2* stats;
+  const void* addend;          // C += addend (same layout as C; may alias C), masked by addend_mask
+  const uint8_t* addend_mask;  // one byte per 16-byte chunk, bit j <-> element j (bn_apply mask)
   int N, Cin, lda, H, W, ish, isw, Ho, Wo, osh, osw, ldc, ldb;
-  int accumulate, stem, nphase;
+  int stem, nphase;
   IgPhase ph[4];
 };
 
@@ -120,7 +122,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IgParams p) {
   const int ntiles = p.N / BN;
   const int nwg = mtiles * ntiles;
   if ((int)blockIdx.x >= nwg) return;
-  if (ph.K == 0 && p.accumulate) return;
+  if (ph.K == 0 && p.addend == p.c && !p.addend_mask) return;  // in-place += 0
   const int bid = xcd_remap(blockIdx.x, nwg);
   const int mt = bid / ntiles, nt = bid - mt * ntiles;
 
@@ -361,12 +363,14 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IgParams p) {
         const int oh = qh * p.osh + ph.oh0, ow = qw * p.osw + ph.ow0;
         T* dst = Cg + (((size_t)nimg * p.Ho + oh) * p.Wo + ow) * p.ldc + nt * BN + c * E;
         u32x4 v = *reinterpret_cast<const u32x4*>(Cs + rr * LD + c * E);
-        if (p.accumulate) {
+        if (p.addend) {
+          const size_t off = (size_t)(dst - Cg);
           float f[E], o[E];
           unpack(v, f);
-          unpack(ld16(dst), o);
+          unpack(ld16(reinterpret_cast<const T*>(p.addend) + off), o);
+          const unsigned mb = p.addend_mask ? p.addend_mask[off / E] : 0xffu;
 #pragma unroll
-          for (int j = 0; j < E; ++j) f[j] += o[j];
+          for (int j = 0; j < E; ++j) f[j] += (mb >> j) & 1u ? o[j] : 0.f;
           v = pack(f);
         }
         st16(dst, v);
@@ -844,7 +848,7 @@ int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, 
   p.stats = reinterpret_cast<float2*>(stats);
   p.N = d.k; p.H = d.h; p.W = d.w; p.ish = d.stride; p.isw = d.stride;
   p.Ho = d.ho; p.Wo = d.wo; p.osh = 1; p.osw = 1; p.ldc = d.k;
-  p.accumulate = 0; p.stem = d.stem; p.nphase = 1;
+  p.addend = nullptr; p.addend_mask = nullptr; p.stem = d.stem; p.nphase = 1;
   IgPhase& ph = p.ph[0];
   ph.M = d.n * d.ho * d.wo; ph.Hq = d.ho; ph.Wq = d.wo; ph.oh0 = 0; ph.ow0 = 0;
   if (d.stem) {
@@ -864,18 +868,19 @@ int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, 
 }
 
 int conv_dgrad(const argus_conv_desc& d, int dtype, const void* dy, const void* wt, void* dx,
-               int accumulate, hipStream_t st) {
+               const void* addend, const uint8_t* addend_mask, hipStream_t st) {
   if (int e = check_desc(d)) return e;
   g_launch_work = 2.0 * d.n * d.ho * d.wo * d.k * d.r * d.s * d.c;  // algorithmic flops / bytes (ktimer)
   g_launch_bytes = (double)(dtype == ARGUS_BF16 ? 2 : 4) *
                    ((double)d.n * d.ho * d.wo * d.k + (double)d.k * d.r * d.s * d.c +
-                    (accumulate ? 2.0 : 1.0) * d.n * d.h * d.w * d.c);
+                    (addend ? 2.0 : 1.0) * d.n * d.h * d.w * d.c) +
+                   (addend_mask ? (double)d.n * d.h * d.w * d.c / (dtype == ARGUS_BF16 ? 8 : 4) : 0.0);
   if (d.stem) { set_error("conv_dgrad: the stem input has no gradient"); return ARGUS_ERR_ARG; }
   IgParams p = {};
   p.a = dy; p.b = wt; p.c = dx;
   p.N = d.c; p.Cin = d.k; p.lda = d.k; p.H = d.ho; p.W = d.wo; p.ish = 1; p.isw = 1;
   p.Ho = d.h; p.Wo = d.w; p.osh = d.stride; p.osw = d.stride; p.ldc = d.c; p.ldb = d.r * d.s * d.k;
-  p.accumulate = accumulate; p.stem = 0;
+  p.addend = addend; p.addend_mask = addend_mask; p.stem = 0;
   const int s = d.stride;
   int np = 0;
   for (int phh = 0; phh < s; ++phh)

@@ -19,7 +19,7 @@ int conv_fwd_stat_tile(const argus_conv_desc& d, int dtype);
 int conv_tuning(int key, int value);
 int conv_launch_info(const argus_conv_desc& d, int dtype, int pass, int64_t* flops);
 int conv_dgrad(const argus_conv_desc& d, int dtype, const void* dy, const void* wt, void* dx,
-               int accumulate, hipStream_t st);
+               const void* addend, const uint8_t* addend_mask, hipStream_t st);
 size_t conv_wgrad_ws(const argus_conv_desc& d, int dtype);
 int conv_wgrad(const argus_conv_desc& d, int dtype, const void* x, const float* sc,
                const float* sh, const void* dy, float* dw, void* ws, size_t ws_bytes,

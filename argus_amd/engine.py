@@ -76,6 +76,7 @@ class ResNetEngine:
         self.dtype = dtype
         self.dt = BF16 if dtype == "bf16" else F32
         self.tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
+        self.E = 8 if dtype == "bf16" else 4  # elements per 16-byte chunk
         self.device = torch.device(device)
         self.blocks = resnet50_blocks()
         self.shape = None
@@ -136,6 +137,8 @@ class ResNetEngine:
                 "y1": self._t(N, h, w, b.width), "y2": self._t(N, ho, wo, b.width),
                 "y3": self._t(N, ho, wo, b.cout), "out": self._t(N, ho, wo, b.cout),
                 "yd": self._t(N, ho, wo, b.cout) if b.has_ds else None,
+                # ReLU mask of `out`, one byte per 16-byte chunk (argus_bn_apply mask_out)
+                "bits": torch.empty(N * ho * wo * b.cout // self.E, dtype=torch.uint8, device=self.device),
             }
             max_elems = max(max_elems, N * h * w * b.cin, N * h * w * b.width, N * ho * wo * b.cout)
             act.append(a)
@@ -171,6 +174,7 @@ class ResNetEngine:
                 max_bwd = max(max_bwd, L.dll.argus_bn_bwd_rows(px, c) * c)
         max_bwd = max(max_bwd, L.dll.argus_bn_bwd_rows(N * H1 * W1, 64) * 64)
         self.bwd_part = self._f(max_bwd * 2)
+        self.bwd_part2 = self._f(max_bwd * 2)  # second branch (downsample BN) of a dual reduce
         ws = max(L.dll.argus_conv_wgrad_workspace_bytes(C.byref(cv.desc), dt) for cv in convs.values())
         self.wg_ws = torch.empty(ws, dtype=torch.uint8, device=self.device)
         self.wg_ws_bytes = ws
@@ -260,10 +264,10 @@ class ResNetEngine:
                 self._conv_bn(P, Bf, pf + ".downsample.0", pf + ".downsample.1", h, a["yd"], None, training)
                 sd = self.bn_state[pf + ".downsample.1"]
                 L.bn_apply(dt, px, b.cout, ptr(a["y3"]), ptr(s3[2]), ptr(s3[3]), ptr(a["yd"]), ptr(sd[2]),
-                           ptr(sd[3]), 1, ptr(a["out"]), s)
+                           ptr(sd[3]), 1, ptr(a["out"]), ptr(a["bits"]), s)
             else:
                 L.bn_apply(dt, px, b.cout, ptr(a["y3"]), ptr(s3[2]), ptr(s3[3]), ptr(h), None, None, 1,
-                           ptr(a["out"]), s)
+                           ptr(a["out"]), ptr(a["bits"]), s)
             h = a["out"]
             if self.debug is not None:
                 self.debug["fwd." + pf] = a["out"].clone()
@@ -339,34 +343,35 @@ class ResNetEngine:
                     dbg[key + "." + pf] = t[:n].view(*shape).clone()
 
             cap("b_dout", dh, px_o * b.cout, (N, ho, wo, b.cout))
-            # bn3 (+ bnd) backward, relu mask from the block output
-            self._bn_bwd(P, G, pf + ".bn3", px_o, b.cout, dh, 1, a["out"], a["y3"], dy3,
-                         None if b.has_ds else dx)
+            # bn3 (+ downsample BN, one dual pass) backward; ReLU mask bits of the block output
             if b.has_ds:
-                self._bn_bwd(P, G, pf + ".downsample.1", px_o, b.cout, dh, 1, a["out"], a["yd"], dyd, None)
+                self._bn_bwd_dual(P, G, pf + ".bn3", pf + ".downsample.1", px_o, b.cout, dh, a["bits"], a["y3"],
+                                  a["yd"], dy3, dyd)
+            else:
+                self._bn_bwd(P, G, pf + ".bn3", px_o, b.cout, dh, 3, a["bits"], a["y3"], dy3, None)
             cap("b_dy3", dy3, px_o * b.cout, (N, ho, wo, b.cout))
             # conv3
             s2 = self.bn_state[pf + ".bn2"]
             self._wgrad(pf + ".conv3", a["y2"], s2, dy3, G)
-            self._dgrad(pf + ".conv3", dy3, dz, 0)
+            self._dgrad(pf + ".conv3", dy3, dz)
             cap("b_dz2", dz, px_o * b.width, (N, ho, wo, b.width))
             self._bn_bwd(P, G, pf + ".bn2", px_o, b.width, dz, 2, None, a["y2"], dyw, None)
             cap("b_dy2", dyw, px_o * b.width, (N, ho, wo, b.width))
             # conv2
             s1 = self.bn_state[pf + ".bn1"]
             self._wgrad(pf + ".conv2", a["y1"], s1, dyw, G)
-            self._dgrad(pf + ".conv2", dyw, dz, 0)
+            self._dgrad(pf + ".conv2", dyw, dz)
             cap("b_dz1", dz, px_i * b.width, (N, hi, wi, b.width))
             self._bn_bwd(P, G, pf + ".bn1", px_i, b.width, dz, 2, None, a["y1"], dyw, None)
             cap("b_dy1", dyw, px_i * b.width, (N, hi, wi, b.width))
             # conv1 (+ downsample)
             self._wgrad(pf + ".conv1", h_in, None, dyw, G)
             if b.has_ds:
-                self._dgrad(pf + ".conv1", dyw, dx, 0)
+                self._dgrad(pf + ".conv1", dyw, dx)
                 self._wgrad(pf + ".downsample.0", h_in, None, dyd, G)
-                self._dgrad(pf + ".downsample.0", dyd, dx, 1)
-            else:
-                self._dgrad(pf + ".conv1", dyw, dx, 1)
+                self._dgrad(pf + ".downsample.0", dyd, dx, addend=dx)
+            else:  # identity skip: dx = dgrad(conv1) + relu'(out) * dout, added in the dgrad epilogue
+                self._dgrad(pf + ".conv1", dyw, dx, addend=dh, mask=a["bits"])
             dh, dx = dx, dh
             if on_ready is not None:
                 on_ready(pf + ".conv1.weight")
@@ -387,13 +392,30 @@ class ResNetEngine:
         L, dt, s = self.L, self.dt, stream()
         st, cf = self.bn_state[name], self.bn_coef[name]
         L.bn_bwd_reduce(dt, px, ch, ptr(dz), mode, ptr(mask_src), ptr(y), ptr(st[2]), ptr(st[3]), ptr(st[0]),
-                        ptr(st[1]), ptr(self.bwd_part), s)
-        rows = L.dll.argus_bn_bwd_rows(px, ch)
-        L.bn_bwd_finalize(ch, rows, ptr(self.bwd_part), px, ptr(P[name + ".weight"]), ptr(st[0]), ptr(st[1]),
-                          ptr(G[name + ".weight"]), ptr(G[name + ".bias"]), ptr(cf[0]), ptr(cf[1]), ptr(cf[2]),
-                          ptr(self.bn_ws), s)
+                        ptr(st[1]), ptr(self.bwd_part), None, None, None, None, s)
+        self._bn_bwd_fin(P, G, name, px, ch, self.bwd_part)
         L.bn_bwd_apply(dt, px, ch, ptr(dz), mode, ptr(mask_src), ptr(y), ptr(st[2]), ptr(st[3]), ptr(cf[0]),
-                       ptr(cf[1]), ptr(cf[2]), ptr(dy_out), ptr(dm_out), s)
+                       ptr(cf[1]), ptr(cf[2]), ptr(dy_out), ptr(dm_out), None, None, None, None, None, s)
+
+    def _bn_bwd_fin(self, P, G, name, px, ch, part):
+        st, cf = self.bn_state[name], self.bn_coef[name]
+        rows = self.L.dll.argus_bn_bwd_rows(px, ch)
+        self.L.bn_bwd_finalize(ch, rows, ptr(part), px, ptr(P[name + ".weight"]), ptr(st[0]), ptr(st[1]),
+                               ptr(G[name + ".weight"]), ptr(G[name + ".bias"]), ptr(cf[0]), ptr(cf[1]), ptr(cf[2]),
+                               ptr(self.bn_ws), stream())
+
+    def _bn_bwd_dual(self, P, G, name, name2, px, ch, dz, bits, y, y2, dy_out, dy2_out):
+        """bn3 and the downsample BN of a bottleneck: both outputs were summed before the block ReLU,
+        so they share dm = relu'(out) * dout; one reduce pass and one apply pass serve both."""
+        L, dt, s = self.L, self.dt, stream()
+        st, st2 = self.bn_state[name], self.bn_state[name2]
+        L.bn_bwd_reduce(dt, px, ch, ptr(dz), 3, ptr(bits), ptr(y), None, None, ptr(st[0]), ptr(st[1]),
+                        ptr(self.bwd_part), ptr(y2), ptr(st2[0]), ptr(st2[1]), ptr(self.bwd_part2), s)
+        self._bn_bwd_fin(P, G, name, px, ch, self.bwd_part)
+        self._bn_bwd_fin(P, G, name2, px, ch, self.bwd_part2)
+        cf, cf2 = self.bn_coef[name], self.bn_coef[name2]
+        L.bn_bwd_apply(dt, px, ch, ptr(dz), 3, ptr(bits), ptr(y), None, None, ptr(cf[0]), ptr(cf[1]), ptr(cf[2]),
+                       ptr(dy_out), None, ptr(y2), ptr(cf2[0]), ptr(cf2[1]), ptr(cf2[2]), ptr(dy2_out), s)
 
     def _wgrad(self, conv, x, pro_state, dy, G):
         cv = self.convs[conv]
@@ -404,10 +426,10 @@ class ResNetEngine:
                                                        ptr(G[conv + ".weight"]), ptr(self.wg_ws), self.wg_ws_bytes,
                                                        stream()))
 
-    def _dgrad(self, conv, dy, dx, accumulate):
+    def _dgrad(self, conv, dy, dx, addend=None, mask=None):
         cv = self.convs[conv]
         self._launch(cv, 1, lambda: self.L.conv_dgrad(C.byref(cv.desc), self.dt, ptr(dy), ptr(cv.wd), ptr(dx),
-                                                       accumulate, stream()))
+                                                       ptr(addend), ptr(mask), stream()))
 
     @staticmethod
     def _launch(cv, pass_, fn):

@@ -68,9 +68,11 @@ int argus_conv_fwd(const argus_conv_desc* d, int dtype, const void* x, const voi
                    argus_stream_t stream);
 int argus_conv_fwd_stat_rows(const argus_conv_desc* d, int dtype);
 int argus_conv_fwd_stat_tile(const argus_conv_desc* d, int dtype);
-/* dx (+)= dgrad(dy, w_dgrad); accumulate != 0 adds into dx. */
+/* dx = dgrad(dy, w_dgrad) [+ addend]: when addend != NULL (same NHWC layout as dx; may be dx itself
+ * for in-place accumulation) it is added, element-wise masked by addend_mask when that is non-NULL
+ * (the bn_apply ReLU mask: the residual path of a bottleneck, dx += relu'(out) * dout). */
 int argus_conv_dgrad(const argus_conv_desc* d, int dtype, const void* dy, const void* w_dgrad,
-                     void* dx, int accumulate, argus_stream_t stream);
+                     void* dx, const void* addend, const uint8_t* addend_mask, argus_stream_t stream);
 /* Tuning knobs (process-wide; for autotuning / experiments): key 0..2 force the row tile (64|128,
  * 0 = heuristic) of pass fwd/dgrad/wgrad, key 3..5 force the column tile, key 6 sets the wgrad
  * split target (workgroups). Returns 0, or -1 for an unknown key. */
@@ -116,17 +118,25 @@ int argus_bn_eval_coeffs(int channels, const float* gamma, const float* beta,
                          const float* running_mean, const float* running_var, float eps,
                          float* scale, float* shift, argus_stream_t stream);
 /* out = [relu]( y*scale+shift + residual' ), residual' = res*res_scale+res_shift (if res_scale),
- * res (if res), else 0. out may alias y. */
+ * res (if res), else 0. out may alias y. If mask_out != NULL it also receives the ReLU mask of out:
+ * one byte per 16-byte chunk (8 bf16 / 4 fp32 channels), bit j set <=> element j of the chunk > 0,
+ * i.e. mask_out[(pixel*channels + c) / E] bit (c % E). */
 int argus_bn_apply(int dtype, int64_t pixels, int channels, const void* y, const float* scale,
                    const float* shift, const void* res, const float* res_scale,
-                   const float* res_shift, int relu, void* out, argus_stream_t stream);
-/* Backward. mask_mode: 0 none; 1 relu mask from `mask_src` (>0, e.g. a block output);
- * 2 relu mask recomputed from y as (y*scale+shift > 0). dm = dz*mask.
- * reduce: part float2[rows][C] = {sum dm, sum dm*(y-mean)*invstd}; rows = argus_bn_bwd_rows(). */
+                   const float* res_shift, int relu, void* out, uint8_t* mask_out,
+                   argus_stream_t stream);
+/* Backward. mask_mode: 0 none; 1 relu mask from the tensor `mask` (>0, e.g. a block output);
+ * 2 relu mask recomputed from y as (y*scale+shift > 0); 3 relu mask from the bits `mask` written
+ * by argus_bn_apply. dm = dz*mask.
+ * reduce: part float2[rows][C] = {sum dm, sum dm*(y-mean)*invstd}; rows = argus_bn_bwd_rows().
+ * Optional second branch (y2 != NULL; modes 0/1/3): a second BN whose output was summed with the
+ * first before the same ReLU (bn3 + the downsample BN of a bottleneck) shares dm, so both are
+ * reduced / applied in one pass: part2 = {sum dm, sum dm*(y2-mean2)*invstd2}, dy2 = ca2*dm + cb2*y2 + cc2. */
 int argus_bn_bwd_rows(int64_t pixels, int channels);
 int argus_bn_bwd_reduce(int dtype, int64_t pixels, int channels, const void* dz, int mask_mode,
-                        const void* mask_src, const void* y, const float* scale,
+                        const void* mask, const void* y, const float* scale,
                         const float* shift, const float* mean, const float* invstd, float* part,
+                        const void* y2, const float* mean2, const float* invstd2, float* part2,
                         argus_stream_t stream);
 /* dgamma/dbeta (fp32, written) and coefficients so that dy = ca*dm + cb*y + cc. */
 int argus_bn_bwd_finalize(int channels, int rows, const float* part, int64_t count,
@@ -135,8 +145,9 @@ int argus_bn_bwd_finalize(int channels, int rows, const float* part, int64_t cou
                           void* workspace, argus_stream_t stream);
 /* dy = ca*dm + cb*y + cc (dtype); if dm_out != NULL also writes dm (the masked dz). */
 int argus_bn_bwd_apply(int dtype, int64_t pixels, int channels, const void* dz, int mask_mode,
-                       const void* mask_src, const void* y, const float* scale, const float* shift,
+                       const void* mask, const void* y, const float* scale, const float* shift,
                        const float* ca, const float* cb, const float* cc, void* dy, void* dm_out,
+                       const void* y2, const float* ca2, const float* cb2, const float* cc2, void* dy2,
                        argus_stream_t stream);
 
 /* ---- pooling (MaxPool2d(3,2,1) fused with the stem's BN+ReLU; AdaptiveAvgPool2d(1)) ----------- */

@@ -97,7 +97,7 @@ def test_conv_fwd_dgrad_wgrad_all_shapes(cuda, dt):
         # dgrad (accumulate onto a non-zero buffer to check both modes)
         dx0 = torch.randn(n, hin, hin, cin)
         dx = dx0.to(cuda, TDT[dt])
-        L.conv_dgrad(C.byref(d), DT[dt], ptr(dyd), ptr(wt), ptr(dx), 1, stream())
+        L.conv_dgrad(C.byref(d), DT[dt], ptr(dyd), ptr(wt), ptr(dx), ptr(dx), None, stream())
         refd = torch.nn.grad.conv2d_input(xr.shape, wr, dyr, stride=s, padding=p) + _q(dx0, dt).permute(0, 3, 1, 2)
         e = _rel(dx.permute(0, 3, 1, 2), refd)
         assert e < TOL[dt], f"dgrad {cin}->{cout} k{k} s{s} {dt}: {e}"
@@ -211,8 +211,13 @@ def test_bn_train_forward_backward(cuda, dt):
     yd = y.to(cuda, TDT[dt])
     o = torch.empty_like(yd)
     resg = res.to(cuda, TDT[dt])
-    L.bn_apply(DT[dt], px, c, ptr(yd), ptr(stt[2]), ptr(stt[3]), ptr(resg), None, None, 1, ptr(o), stream())
+    E = 8 if dt == "bf16" else 4
+    bits = torch.empty(px * c // E, dtype=torch.uint8, device=cuda)
+    L.bn_apply(DT[dt], px, c, ptr(yd), ptr(stt[2]), ptr(stt[3]), ptr(resg), None, None, 1, ptr(o), ptr(bits),
+               stream())
     assert _rel(o.permute(0, 3, 1, 2), out) < TOL[dt]
+    want_bits = ((o.reshape(-1, E) > 0).int() << torch.arange(E, device=cuda)).sum(1).to(torch.uint8)
+    assert torch.equal(bits, want_bits), "ReLU mask bits"
     # backward: mask from the block output (mode 1), dm_out = masked grad
     dout = torch.randn(n, h, w, c)
     doutq = _q(dout, dt)
@@ -220,18 +225,28 @@ def test_bn_train_forward_backward(cuda, dt):
     bpart = torch.empty(L.dll.argus_bn_bwd_rows(px, c), c, 2, device=cuda)
     doutg = dout.to(cuda, TDT[dt])
     L.bn_bwd_reduce(DT[dt], px, c, ptr(doutg), 1, ptr(o), ptr(yd), ptr(stt[2]), ptr(stt[3]),
-                    ptr(stt[0]), ptr(stt[1]), ptr(bpart), stream())
+                    ptr(stt[0]), ptr(stt[1]), ptr(bpart), None, None, None, None, stream())
     dg, db = torch.empty(c, device=cuda), torch.empty(c, device=cuda)
     cf = torch.empty(3, c, device=cuda)
     L.bn_bwd_finalize(c, bpart.shape[0], ptr(bpart), px, ptr(gd), ptr(stt[0]), ptr(stt[1]), ptr(dg), ptr(db),
                       ptr(cf[0]), ptr(cf[1]), ptr(cf[2]), ptr(ws), stream())
     dyo, dmo = torch.empty_like(yd), torch.empty_like(yd)
     L.bn_bwd_apply(DT[dt], px, c, ptr(doutg), 1, ptr(o), ptr(yd), ptr(stt[2]), ptr(stt[3]), ptr(cf[0]),
-                   ptr(cf[1]), ptr(cf[2]), ptr(dyo), ptr(dmo), stream())
+                   ptr(cf[1]), ptr(cf[2]), ptr(dyo), ptr(dmo), None, None, None, None, None, stream())
     tol = TOL[dt] * (3 if dt == "bf16" else 1)
     assert _rel(dg, bn.weight.grad) < tol, "dgamma"
     assert _rel(db, bn.bias.grad) < tol, "dbeta"
     assert _rel(dyo.permute(0, 3, 1, 2), xin.grad) < tol * 2, "dx"
+    # mode 3 (mask bits) gives exactly mode 1's results
+    bpart3, dg3, db3, cf3 = torch.empty_like(bpart), torch.empty_like(dg), torch.empty_like(db), torch.empty_like(cf)
+    dyo3 = torch.empty_like(yd)
+    L.bn_bwd_reduce(DT[dt], px, c, ptr(doutg), 3, ptr(bits), ptr(yd), None, None,
+                    ptr(stt[0]), ptr(stt[1]), ptr(bpart3), None, None, None, None, stream())
+    L.bn_bwd_finalize(c, bpart.shape[0], ptr(bpart3), px, ptr(gd), ptr(stt[0]), ptr(stt[1]), ptr(dg3), ptr(db3),
+                      ptr(cf3[0]), ptr(cf3[1]), ptr(cf3[2]), ptr(ws), stream())
+    L.bn_bwd_apply(DT[dt], px, c, ptr(doutg), 3, ptr(bits), ptr(yd), None, None, ptr(cf3[0]),
+                   ptr(cf3[1]), ptr(cf3[2]), ptr(dyo3), None, None, None, None, None, None, stream())
+    assert torch.equal(bpart3, bpart) and torch.equal(dyo3, dyo), "mode 3 == mode 1"
     # mode 2 (relu mask recomputed from y via scale/shift)
     xin2 = yq.permute(0, 3, 1, 2).clone().requires_grad_(True)
     bn2 = torch.nn.BatchNorm2d(c).double()
@@ -240,13 +255,86 @@ def test_bn_train_forward_backward(cuda, dt):
         bn2.bias.copy_(beta)
     torch.relu(bn2(xin2)).backward(doutq.permute(0, 3, 1, 2))
     L.bn_bwd_reduce(DT[dt], px, c, ptr(doutg), 2, None, ptr(yd), ptr(stt[2]), ptr(stt[3]),
-                    ptr(stt[0]), ptr(stt[1]), ptr(bpart), stream())
+                    ptr(stt[0]), ptr(stt[1]), ptr(bpart), None, None, None, None, stream())
     L.bn_bwd_finalize(c, bpart.shape[0], ptr(bpart), px, ptr(gd), ptr(stt[0]), ptr(stt[1]), ptr(dg), ptr(db),
                       ptr(cf[0]), ptr(cf[1]), ptr(cf[2]), ptr(ws), stream())
     L.bn_bwd_apply(DT[dt], px, c, ptr(doutg), 2, None, ptr(yd), ptr(stt[2]), ptr(stt[3]), ptr(cf[0]),
-                   ptr(cf[1]), ptr(cf[2]), ptr(dyo), None, stream())
+                   ptr(cf[1]), ptr(cf[2]), ptr(dyo), None, None, None, None, None, None, stream())
     assert _rel(dyo.permute(0, 3, 1, 2), xin2.grad) < tol * 2, "dx mode 2"
     assert _rel(dg, bn2.weight.grad) < tol, "dgamma mode 2"
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+def test_bn_dual_branch_backward(cuda, dt):
+    """out = relu(bnA(y) + bnB(y2)) (bn3 + downsample BN): one dual reduce/apply pass with mask bits
+    vs autograd, and the masked residual addend of conv_dgrad."""
+    torch.manual_seed(5)
+    L = lib()
+    n, h, w, c = 3, 6, 5, 128
+    px = n * h * w
+    E = 8 if dt == "bf16" else 4
+    ya, yb = _q(torch.randn(n, h, w, c) * 1.5 + 0.3, dt), _q(torch.randn(n, h, w, c) - 0.2, dt)
+    gA, bA, gB, bB = torch.rand(c) + 0.5, torch.randn(c), torch.rand(c) + 0.5, torch.randn(c)
+    ws = torch.empty(L.dll.argus_bn_workspace_bytes(c), dtype=torch.uint8, device=cuda)
+
+    def finalize(yq, g, b):
+        yy = yq.reshape(px, c).reshape(-1, 5, c)
+        part = torch.stack([yy.sum(1), ((yy - yy.mean(1, keepdim=True)) ** 2).sum(1)], -1).float().to(cuda)
+        stt = torch.empty(4, c, device=cuda)
+        L.bn_finalize(c, part.shape[0], 5, ptr(part), px, ptr(g), ptr(b), C.c_float(1e-5), C.c_float(0.1), None,
+                      None, None, ptr(stt[0]), ptr(stt[1]), ptr(stt[2]), ptr(stt[3]), ptr(ws), stream())
+        return stt
+
+    gAd, bAd, gBd, bBd = gA.to(cuda), bA.to(cuda), gB.to(cuda), bB.to(cuda)
+    sA, sB = finalize(ya, gAd, bAd), finalize(yb, gBd, bBd)
+    yad, ybd = ya.to(cuda, TDT[dt]), yb.to(cuda, TDT[dt])
+    o = torch.empty_like(yad)
+    bits = torch.empty(px * c // E, dtype=torch.uint8, device=cuda)
+    L.bn_apply(DT[dt], px, c, ptr(yad), ptr(sA[2]), ptr(sA[3]), ptr(ybd), ptr(sB[2]), ptr(sB[3]), 1, ptr(o),
+               ptr(bits), stream())
+    bnA, bnB = torch.nn.BatchNorm2d(c).double(), torch.nn.BatchNorm2d(c).double()
+    with torch.no_grad():
+        bnA.weight.copy_(gA); bnA.bias.copy_(bA); bnB.weight.copy_(gB); bnB.bias.copy_(bB)
+    xa = ya.permute(0, 3, 1, 2).double().requires_grad_(True)
+    xb = yb.permute(0, 3, 1, 2).double().requires_grad_(True)
+    out = torch.relu(bnA(xa) + bnB(xb))
+    assert _rel(o.permute(0, 3, 1, 2), out) < TOL[dt]
+    dout = _q(torch.randn(n, h, w, c), dt)
+    out.backward(dout.permute(0, 3, 1, 2).double())
+    doutg = dout.to(cuda, TDT[dt])
+    rows = L.dll.argus_bn_bwd_rows(px, c)
+    pA, pB = torch.empty(rows, c, 2, device=cuda), torch.empty(rows, c, 2, device=cuda)
+    L.bn_bwd_reduce(DT[dt], px, c, ptr(doutg), 3, ptr(bits), ptr(yad), None, None, ptr(sA[0]), ptr(sA[1]), ptr(pA),
+                    ptr(ybd), ptr(sB[0]), ptr(sB[1]), ptr(pB), stream())
+    grads = {}
+    for nm, part, g, st in (("A", pA, gAd, sA), ("B", pB, gBd, sB)):
+        dg, db, cf = torch.empty(c, device=cuda), torch.empty(c, device=cuda), torch.empty(3, c, device=cuda)
+        L.bn_bwd_finalize(c, rows, ptr(part), px, ptr(g), ptr(st[0]), ptr(st[1]), ptr(dg), ptr(db), ptr(cf[0]),
+                          ptr(cf[1]), ptr(cf[2]), ptr(ws), stream())
+        grads[nm] = (dg, db, cf)
+    dya, dyb = torch.empty_like(yad), torch.empty_like(yad)
+    cfa, cfb = grads["A"][2], grads["B"][2]
+    L.bn_bwd_apply(DT[dt], px, c, ptr(doutg), 3, ptr(bits), ptr(yad), None, None, ptr(cfa[0]), ptr(cfa[1]),
+                   ptr(cfa[2]), ptr(dya), None, ptr(ybd), ptr(cfb[0]), ptr(cfb[1]), ptr(cfb[2]), ptr(dyb), stream())
+    tol = TOL[dt] * (3 if dt == "bf16" else 1)
+    assert _rel(grads["A"][0], bnA.weight.grad) < tol and _rel(grads["A"][1], bnA.bias.grad) < tol
+    assert _rel(grads["B"][0], bnB.weight.grad) < tol and _rel(grads["B"][1], bnB.bias.grad) < tol
+    assert _rel(dya.permute(0, 3, 1, 2), xa.grad) < tol * 2 and _rel(dyb.permute(0, 3, 1, 2), xb.grad) < tol * 2
+    # masked residual addend in the dgrad epilogue: dx = dgrad(dy) + relu'(out) * dout
+    d, p = _desc(n, h, w, 64, c, 1, 1)
+    wt = torch.randn(c, 1, 1, 64) * 0.1
+    wf, wdg = _prep(d, dt, wt.to(cuda), cuda)
+    dyc = _q(torch.randn(n, h, w, c), dt)
+    dycg = dyc.to(cuda, TDT[dt])
+    dx = torch.empty(n, h, w, 64, dtype=TDT[dt], device=cuda)
+    res = _q(torch.randn(n, h, w, 64), dt)
+    resg = res.to(cuda, TDT[dt])
+    keep = res.float() > 0.3  # one fp32 mask for both the bits and the reference
+    rbits = ((keep.reshape(-1, E).int() << torch.arange(E)).sum(1)).to(torch.uint8).to(cuda)
+    L.conv_dgrad(C.byref(d), DT[dt], ptr(dycg), ptr(wdg), ptr(dx), ptr(resg), ptr(rbits), stream())
+    ref = torch.nn.grad.conv2d_input((n, 64, h, w), _q(wt, dt).permute(0, 3, 1, 2), dyc.permute(0, 3, 1, 2))
+    ref = ref + (res * keep).permute(0, 3, 1, 2)
+    assert _rel(dx.permute(0, 3, 1, 2), ref) < TOL[dt]
 
 
 @pytest.mark.parametrize("dt", ["fp32", "bf16"])

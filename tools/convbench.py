@@ -49,7 +49,7 @@ def main():
             2: lambda: L.conv_wgrad(C.byref(d), dt, ptr(x), None, None, ptr(dy), ptr(dw), ptr(ws), ws.numel(), stream()),
         }
         if not d.stem:
-            fns[1] = lambda: L.conv_dgrad(C.byref(d), dt, ptr(dy), ptr(wd), ptr(dx), 0, stream())
+            fns[1] = lambda: L.conv_dgrad(C.byref(d), dt, ptr(dy), ptr(wd), ptr(dx), None, None, stream())
         row = [name]
         for ps, fn in fns.items():
             with KernelTimer() as kt:

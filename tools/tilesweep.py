@@ -67,7 +67,7 @@ def main():
                     if ps == 0:
                         fn = lambda: L.conv_fwd(C.byref(d), dt, ptr(x), ptr(cv.wf), ptr(y), None, None, ptr(st), stream())
                     elif ps == 1:
-                        fn = lambda: L.conv_dgrad(C.byref(d), dt, ptr(dy), ptr(cv.wd), ptr(dx), 0, stream())
+                        fn = lambda: L.conv_dgrad(C.byref(d), dt, ptr(dy), ptr(cv.wd), ptr(dx), None, None, stream())
                     else:
                         wsb = L.dll.argus_conv_wgrad_workspace_bytes(C.byref(d), dt)
                         ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
