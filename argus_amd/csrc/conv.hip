@@ -108,13 +108,17 @@ template <typename T> struct ProCoef {
 // Returns the LDS element stride of a staged row.
 template <typename T, int BN> constexpr int epi_ld() { return BN + 16 / (int)sizeof(T); }
 
-template <typename T, int BM, int BN, bool STEM, bool PRO>
-__global__ __launch_bounds__(256, 2) void igemm_kernel(const IgParams p) {
+// OCC = workgroups per CU the kernel is built for: 2 -> double-buffered LDS + 2-deep register
+// prefetch ring (deep-K GEMMs); 3 or 4 -> one LDS buffer, no ring, <= 168 / 128 VGPRs (K <= 2
+// k-steps: the 1x1 convs whose time is load/epilogue latency, hidden by more resident workgroups).
+template <typename T, int BM, int BN, bool STEM, bool PRO, int OCC>
+__global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
   constexpr int E = Chunk<T>::E;
   constexpr int BKE = 8 * E;  // K elements per k-step (8 chunks of 16 B per LDS row)
   constexpr int MI = BM / 32, NI = BN / 32;
   constexpr int AR = BM / 32, BR = BN / 32;
-  constexpr int LDS_BYTES = 2 * (BM + BN) * 128;
+  constexpr int NBUF = OCC >= 3 ? 1 : 2;
+  constexpr int LDS_BYTES = NBUF * (BM + BN) * 128;
   __shared__ __attribute__((aligned(16))) u32x4 lds[LDS_BYTES / 16];
 
   const IgPhase& ph = p.ph[blockIdx.z];
@@ -257,7 +261,16 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const IgParams p) {
   // Main loop: LDS double buffer + 2-deep register prefetch ring (S0/S1). At the MFMAs of step kt,
   // the global loads of steps kt+1 and kt+2 are in flight.
   const int nk = ph.K / BKE;
-  if (nk > 0) {
+  if constexpr (NBUF == 1) {
+    for (int kt = 0; kt < nk; ++kt) {
+      Stage S0;
+      load(kt, S0);
+      store(0, S0);
+      __syncthreads();
+      compute(0);
+      __syncthreads();
+    }
+  } else if (nk > 0) {
     Stage S0, S1;
     load(0, S0);
     store(0, S0);
@@ -756,43 +769,54 @@ static int check_desc(const argus_conv_desc& d) {
   return ARGUS_OK;
 }
 
-template <typename T, int BM, int BN, bool STEM, bool PRO>
+template <typename T, int BM, int BN, bool STEM, bool PRO, int OCC>
 static const char* ig_name() {
   static const std::string s = std::string("argus::igemm_kernel<") + type_name<T>() + ", " + std::to_string(BM) +
-                               ", " + std::to_string(BN) + ", " + bool_name(STEM) + ", " + bool_name(PRO) + ">";
+                               ", " + std::to_string(BN) + ", " + bool_name(STEM) + ", " + bool_name(PRO) + ", " +
+                               std::to_string(OCC) + ">";
   return s.c_str();
 }
 
-template <typename T, int BM, int BN, bool STEM, bool PRO>
+template <typename T, int BM, int BN, bool STEM, bool PRO, int OCC>
 static void launch_ig(const IgParams& p, int maxM, hipStream_t st) {
   const int ntiles = p.N / BN;
   dim3 grid(cdiv(maxM, BM) * ntiles, 1, p.nphase);
-  timed_launch(ig_name<T, BM, BN, STEM, PRO>(), igemm_kernel<T, BM, BN, STEM, PRO>, grid, dim3(256), st, p);
+  timed_launch(ig_name<T, BM, BN, STEM, PRO, OCC>(), igemm_kernel<T, BM, BN, STEM, PRO, OCC>, grid, dim3(256), st,
+               p);
 }
 
-template <typename T, bool PRO>
+template <typename T, bool PRO, int OCC>
 static void dispatch_ig(const IgParams& p, int maxM, int bm, int bn, hipStream_t st) {
   const bool bn128 = bn == 128;
   if (bm == 128) {
-    if (bn128) launch_ig<T, 128, 128, false, PRO>(p, maxM, st);
-    else launch_ig<T, 128, 64, false, PRO>(p, maxM, st);
+    // the single-buffer 128x128 tile needs > 128 VGPRs: 3 workgroups per CU instead of 4
+    if (bn128) launch_ig<T, 128, 128, false, PRO, (OCC == 4 ? 3 : OCC)>(p, maxM, st);
+    else launch_ig<T, 128, 64, false, PRO, OCC>(p, maxM, st);
   } else {
-    if (bn128) launch_ig<T, 64, 128, false, PRO>(p, maxM, st);
-    else launch_ig<T, 64, 64, false, PRO>(p, maxM, st);
+    if (bn128) launch_ig<T, 64, 128, false, PRO, OCC>(p, maxM, st);
+    else launch_ig<T, 64, 64, false, PRO, OCC>(p, maxM, st);
   }
 }
 
+static int g_smallk_max = 128;  // argus_conv_tuning key 7: largest K (elements) served by the OCC=4 kernel
+
 template <typename T>
 static int run_ig(const IgParams& p, hipStream_t st, int bm, int bn) {
-  int maxM = 0;
-  for (int i = 0; i < p.nphase; ++i) maxM = p.ph[i].M > maxM ? p.ph[i].M : maxM;
+  int maxM = 0, maxK = 0;
+  for (int i = 0; i < p.nphase; ++i) {
+    maxM = p.ph[i].M > maxM ? p.ph[i].M : maxM;
+    maxK = p.ph[i].K > maxK ? p.ph[i].K : maxK;
+  }
+  const bool smallk = maxK <= g_smallk_max;
   if (p.stem) {
     if (p.N != 64 || bm != 128) { set_error("igemm: stem expects 64 output channels"); return ARGUS_ERR_SHAPE; }
-    launch_ig<T, 128, 64, true, false>(p, maxM, st);
+    launch_ig<T, 128, 64, true, false, 2>(p, maxM, st);
   } else if (p.pro_scale) {
-    dispatch_ig<T, true>(p, maxM, bm, bn, st);
+    if (smallk) dispatch_ig<T, true, 4>(p, maxM, bm, bn, st);
+    else dispatch_ig<T, true, 2>(p, maxM, bm, bn, st);
   } else {
-    dispatch_ig<T, false>(p, maxM, bm, bn, st);
+    if (smallk) dispatch_ig<T, false, 4>(p, maxM, bm, bn, st);
+    else dispatch_ig<T, false, 2>(p, maxM, bm, bn, st);
   }
   return check_launch("igemm_kernel");
 }
@@ -806,6 +830,7 @@ int conv_tuning(int key, int value) {
   if (key >= 0 && key < 3) { g_force_bm[key] = value; return 0; }
   if (key >= 3 && key < 6) { g_force_bn[key - 3] = value; return 0; }
   if (key == 6) { g_wgrad_target_blocks = value; return 0; }
+  if (key == 7) { g_smallk_max = value; return 0; }
   return -1;
 }
 

@@ -75,7 +75,8 @@ int argus_conv_dgrad(const argus_conv_desc* d, int dtype, const void* dy, const 
                      void* dx, const void* addend, const uint8_t* addend_mask, argus_stream_t stream);
 /* Tuning knobs (process-wide; for autotuning / experiments): key 0..2 force the row tile (64|128,
  * 0 = heuristic) of pass fwd/dgrad/wgrad, key 3..5 force the column tile, key 6 sets the wgrad
- * split target (workgroups). Returns 0, or -1 for an unknown key. */
+ * split target (workgroups), key 7 the largest K (= taps*C) served by the 4-workgroups-per-CU
+ * single-buffer forward/dgrad kernel (default 128). Returns 0, or -1 for an unknown key. */
 int argus_conv_tuning(int key, int value);
 /* Which tile a pass launches and its algorithmic work: pass 0 fwd, 1 dgrad, 2 wgrad. Returns a
  * tag (kind*10^7 + dtype*10^6 + tile_m*1000 + tile_n; kind 1 igemm, 2 wgrad) and writes

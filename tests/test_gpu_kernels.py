@@ -487,7 +487,7 @@ def test_kernel_timer_records_exact_instantiations(cuda):
     fl = C.c_int64()
     tag = L.dll.argus_conv_launch_info(C.byref(d), BF16, 0, C.byref(fl))
     bm, bn = divmod(tag % 1000000, 1000)
-    assert name == f"argus::igemm_kernel<__bf16, {bm}, {bn}, false, false>"
+    assert name == f"argus::igemm_kernel<__bf16, {bm}, {bn}, false, false, 2>"  # K = 576 > 128: OCC 2
     assert v["launches"] == 3 and v["flops_per_launch"] == fl.value and v["avg_us"] > 0
     assert v["bytes_per_launch"] == 2 * (4 * 32 * 32 * 64 + 128 * 9 * 64 + 4 * 32 * 32 * 128)
     with KernelTimer("argus::wgrad") as t:  # filtered out: nothing recorded
