@@ -19,6 +19,8 @@ namespace argus {
 
 constexpr int kWave = 64;
 
+static inline __host__ __device__ int cdiv(int a, int b) { return (a + b - 1) / b; }
+
 ARGUS_DEV float to_f32(float x) { return x; }
 ARGUS_DEV float to_f32(bf16 x) { return (float)x; }
 template <typename T> ARGUS_DEV T from_f32(float x);

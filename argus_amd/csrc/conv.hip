@@ -20,51 +20,13 @@
 #include "common.h"
 #include "internal.h"
 #include "ktimer.h"
+#include "igemm.h"
 
 namespace argus {
 
 // ------------------------------------------------------------------------------------------------
 // implicit GEMM (forward / dgrad)
 // ------------------------------------------------------------------------------------------------
-struct IgPhase {
-  int M;          // GEMM rows of this phase = images * Hq * Wq
-  int Hq, Wq;     // output grid of this phase
-  int oh0, ow0;   // output pixel = (qh*osh + oh0, qw*osw + ow0)
-  int K;          // ntaps * Cin (0: this phase has no taps -> output = addend or zeros)
-  int dh[9], dw[9], boff[9];  // per tap: input offset (input = q*is + d) and B-row element offset
-};
-
-struct IgParams {
-  const void* a;
-  const void* b;
-  void* c;
-  const float* pro_scale;
-  const float* pro_shift;
-  float2* stats;
-  const void* addend;          // C += addend (same layout as C; may alias C), masked by addend_mask
-  const uint8_t* addend_mask;  // one byte per 16-byte chunk, bit j <-> element j (bn_apply mask)
-  int N, Cin, lda, H, W, ish, isw, Ho, Wo, osh, osw, ldc, ldb;
-  int stem, nphase;
-  IgPhase ph[4];
-};
-
-template <typename T> struct Mma;
-template <> struct Mma<bf16> {
-  static ARGUS_DEV void run(f32x4& acc, u32x4 a, u32x4 b) {
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
-                                                  __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
-  }
-};
-template <> struct Mma<float> {
-  // lane group g supplies k = 4g + j at sub-step j (same mapping for A and B)
-  static ARGUS_DEV void run(f32x4& acc, u32x4 a, u32x4 b) {
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.x), __uint_as_float(b.x), acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.y), __uint_as_float(b.y), acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.z), __uint_as_float(b.z), acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), acc, 0, 0, 0);
-  }
-};
-
 template <typename T>
 ARGUS_DEV u32x4 bn_relu_chunk(u32x4 v, const float* __restrict__ sc, const float* __restrict__ sh, int ch) {
   constexpr int E = Chunk<T>::E;
@@ -73,13 +35,6 @@ ARGUS_DEV u32x4 bn_relu_chunk(u32x4 v, const float* __restrict__ sc, const float
 #pragma unroll
   for (int j = 0; j < E; ++j) f[j] = fmaxf(fmaf(f[j], sc[ch + j], sh[ch + j]), 0.f);
   return pack(f);
-}
-
-ARGUS_DEV int swz8(int row) { return (row >> 1) & 7; }
-
-ARGUS_DEV u32x4 sel(bool ok, u32x4 v) {
-  const u32x4 z = {0u, 0u, 0u, 0u};
-  return ok ? v : z;
 }
 
 // Per-thread BN+ReLU coefficients for one 16-byte chunk of channels.
@@ -742,7 +697,6 @@ __global__ __launch_bounds__(256) void weight_prep_kernel(const float* __restric
 // ------------------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------------------
-static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
 static int check_desc(const argus_conv_desc& d) {
   if (d.n <= 0 || d.h <= 0 || d.w <= 0 || d.k <= 0 || d.r <= 0 || d.s <= 0 || d.stride <= 0) {
@@ -798,6 +752,8 @@ static void dispatch_ig(const IgParams& p, int maxM, int bm, int bn, hipStream_t
   }
 }
 
+extern int g_glds_min_k, g_glds_min_grid;  // conv_glds.hip
+extern int g_halo_enable;                  // conv_halo.hip
 static int g_smallk_max = 128;  // argus_conv_tuning key 7: largest K (elements) served by the OCC=4 kernel
 
 template <typename T>
@@ -808,6 +764,10 @@ static int run_ig(const IgParams& p, hipStream_t st, int bm, int bn) {
     maxK = p.ph[i].K > maxK ? p.ph[i].K : maxK;
   }
   const bool smallk = maxK <= g_smallk_max;
+  if constexpr (sizeof(T) == 2) {
+    if (conv3x3_halo_launch(p, st)) return check_launch("conv3x3_halo_kernel");
+    if (igemm_glds_launch(p, maxM, maxK, st)) return check_launch("igemm_glds_kernel");
+  }
   if (p.stem) {
     if (p.N != 64 || bm != 128) { set_error("igemm: stem expects 64 output channels"); return ARGUS_ERR_SHAPE; }
     launch_ig<T, 128, 64, true, false, 2>(p, maxM, st);
@@ -831,6 +791,9 @@ int conv_tuning(int key, int value) {
   if (key >= 3 && key < 6) { g_force_bn[key - 3] = value; return 0; }
   if (key == 6) { g_wgrad_target_blocks = value; return 0; }
   if (key == 7) { g_smallk_max = value; return 0; }
+  if (key == 8) { g_glds_min_k = value; return 0; }
+  if (key == 9) { g_glds_min_grid = value; return 0; }
+  if (key == 10) { g_halo_enable = value; return 0; }
   return -1;
 }
 
@@ -889,6 +852,7 @@ int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, 
       }
   }
   const int bm = fwd_bm(d), bn = d.stem ? 64 : pick_bn(0, d.k);
+  p.stat_tile = bm;
   return dtype == ARGUS_BF16 ? run_ig<bf16>(p, st, bm, bn) : run_ig<float>(p, st, bm, bn);
 }
 

@@ -1,0 +1,281 @@
+// Implicit-GEMM convolution (forward / dgrad, bf16, no BN prologue) with global->LDS DMA staging.
+//
+// Why a second kernel: the register-staged igemm_kernel (conv.hip) moves every operand byte
+// global -> VGPR -> LDS; on gfx950 a ds_write_b128 costs ~13 cycles of VGPR->LDS transfer per wave
+// instruction (~79 B/clk/CU, MI355X_MICROARCH.md §LDS), which for its 128x128 tile exceeds the MFMA
+// time per k-step. Here both operands go straight to LDS with global_load_lds_dwordx4 (no VGPR, no
+// ds_write), through a 3-stage LDS ring with a counted vmcnt and raw s_barrier, so two k-steps of
+// loads are in flight while the MFMAs of the current one run (cdna_hip_programming.md §5,
+// "Pipelining across barriers").
+//
+// Geometry: each wave computes a 64x64 output tile (4x4 v_mfma_f32_16x16x32_bf16 blocks); the
+// workgroup is (BM/64) x (BN/64) waves: 256x128 (8 waves) or 256x64 (4 waves). K-step = one tap x 64
+// input channels. LDS images are [row][64 k] bf16 (128 B rows), 16-byte slot j of row r holding
+// k-chunk j ^ swz8(r) (conflict-free ds_read_b128 fragment reads); glds writes lane-linear 1 KB
+// pieces (8 rows), so the swizzle is applied on the per-lane global source address. Out-of-image
+// taps and rows past M read a 16-byte zero page. BN statistics are emitted per 64-row wave tile or
+// per 128-row half tile, in the same partial layout as igemm_kernel's 64- / 128-row tiles.
+#include "common.h"
+#include "igemm.h"
+#include "internal.h"
+#include "ktimer.h"
+
+namespace argus {
+
+__device__ __attribute__((aligned(64))) u32x4 g_zero_page[4];  // zero-initialised (static storage)
+
+// s_waitcnt vmcnt(N) with expcnt / lgkmcnt left at their maxima (gfx9 encoding).
+template <int N> ARGUS_DEV void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+
+ARGUS_DEV void glds16(const void* src, uint32_t lds_byte_addr) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(uintptr_t)lds_byte_addr, 16, 0,
+                                   0);
+}
+
+ARGUS_DEV void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int BM, int BN>
+__global__ __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) void igemm_glds_kernel(const IgParams p) {
+  constexpr int WM = BM / 64, WN = BN / 64, NW = WM * WN, NT = NW * 64;
+  constexpr int STAGE = (BM + BN) * 128;      // bytes per pipeline stage (A image, then B image)
+  constexpr int NSTAGE = 3;
+  constexpr int LD = BN + 8;                   // epilogue C row stride (elements)
+  constexpr int EPI = BM * LD * 2;
+  constexpr int LDS_BYTES = NSTAGE * STAGE > EPI ? NSTAGE * STAGE : EPI;
+  constexpr int AI = BM * 8 / NT;              // A glds per thread per stage
+  constexpr int BI = BN * 8 / NT;              // B glds per thread per stage
+  constexpr int GPS = AI + BI;                 // glds per wave per stage (vmcnt unit)
+  static_assert(AI * NT == BM * 8 && BI * NT == BN * 8, "tile / thread mismatch");
+  __shared__ __attribute__((aligned(1024))) u32x4 lds[LDS_BYTES / 16];
+
+  const IgPhase& ph = p.ph[blockIdx.z];
+  const int mtiles = (ph.M + BM - 1) / BM;
+  const int ntiles = p.N / BN;
+  const int nwg = mtiles * ntiles;
+  if ((int)blockIdx.x >= nwg) return;
+  if (ph.K == 0 && p.addend == p.c && !p.addend_mask) return;  // in-place += 0
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int mt = bid / ntiles, nt = bid - mt * ntiles;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave - wm * WN;
+  const bf16* __restrict__ A = reinterpret_cast<const bf16*>(p.a);
+  const bf16* __restrict__ B = reinterpret_cast<const bf16*>(p.b);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)lds;
+
+  // this thread's A rows (output pixels) and the k-chunk each of its glds fetches
+  const int HWq = ph.Hq * ph.Wq;
+  int a_off[AI], a_ih[AI], a_iw[AI], a_ch[AI];
+  bool a_ok[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int row = 8 * (i * NW + wave) + (lane >> 3);
+    const int m = mt * BM + row;
+    a_ok[i] = m < ph.M;
+    const int mm = a_ok[i] ? m : 0;
+    const int nimg = mm / HWq, rem = mm - nimg * HWq;
+    const int qh = rem / ph.Wq, qw = rem - qh * ph.Wq;
+    a_ih[i] = qh * p.ish;
+    a_iw[i] = qw * p.isw;
+    a_off[i] = ((nimg * p.H + a_ih[i]) * p.W + a_iw[i]) * p.lda;
+    a_ch[i] = ((lane & 7) ^ swz8(row)) * 8;
+  }
+  const bf16* b_src[BI];
+#pragma unroll
+  for (int i = 0; i < BI; ++i) {
+    const int row = 8 * (i * NW + wave) + (lane >> 3);
+    b_src[i] = B + (size_t)(nt * BN + row) * p.ldb + ((lane & 7) ^ swz8(row)) * 8;
+  }
+  const void* zero = (const void*)g_zero_page;
+
+  auto issue = [&](int kt, int stage) {
+    const int k0 = kt * 64;
+    const int t = k0 / p.Cin;
+    const int ci0 = k0 - t * p.Cin;
+    const int dh = ph.dh[t], dw = ph.dw[t], boff = ph.boff[t];
+    const int tap = (dh * p.W + dw) * p.lda + ci0;
+    const uint32_t base = lds0 + stage * STAGE + wave * 1024;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int ih = a_ih[i] + dh, iw = a_iw[i] + dw;
+      const bool ok = a_ok[i] && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+      glds16(ok ? (const void*)(A + a_off[i] + tap + a_ch[i]) : zero, base + i * NW * 1024);
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i) glds16(b_src[i] + boff + ci0, base + BM * 128 + i * NW * 1024);
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int g = lane >> 4, i16 = lane & 15;
+  auto compute = [&](int stage) {
+    const char* L = reinterpret_cast<const char*>(lds) + stage * STAGE;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      u32x4 fa[4], fb[4];
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        const int row = wm * 64 + mi * 16 + i16;
+        fa[mi] = *reinterpret_cast<const u32x4*>(L + row * 128 + (((4 * s2 + g) ^ swz8(row)) << 4));
+      }
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const int row = wn * 64 + ni * 16 + i16;
+        fb[ni] = *reinterpret_cast<const u32x4*>(L + BM * 128 + row * 128 + (((4 * s2 + g) ^ swz8(row)) << 4));
+      }
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) Mma<bf16>::run(acc[mi][ni], fa[mi], fb[ni]);
+    }
+  };
+
+  // ---- main loop: 3-stage ring, k-steps kt+1 and kt+2 in flight during compute(kt) ----
+  const int nk = ph.K / 64;
+  if (nk > 0) issue(0, 0);
+  if (nk > 1) issue(1, 1);
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) wait_vmcnt<GPS>(); else wait_vmcnt<0>();
+    raw_barrier();  // stage kt landed for every wave; every wave finished reading stage kt-1
+    if (kt + 2 < nk) issue(kt + 2, (kt + 2) % NSTAGE);
+    compute(kt % NSTAGE);
+  }
+  wait_vmcnt<0>();
+  __syncthreads();  // LDS is reused below
+
+  // ---- BN statistics per 64-row (one wave) or 128-row (two waves) tile: {sum, M2} per column ----
+  if (p.stats) {
+    float2* red = reinterpret_cast<float2*>(lds);  // [WM][BN]
+    int nvalid_w = ph.M - (mt * BM + wm * 64);
+    nvalid_w = nvalid_w < 0 ? 0 : (nvalid_w > 64 ? 64 : nvalid_w);
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      float s = 0.f;
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s += mi * 16 + g * 4 + r < nvalid_w ? acc[mi][ni][r] : 0.f;
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      const float mean_w = nvalid_w > 0 ? s / (float)nvalid_w : 0.f;
+      float q = 0.f;
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float d = acc[mi][ni][r] - mean_w;
+          q = mi * 16 + g * 4 + r < nvalid_w ? fmaf(d, d, q) : q;
+        }
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      if (p.stat_tile == 64) {  // a wave's 64 rows are one partial row
+        if (lane < 16 && nvalid_w > 0)
+          p.stats[(size_t)(mt * WM + wm) * p.N + nt * BN + wn * 64 + ni * 16 + lane] = make_float2(s, q);
+      } else if (lane < 16) {
+        red[wm * BN + wn * 64 + ni * 16 + lane] = make_float2(s, q);
+      }
+    }
+    __syncthreads();
+    constexpr int HALVES = BM / 128;
+    if (p.stat_tile == 128)
+    for (int idx = tid; idx < HALVES * BN; idx += NT) {
+      const int h = idx / BN, col = idx - h * BN;
+      const int r0 = mt * BM + h * 128;
+      if (r0 >= ph.M) continue;
+      int na = ph.M - r0;
+      na = na > 64 ? 64 : na;
+      int nb = ph.M - (r0 + 64);
+      nb = nb < 0 ? 0 : (nb > 64 ? 64 : nb);
+      const float2 a0 = red[(2 * h) * BN + col], a1 = red[(2 * h + 1) * BN + col];
+      float m2 = a0.y + a1.y;
+      if (na > 0 && nb > 0) {
+        const float d = a0.x / (float)na - a1.x / (float)nb;
+        m2 += d * d * ((float)na * (float)nb / (float)(na + nb));
+      }
+      p.stats[(size_t)(mt * HALVES + h) * p.N + nt * BN + col] = make_float2(a0.x + a1.x, m2);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: stage the C tile in LDS, then 16-byte coalesced (+addend) stores ----
+  bf16* Cs = reinterpret_cast<bf16*>(lds);
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * 64 + mi * 16 + g * 4 + r;
+        const int col = wn * 64 + ni * 16 + i16;
+        Cs[row * LD + col] = (bf16)acc[mi][ni][r];
+      }
+  __syncthreads();
+  constexpr int CPR = BN / 8;   // 16-byte chunks per row
+  constexpr int RPP = NT / CPR;  // rows per store pass
+  bf16* __restrict__ Cg = reinterpret_cast<bf16*>(p.c);
+  const int c = tid % CPR;
+#pragma unroll 4
+  for (int rr = tid / CPR; rr < BM; rr += RPP) {
+    const int m = mt * BM + rr;
+    if (m >= ph.M) continue;
+    const int nimg = m / HWq, rem = m - nimg * HWq;
+    const int qh = rem / ph.Wq, qw = rem - qh * ph.Wq;
+    const int oh = qh * p.osh + ph.oh0, ow = qw * p.osw + ph.ow0;
+    bf16* dst = Cg + (((size_t)nimg * p.Ho + oh) * p.Wo + ow) * p.ldc + nt * BN + c * 8;
+    u32x4 v = *reinterpret_cast<const u32x4*>(Cs + rr * LD + c * 8);
+    if (p.addend) {
+      const size_t off = (size_t)(dst - Cg);
+      float f[8], o[8];
+      unpack(v, f);
+      unpack(ld16(reinterpret_cast<const bf16*>(p.addend) + off), o);
+      const unsigned mb = p.addend_mask ? p.addend_mask[off / 8] : 0xffu;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] += (mb >> j) & 1u ? o[j] : 0.f;
+      v = pack(f);
+    }
+    st16(dst, v);
+  }
+}
+
+template <int BM, int BN>
+static const char* glds_name() {
+  static const std::string s =
+      std::string("argus::igemm_glds_kernel<") + std::to_string(BM) + ", " + std::to_string(BN) + ">";
+  return s.c_str();
+}
+
+template <int BM, int BN>
+static void launch_glds(const IgParams& p, int maxM, hipStream_t st) {
+  dim3 grid(cdiv(maxM, BM) * (p.N / BN), 1, p.nphase);
+  timed_launch(glds_name<BM, BN>(), igemm_glds_kernel<BM, BN>, grid, dim3((BM / 64) * (BN / 64) * 64), st, p);
+}
+
+int g_glds_min_k = 512;      // argus_conv_tuning key 8: smallest K (taps*C) served by the glds kernel (0 = off)
+int g_glds_min_grid = 256;  // key 9: fewest workgroups for which it is chosen
+
+bool igemm_glds_launch(const IgParams& p, int maxM, int maxK, hipStream_t st) {
+  if (g_glds_min_k <= 0 || p.stem || p.pro_scale || maxK < g_glds_min_k || p.Cin % 64 || p.lda % 8 ||
+      p.ldb % 8 || maxM < 4 * 256)
+    return false;
+  if (p.stats && p.stat_tile != 128 && p.stat_tile != 64) return false;
+  for (int i = 0; i < p.nphase; ++i)
+    if (p.ph[i].K % 64) return false;
+  // measured (tools/convbench.py): a win only with >= one 8-wave workgroup per CU; the 4-wave
+  // 256x64 tile and sub-CU-count grids lose to the register-staged kernel
+  if (p.N % 128 || cdiv(maxM, 256) * (p.N / 128) < g_glds_min_grid) return false;
+  launch_glds<256, 128>(p, maxM, st);
+  return true;
+}
+
+}  // namespace argus

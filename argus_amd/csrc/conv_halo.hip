@@ -1,0 +1,336 @@
+// 3x3 stride-1 pad-1 convolution (forward and dgrad, bf16) with the input tile held in LDS once per
+// 64-channel chunk, halo included, and the nine taps read as shifted windows of it.
+//
+// Why: the implicit GEMM (conv.hip / conv_glds.hip) re-fetches its A tile from L2 once per tap, 9x
+// per channel chunk; measured on MI355X (SQ counters, tools/convbench.py) both of those kernels sit
+// at ~38 % MFMA utilisation on the 3x3 layers with waves parked on loads, and a 256x128x64 step needs
+// ~96 GB/s per CU of L2->LDS traffic against the ~70 GB/s per CU an L2-resident gather sustains
+// (MI355X_MICROARCH.md, "Indexed rows: gather into LDS"). With the halo tile, per chunk a workgroup
+// loads (rows+2) x (W+2) input pixels once plus 9 weight tiles: L2 intensity ~190 FLOP/B instead of
+// ~87.
+//
+// Geometry: a workgroup owns 256 consecutive output pixels (NHW order) x BN output channels; the 256
+// pixels are whole rows of one image (W in {16, 32, 64, ...}) or whole images (H*W in {64, 128}).
+// Waves: 4 x (BN/64), each a 64x64 tile of 4x4 v_mfma_f32_16x16x32_bf16. Per chunk cc (64 input
+// channels) and tap t, A[m][k] = halo[pos(m) + off(t)][k], B = w[n][tap t][cc*64 + k].
+// LDS: two halo images (double-buffered over chunks, 448 positions x 128 B; slot j of position q holds
+// channel chunk j ^ swz8(q)) + a 3-stage ring of weight tiles, all filled by global_load_lds_dwordx4
+// (lane-linear 1 KB pieces, swizzle on the source address, zero page for halo positions outside the
+// image). With PRO (forward of conv2: the producer's BN + ReLU), the landed halo of each chunk is
+// transformed in place once (positions outside the image set to 0 = PyTorch's zero padding of the
+// post-ReLU tensor) before its nine taps run.
+#include "common.h"
+#include "igemm.h"
+#include "internal.h"
+#include "ktimer.h"
+
+namespace argus {
+
+namespace {
+
+__device__ __attribute__((aligned(64))) u32x4 halo_zero_page[4];  // zero-initialised (static storage)
+
+template <int N> ARGUS_DEV void waitvm() {
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+ARGUS_DEV void gl16(const void* src, uint32_t lds_byte_addr) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(uintptr_t)lds_byte_addr, 16, 0,
+                                   0);
+}
+ARGUS_DEV void sbar() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+}  // namespace
+
+constexpr int kHaloPos = 448;  // halo positions per image buffer (max (rows+2)*(W+2) over the shapes served)
+
+template <int BN, bool PRO>
+__global__ __launch_bounds__(4 * (BN / 64) * 64, 1) void conv3x3_halo_kernel(const IgParams p) {
+  constexpr int WN = BN / 64, NW = 4 * WN, NT = NW * 64;
+  constexpr int HALO = kHaloPos * 128;          // bytes per halo image
+  constexpr int BST = BN * 128;                 // bytes per weight stage
+  constexpr int NBS = 3;
+  constexpr int LD = BN + 8;
+  constexpr int EPI = 256 * LD * 2;
+  constexpr int MAIN = 2 * HALO + NBS * BST;
+  constexpr int LDS_BYTES = MAIN > EPI ? MAIN : EPI;
+  constexpr int HG = kHaloPos / (8 * NW);       // halo glds per wave per chunk
+  constexpr int BG = BN * 8 / NT;               // weight glds per wave per tap
+  static_assert(HG * 8 * NW == kHaloPos && BG * NT == BN * 8, "halo / tile partition");
+  __shared__ __attribute__((aligned(1024))) u32x4 lds[LDS_BYTES / 16];
+
+  const IgPhase& ph = p.ph[0];
+  const int mtiles = ph.M / 256;
+  const int ntiles = p.N / BN;
+  const int nwg = mtiles * ntiles;
+  if ((int)blockIdx.x >= nwg) return;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int mt = bid / ntiles, nt = bid - mt * ntiles;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave - wm * WN;
+  const bf16* __restrict__ X = reinterpret_cast<const bf16*>(p.a);
+  const bf16* __restrict__ Wt = reinterpret_cast<const bf16*>(p.b);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)lds;
+
+  // block geometry: NI images x R rows x W columns of output = input (stride 1)
+  const int H = p.H, W = p.W, HWi = H * W;
+  int NI, R, r0, img0;
+  if (HWi >= 256) { NI = 1; R = 256 / W; img0 = (mt * 256) / HWi; r0 = (mt * 256 - img0 * HWi) / W; }
+  else { NI = 256 / HWi; R = H; img0 = mt * NI; r0 = 0; }
+  const int HWD = W + 2, HR = R + 2, IMGP = HR * HWD;
+  const int npos = NI * IMGP;
+
+  // halo glds sources: position q = 8*(i*NW + wave) + lane/8, channel chunk (lane&7)^swz8(q)
+  int h_off[HG];
+  bool h_ok[HG];
+#pragma unroll
+  for (int i = 0; i < HG; ++i) {
+    const int q = 8 * (i * NW + wave) + (lane >> 3);
+    const int ii = q / IMGP, rem = q - ii * IMGP;
+    const int hr = rem / HWD, hc = rem - hr * HWD;
+    const int ih = r0 + hr - 1, iw = hc - 1;
+    h_ok[i] = q < npos && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+    h_off[i] = h_ok[i] ? (((img0 + ii) * H + ih) * W + iw) * p.lda + ((lane & 7) ^ swz8(q)) * 8 : 0;
+  }
+  const bf16* b_src[BG];
+#pragma unroll
+  for (int i = 0; i < BG; ++i) {
+    const int row = 8 * (i * NW + wave) + (lane >> 3);
+    b_src[i] = Wt + (size_t)(nt * BN + row) * p.ldb + ((lane & 7) ^ swz8(row)) * 8;
+  }
+  const void* zero = (const void*)halo_zero_page;
+  const int nch = p.Cin / 64;
+  const int nk = 9 * nch;
+
+  auto issue_halo = [&](int cc) {
+    const uint32_t base = lds0 + (cc & 1) * HALO + wave * 1024;
+    const int ci0 = cc * 64;
+#pragma unroll
+    for (int i = 0; i < HG; ++i) gl16(h_ok[i] ? (const void*)(X + h_off[i] + ci0) : zero, base + i * NW * 1024);
+  };
+  auto issue_b = [&](int kt) {
+    const int cc = kt / 9, t = kt - cc * 9;
+    const int off = ph.boff[t] + cc * 64;
+    const uint32_t base = lds0 + 2 * HALO + (kt % NBS) * BST + wave * 1024;
+#pragma unroll
+    for (int i = 0; i < BG; ++i) gl16(b_src[i] + off, base + i * NW * 1024);
+  };
+
+  // per-thread fragment rows: halo position of output pixel m at tap (0,0)
+  const int g = lane >> 4, i16 = lane & 15;
+  int hb[4];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+    const int m = wm * 64 + mi * 16 + i16;
+    const int ii = m / (R * W), rem = m - ii * (R * W);
+    const int lr = rem / W, lc = rem - lr * W;
+    hb[mi] = ii * IMGP + lr * HWD + lc;
+  }
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int kt) {
+    const int cc = kt / 9, t = kt - cc * 9;
+    const int toff = (ph.dh[t] + 1) * HWD + (ph.dw[t] + 1);
+    const char* Hl = reinterpret_cast<const char*>(lds) + (cc & 1) * HALO;
+    const char* Bl = reinterpret_cast<const char*>(lds) + 2 * HALO + (kt % NBS) * BST;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      u32x4 fa[4], fb[4];
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        const int q = hb[mi] + toff;
+        fa[mi] = *reinterpret_cast<const u32x4*>(Hl + q * 128 + (((4 * s2 + g) ^ swz8(q)) << 4));
+      }
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const int row = wn * 64 + ni * 16 + i16;
+        fb[ni] = *reinterpret_cast<const u32x4*>(Bl + row * 128 + (((4 * s2 + g) ^ swz8(row)) << 4));
+      }
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) Mma<bf16>::run(acc[mi][ni], fa[mi], fb[ni]);
+    }
+  };
+
+  // BN + ReLU of the producer, applied once per chunk to the landed halo image (in place)
+  auto transform_halo = [&](int cc) {
+    char* Hl = reinterpret_cast<char*>(lds) + (cc & 1) * HALO;
+    for (int idx = tid; idx < npos * 8; idx += NT) {
+      const int q = idx >> 3, slot = idx & 7;
+      const int ii = q / IMGP, rem = q - ii * IMGP;
+      const int hr = rem / HWD, hc = rem - hr * HWD;
+      const int ih = r0 + hr - 1, iw = hc - 1;
+      u32x4* ptr = reinterpret_cast<u32x4*>(Hl + q * 128 + slot * 16);
+      if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) {
+        const int ch = cc * 64 + (slot ^ swz8(q)) * 8;
+        float f[8];
+        unpack(*ptr, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], p.pro_scale[ch + j], p.pro_shift[ch + j]), 0.f);
+        *ptr = pack(f);
+      } else {
+        *ptr = u32x4{0u, 0u, 0u, 0u};
+      }
+    }
+  };
+
+  // ---- main loop over k-steps kt = chunk*9 + tap ----
+  // issue order: H(0) B(0) B(1) | per step j: [H(chunk(j)+1) if tap(j)==0] [B(j+2)]
+  issue_halo(0);
+  issue_b(0);
+  if (nk > 1) issue_b(1);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int t = kt % 9, cc = kt / 9;
+    // loads allowed to stay in flight: everything issued after B(kt)
+    bool halo_after = false;
+    if (kt >= 1) {
+      const int j = kt - 1;
+      halo_after = (j % 9 == 0) && (j / 9 + 1 < nch);
+    }
+    const bool b_after = kt + 1 < nk;
+    if (halo_after && b_after) waitvm<HG + BG>();
+    else if (halo_after) waitvm<HG>();
+    else if (b_after) waitvm<BG>();
+    else waitvm<0>();
+    sbar();
+    if constexpr (PRO) {
+      // before issuing new glds: the coefficient loads' vmcnt wait then drains only B(kt+1)
+      if (t == 0) {
+        transform_halo(cc);
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's rewritten halo is in LDS
+        sbar();
+      }
+    }
+    if (t == 0 && cc + 1 < nch) issue_halo(cc + 1);
+    if (kt + 2 < nk) issue_b(kt + 2);
+    compute(kt);
+  }
+  waitvm<0>();
+  __syncthreads();
+
+  // ---- BN statistics (forward): one partial per 64-row wave tile or 128-row pair ----
+  if (p.stats) {
+    float2* red = reinterpret_cast<float2*>(lds);
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      float s = 0.f;
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s += acc[mi][ni][r];
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      const float mean_w = s * (1.f / 64.f);
+      float q = 0.f;
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float d = acc[mi][ni][r] - mean_w;
+          q = fmaf(d, d, q);
+        }
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      const int col = wn * 64 + ni * 16 + lane;
+      if (p.stat_tile == 64) {
+        if (lane < 16) p.stats[(size_t)(mt * 4 + wm) * p.N + nt * BN + col] = make_float2(s, q);
+      } else if (lane < 16) {
+        red[wm * BN + col] = make_float2(s, q);
+      }
+    }
+    __syncthreads();
+    if (p.stat_tile == 128) {
+      for (int idx = tid; idx < 2 * BN; idx += NT) {
+        const int h = idx / BN, col = idx - h * BN;
+        const float2 a0 = red[(2 * h) * BN + col], a1 = red[(2 * h + 1) * BN + col];
+        const float d = (a0.x - a1.x) * (1.f / 64.f);
+        p.stats[(size_t)(mt * 2 + h) * p.N + nt * BN + col] = make_float2(a0.x + a1.x, a0.y + a1.y + d * d * 32.f);
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: LDS-staged C tile, 16-byte coalesced (+addend) stores; output pixels are contiguous ----
+  bf16* Cs = reinterpret_cast<bf16*>(lds);
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        Cs[(wm * 64 + mi * 16 + g * 4 + r) * LD + wn * 64 + ni * 16 + i16] = (bf16)acc[mi][ni][r];
+  __syncthreads();
+  constexpr int CPR = BN / 8, RPP = NT / CPR;
+  bf16* __restrict__ Cg = reinterpret_cast<bf16*>(p.c);
+  const int c = tid % CPR;
+#pragma unroll 4
+  for (int rr = tid / CPR; rr < 256; rr += RPP) {
+    const size_t off = (size_t)(mt * 256 + rr) * p.ldc + nt * BN + c * 8;
+    u32x4 v = *reinterpret_cast<const u32x4*>(Cs + rr * LD + c * 8);
+    if (p.addend) {
+      float f[8], o[8];
+      unpack(v, f);
+      unpack(ld16(reinterpret_cast<const bf16*>(p.addend) + off), o);
+      const unsigned mb = p.addend_mask ? p.addend_mask[off / 8] : 0xffu;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] += (mb >> j) & 1u ? o[j] : 0.f;
+      v = pack(f);
+    }
+    st16(Cg + off, v);
+  }
+}
+
+template <int BN, bool PRO>
+static const char* halo_name() {
+  static const std::string s = std::string("argus::conv3x3_halo_kernel<") + std::to_string(BN) + ", " +
+                               bool_name(PRO) + ">";
+  return s.c_str();
+}
+
+template <int BN, bool PRO>
+static void launch_halo(const IgParams& p, hipStream_t st) {
+  dim3 grid((p.ph[0].M / 256) * (p.N / BN));
+  timed_launch(halo_name<BN, PRO>(), conv3x3_halo_kernel<BN, PRO>, grid, dim3(4 * (BN / 64) * 64), st, p);
+}
+
+int g_halo_enable = 1;  // argus_conv_tuning key 10
+
+// 3x3 / stride 1 / pad 1, same input and output grid, one phase, whole-row / whole-image 256-pixel tiles
+bool conv3x3_halo_launch(const IgParams& p, hipStream_t st) {
+  if (!g_halo_enable || p.stem || p.nphase != 1 || p.ish != 1 || p.isw != 1 || p.osh != 1 || p.osw != 1) return false;
+  const IgPhase& ph = p.ph[0];
+  if (ph.K != 9 * p.Cin || p.Cin % 64 || p.lda % 8 || p.ldb % 8 || p.H != p.Ho || p.W != p.Wo) return false;
+  for (int t = 0; t < 9; ++t)
+    if (ph.dh[t] < -1 || ph.dh[t] > 1 || ph.dw[t] < -1 || ph.dw[t] > 1) return false;
+  const int HWi = p.H * p.W;
+  if (ph.M % 256) return false;
+  int npos;
+  if (HWi >= 256) {
+    if (256 % p.W || HWi % 256) return false;
+    npos = (256 / p.W + 2) * (p.W + 2);
+  } else {
+    if (256 % HWi) return false;
+    npos = (256 / HWi) * (p.H + 2) * (p.W + 2);
+  }
+  if (npos > kHaloPos) return false;
+  if (p.stats && p.stat_tile != 64 && p.stat_tile != 128) return false;
+  if (p.N % 128 == 0) {
+    if (p.pro_scale) launch_halo<128, true>(p, st); else launch_halo<128, false>(p, st);
+  } else if (p.N % 64 == 0) {
+    if (p.pro_scale) launch_halo<64, true>(p, st); else launch_halo<64, false>(p, st);
+  } else {
+    return false;
+  }
+  return true;
+}
+
+}  // namespace argus

@@ -76,7 +76,11 @@ int argus_conv_dgrad(const argus_conv_desc* d, int dtype, const void* dy, const 
 /* Tuning knobs (process-wide; for autotuning / experiments): key 0..2 force the row tile (64|128,
  * 0 = heuristic) of pass fwd/dgrad/wgrad, key 3..5 force the column tile, key 6 sets the wgrad
  * split target (workgroups), key 7 the largest K (= taps*C) served by the 4-workgroups-per-CU
- * single-buffer forward/dgrad kernel (default 128). Returns 0, or -1 for an unknown key. */
+ * single-buffer forward/dgrad kernel (default 128), key 8 the smallest K served by the bf16
+ * global->LDS (glds) forward/dgrad kernel (default 512; 0 disables it), key 9 the fewest
+ * workgroups for which that kernel is chosen (default 256), key 10 enables (1, default) or
+ * disables (0) the LDS-halo kernel for 3x3 stride-1 forward/dgrad. Returns 0, or -1 for an
+ * unknown key. */
 int argus_conv_tuning(int key, int value);
 /* Which tile a pass launches and its algorithmic work: pass 0 fwd, 1 dgrad, 2 wgrad. Returns a
  * tag (kind*10^7 + dtype*10^6 + tile_m*1000 + tile_n; kind 1 igemm, 2 wgrad) and writes

@@ -495,3 +495,114 @@ def test_kernel_timer_records_exact_instantiations(cuda):
     assert t.summary() == {}
     L.conv_fwd(C.byref(d), BF16, ptr(x), ptr(wf), ptr(y), None, None, None, stream())  # disabled: plain launch
     torch.cuda.synchronize()
+
+
+GLDS_SHAPES = [  # (cin, cout, k, s, hin, n): M >= 1024 rows so the glds kernel is eligible
+    (64, 64, 3, 1, 24, 2), (128, 128, 3, 2, 25, 2), (512, 256, 1, 1, 24, 2), (256, 512, 1, 2, 32, 2),
+    (64, 128, 3, 1, 20, 3), (576, 64, 1, 1, 23, 2),
+]
+
+
+def test_conv_glds_kernel_parity(cuda):
+    """The bf16 global->LDS implicit-GEMM kernel (forced on with tuning key 8) vs torch: forward with
+    BN-statistic partials (M tails, 2 x 128-row halves per 256-row tile), dgrad over stride phases,
+    in-place and masked addends; the kernel timer confirms it ran."""
+    from argus_amd.profiling import KernelTimer
+
+    torch.manual_seed(11)
+    L = lib()
+    assert L.dll.argus_conv_tuning(8, 64) == 0 and L.dll.argus_conv_tuning(9, 1) == 0
+    try:
+        for cin, cout, k, s, hin, n in GLDS_SHAPES:
+            d, p = _desc(n, hin, hin, cin, cout, k, s)
+            x = torch.randn(n, hin, hin, cin)
+            w = torch.randn(cout, k, k, cin) * (2.0 / (k * k * cin)) ** 0.5
+            dy = torch.randn(n, d.ho, d.wo, cout)
+            xd, dyd = x.to(cuda, torch.bfloat16), dy.to(cuda, torch.bfloat16)
+            wf, wt = _prep(d, "bf16", w.to(cuda), cuda)
+            y = torch.empty(n, d.ho, d.wo, cout, dtype=torch.bfloat16, device=cuda)
+            rows = L.dll.argus_conv_fwd_stat_rows(C.byref(d), BF16)
+            stats = torch.empty(rows, cout, 2, device=cuda)
+            with KernelTimer("argus::igemm_glds_kernel") as t:
+                L.conv_fwd(C.byref(d), BF16, ptr(xd), ptr(wf), ptr(y), None, None, ptr(stats), stream())
+            M = n * d.ho * d.wo
+            if M >= 1024 and k * k * cin >= 64 and cout % 128 == 0:
+                assert len(t.summary()) == 1, (cin, cout, k, s, hin)
+            xr, wr, dyr = _q(x, "bf16").permute(0, 3, 1, 2), _q(w, "bf16").permute(0, 3, 1, 2), _q(dy, "bf16").permute(0, 3, 1, 2)
+            ref = F.conv2d(xr, wr, stride=s, padding=p)
+            assert _rel(y.permute(0, 3, 1, 2), ref) < TOL["bf16"], ("fwd", cin, cout, k, s)
+            tile = L.dll.argus_conv_fwd_stat_tile(C.byref(d), BF16)
+            mean, var = _merge_stats(stats.double().cpu(), tile, M)
+            yr = ref.permute(0, 2, 3, 1).reshape(-1, cout)
+            assert (mean - yr.mean(0)).abs().max() < 2e-2 * yr.std(0).max(), ("stats mean", cin, cout)
+            assert _rel(var, yr.var(0, unbiased=False)) < 2e-2, ("stats var", cin, cout)
+            # dgrad: plain, in-place accumulate, masked addend from another buffer
+            dx0 = torch.randn(n, hin, hin, cin)
+            dx = dx0.to(cuda, torch.bfloat16)
+            L.conv_dgrad(C.byref(d), BF16, ptr(dyd), ptr(wt), ptr(dx), ptr(dx), None, stream())
+            refd = torch.nn.grad.conv2d_input(xr.shape, wr, dyr, stride=s, padding=p)
+            assert _rel(dx.permute(0, 3, 1, 2), refd + _q(dx0, "bf16").permute(0, 3, 1, 2)) < TOL["bf16"], ("dgrad+", cin)
+            res = _q(torch.randn(n, hin, hin, cin), "bf16")
+            keep = res > 0
+            bits = ((keep.reshape(-1, 8).int() << torch.arange(8)).sum(1)).to(torch.uint8).to(cuda)
+            resg = res.to(cuda, torch.bfloat16)
+            L.conv_dgrad(C.byref(d), BF16, ptr(dyd), ptr(wt), ptr(dx), ptr(resg), ptr(bits), stream())
+            assert _rel(dx.permute(0, 3, 1, 2), refd + (res * keep).permute(0, 3, 1, 2)) < TOL["bf16"], ("dgrad mask", cin)
+    finally:
+        L.dll.argus_conv_tuning(8, 512)
+        L.dll.argus_conv_tuning(9, 256)
+
+
+HALO_SHAPES = [  # (cin, cout, hw, n): 256-pixel tiles = 4 rows / 8 rows / 1 image / 4 images
+    (64, 64, 64, 1), (128, 128, 32, 1), (64, 128, 16, 2), (256, 256, 16, 1), (128, 64, 8, 4), (512, 512, 8, 4),
+]
+
+
+def test_conv3x3_halo_kernel_parity(cuda):
+    """3x3 stride-1 LDS-halo kernel vs torch (bf16): forward with and without the fused BN+ReLU
+    prologue (zero padding of the post-ReLU tensor), BN partials at 64- and 128-row tiles, dgrad with
+    in-place and masked addends; the kernel timer confirms the halo kernel served every call."""
+    from argus_amd.profiling import KernelTimer
+
+    torch.manual_seed(13)
+    L = lib()
+    for cin, cout, hw, n in HALO_SHAPES:
+        d, p = _desc(n, hw, hw, cin, cout, 3, 1)
+        x = torch.randn(n, hw, hw, cin) * 1.5 + 0.2
+        w = torch.randn(cout, 3, 3, cin) * (2.0 / (9 * cin)) ** 0.5
+        sc, sh = torch.rand(cin) + 0.5, torch.randn(cin) * 0.5
+        xd, scd, shd = x.to(cuda, torch.bfloat16), sc.to(cuda), sh.to(cuda)
+        wf, wt = _prep(d, "bf16", w.to(cuda), cuda)
+        xr, wr = _q(x, "bf16").permute(0, 3, 1, 2), _q(w, "bf16").permute(0, 3, 1, 2)
+        rows = L.dll.argus_conv_fwd_stat_rows(C.byref(d), BF16)
+        tile = L.dll.argus_conv_fwd_stat_tile(C.byref(d), BF16)
+        M = n * hw * hw
+        for pro in (False, True):
+            y = torch.empty(n, hw, hw, cout, dtype=torch.bfloat16, device=cuda)
+            stats = torch.empty(rows, cout, 2, device=cuda)
+            with KernelTimer("argus::conv3x3_halo_kernel") as t:
+                L.conv_fwd(C.byref(d), BF16, ptr(xd), ptr(wf), ptr(y), ptr(scd) if pro else None,
+                           ptr(shd) if pro else None, ptr(stats), stream())
+            assert len(t.summary()) == 1, ("halo kernel not used", cin, cout, hw, n, pro)
+            xin = torch.relu(xr * sc[None, :, None, None] + sh[None, :, None, None]) if pro else xr
+            xin = _q(xin.permute(0, 2, 3, 1), "bf16").permute(0, 3, 1, 2) if pro else xin
+            ref = F.conv2d(xin, wr, padding=1)
+            assert _rel(y.permute(0, 3, 1, 2), ref) < TOL["bf16"], ("fwd", cin, cout, hw, pro)
+            mean, var = _merge_stats(stats.double().cpu(), tile, M)
+            yr = ref.permute(0, 2, 3, 1).reshape(-1, cout)
+            assert (mean - yr.mean(0)).abs().max() < 2e-2 * yr.std(0).max(), ("stats mean", cin, cout, hw)
+            assert _rel(var, yr.var(0, unbiased=False)) < 2e-2, ("stats var", cin, cout, hw)
+        dy = torch.randn(n, hw, hw, cout)
+        dyd = dy.to(cuda, torch.bfloat16)
+        refd = torch.nn.grad.conv2d_input(xr.shape, wr, _q(dy, "bf16").permute(0, 3, 1, 2), padding=1)
+        dx0 = _q(torch.randn(n, hw, hw, cin), "bf16")
+        dx = dx0.to(cuda, torch.bfloat16)
+        with KernelTimer("argus::conv3x3_halo_kernel") as t:
+            L.conv_dgrad(C.byref(d), BF16, ptr(dyd), ptr(wt), ptr(dx), ptr(dx), None, stream())
+        assert len(t.summary()) == 1, ("halo dgrad not used", cin, cout, hw, n)
+        assert _rel(dx.permute(0, 3, 1, 2), refd + dx0.permute(0, 3, 1, 2)) < TOL["bf16"], ("dgrad+", cin, cout, hw)
+        keep = dx0 > 0
+        bits = ((keep.reshape(-1, 8).int() << torch.arange(8)).sum(1)).to(torch.uint8).to(cuda)
+        res = dx0.to(cuda, torch.bfloat16)
+        L.conv_dgrad(C.byref(d), BF16, ptr(dyd), ptr(wt), ptr(dx), ptr(res), ptr(bits), stream())
+        assert _rel(dx.permute(0, 3, 1, 2), refd + (dx0 * keep).permute(0, 3, 1, 2)) < TOL["bf16"], ("dgrad m", cin)
