@@ -38,6 +38,10 @@ SIGNATURES = {
     "argus_last_error": (C.c_char_p, []),
     "argus_images_to_nhwc4": (_I, [_I, _I64, _I, _I, _P, _P, _P]),
     "argus_conv_weight_prep": (_I, [_DESC, _I, _P, _P, _P, _P, _P]),
+    "argus_conv_weight_prep_table_bytes": (_SZ, [_I]),
+    "argus_conv_weight_prep_table": (_I, [_I, _DESC, C.POINTER(_P), C.POINTER(C.c_int64), C.POINTER(_P),
+                                          C.POINTER(_P), _P, _SZ, C.POINTER(_I)]),
+    "argus_conv_weight_prep_batch": (_I, [_I, _I, _P, _I, _P]),
     "argus_conv_fwd": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P, _P]),
     "argus_conv_fwd_stat_rows": (_I, [_DESC, _I]),
     "argus_conv_fwd_stat_tile": (_I, [_DESC, _I]),

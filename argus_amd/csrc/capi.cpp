@@ -42,6 +42,18 @@ int argus_conv_weight_prep(const argus_conv_desc* d, int dtype, const float* w, 
   return conv_weight_prep(*d, dtype, w, strides, wf, wd, (hipStream_t)stream);
 }
 
+size_t argus_conv_weight_prep_table_bytes(int count) { return conv_weight_prep_table_bytes(count); }
+
+int argus_conv_weight_prep_table(int count, const argus_conv_desc* descs, const float* const* w_master,
+                                 const int64_t* strides, void* const* w_fwd, void* const* w_dgrad, void* host_table,
+                                 size_t table_bytes, int* nblocks) {
+  return conv_weight_prep_table(count, descs, w_master, strides, w_fwd, w_dgrad, host_table, table_bytes, nblocks);
+}
+
+int argus_conv_weight_prep_batch(int dtype, int count, const void* device_table, int nblocks, argus_stream_t stream) {
+  return conv_weight_prep_batch(dtype, count, device_table, nblocks, (hipStream_t)stream);
+}
+
 int argus_conv_fwd(const argus_conv_desc* d, int dtype, const void* x, const void* w, void* y, const float* sc,
                    const float* sh, float* stats, argus_stream_t stream) {
   if (!d || !x || !w || !y || (sc == nullptr) != (sh == nullptr)) {

@@ -694,6 +694,49 @@ __global__ __launch_bounds__(256) void weight_prep_kernel(const float* __restric
   }
 }
 
+// Batched weight_prep: one launch converts every conv of the network. Workgroup b handles
+// elements [(b - blk0[e]) * kWpChunk, ...) of table entry e (found by binary search on blk0).
+struct WpEntry {
+  const float* w;
+  long long sk, sc, sr, ss;
+  void* wf;
+  void* wd;
+  int K, R, S, C, stem, blk0;  // blk0: first workgroup of this entry
+};
+constexpr int kWpChunk = 2048;
+
+template <typename T>
+__global__ __launch_bounds__(256) void weight_prep_batch_kernel(const WpEntry* __restrict__ tab, int count) {
+  int lo = 0, hi = count - 1;
+  const int b = blockIdx.x;
+  while (lo < hi) {  // last entry with blk0 <= b
+    const int mid = (lo + hi + 1) >> 1;
+    if (tab[mid].blk0 <= b) lo = mid; else hi = mid - 1;
+  }
+  const WpEntry e = tab[lo];
+  const int total = e.stem ? e.K * 256 : e.K * e.R * e.S * e.C;
+  const int i0 = (b - e.blk0) * kWpChunk;
+  T* __restrict__ wf = reinterpret_cast<T*>(e.wf);
+  T* __restrict__ wd = reinterpret_cast<T*>(e.wd);
+  for (int i = i0 + threadIdx.x; i < i0 + kWpChunk && i < total; i += 256) {
+    if (e.stem) {
+      const int k = i >> 8, col = i & 255;
+      const int r = col >> 5, s = (col & 31) >> 2, c = col & 3;
+      float v = 0.f;
+      if (r < 7 && s < 7 && c < 3) v = e.w[k * e.sk + c * e.sc + r * e.sr + s * e.ss];
+      wf[i] = from_f32<T>(v);
+    } else {
+      const int RSC = e.R * e.S * e.C;
+      const int k = i / RSC, rem = i - k * RSC;
+      const int rs = rem / e.C, c = rem - rs * e.C;
+      const int r = rs / e.S, s = rs - r * e.S;
+      const float v = e.w[k * e.sk + c * e.sc + r * e.sr + s * e.ss];
+      wf[i] = from_f32<T>(v);
+      if (wd) wd[((size_t)c * e.R * e.S + rs) * e.K + k] = from_f32<T>(v);
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------------------
@@ -753,7 +796,7 @@ static void dispatch_ig(const IgParams& p, int maxM, int bm, int bn, hipStream_t
 }
 
 extern int g_glds_min_k, g_glds_min_grid;  // conv_glds.hip
-extern int g_halo_enable;                  // conv_halo.hip
+extern int g_halo_enable, g_wg_halo_enable, g_wg_halo_target_blocks;  // conv_halo.hip
 static int g_smallk_max = 128;  // argus_conv_tuning key 7: largest K (elements) served by the OCC=4 kernel
 
 template <typename T>
@@ -794,6 +837,8 @@ int conv_tuning(int key, int value) {
   if (key == 8) { g_glds_min_k = value; return 0; }
   if (key == 9) { g_glds_min_grid = value; return 0; }
   if (key == 10) { g_halo_enable = value; return 0; }
+  if (key == 11) { g_wg_halo_enable = value; return 0; }
+  if (key == 12) { g_wg_halo_target_blocks = value; return 0; }
   return -1;
 }
 
@@ -931,7 +976,13 @@ static WgPlan wgrad_plan(const argus_conv_desc& d, int dtype) {
 size_t conv_wgrad_ws(const argus_conv_desc& d, int dtype) {
   if (check_desc(d)) return 0;
   const WgPlan pl = wgrad_plan(d, dtype);
-  return (size_t)pl.splits * d.k * pl.N * sizeof(float);
+  size_t b = (size_t)pl.splits * d.k * pl.N * sizeof(float);
+  int hs, htps;
+  if (wgrad3x3_halo_plan(d, dtype, &hs, &htps)) {
+    const size_t hb = (size_t)hs * d.k * 9 * d.c * sizeof(float);
+    b = hb > b ? hb : b;
+  }
+  return b;
 }
 
 template <typename T, int BM, int BN, bool STEM, bool PRO, bool FAST>
@@ -992,15 +1043,20 @@ int conv_wgrad(const argus_conv_desc& d, int dtype, const void* x, const float* 
   p.H = d.h; p.W = d.w; p.Ho = d.ho; p.Wo = d.wo; p.stride = d.stride; p.pad = d.pad; p.S = d.s;
   p.P = d.n * d.ho * d.wo; p.pps = pl.pps; p.stem = d.stem;
   if (d.stem && sc) { set_error("conv_wgrad: stem has no prologue"); return ARGUS_ERR_ARG; }
-  if (dtype == ARGUS_BF16) dispatch_wg<bf16>(p, pl, st);
-  else dispatch_wg<float>(p, pl, st);
-  if (int e = check_launch("wgrad_kernel")) return e;
+  int splits = pl.splits;
+  if (wgrad3x3_halo_launch(d, dtype, x, sc, sh, dy, ws, ws_bytes, &splits, st)) {
+    if (int e = check_launch("wgrad3x3_halo_kernel")) return e;
+  } else {
+    if (dtype == ARGUS_BF16) dispatch_wg<bf16>(p, pl, st);
+    else dispatch_wg<float>(p, pl, st);
+    if (int e = check_launch("wgrad_kernel")) return e;
+  }
   const size_t total4 = (size_t)d.k * pl.N / 4;
   int cw = 64;  // float4 columns per block: aim for >= 512 blocks, more split lanes when few columns
   while (cw > 4 && (total4 + cw - 1) / cw < 512) cw >>= 1;
   const int blocks = (int)((total4 + cw - 1) / cw);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, reinterpret_cast<const float*>(ws),
-                     pl.splits, d.k, pl.N, d.stem, cw, dw);
+                     splits, d.k, pl.N, d.stem, cw, dw);
   return check_launch("wgrad_reduce_kernel");
 }
 
@@ -1033,6 +1089,46 @@ int conv_weight_prep(const argus_conv_desc& d, int dtype, const float* w, const 
     hipLaunchKernelGGL(weight_prep_kernel<float>, dim3(blocks), dim3(256), 0, st, w, ws, (float*)wf,
                        (float*)(d.stem ? nullptr : wd), d.k, d.r, d.s, d.c, d.stem);
   return check_launch("weight_prep_kernel");
+}
+
+size_t conv_weight_prep_table_bytes(int count) { return count > 0 ? (size_t)count * sizeof(WpEntry) : 0; }
+
+int conv_weight_prep_table(int count, const argus_conv_desc* descs, const float* const* w, const int64_t* strides,
+                           void* const* wf, void* const* wd, void* host_table, size_t bytes, int* nblocks) {
+  if (count <= 0 || !descs || !w || !wf || !host_table || bytes < conv_weight_prep_table_bytes(count)) {
+    set_error("conv_weight_prep_table: bad arguments");
+    return ARGUS_ERR_ARG;
+  }
+  WpEntry* tab = reinterpret_cast<WpEntry*>(host_table);
+  int blk = 0;
+  for (int i = 0; i < count; ++i) {
+    const argus_conv_desc& d = descs[i];
+    if (int e = check_desc(d)) return e;
+    if (!w[i] || !wf[i]) { set_error("conv_weight_prep_table: null pointer"); return ARGUS_ERR_ARG; }
+    WpEntry& t = tab[i];
+    t.w = w[i];
+    if (strides) { t.sk = strides[4 * i]; t.sc = strides[4 * i + 1]; t.sr = strides[4 * i + 2]; t.ss = strides[4 * i + 3]; }
+    else { t.sk = (long long)d.r * d.s * d.c; t.sc = 1; t.sr = (long long)d.s * d.c; t.ss = d.c; }
+    t.wf = wf[i];
+    t.wd = (d.stem || !wd) ? nullptr : wd[i];
+    t.K = d.k; t.R = d.r; t.S = d.s; t.C = d.c; t.stem = d.stem; t.blk0 = blk;
+    const long total = d.stem ? (long)d.k * 256 : (long)d.k * d.r * d.s * d.c;
+    blk += (int)((total + kWpChunk - 1) / kWpChunk);
+  }
+  if (nblocks) *nblocks = blk;
+  return ARGUS_OK;
+}
+
+int conv_weight_prep_batch(int dtype, int count, const void* device_table, int nblocks, hipStream_t st) {
+  if (count <= 0 || nblocks <= 0 || !device_table) { set_error("conv_weight_prep_batch: bad arguments"); return ARGUS_ERR_ARG; }
+  g_launch_work = 0.0;
+  if (dtype == ARGUS_BF16)
+    hipLaunchKernelGGL(weight_prep_batch_kernel<bf16>, dim3(nblocks), dim3(256), 0, st,
+                       reinterpret_cast<const WpEntry*>(device_table), count);
+  else
+    hipLaunchKernelGGL(weight_prep_batch_kernel<float>, dim3(nblocks), dim3(256), 0, st,
+                       reinterpret_cast<const WpEntry*>(device_table), count);
+  return check_launch("weight_prep_batch_kernel");
 }
 
 int images_to_nhwc4(int dtype, int64_t nimg, int h, int w, const float* x, void* out, hipStream_t st) {

@@ -333,4 +333,249 @@ bool conv3x3_halo_launch(const IgParams& p, hipStream_t st) {
   return true;
 }
 
+
+// ================================================================================================
+// 3x3 stride-1 weight gradient with the input halo tile in LDS (dW[k][tap][c] = sum_p dy[p][k] *
+// x'[p + off(tap)][c], x' = relu(x*scale+shift) with PRO). A workgroup (8 waves, 2 x 4) owns 64
+// output channels x 9 taps x 64 input channels (a 64 x 576 tile; wave (wm, wn) holds rows 32wm..+31
+// and the 9 column blocks of 16 at 9wn..9wn+8) and reduces over a range of 128-pixel tiles (whole
+// rows of one image, or whole images when H*W < 128). Per tile it glds-loads dy [128 px][64 k] and
+// the x halo [(rows+2)*(W+2) positions][64 c] once (7 uniform 1 KB pieces per wave, double-buffered
+// over tiles with a counted vmcnt); both MFMA operands are k(=pixel)-major, read with
+// ds_read_b64_tr_b16. Images are [row][128 B], 16-byte slot j of row r at slot j ^ wsw(r): the eight
+// rows a 32-lane half touches in one transposed read (r0..r0+3, r0+8..r0+11) hit distinct banks.
+// fp32 partials go to part[split][K][9C]; wgrad_reduce_kernel sums them in fixed order.
+// ================================================================================================
+struct WgHaloParams {
+  const bf16* x;
+  const bf16* dy;
+  const float* pro_scale;
+  const float* pro_shift;
+  float* part;
+  int n, H, W, C, K;
+  int ptiles, tps;  // 128-pixel tiles in total, tiles per split
+};
+
+constexpr int kWgHaloPos = 320;
+
+ARGUS_DEV int wsw(int r) { return (((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2); }
+
+ARGUS_DEV u32x4 tr_frag(const char* img, int r_lo, int r_hi, int slot, int half8) {
+  // two ds_read_b64_tr_b16: rows r_lo (elements 0..3) and r_hi (elements 4..7) of this lane's group
+  const char* a0 = img + r_lo * 128 + ((slot ^ wsw(r_lo)) << 4) + half8;
+  const char* a1 = img + r_hi * 128 + ((slot ^ wsw(r_hi)) << 4) + half8;
+  const s16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (s16x4 __attribute__((address_space(3)))*)(uintptr_t)(uint32_t)(uintptr_t)a0);
+  const s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (s16x4 __attribute__((address_space(3)))*)(uintptr_t)(uint32_t)(uintptr_t)a1);
+  const uint2 u0 = __builtin_bit_cast(uint2, t0), u1 = __builtin_bit_cast(uint2, t1);
+  return u32x4{u0.x, u0.y, u1.x, u1.y};
+}
+
+template <bool PRO>
+__global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(const WgHaloParams p) {
+  constexpr int DYB = 128 * 128;                // dy image bytes
+  constexpr int HXB = kWgHaloPos * 128;         // halo image bytes
+  constexpr int STG = DYB + HXB;                // one stage
+  constexpr int PIECES = STG / 1024;            // 1 KB glds pieces per stage (56)
+  constexpr int GPW = PIECES / 8;               // per wave (7)
+  static_assert(GPW * 8 == PIECES && DYB / 1024 == 16, "stage partition");
+  __shared__ __attribute__((aligned(1024))) u32x4 lds[(2 * STG + 512) / 16];
+
+  const int ctiles = p.C / 64;
+  const int kt = blockIdx.x / ctiles, ct = blockIdx.x - kt * ctiles;
+  const int split = blockIdx.y;
+  const int t0 = split * p.tps, t1 = min(p.ptiles, t0 + p.tps);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)lds;
+  float* coef = reinterpret_cast<float*>(reinterpret_cast<char*>(lds) + 2 * STG);  // [2][64]
+
+  const int H = p.H, W = p.W, HWi = H * W;
+  int NI, R;
+  if (HWi >= 128) { NI = 1; R = 128 / W; } else { NI = 128 / HWi; R = H; }
+  const int HWD = W + 2, IMGP = (R + 2) * HWD, npos = NI * IMGP;
+
+  if constexpr (PRO) {
+    if (tid < 128) coef[tid] = tid < 64 ? p.pro_scale[ct * 64 + tid] : p.pro_shift[ct * 64 + tid - 64];
+  }
+
+  // fragment geometry: pixel 32*s2 + 8g + 4h + q of the tile -> halo row at tap (0,0)
+  const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, pp = i16 & 3;
+  const int half8 = (pp & 1) * 8;
+  auto halo_row = [&](int m) {
+    const int ii = m / (R * W), rem = m - ii * (R * W);
+    const int lr = rem / W, lc = rem - lr * W;
+    return ii * IMGP + lr * HWD + lc;
+  };
+  // glds pieces of this wave: i = 0, 1 -> dy rows; i = 2..6 -> halo positions
+  int pos_ii[GPW - 2], pos_hr[GPW - 2], pos_hc[GPW - 2];
+  bool pos_in[GPW - 2];
+#pragma unroll
+  for (int i = 2; i < GPW; ++i) {
+    const int qq = 8 * (wave + 8 * (i - 2)) + (lane >> 3);
+    const int ii = qq / IMGP, rem = qq - ii * IMGP;
+    pos_ii[i - 2] = ii;
+    pos_hr[i - 2] = rem / HWD;
+    pos_hc[i - 2] = rem - pos_hr[i - 2] * HWD;
+    pos_in[i - 2] = qq < npos;
+  }
+  const void* zero = (const void*)halo_zero_page;
+
+  auto issue = [&](int tile, int stage) {
+    int img0, r0;
+    if (HWi >= 128) { img0 = (tile * 128) / HWi; r0 = (tile * 128 - img0 * HWi) / W; }
+    else { img0 = tile * NI; r0 = 0; }
+    const uint32_t base = lds0 + stage * STG;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = 8 * (wave + 8 * i) + (lane >> 3);
+      gl16(p.dy + (size_t)(tile * 128 + row) * p.K + kt * 64 + ((lane & 7) ^ wsw(row)) * 8,
+           base + (wave + 8 * i) * 1024);
+    }
+#pragma unroll
+    for (int i = 2; i < GPW; ++i) {
+      const int qq = 8 * (wave + 8 * (i - 2)) + (lane >> 3);
+      const int ih = r0 + pos_hr[i - 2] - 1, iw = pos_hc[i - 2] - 1;
+      const bool ok = pos_in[i - 2] && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+      const bf16* src = p.x + ((size_t)((img0 + pos_ii[i - 2]) * H + ih) * W + iw) * p.C + ct * 64 +
+                        ((lane & 7) ^ wsw(qq)) * 8;
+      gl16(ok ? (const void*)src : zero, base + DYB + (wave + 8 * (i - 2)) * 1024);
+    }
+  };
+
+  f32x4 acc[2][9];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 9; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (t0 < t1) issue(t0, 0);
+  for (int tile = t0; tile < t1; ++tile) {
+    const int stage = (tile - t0) & 1;
+    const bool more = tile + 1 < t1;
+    if (more) issue(tile + 1, stage ^ 1);  // its buffer was last read before the previous barrier
+    if (more) waitvm<GPW>(); else waitvm<0>();
+    sbar();
+    const char* DYI = reinterpret_cast<const char*>(lds) + stage * STG;
+    const char* HXI = DYI + DYB;
+    if constexpr (PRO) {
+      int img0, r0;
+      if (HWi >= 128) { img0 = (tile * 128) / HWi; r0 = (tile * 128 - img0 * HWi) / W; }
+      else { img0 = tile * NI; r0 = 0; }
+      (void)img0;
+      char* Hl = reinterpret_cast<char*>(lds) + stage * STG + DYB;
+      for (int idx = tid; idx < npos * 8; idx += 512) {
+        const int qq = idx >> 3, slot = idx & 7;
+        const int ii = qq / IMGP, rem = qq - ii * IMGP;
+        const int hr = rem / HWD, hc = rem - hr * HWD;
+        const int ih = r0 + hr - 1, iw = hc - 1;
+        (void)ii;
+        u32x4* ptr = reinterpret_cast<u32x4*>(Hl + qq * 128 + slot * 16);
+        if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) {
+          const int ch = (slot ^ wsw(qq)) * 8;
+          float f[8];
+          unpack(*ptr, f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], coef[ch + j], coef[64 + ch + j]), 0.f);
+          *ptr = pack(f);
+        } else {
+          *ptr = u32x4{0u, 0u, 0u, 0u};
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+      sbar();
+    }
+#pragma unroll 1
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const int rlo = 32 * s2 + 8 * g + q;
+      const int h0 = halo_row(rlo), h1 = halo_row(rlo + 4);
+      u32x4 fa[2];
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) fa[mi] = tr_frag(DYI, rlo, rlo + 4, 2 * (2 * wm + mi) + (pp >> 1), half8);
+#pragma unroll
+      for (int ni = 0; ni < 9; ++ni) {
+        const int nb = 9 * wn + ni;  // 16-column block of the 576 columns: tap nb/4, channels 16*(nb%4)
+        const int t = nb >> 2, cb = nb & 3;
+        const int toff = (t / 3) * HWD + (t % 3);
+        const u32x4 fb = tr_frag(HXI, h0 + toff, h1 + toff, 2 * cb + (pp >> 1), half8);
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi) Mma<bf16>::run(acc[mi][ni], fa[mi], fb);
+      }
+    }
+    sbar();  // every wave is done with this stage before it is refilled
+  }
+
+  // ---- fp32 partial tile: part[split][k][tap*C + c] ----
+  float* out = p.part + (size_t)split * p.K * (9 * p.C);
+#pragma unroll
+  for (int ni = 0; ni < 9; ++ni) {
+    const int nb = 9 * wn + ni;
+    const int t = nb >> 2, cb = nb & 3;
+    const int col = t * p.C + ct * 64 + cb * 16 + i16;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        out[(size_t)(kt * 64 + wm * 32 + mi * 16 + g * 4 + r) * (9 * p.C) + col] = acc[mi][ni][r];
+  }
+}
+
+template <bool PRO>
+static const char* wg_halo_name() {
+  static const std::string s = std::string("argus::wgrad3x3_halo_kernel<") + bool_name(PRO) + ">";
+  return s.c_str();
+}
+
+int g_wg_halo_enable = 1;          // argus_conv_tuning key 11
+int g_wg_halo_target_blocks = 512;  // key 12
+
+// Plan for a 3x3 / stride 1 / pad 1 bf16 weight gradient: false when not served. splits * K * 9C
+// fp32 partials.
+bool wgrad3x3_halo_plan(const argus_conv_desc& d, int dtype, int* splits, int* tps) {
+  if (!g_wg_halo_enable || dtype != ARGUS_BF16 || d.stem || d.r != 3 || d.s != 3 || d.stride != 1 || d.pad != 1 ||
+      d.c % 64 || d.k % 64 || d.ho != d.h || d.wo != d.w)
+    return false;
+  const int HWi = d.h * d.w;
+  int npos;
+  if (HWi >= 128) {
+    if (128 % d.w || HWi % 128) return false;
+    npos = (128 / d.w + 2) * (d.w + 2);
+  } else {
+    if (128 % HWi) return false;
+    npos = (128 / HWi) * (d.h + 2) * (d.w + 2);
+  }
+  if (npos > kWgHaloPos) return false;
+  const long ptiles = (long)d.n * HWi / 128;
+  const long tiles = (long)(d.k / 64) * (d.c / 64);
+  long s = (g_wg_halo_target_blocks + tiles - 1) / tiles;
+  if (s < 1) s = 1;
+  if (s > ptiles) s = ptiles;
+  const long per = (ptiles + s - 1) / s;
+  *tps = (int)per;
+  *splits = (int)((ptiles + per - 1) / per);
+  return true;
+}
+
+bool wgrad3x3_halo_launch(const argus_conv_desc& d, int dtype, const void* x, const float* sc, const float* sh,
+                          const void* dy, void* ws, size_t ws_bytes, int* splits_out, hipStream_t st) {
+  int splits, tps;
+  if (!wgrad3x3_halo_plan(d, dtype, &splits, &tps)) return false;
+  if (ws_bytes < (size_t)splits * d.k * 9 * d.c * sizeof(float)) return false;
+  WgHaloParams p;
+  p.x = reinterpret_cast<const bf16*>(x);
+  p.dy = reinterpret_cast<const bf16*>(dy);
+  p.pro_scale = sc;
+  p.pro_shift = sh;
+  p.part = reinterpret_cast<float*>(ws);
+  p.n = d.n; p.H = d.h; p.W = d.w; p.C = d.c; p.K = d.k;
+  p.ptiles = d.n * d.h * d.w / 128;
+  p.tps = tps;
+  dim3 grid((d.k / 64) * (d.c / 64), splits);
+  if (sc) timed_launch(wg_halo_name<true>(), wgrad3x3_halo_kernel<true>, grid, dim3(512), st, p);
+  else timed_launch(wg_halo_name<false>(), wgrad3x3_halo_kernel<false>, grid, dim3(512), st, p);
+  *splits_out = splits;
+  return true;
+}
+
 }  // namespace argus

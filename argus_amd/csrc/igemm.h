@@ -2,6 +2,7 @@
 // global->LDS (glds) kernel (conv_glds.hip).
 #pragma once
 #include "common.h"
+#include "../../include/argus_hip.h"
 
 namespace argus {
 
@@ -58,5 +59,10 @@ ARGUS_DEV u32x4 sel(bool ok, u32x4 v) {
 bool igemm_glds_launch(const IgParams& p, int maxM, int maxK, hipStream_t st);
 // 3x3 stride-1 forward / dgrad with an LDS-resident halo tile (conv_halo.hip); false = not served
 bool conv3x3_halo_launch(const IgParams& p, hipStream_t st);
+// 3x3 stride-1 weight gradient with an LDS-resident halo tile (conv_halo.hip): plan / launch of the
+// split partials (fp32 [splits][K][9C]); false = not served
+bool wgrad3x3_halo_plan(const argus_conv_desc& d, int dtype, int* splits, int* tiles_per_split);
+bool wgrad3x3_halo_launch(const argus_conv_desc& d, int dtype, const void* x, const float* sc, const float* sh,
+                          const void* dy, void* ws, size_t ws_bytes, int* splits, hipStream_t st);
 
 }  // namespace argus

@@ -18,6 +18,10 @@ int conv_fwd_stat_rows(const argus_conv_desc& d, int dtype);
 int conv_fwd_stat_tile(const argus_conv_desc& d, int dtype);
 int conv_tuning(int key, int value);
 int conv_launch_info(const argus_conv_desc& d, int dtype, int pass, int64_t* flops);
+size_t conv_weight_prep_table_bytes(int count);
+int conv_weight_prep_table(int count, const argus_conv_desc* descs, const float* const* w, const int64_t* strides,
+                           void* const* wf, void* const* wd, void* host_table, size_t bytes, int* nblocks);
+int conv_weight_prep_batch(int dtype, int count, const void* device_table, int nblocks, hipStream_t st);
 int conv_dgrad(const argus_conv_desc& d, int dtype, const void* dy, const void* wt, void* dx,
                const void* addend, const uint8_t* addend_mask, hipStream_t st);
 size_t conv_wgrad_ws(const argus_conv_desc& d, int dtype);

@@ -226,13 +226,30 @@ class ResNetEngine:
             self._bn_eval(P, Bf, bn)
 
     def prepare_weights(self, P) -> None:
-        s = stream()
-        for name, cv in self.convs.items():
+        """fp32 master weights -> compute-dtype GEMM copies (w_fwd, w_dgrad) of every conv, one launch
+        (argus_conv_weight_prep_batch); the device table is rebuilt only when a weight moves."""
+        ws = []
+        for name in self.convs:
             w = P[name + ".weight"]
             if w.dtype != torch.float32 or w.device != self.device:
                 raise TypeError(f"{name}.weight must be fp32 on {self.device}")
-            strides = (C.c_int64 * 4)(*w.stride())
-            self.L.conv_weight_prep(C.byref(cv.desc), self.dt, ptr(w), strides, ptr(cv.wf), ptr(cv.wd), s)
+            ws.append(w)
+        key = tuple((w.data_ptr(), w.stride()) for w in ws)
+        if getattr(self, "_wp_key", None) != key:
+            cvs = list(self.convs.values())
+            n = len(cvs)
+            descs = (ConvDesc * n)(*[cv.desc for cv in cvs])
+            masters = (C.c_void_p * n)(*[w.data_ptr() for w in ws])
+            strides = (C.c_int64 * (4 * n))(*[x for w in ws for x in w.stride()])
+            wfs = (C.c_void_p * n)(*[cv.wf.data_ptr() for cv in cvs])
+            wds = (C.c_void_p * n)(*[cv.wd.data_ptr() if cv.wd is not None else None for cv in cvs])
+            nbytes = self.L.dll.argus_conv_weight_prep_table_bytes(n)
+            host = (C.c_uint8 * nbytes)()
+            nblk = C.c_int(0)
+            self.L.conv_weight_prep_table(n, descs, masters, strides, wfs, wds, host, nbytes, C.byref(nblk))
+            self._wp_table = torch.frombuffer(bytearray(host), dtype=torch.uint8).to(self.device)
+            self._wp_n, self._wp_blocks, self._wp_key = n, nblk.value, key
+        self.L.conv_weight_prep_batch(self.dt, self._wp_n, ptr(self._wp_table), self._wp_blocks, stream())
 
     # ------------------------------------------------------------------ forward
     def forward(self, x: torch.Tensor, P: dict, Bf: dict, training: bool) -> torch.Tensor:

@@ -58,6 +58,18 @@ int argus_conv_weight_prep(const argus_conv_desc* d, int dtype, const float* w_m
                            argus_stream_t stream);
 
 /* ---- convolution (torchvision Conv2d, bias=False; models.py:43) ------------------------------ */
+/* Batched weight_prep (one launch for a whole network): the host writes a table of `count`
+ * conversions (argus_conv_weight_prep_table: per conv its descriptor, fp32 master pointer and
+ * element strides {sk, sc, sr, ss} (NULL strides = OHWI contiguous), w_fwd and w_dgrad destinations
+ * (w_dgrad array NULL or entry ignored for the stem)) into host_table, copies it to device memory
+ * once, and then argus_conv_weight_prep_batch does what argus_conv_weight_prep does for every entry.
+ * The table holds raw device pointers: rebuild it if any of them changes. */
+size_t argus_conv_weight_prep_table_bytes(int count);
+int argus_conv_weight_prep_table(int count, const argus_conv_desc* descs, const float* const* w_master,
+                                 const int64_t* strides, void* const* w_fwd, void* const* w_dgrad,
+                                 void* host_table, size_t table_bytes, int* nblocks);
+int argus_conv_weight_prep_batch(int dtype, int count, const void* device_table, int nblocks,
+                                 argus_stream_t stream);
 /* y = conv(x', w) where x' = relu(x*pro_scale+pro_shift) per input channel when pro_scale != NULL
  * (the producer's BatchNorm+ReLU applied while staging; zero padding stays zero), else x.
  * If stat_part != NULL, per-(row-tile, channel) {sum, M2} of y (fp32 accumulators, before
@@ -79,8 +91,9 @@ int argus_conv_dgrad(const argus_conv_desc* d, int dtype, const void* dy, const 
  * single-buffer forward/dgrad kernel (default 128), key 8 the smallest K served by the bf16
  * global->LDS (glds) forward/dgrad kernel (default 512; 0 disables it), key 9 the fewest
  * workgroups for which that kernel is chosen (default 256), key 10 enables (1, default) or
- * disables (0) the LDS-halo kernel for 3x3 stride-1 forward/dgrad. Returns 0, or -1 for an
- * unknown key. */
+ * disables (0) the LDS-halo kernel for 3x3 stride-1 forward/dgrad, key 11 the same for the 3x3
+ * stride-1 weight gradient and key 12 its split target (workgroups, default 512). Returns 0, or -1
+ * for an unknown key. */
 int argus_conv_tuning(int key, int value);
 /* Which tile a pass launches and its algorithmic work: pass 0 fwd, 1 dgrad, 2 wgrad. Returns a
  * tag (kind*10^7 + dtype*10^6 + tile_m*1000 + tile_n; kind 1 igemm, 2 wgrad) and writes
