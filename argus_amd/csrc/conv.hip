@@ -73,7 +73,8 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
   constexpr int MI = BM / 32, NI = BN / 32;
   constexpr int AR = BM / 32, BR = BN / 32;
   constexpr int NBUF = OCC >= 3 ? 1 : 2;
-  constexpr int LDS_BYTES = NBUF * (BM + BN) * 128;
+  constexpr int HALF_C = (BM / 2) * (BN + 16 / (int)sizeof(T)) * (int)sizeof(T);  // epilogue pass of BM/2 rows
+  constexpr int LDS_BYTES = NBUF * (BM + BN) * 128 > HALF_C ? NBUF * (BM + BN) * 128 : HALF_C;
   __shared__ __attribute__((aligned(16))) u32x4 lds[LDS_BYTES / 16];
 
   const IgPhase& ph = p.ph[blockIdx.z];
@@ -302,6 +303,7 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
   constexpr int LD = epi_ld<T, BN>();
   constexpr int EPASS = (BM * LD * (int)sizeof(T) > LDS_BYTES) ? 2 : 1;
   constexpr int ROWS = BM / EPASS;
+  static_assert(ROWS * LD * (int)sizeof(T) <= LDS_BYTES, "epilogue C tile exceeds the LDS array");
   constexpr int CPR = BN * (int)sizeof(T) / 16;  // 16-byte chunks per row
   constexpr int RPP = 256 / CPR;                  // rows per store pass
   T* Cs = reinterpret_cast<T*>(lds);
@@ -796,7 +798,8 @@ static void dispatch_ig(const IgParams& p, int maxM, int bm, int bn, hipStream_t
 }
 
 extern int g_glds_min_k, g_glds_min_grid;  // conv_glds.hip
-extern int g_halo_enable, g_wg_halo_enable, g_wg_halo_target_blocks;  // conv_halo.hip
+extern int g_halo_enable, g_wg_halo_enable, g_wg_halo_target_blocks, g_halo_min_grid,
+    g_wg_halo_max_tiles;  // conv_halo.hip
 static int g_smallk_max = 128;  // argus_conv_tuning key 7: largest K (elements) served by the OCC=4 kernel
 
 template <typename T>
@@ -839,6 +842,8 @@ int conv_tuning(int key, int value) {
   if (key == 10) { g_halo_enable = value; return 0; }
   if (key == 11) { g_wg_halo_enable = value; return 0; }
   if (key == 12) { g_wg_halo_target_blocks = value; return 0; }
+  if (key == 13) { g_halo_min_grid = value; return 0; }
+  if (key == 14) { g_wg_halo_max_tiles = value; return 0; }
   return -1;
 }
 

@@ -302,7 +302,8 @@ static void launch_halo(const IgParams& p, hipStream_t st) {
   timed_launch(halo_name<BN, PRO>(), conv3x3_halo_kernel<BN, PRO>, grid, dim3(4 * (BN / 64) * 64), st, p);
 }
 
-int g_halo_enable = 1;  // argus_conv_tuning key 10
+int g_halo_enable = 1;      // argus_conv_tuning key 10
+int g_halo_min_grid = 256;  // key 13: fewest workgroups for which the fwd/dgrad halo kernel is chosen
 
 // 3x3 / stride 1 / pad 1, same input and output grid, one phase, whole-row / whole-image 256-pixel tiles
 bool conv3x3_halo_launch(const IgParams& p, hipStream_t st) {
@@ -323,14 +324,17 @@ bool conv3x3_halo_launch(const IgParams& p, hipStream_t st) {
   }
   if (npos > kHaloPos) return false;
   if (p.stats && p.stat_tile != 64 && p.stat_tile != 128) return false;
-  if (p.N % 128 == 0) {
+  // measured (tools/convbench.py, B=64): wins only with 8-wave workgroups (N % 128) filling every CU;
+  // the 4-wave BN=64 tile and sub-CU-count grids lose to the register-staged kernel
+  if (p.N % 128 == 0 && (ph.M / 256) * (p.N / 128) >= g_halo_min_grid) {
     if (p.pro_scale) launch_halo<128, true>(p, st); else launch_halo<128, false>(p, st);
-  } else if (p.N % 64 == 0) {
-    if (p.pro_scale) launch_halo<64, true>(p, st); else launch_halo<64, false>(p, st);
-  } else {
-    return false;
+    return true;
   }
-  return true;
+  if (g_halo_min_grid <= 1 && p.N % 64 == 0) {  // forced (tests): the 4-wave variant
+    if (p.pro_scale) launch_halo<64, true>(p, st); else launch_halo<64, false>(p, st);
+    return true;
+  }
+  return false;
 }
 
 
@@ -529,6 +533,7 @@ static const char* wg_halo_name() {
 
 int g_wg_halo_enable = 1;          // argus_conv_tuning key 11
 int g_wg_halo_target_blocks = 512;  // key 12
+int g_wg_halo_max_tiles = 4;        // key 14
 
 // Plan for a 3x3 / stride 1 / pad 1 bf16 weight gradient: false when not served. splits * K * 9C
 // fp32 partials.
@@ -545,9 +550,12 @@ bool wgrad3x3_halo_plan(const argus_conv_desc& d, int dtype, int* splits, int* t
     if (128 % HWi) return false;
     npos = (128 / HWi) * (d.h + 2) * (d.w + 2);
   }
-  if (npos > kWgHaloPos) return false;
+  if (npos > kWgHaloPos || ((long)d.n * HWi) % 128) return false;  // whole 128-pixel tiles only
   const long ptiles = (long)d.n * HWi / 128;
   const long tiles = (long)(d.k / 64) * (d.c / 64);
+  // measured: a win for <= 4 (k, c) tiles (the 64- and 128-channel layers); beyond, its two tr16
+  // operand streams make it LDS-read-bound and the register-staged wgrad_kernel is faster
+  if (tiles > g_wg_halo_max_tiles) return false;
   long s = (g_wg_halo_target_blocks + tiles - 1) / tiles;
   if (s < 1) s = 1;
   if (s > ptiles) s = ptiles;

@@ -234,7 +234,8 @@ class ResNetEngine:
             if w.dtype != torch.float32 or w.device != self.device:
                 raise TypeError(f"{name}.weight must be fp32 on {self.device}")
             ws.append(w)
-        key = tuple((w.data_ptr(), w.stride()) for w in ws)
+        key = tuple((w.data_ptr(), w.stride(), cv.wf.data_ptr(), cv.wd.data_ptr() if cv.wd is not None else 0)
+                    for w, cv in zip(ws, self.convs.values()))
         if getattr(self, "_wp_key", None) != key:
             cvs = list(self.convs.values())
             n = len(cvs)

@@ -566,6 +566,16 @@ def test_conv3x3_halo_kernel_parity(cuda):
 
     torch.manual_seed(13)
     L = lib()
+    assert L.dll.argus_conv_tuning(13, 1) == 0  # force the halo kernel on every eligible shape
+    try:
+        _halo_cases(L, cuda)
+    finally:
+        L.dll.argus_conv_tuning(13, 256)
+
+
+def _halo_cases(L, cuda):
+    from argus_amd.profiling import KernelTimer
+
     for cin, cout, hw, n in HALO_SHAPES:
         d, p = _desc(n, hw, hw, cin, cout, 3, 1)
         x = torch.randn(n, hw, hw, cin) * 1.5 + 0.2
@@ -656,7 +666,17 @@ def test_wgrad3x3_halo_kernel_parity(cuda, pro):
 
     torch.manual_seed(19)
     L = lib()
-    for cin, cout, hw, n in [(64, 64, 64, 1), (128, 128, 32, 1), (64, 128, 16, 2), (128, 64, 8, 4)]:
+    assert L.dll.argus_conv_tuning(14, 1 << 20) == 0  # every channel-tile count
+    try:
+        _wgrad_halo_cases(L, cuda, pro)
+    finally:
+        L.dll.argus_conv_tuning(14, 4)
+
+
+def _wgrad_halo_cases(L, cuda, pro):
+    from argus_amd.profiling import KernelTimer
+
+    for cin, cout, hw, n in [(64, 64, 64, 1), (128, 128, 32, 1), (64, 128, 16, 2), (128, 64, 8, 4), (256, 128, 16, 1)]:
         d, p = _desc(n, hw, hw, cin, cout, 3, 1)
         x = _q(torch.randn(n, hw, hw, cin) * 1.3 + 0.1, "bf16")
         dy = _q(torch.randn(n, hw, hw, cout), "bf16")
@@ -675,3 +695,28 @@ def test_wgrad3x3_halo_kernel_parity(cuda, pro):
                      "bf16").permute(0, 3, 1, 2)
         ref = torch.nn.grad.conv2d_weight(xin.double(), (cout, cin, 3, 3), dy.permute(0, 3, 1, 2).double(), padding=1)
         assert _rel(dw.permute(0, 3, 1, 2), ref) < 2e-3, ("wgrad", cin, cout, hw, n, pro)
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+def test_conv_large_tile_small_k(cuda, dt):
+    """1x1 convs with K <= 128 on 128-row tiles (M >= 16K): the single-buffer small-K kernel, whose
+    epilogue stages half a C tile (fp32: 64 x 132 floats) in its LDS array."""
+    torch.manual_seed(23)
+    L = lib()
+    for cin, cout in ((64, 128), (64, 256), (128, 64)):
+        n, hw = 4, 64
+        d, p = _desc(n, hw, hw, cin, cout, 1, 1)
+        x = torch.randn(n, hw, hw, cin)
+        w = torch.randn(cout, 1, 1, cin) * (1.0 / cin) ** 0.5
+        xd = x.to(cuda, TDT[dt])
+        wf, wt = _prep(d, dt, w.to(cuda), cuda)
+        y = torch.empty(n, hw, hw, cout, dtype=TDT[dt], device=cuda)
+        rows = L.dll.argus_conv_fwd_stat_rows(C.byref(d), DT[dt])
+        stats = torch.empty(rows, cout, 2, device=cuda)
+        L.conv_fwd(C.byref(d), DT[dt], ptr(xd), ptr(wf), ptr(y), None, None, ptr(stats), stream())
+        ref = F.conv2d(_q(x, dt).permute(0, 3, 1, 2), _q(w, dt).permute(0, 3, 1, 2))
+        assert _rel(y.permute(0, 3, 1, 2), ref) < TOL[dt], (dt, cin, cout)
+        tile = L.dll.argus_conv_fwd_stat_tile(C.byref(d), DT[dt])
+        mean, var = _merge_stats(stats.double().cpu(), tile, n * hw * hw)
+        yr = ref.permute(0, 2, 3, 1).reshape(-1, cout)
+        assert _rel(var, yr.var(0, unbiased=False)) < (1e-4 if dt == "fp32" else 2e-2), (dt, cin, cout)
