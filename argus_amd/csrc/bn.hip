@@ -163,6 +163,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(int64_t pixels, int C, in
     ra[j] = rsc ? rsc[c0 + j] : 1.f;
     rb[j] = rsc ? rsh[c0 + j] : 0.f;
   }
+#pragma unroll 4
   for (int64_t px = p0 + pl; px < p1; px += PL) {
     const int64_t off = px * C + c0;
     float f[E], r[E];

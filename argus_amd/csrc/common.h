@@ -8,6 +8,7 @@
 #include <stdint.h>
 
 #define ARGUS_DEV __device__ __forceinline__
+#define ARGUS_HOST_DEV __host__ __device__
 
 typedef __bf16 bf16;
 typedef float f32x4 __attribute__((ext_vector_type(4)));

@@ -696,8 +696,10 @@ __global__ __launch_bounds__(256) void weight_prep_kernel(const float* __restric
   }
 }
 
-// Batched weight_prep: one launch converts every conv of the network. Workgroup b handles
-// elements [(b - blk0[e]) * kWpChunk, ...) of table entry e (found by binary search on blk0).
+// Batched weight_prep: one launch converts every conv of the network. Non-stem convs go in 64(k) x
+// 64(c) tiles of one tap: the tile is read once (rows of c), written to w_fwd[k][tap][c] as rows and
+// transposed through LDS into w_dgrad[c][tap][k] as rows, so both writes are coalesced. The stem
+// (C = 3, no w_dgrad) is an element-wise pad + convert, kWpChunk elements per workgroup.
 struct WpEntry {
   const float* w;
   long long sk, sc, sr, ss;
@@ -705,7 +707,11 @@ struct WpEntry {
   void* wd;
   int K, R, S, C, stem, blk0;  // blk0: first workgroup of this entry
 };
-constexpr int kWpChunk = 2048;
+constexpr int kWpChunk = 4096;
+
+ARGUS_HOST_DEV inline int wp_blocks(int K, int R, int S, int C, int stem) {
+  return stem ? (K * 256 + kWpChunk - 1) / kWpChunk : (K / 64) * (C / 64) * R * S;
+}
 
 template <typename T>
 __global__ __launch_bounds__(256) void weight_prep_batch_kernel(const WpEntry* __restrict__ tab, int count) {
@@ -716,26 +722,59 @@ __global__ __launch_bounds__(256) void weight_prep_batch_kernel(const WpEntry* _
     if (tab[mid].blk0 <= b) lo = mid; else hi = mid - 1;
   }
   const WpEntry e = tab[lo];
-  const int total = e.stem ? e.K * 256 : e.K * e.R * e.S * e.C;
-  const int i0 = (b - e.blk0) * kWpChunk;
   T* __restrict__ wf = reinterpret_cast<T*>(e.wf);
   T* __restrict__ wd = reinterpret_cast<T*>(e.wd);
-  for (int i = i0 + threadIdx.x; i < i0 + kWpChunk && i < total; i += 256) {
-    if (e.stem) {
+  const int local = b - e.blk0;
+  if (e.stem) {
+    const int total = e.K * 256;
+    for (int i = local * kWpChunk + threadIdx.x; i < (local + 1) * kWpChunk && i < total; i += 256) {
       const int k = i >> 8, col = i & 255;
       const int r = col >> 5, s = (col & 31) >> 2, c = col & 3;
       float v = 0.f;
       if (r < 7 && s < 7 && c < 3) v = e.w[k * e.sk + c * e.sc + r * e.sr + s * e.ss];
       wf[i] = from_f32<T>(v);
-    } else {
-      const int RSC = e.R * e.S * e.C;
-      const int k = i / RSC, rem = i - k * RSC;
-      const int rs = rem / e.C, c = rem - rs * e.C;
-      const int r = rs / e.S, s = rs - r * e.S;
-      const float v = e.w[k * e.sk + c * e.sc + r * e.sr + s * e.ss];
-      wf[i] = from_f32<T>(v);
-      if (wd) wd[((size_t)c * e.R * e.S + rs) * e.K + k] = from_f32<T>(v);
     }
+    return;
+  }
+  const int RS = e.R * e.S, ct = e.C / 64;
+  const int rs = local % RS, rem = local / RS;
+  const int c0 = (rem % ct) * 64, k0 = (rem / ct) * 64;
+  const int r = rs / e.S, s = rs - r * e.S;
+  __shared__ T tile[64][65];
+  const int row = threadIdx.x >> 2, cq = (threadIdx.x & 3) * 16;  // 4 threads x 16 elements per row
+  {
+    const float* src = e.w + (long long)(k0 + row) * e.sk + r * e.sr + s * e.ss + (long long)(c0 + cq) * e.sc;
+    T* dst = wf + ((size_t)(k0 + row) * RS + rs) * e.C + c0 + cq;
+    float f[16];
+    if (e.sc == 1 && ((uintptr_t)src & 15) == 0) {  // channel-contiguous master (OHWI storage): 16-byte loads
+#pragma unroll
+      for (int j = 0; j < 16; j += 4) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(src + j);
+        f[j] = v.x; f[j + 1] = v.y; f[j + 2] = v.z; f[j + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) f[j] = src[j * e.sc];
+    }
+    constexpr int E = Chunk<T>::E;
+#pragma unroll
+    for (int j = 0; j < 16; j += E) {
+      float g[E];
+#pragma unroll
+      for (int u = 0; u < E; ++u) { g[u] = f[j + u]; tile[row][cq + j + u] = from_f32<T>(f[j + u]); }
+      st16(dst + j, pack(g));
+    }
+  }
+  if (!wd) return;
+  __syncthreads();
+  T* dst = wd + ((size_t)(c0 + row) * RS + rs) * e.K + k0 + cq;  // row = c, 16 consecutive k
+  constexpr int E = Chunk<T>::E;
+#pragma unroll
+  for (int j = 0; j < 16; j += E) {
+    float g[E];
+#pragma unroll
+    for (int u = 0; u < E; ++u) g[u] = to_f32(tile[cq + j + u][row]);
+    st16(dst + j, pack(g));
   }
 }
 
@@ -1117,8 +1156,8 @@ int conv_weight_prep_table(int count, const argus_conv_desc* descs, const float*
     t.wf = wf[i];
     t.wd = (d.stem || !wd) ? nullptr : wd[i];
     t.K = d.k; t.R = d.r; t.S = d.s; t.C = d.c; t.stem = d.stem; t.blk0 = blk;
-    const long total = d.stem ? (long)d.k * 256 : (long)d.k * d.r * d.s * d.c;
-    blk += (int)((total + kWpChunk - 1) / kWpChunk);
+    if (!d.stem && (d.k % 64 || d.c % 64)) { set_error("conv_weight_prep_table: channels must be multiples of 64"); return ARGUS_ERR_SHAPE; }
+    blk += wp_blocks(d.k, d.r, d.s, d.c, d.stem);
   }
   if (nblocks) *nblocks = blk;
   return ARGUS_OK;
