@@ -10,6 +10,7 @@
 // reduction (deterministic, run-to-run bitwise reproducible).
 #include "common.h"
 #include "internal.h"
+#include "ktimer.h"
 
 namespace argus {
 
@@ -456,6 +457,20 @@ __global__ __launch_bounds__(256) void avgpool_bwd_kernel(int64_t nchunks, int h
   }
 }
 
+// demangled kernel names for the kernel timer (ktimer.h), one static string per instantiation
+template <typename T> static const char* apply_name() {
+  static const std::string s = std::string("argus::bn_apply_kernel<") + type_name<T>() + ">";
+  return s.c_str();
+}
+template <typename T, bool DU> static const char* bred_name() {
+  static const std::string s = std::string("argus::bn_bwd_reduce_kernel<") + type_name<T>() + ", " + bool_name(DU) + ">";
+  return s.c_str();
+}
+template <typename T, bool DU> static const char* bapp_name() {
+  static const std::string s = std::string("argus::bn_bwd_apply_kernel<") + type_name<T>() + ", " + bool_name(DU) + ">";
+  return s.c_str();
+}
+
 static int grid_for(int64_t work) {
   int64_t b = (work + 255) / 256;
   if (b > 8192) b = 8192;
@@ -510,12 +525,15 @@ int argus_bn_apply(int dtype, int64_t pixels, int C, const void* y, const float*
   const EwGeom g = ew_geom(C, E, pixels, 2048);
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(g.cgroups, g.rows);
+  const double pc = (double)pixels * C;
+  g_launch_work = 0.0;  // algorithmic bytes: y, residual, out, mask bits
+  g_launch_bytes = (16.0 / E) * pc * (2.0 + (res ? 1.0 : 0.0)) + (mask_out ? pc / E : 0.0);
   if (dtype == ARGUS_BF16)
-    hipLaunchKernelGGL(bn_apply_kernel<bf16>, grid, dim3(256), 0, st, pixels, C, g.CC, g.PL, g.ppb, (const bf16*)y,
-                       scale, shift, (const bf16*)res, rsc, rsh, relu, (bf16*)out, mask_out);
+    timed_launch(apply_name<bf16>(), bn_apply_kernel<bf16>, grid, dim3(256), st, pixels, C, g.CC, g.PL,
+                 g.ppb, (const bf16*)y, scale, shift, (const bf16*)res, rsc, rsh, relu, (bf16*)out, mask_out);
   else
-    hipLaunchKernelGGL(bn_apply_kernel<float>, grid, dim3(256), 0, st, pixels, C, g.CC, g.PL, g.ppb, (const float*)y,
-                       scale, shift, (const float*)res, rsc, rsh, relu, (float*)out, mask_out);
+    timed_launch(apply_name<float>(), bn_apply_kernel<float>, grid, dim3(256), st, pixels, C, g.CC,
+                 g.PL, g.ppb, (const float*)y, scale, shift, (const float*)res, rsc, rsh, relu, (float*)out, mask_out);
   return check_launch("bn_apply_kernel");
 }
 
@@ -544,10 +562,16 @@ int argus_bn_bwd_reduce(int dtype, int64_t pixels, int C, const void* dz, int mo
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(cg, rows);
   const uint8_t* mb = mode == 3 ? (const uint8_t*)mask : nullptr;
-#define ARGUS_BWD_REDUCE(TT, DU)                                                                                  \
-  hipLaunchKernelGGL((bn_bwd_reduce_kernel<TT, DU>), grid, dim3(256), 0, st, pixels, C, CC, PL, ppb, (const TT*)dz, \
-                     mode, mode == 1 ? (const TT*)mask : (const TT*)nullptr, mb, (const TT*)y, scale, shift, mean,     \
-                     invstd, (float2*)part, (const TT*)y2, mean2, invstd2, (float2*)part2)
+  {
+    const double pc = (double)pixels * C;
+    g_launch_work = 0.0;  // algorithmic bytes: dz, y (, y2), mask tensor or bits
+    g_launch_bytes = (16.0 / E) * pc * (2.0 + (mode == 1 ? 1.0 : 0.0) + (dual ? 1.0 : 0.0)) + (mode == 3 ? pc / E : 0.0);
+  }
+#define ARGUS_BWD_REDUCE(TT, DU)                                                                                   \
+  timed_launch(bred_name<TT, DU>(), bn_bwd_reduce_kernel<TT, DU>, grid, dim3(256), st,   \
+               pixels, C, CC, PL, ppb, (const TT*)dz, mode, mode == 1 ? (const TT*)mask : (const TT*)nullptr, mb,  \
+               (const TT*)y, scale, shift, mean, invstd, (float2*)part, (const TT*)y2, mean2, invstd2,            \
+               (float2*)part2)
   if (dtype == ARGUS_BF16) {
     if (dual) ARGUS_BWD_REDUCE(bf16, true); else ARGUS_BWD_REDUCE(bf16, false);
   } else {
@@ -585,10 +609,18 @@ int argus_bn_bwd_apply(int dtype, int64_t pixels, int C, const void* dz, int mod
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(g.cgroups, g.rows);
   const uint8_t* mb = mode == 3 ? (const uint8_t*)mask : nullptr;
-#define ARGUS_BWD_APPLY(TT, DU)                                                                                      \
-  hipLaunchKernelGGL((bn_bwd_apply_kernel<TT, DU>), grid, dim3(256), 0, st, pixels, C, g.CC, g.PL, g.ppb,           \
-                     (const TT*)dz, mode, mode == 1 ? (const TT*)mask : (const TT*)nullptr, mb, (const TT*)y, scale,  \
-                     shift, ca, cb, cc, (TT*)dy, (TT*)dm_out, (const TT*)y2, ca2, cb2, cc2, (TT*)dy2)
+  {
+    const double pc = (double)pixels * C;
+    g_launch_work = 0.0;  // algorithmic bytes: dz, y, dy (, y2, dy2) (, dm), mask tensor or bits
+    g_launch_bytes = (16.0 / E) * pc *
+                         (3.0 + (mode == 1 ? 1.0 : 0.0) + (dual ? 2.0 : 0.0) + (dm_out ? 1.0 : 0.0)) +
+                     (mode == 3 ? pc / E : 0.0);
+  }
+#define ARGUS_BWD_APPLY(TT, DU)                                                                                    \
+  timed_launch(bapp_name<TT, DU>(), bn_bwd_apply_kernel<TT, DU>, grid, dim3(256), st,     \
+               pixels, C, g.CC, g.PL, g.ppb, (const TT*)dz, mode, mode == 1 ? (const TT*)mask : (const TT*)nullptr,  \
+               mb, (const TT*)y, scale, shift, ca, cb, cc, (TT*)dy, (TT*)dm_out, (const TT*)y2, ca2, cb2, cc2,      \
+               (TT*)dy2)
   if (dtype == ARGUS_BF16) {
     if (dual) ARGUS_BWD_APPLY(bf16, true); else ARGUS_BWD_APPLY(bf16, false);
   } else {

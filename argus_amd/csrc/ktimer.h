@@ -1,4 +1,5 @@
-// Live per-launch kernel timing for bench.py's roofline: while enabled, every launch of a kernel
+// Live per-launch kernel timing for bench.py's roofline: while enabled, every launch of a conv or
+// BN / elementwise kernel
 // whose instantiation name starts with the filter goes through hipExtLaunchKernelGGL with a
 // start/stop event pair carried by the dispatch packet itself, so the measured span is the
 // kernel's own execution on its stream (what rocprofv3 --kernel-trace reports), not the gap

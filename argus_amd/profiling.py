@@ -9,7 +9,7 @@ from argus_amd._lib import lib
 
 
 class KernelTimer:
-    """``with KernelTimer(prefix) as t: ...; t.summary()`` -> per-instantiation timing of conv kernels."""
+    """``with KernelTimer(prefix) as t: ...; t.summary()`` -> per-instantiation timing of conv and BN kernels."""
 
     def __init__(self, prefix: str | None = None):
         self.prefix = prefix

@@ -12,7 +12,8 @@ Weights: seeded random init (torch.manual_seed(42)) of the reference architectur
 value = images/s over all ranks (one sample = 2 camera images); weak scaling (B per rank fixed).
 
 Also reported:
-  roofline     - the dominant conv kernel instantiation (largest total time in one probe step),
+  roofline     - the dominant kernel instantiation (conv GEMM or BN pass; largest total time in one
+                 probe step),
                  timed live over the timed region by the library's kernel timer (start/stop HIP
                  events carried by each of its dispatch packets, on its launch stream). bound =
                  "mfma" if its algorithmic FLOP/byte is above the ridge (peak FLOP/s / 8 TB/s), else
@@ -132,7 +133,7 @@ def main() -> None:
 
     for _ in range(args.warmup):
         trainer.step(images, targets)
-    # find the dominant conv kernel instantiation (largest total time) over one instrumented step
+    # find the dominant kernel instantiation (largest total time) over one instrumented step
     probe = KernelTimer()
     probe.start()
     trainer.step(images, targets)

@@ -108,14 +108,14 @@ int argus_conv_wgrad(const argus_conv_desc* d, int dtype, const void* x, const f
                      size_t workspace_bytes, argus_stream_t stream);
 
 /* ---- kernel timer (bench.py roofline) ------------------------------------------------------------
- * While enabled, conv kernel launches whose demangled instantiation name (e.g.
+ * While enabled, conv and BN kernel launches whose demangled instantiation name (e.g.
  * "argus::igemm_kernel<__bf16, 128, 128, false, true>", as c++filt prints rocprofv3's kernel name)
  * starts with `filter` (NULL or "" = all) are dispatched with hipExtLaunchKernelGGL start/stop
  * events, i.e. timed by the dispatch packet on the launch stream. enable() clears old records;
  * count() synchronizes the recorded events, aggregates per name and returns the number of names;
- * get(i) returns name, launches, total milliseconds, total algorithmic flops and total algorithmic
- * HBM bytes (each operand read once and each result written once; for wgrad the fp32 split partials
- * it writes count too). */
+ * get(i) returns name, launches, total milliseconds, total algorithmic flops (0 for BN kernels) and
+ * total algorithmic HBM bytes (each operand read once and each result written once; for wgrad the
+ * fp32 split partials it writes count too). */
 int argus_ktimer_enable(const char* filter);
 int argus_ktimer_disable(void);
 int argus_ktimer_count(void);
