@@ -353,24 +353,14 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
 // ------------------------------------------------------------------------------------------------
 // weight gradient (split over pixel ranges)
 // ------------------------------------------------------------------------------------------------
-struct WgParams {
-  const void* x;
-  const void* dy;
-  const float* pro_scale;
-  const float* pro_shift;
-  float* part;  // [splits][M][N]
-  int M, N, Cin, lda, H, W, Ho, Wo, stride, pad, S;
-  int P;
-  int pps;  // pixels per split (multiple of the k-step)
-  int stem;
-};
-
 // bf16 LDS image: rows of 256 B = 8 slots of 32 B; slot XOR swz32(row) makes the 8 rows a
 // ds_read_b64_tr_b16 half-wave touches land on 8 distinct slots.
 ARGUS_DEV int swz32(int row) { return (row & 3) | (((row >> 3) & 1) << 2); }
 
-template <typename T, int BM, int BN, bool STEM, bool PRO, bool FAST>
-__global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgParams p) {
+// OCC: 2 = two workgroups per CU, no register prefetch ring on the 128x128 tile (historical default);
+// 1 = one per CU with the ring; 3 = two per CU with the ring (fits: ~220 VGPRs)
+template <typename T, int BM, int BN, bool STEM, bool PRO, bool FAST, int OCC = 2>
+__global__ __launch_bounds__(256, OCC == 1 ? 1 : 2) void wgrad_kernel(const WgParams p) {
   constexpr int E = Chunk<T>::E;
   constexpr bool BF = (E == 8);
   constexpr int BKP = BF ? 64 : 32;               // pixels per k-step
@@ -565,7 +555,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgParams p) {
 
   // LDS double buffer + 2-deep register prefetch ring (as igemm_kernel); the 128x128 tile keeps a
   // single staged k-step (the ring would not fit two waves per SIMD without spilling)
-  constexpr bool RING = !(BM == 128 && BN == 128);
+  constexpr bool RING = !(BM == 128 && BN == 128) || OCC != 2;
   const int nk = pend > pbeg ? (pend - pbeg + BKP - 1) / BKP : 0;
   if (!RING && nk > 0) {
     Stage S0;
@@ -836,7 +826,8 @@ static void dispatch_ig(const IgParams& p, int maxM, int bm, int bn, hipStream_t
   }
 }
 
-extern int g_glds_min_k, g_glds_min_grid;  // conv_glds.hip
+extern int g_glds_min_k, g_glds_min_grid, g_wg_glds_enable, g_wg_glds_target;  // conv_glds.hip
+static int g_wg_occ128 = 2;  // argus_conv_tuning key 15: workgroups/CU of the 128x128 wgrad tile (1 = with ring)
 extern int g_halo_enable, g_wg_halo_enable, g_wg_halo_target_blocks, g_halo_min_grid,
     g_wg_halo_max_tiles;  // conv_halo.hip
 static int g_smallk_max = 128;  // argus_conv_tuning key 7: largest K (elements) served by the OCC=4 kernel
@@ -883,6 +874,9 @@ int conv_tuning(int key, int value) {
   if (key == 12) { g_wg_halo_target_blocks = value; return 0; }
   if (key == 13) { g_halo_min_grid = value; return 0; }
   if (key == 14) { g_wg_halo_max_tiles = value; return 0; }
+  if (key == 15) { g_wg_occ128 = value; return 0; }
+  if (key == 16) { g_wg_glds_enable = value; return 0; }
+  if (key == 17) { g_wg_glds_target = value; return 0; }
   return -1;
 }
 
@@ -1026,27 +1020,36 @@ size_t conv_wgrad_ws(const argus_conv_desc& d, int dtype) {
     const size_t hb = (size_t)hs * d.k * 9 * d.c * sizeof(float);
     b = hb > b ? hb : b;
   }
+  int gs, gpps;
+  if (wgrad_glds_plan(d, dtype, false, &gs, &gpps)) {
+    const size_t gb = (size_t)gs * d.k * pl.N * sizeof(float);
+    b = gb > b ? gb : b;
+  }
   return b;
 }
 
-template <typename T, int BM, int BN, bool STEM, bool PRO, bool FAST>
+template <typename T, int BM, int BN, bool STEM, bool PRO, bool FAST, int OCC>
 static const char* wg_name() {
   static const std::string s = std::string("argus::wgrad_kernel<") + type_name<T>() + ", " + std::to_string(BM) +
                                ", " + std::to_string(BN) + ", " + bool_name(STEM) + ", " + bool_name(PRO) + ", " +
-                               bool_name(FAST) + ">";
+                               bool_name(FAST) + ", " + std::to_string(OCC) + ">";
   return s.c_str();
 }
 
-template <typename T, int BM, int BN, bool STEM, bool PRO, bool FAST>
+template <typename T, int BM, int BN, bool STEM, bool PRO, bool FAST, int OCC = 2>
 static void launch_wg(const WgParams& p, const WgPlan& pl, hipStream_t st) {
   dim3 grid(pl.mt * pl.nt, pl.splits);
-  timed_launch(wg_name<T, BM, BN, STEM, PRO, FAST>(), wgrad_kernel<T, BM, BN, STEM, PRO, FAST>, grid, dim3(256), st,
-               p);
+  timed_launch(wg_name<T, BM, BN, STEM, PRO, FAST, OCC>(), wgrad_kernel<T, BM, BN, STEM, PRO, FAST, OCC>, grid,
+               dim3(256), st, p);
 }
 
 template <typename T, bool PRO, bool FAST>
 static void dispatch_wg_tiles(const WgParams& p, const WgPlan& pl, hipStream_t st) {
-  if (pl.bm == 128 && pl.bn == 128) launch_wg<T, 128, 128, false, PRO, FAST>(p, pl, st);
+  if (pl.bm == 128 && pl.bn == 128) {
+    if (g_wg_occ128 == 1) launch_wg<T, 128, 128, false, PRO, FAST, 1>(p, pl, st);
+    else if (g_wg_occ128 == 3) launch_wg<T, 128, 128, false, PRO, FAST, 3>(p, pl, st);
+    else launch_wg<T, 128, 128, false, PRO, FAST, 2>(p, pl, st);
+  }
   else if (pl.bm == 128) launch_wg<T, 128, 64, false, PRO, FAST>(p, pl, st);
   else if (pl.bn == 128) launch_wg<T, 64, 128, false, PRO, FAST>(p, pl, st);
   else launch_wg<T, 64, 64, false, PRO, FAST>(p, pl, st);
@@ -1088,8 +1091,14 @@ int conv_wgrad(const argus_conv_desc& d, int dtype, const void* x, const float* 
   p.P = d.n * d.ho * d.wo; p.pps = pl.pps; p.stem = d.stem;
   if (d.stem && sc) { set_error("conv_wgrad: stem has no prologue"); return ARGUS_ERR_ARG; }
   int splits = pl.splits;
+  int gs, gpps;
   if (wgrad3x3_halo_launch(d, dtype, x, sc, sh, dy, ws, ws_bytes, &splits, st)) {
     if (int e = check_launch("wgrad3x3_halo_kernel")) return e;
+  } else if (wgrad_glds_plan(d, dtype, sc != nullptr, &gs, &gpps) &&
+             ws_bytes >= (size_t)gs * d.k * pl.N * sizeof(float)) {
+    wgrad_glds_launch(d, p, gs, gpps, st);
+    splits = gs;
+    if (int e = check_launch("wgrad_glds_kernel")) return e;
   } else {
     if (dtype == ARGUS_BF16) dispatch_wg<bf16>(p, pl, st);
     else dispatch_wg<float>(p, pl, st);

@@ -29,6 +29,18 @@ struct IgParams {
   IgPhase ph[4];
 };
 
+struct WgParams {
+  const void* x;
+  const void* dy;
+  const float* pro_scale;
+  const float* pro_shift;
+  float* part;  // [splits][M][N]
+  int M, N, Cin, lda, H, W, Ho, Wo, stride, pad, S;
+  int P;
+  int pps;  // pixels per split (multiple of the k-step)
+  int stem;
+};
+
 template <typename T> struct Mma;
 template <> struct Mma<bf16> {
   static ARGUS_DEV void run(f32x4& acc, u32x4 a, u32x4 b) {
@@ -61,6 +73,9 @@ bool igemm_glds_launch(const IgParams& p, int maxM, int maxK, hipStream_t st);
 bool conv3x3_halo_launch(const IgParams& p, hipStream_t st);
 // 3x3 stride-1 weight gradient with an LDS-resident halo tile (conv_halo.hip): plan / launch of the
 // split partials (fp32 [splits][K][9C]); false = not served
+// bf16 weight gradient on global->LDS staged operands (conv_glds.hip): plan / launch; false = not served
+bool wgrad_glds_plan(const argus_conv_desc& d, int dtype, bool pro, int* splits, int* pps);
+bool wgrad_glds_launch(const argus_conv_desc& d, const WgParams& base, int splits, int pps, hipStream_t st);
 bool wgrad3x3_halo_plan(const argus_conv_desc& d, int dtype, int* splits, int* tiles_per_split);
 bool wgrad3x3_halo_launch(const argus_conv_desc& d, int dtype, const void* x, const float* sc, const float* sh,
                           const void* dy, void* ws, size_t ws_bytes, int* splits, hipStream_t st);

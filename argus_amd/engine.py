@@ -22,6 +22,7 @@ Eval mode uses running statistics (bn_eval_coeffs) and skips all statistics / ru
 from __future__ import annotations
 
 import ctypes as C
+import os
 from dataclasses import dataclass
 
 import torch
@@ -77,6 +78,11 @@ class ResNetEngine:
         self.dt = BF16 if dtype == "bf16" else F32
         self.tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
         self.E = 8 if dtype == "bf16" else 4  # elements per 16-byte chunk
+        # materialize a = relu(bn(y)) of bn1/bn2 once per forward (one extra HBM pass each) so that
+        # conv2/conv3 forward and weight gradients run without the BN prologue, on the global->LDS
+        # kernels; fp32 (parity path) keeps the fused prologue. ARGUS_MATERIALIZE=0/1 overrides.
+        env = os.environ.get("ARGUS_MATERIALIZE")
+        self.materialize = (dtype == "bf16") if env is None else env == "1"
         self.device = torch.device(device)
         self.blocks = resnet50_blocks()
         self.shape = None
@@ -137,6 +143,8 @@ class ResNetEngine:
                 "y1": self._t(N, h, w, b.width), "y2": self._t(N, ho, wo, b.width),
                 "y3": self._t(N, ho, wo, b.cout), "out": self._t(N, ho, wo, b.cout),
                 "yd": self._t(N, ho, wo, b.cout) if b.has_ds else None,
+                "a1": self._t(N, h, w, b.width) if self.materialize else None,
+                "a2": self._t(N, ho, wo, b.width) if self.materialize else None,
                 # ReLU mask of `out`, one byte per 16-byte chunk (argus_bn_apply mask_out)
                 "bits": torch.empty(N * ho * wo * b.cout // self.E, dtype=torch.uint8, device=self.device),
             }
@@ -225,6 +233,11 @@ class ResNetEngine:
         else:
             self._bn_eval(P, Bf, bn)
 
+    def _act(self, bn, y, out, px, ch):
+        """out = relu(y*scale + shift) with the finalized coefficients of BN layer ``bn``."""
+        st = self.bn_state[bn]
+        self.L.bn_apply(self.dt, px, ch, ptr(y), ptr(st[2]), ptr(st[3]), None, None, None, 1, ptr(out), None, stream())
+
     def prepare_weights(self, P) -> None:
         """fp32 master weights -> compute-dtype GEMM copies (w_fwd, w_dgrad) of every conv, one launch
         (argus_conv_weight_prep_batch); the device table is rebuilt only when a weight moves."""
@@ -274,8 +287,14 @@ class ResNetEngine:
         for b, a in zip(self.blocks, self.act):
             pf = b.prefix
             self._conv_bn(P, Bf, pf + ".conv1", pf + ".bn1", h, a["y1"], None, training)
-            self._conv_bn(P, Bf, pf + ".conv2", pf + ".bn2", a["y1"], a["y2"], pf + ".bn1", training)
-            self._conv_bn(P, Bf, pf + ".conv3", pf + ".bn3", a["y2"], a["y3"], pf + ".bn2", training)
+            if self.materialize:
+                self._act(pf + ".bn1", a["y1"], a["a1"], N * a["hw_in"][0] * a["hw_in"][1], b.width)
+                self._conv_bn(P, Bf, pf + ".conv2", pf + ".bn2", a["a1"], a["y2"], None, training)
+                self._act(pf + ".bn2", a["y2"], a["a2"], N * a["hw"][0] * a["hw"][1], b.width)
+                self._conv_bn(P, Bf, pf + ".conv3", pf + ".bn3", a["a2"], a["y3"], None, training)
+            else:
+                self._conv_bn(P, Bf, pf + ".conv2", pf + ".bn2", a["y1"], a["y2"], pf + ".bn1", training)
+                self._conv_bn(P, Bf, pf + ".conv3", pf + ".bn3", a["y2"], a["y3"], pf + ".bn2", training)
             s3 = self.bn_state[pf + ".bn3"]
             px = N * a["hw"][0] * a["hw"][1]
             if b.has_ds:
@@ -370,14 +389,20 @@ class ResNetEngine:
             cap("b_dy3", dy3, px_o * b.cout, (N, ho, wo, b.cout))
             # conv3
             s2 = self.bn_state[pf + ".bn2"]
-            self._wgrad(pf + ".conv3", a["y2"], s2, dy3, G)
+            if self.materialize:
+                self._wgrad(pf + ".conv3", a["a2"], None, dy3, G)
+            else:
+                self._wgrad(pf + ".conv3", a["y2"], s2, dy3, G)
             self._dgrad(pf + ".conv3", dy3, dz)
             cap("b_dz2", dz, px_o * b.width, (N, ho, wo, b.width))
             self._bn_bwd(P, G, pf + ".bn2", px_o, b.width, dz, 2, None, a["y2"], dyw, None)
             cap("b_dy2", dyw, px_o * b.width, (N, ho, wo, b.width))
             # conv2
             s1 = self.bn_state[pf + ".bn1"]
-            self._wgrad(pf + ".conv2", a["y1"], s1, dyw, G)
+            if self.materialize:
+                self._wgrad(pf + ".conv2", a["a1"], None, dyw, G)
+            else:
+                self._wgrad(pf + ".conv2", a["y1"], s1, dyw, G)
             self._dgrad(pf + ".conv2", dyw, dz)
             cap("b_dz1", dz, px_i * b.width, (N, hi, wi, b.width))
             self._bn_bwd(P, G, pf + ".bn1", px_i, b.width, dz, 2, None, a["y1"], dyw, None)

@@ -94,8 +94,10 @@ int argus_conv_dgrad(const argus_conv_desc* d, int dtype, const void* dy, const 
  * disables (0) the LDS-halo kernel for 3x3 stride-1 forward/dgrad, key 11 the same for the 3x3
  * stride-1 weight gradient and key 12 its split target (workgroups, default 512), key 13 the fewest
  * workgroups for the fwd/dgrad halo kernel (default 256; 1 also allows its 64-channel variant),
- * key 14 the most (64 x 64) channel tiles for the wgrad halo kernel (default 4). Returns 0, or -1
- * for an unknown key. */
+ * key 14 the most (64 x 64) channel tiles for the wgrad halo kernel (default 4), key 15 the
+ * 128x128 register-staged wgrad variant (2 default, 1 / 3 with the prefetch ring), key 16 enables
+ * (1, default) or disables the bf16 glds wgrad kernel, key 17 its split target (default 512).
+ * Returns 0, or -1 for an unknown key. */
 int argus_conv_tuning(int key, int value);
 /* Which tile a pass launches and its algorithmic work: pass 0 fwd, 1 dgrad, 2 wgrad. Returns a
  * tag (kind*10^7 + dtype*10^6 + tile_m*1000 + tile_n; kind 1 igemm, 2 wgrad) and writes
