@@ -729,6 +729,14 @@ def test_wgrad_glds_kernel_parity(cuda):
 
     torch.manual_seed(29)
     L = lib()
+    assert L.dll.argus_conv_tuning(11, 0) == 0  # the 3x3 halo wgrad would take the 128-channel 3x3 case
+    try:
+        _wgrad_glds_cases(cuda, L, KernelTimer)
+    finally:
+        L.dll.argus_conv_tuning(11, 1)
+
+
+def _wgrad_glds_cases(cuda, L, KernelTimer):
     for cin, cout, k, s, hw, n in [(128, 128, 3, 1, 16, 2), (256, 512, 1, 1, 16, 4), (256, 256, 3, 2, 16, 2),
                                    (512, 256, 1, 1, 8, 2), (128, 256, 3, 1, 32, 1), (256, 128, 1, 2, 16, 2)]:
         d, p = _desc(n, hw, hw, cin, cout, k, s)
