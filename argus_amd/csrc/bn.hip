@@ -2,10 +2,10 @@
 // ResNet-50 backbone (torchvision, argus/models.py:43,55), NHWC, fp32 statistics.
 //
 // Train-mode BN is a two-phase dependency: the conv epilogue (conv.hip) emits per-row-tile
-// {sum, sumsq} partials; bn_colreduce + bn_finalize turn them into mean / invstd and the fused
+// {sum, M2} partials; stats_finalize_kernel (one launch) turns them into mean / invstd and the fused
 // coefficients scale/shift that the *consumer* applies (next conv's staging prologue, or
 // bn_apply_kernel for block outputs). Backward: bn_bwd_reduce_kernel emits {sum dm, sum dm*xhat}
-// partials, bn_bwd_finalize gives dgamma/dbeta and dy = ca*dm + cb*y + cc coefficients,
+// partials, bwd_finalize_kernel gives dgamma/dbeta and dy = ca*dm + cb*y + cc coefficients,
 // bn_bwd_apply_kernel materialises dy. Every cross-workgroup reduction is a fixed-order two-level
 // reduction (deterministic, run-to-run bitwise reproducible).
 #include "common.h"
@@ -19,97 +19,111 @@ namespace argus {
 // S = sum_t sum_t, Q = sum_t (M2_t + sum_t^2 / n_t)  ->  mean = S/n, M2 = Q - S^2/n
 // (= sum_t M2_t + sum_t n_t (mean_t - mean)^2, the exact parallel-variance merge; the within-tile
 // M2_t carry the large part, so fp64 leaves no cancellation problem).
-__global__ __launch_bounds__(256) void stats_reduce_kernel(const float2* __restrict__ part, int rows, int C,
-                                                           int rows_per_group, int64_t count, int tile_rows,
-                                                           double2* __restrict__ out) {
+// Backward partials {sum dm, sum dm*xhat} are plain column sums.
+static int reduce_groups(int rows) { return rows < 64 ? 1 : (rows < 512 ? 8 : (rows < 4096 ? 32 : 64)); }
+
+// ---- one-launch statistics merge + finalize ---------------------------------------------------------
+// Grid (C/64, G): block (x, g) merges partial rows [g*rpg, (g+1)*rpg) of its 64 channels into
+// red[g][c] (fp64) exactly as the two-kernel form did, then takes a ticket on cnt[x]; the block that
+// draws G-1 merges the G group results in a fixed order (deterministic) and finalizes its 64 channels.
+// Hand-off: plain slab stores, every wave drains, agent-scope release, relaxed agent ticket; the
+// reducer's agent-scope acquire precedes its plain loads (cdna_hip_programming.md §6 Guideline 16,
+// counter form; correct for any workgroup -> XCD placement). The reducer resets cnt[x], so the
+// counters stay zero between calls; they are zeroed once when the workspace is allocated.
+ARGUS_DEV bool ticket_last(unsigned* cnt, int G, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = t == (unsigned)(G - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
+// fixed-order sum over the G group results of this block's 64 channels: 4 row lanes, then lanes 0..3
+ARGUS_DEV double2 merge_groups(const double2* red, int G, int C, int c, double2 (*lds)[64]) {
+  const int lane_r = threadIdx.x >> 6, cl = threadIdx.x & 63;
+  double S = 0.0, Q = 0.0;
+  if (c < C)
+    for (int g = lane_r; g < G; g += 4) {
+      const double2 v = red[(size_t)g * C + c];
+      S += v.x;
+      Q += v.y;
+    }
+  lds[lane_r][cl] = make_double2(S, Q);
+  __syncthreads();
+  double2 a = lds[0][cl];
+  for (int i = 1; i < 4; ++i) { a.x += lds[i][cl].x; a.y += lds[i][cl].y; }
+  return a;
+}
+
+struct BnFinArgs {
+  const float2* part;
+  int rows, C, rpg, tile_rows, G;
+  int64_t count;
+  double2* red;
+  unsigned* cnt;
+  const float *gamma, *beta;
+  float eps, momentum;
+  float *running_mean, *running_var;
+  int64_t* nbt;
+  float *mean_o, *invstd_o, *scale_o, *shift_o;
+};
+
+__global__ __launch_bounds__(256) void stats_finalize_kernel(const BnFinArgs a) {
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int lane_r = threadIdx.x >> 6;
   const int g = blockIdx.y;
-  const int r0 = g * rows_per_group, r1 = min(rows, r0 + rows_per_group);
-  const double inv_full = 1.0 / (double)tile_rows;
+  const int r0 = g * a.rpg, r1 = min(a.rows, r0 + a.rpg);
+  const double inv_full = 1.0 / (double)a.tile_rows;
   double S = 0.0, Q = 0.0;
-  if (c < C)
+  if (c < a.C)
 #pragma unroll 8
     for (int r = r0 + lane_r; r < r1; r += 4) {
-      const float2 v = part[(size_t)r * C + c];
-      const int64_t left = count - (int64_t)r * tile_rows;
-      const double inv = left >= tile_rows ? inv_full : 1.0 / (double)left;
+      const float2 v = a.part[(size_t)r * a.C + c];
+      const int64_t left = a.count - (int64_t)r * a.tile_rows;
+      const double inv = left >= a.tile_rows ? inv_full : 1.0 / (double)left;
       S += (double)v.x;
       Q += (double)v.y + (double)v.x * (double)v.x * inv;
     }
   __shared__ double2 red[4][64];
+  __shared__ int flag;
   red[lane_r][threadIdx.x & 63] = make_double2(S, Q);
   __syncthreads();
-  if (lane_r == 0 && c < C) {
-    double2 a = red[0][threadIdx.x];
-    for (int i = 1; i < 4; ++i) { a.x += red[i][threadIdx.x].x; a.y += red[i][threadIdx.x].y; }
-    out[(size_t)g * C + c] = a;
+  if (lane_r == 0 && c < a.C) {
+    double2 t = red[0][threadIdx.x];
+    for (int i = 1; i < 4; ++i) { t.x += red[i][threadIdx.x].x; t.y += red[i][threadIdx.x].y; }
+    a.red[(size_t)g * a.C + c] = t;
   }
-}
-
-// ---- backward partial sums: plain two-level column reduction float2 -> double2 -------------------
-__global__ __launch_bounds__(256) void colreduce_kernel(const float2* __restrict__ part, int rows, int C,
-                                                        int rows_per_group, double2* __restrict__ out) {
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int lane_r = threadIdx.x >> 6;  // 4 row lanes
-  const int g = blockIdx.y;
-  const int r0 = g * rows_per_group, r1 = min(rows, r0 + rows_per_group);
-  double s = 0.0, q = 0.0;
-  if (c < C)
-#pragma unroll 8
-    for (int r = r0 + lane_r; r < r1; r += 4) {
-      const float2 v = part[(size_t)r * C + c];
-      s += v.x;
-      q += v.y;
-    }
-  __shared__ double2 red[4][64];
-  red[lane_r][threadIdx.x & 63] = make_double2(s, q);
+  if (!ticket_last(a.cnt + blockIdx.x, a.G, &flag)) return;
   __syncthreads();
-  if (lane_r == 0 && c < C) {
-    double2 a = red[0][threadIdx.x];
-    for (int i = 1; i < 4; ++i) { a.x += red[i][threadIdx.x].x; a.y += red[i][threadIdx.x].y; }
-    out[(size_t)g * C + c] = a;
-  }
-}
-
-static int reduce_groups(int rows) { return rows < 64 ? 1 : (rows < 512 ? 8 : (rows < 4096 ? 32 : 64)); }
-
-static int colreduce(const float* part, int rows, int C, void* ws, int& G, hipStream_t st) {
-  G = reduce_groups(rows);
-  const int rpg = (rows + G - 1) / G;
-  hipLaunchKernelGGL(colreduce_kernel, dim3((C + 63) / 64, G), dim3(256), 0, st,
-                     reinterpret_cast<const float2*>(part), rows, C, rpg, reinterpret_cast<double2*>(ws));
-  return check_launch("colreduce_kernel");
-}
-
-__global__ void bn_finalize_kernel(const double2* __restrict__ red, int G, int C, double count, const float* gamma,
-                                   const float* beta, float eps, float momentum, float* running_mean,
-                                   float* running_var, int64_t* nbt, float* mean_o, float* invstd_o,
-                                   float* scale_o, float* shift_o) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c == 0 && nbt) nbt[0] += 1;
-  if (c >= C) return;
-  double S = 0.0, Q = 0.0;
-#pragma unroll 8
-  for (int g = 0; g < G; ++g) {
-    const double2 v = red[(size_t)g * C + c];
-    S += v.x;
-    Q += v.y;
-  }
-  const double mean = S / count;
-  double m2 = Q - S * mean;
+  const double2 tot = merge_groups(a.red, a.G, a.C, c, red);
+  if (blockIdx.x == 0 && threadIdx.x == 0 && a.nbt) a.nbt[0] += 1;
+  if (lane_r != 0 || c >= a.C) return;
+  const double count = (double)a.count;
+  const double mean = tot.x / count;
+  double m2 = tot.y - tot.x * mean;
   if (m2 < 0.0) m2 = 0.0;
   const double var = m2 / count;
-  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
-  const float sc = gamma[c] * invstd;
-  if (mean_o) mean_o[c] = (float)mean;
-  if (invstd_o) invstd_o[c] = invstd;
-  if (scale_o) scale_o[c] = sc;
-  if (shift_o) shift_o[c] = beta[c] - (float)mean * sc;
-  if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
-  if (running_var) {
+  const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
+  const float sc = a.gamma[c] * invstd;
+  if (a.mean_o) a.mean_o[c] = (float)mean;
+  if (a.invstd_o) a.invstd_o[c] = invstd;
+  if (a.scale_o) a.scale_o[c] = sc;
+  if (a.shift_o) a.shift_o[c] = a.beta[c] - (float)mean * sc;
+  if (a.running_mean) a.running_mean[c] = (1.f - a.momentum) * a.running_mean[c] + a.momentum * (float)mean;
+  if (a.running_var) {
     const double unbiased = count > 1.0 ? m2 / (count - 1.0) : var;
-    running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unbiased;
+    a.running_var[c] = (1.f - a.momentum) * a.running_var[c] + a.momentum * (float)unbiased;
   }
 }
 
@@ -285,21 +299,51 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(int64_t pixels, int 
   }
 }
 
-__global__ void bn_bwd_finalize_kernel(const double2* __restrict__ red, int G, int C, double count,
-                                       const float* gamma, const float* mean, const float* invstd, float* dgamma,
-                                       float* dbeta, float* ca, float* cb, float* cc) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double S = 0.0, Tt = 0.0;
+struct BnBwdFinArgs {
+  const float2* part;
+  int rows, C, rpg, G;
+  double count;
+  double2* red;
+  unsigned* cnt;
+  const float *gamma, *mean, *invstd;
+  float *dgamma, *dbeta, *ca, *cb, *cc;
+};
+
+// backward column sums + dgamma/dbeta/coefficients in one launch (same ticket hand-off)
+__global__ __launch_bounds__(256) void bwd_finalize_kernel(const BnBwdFinArgs a) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int lane_r = threadIdx.x >> 6;
+  const int g = blockIdx.y;
+  const int r0 = g * a.rpg, r1 = min(a.rows, r0 + a.rpg);
+  double s = 0.0, q = 0.0;
+  if (c < a.C)
 #pragma unroll 8
-  for (int g = 0; g < G; ++g) { S += red[(size_t)g * C + c].x; Tt += red[(size_t)g * C + c].y; }
-  if (dgamma) dgamma[c] = (float)Tt;
-  if (dbeta) dbeta[c] = (float)S;
-  const double gi = (double)gamma[c] * invstd[c];
-  const double gi2 = gi * invstd[c];
-  ca[c] = (float)gi;
-  cb[c] = (float)(-gi2 * Tt / count);
-  cc[c] = (float)(-gi * S / count + gi2 * Tt / count * mean[c]);
+    for (int r = r0 + lane_r; r < r1; r += 4) {
+      const float2 v = a.part[(size_t)r * a.C + c];
+      s += v.x;
+      q += v.y;
+    }
+  __shared__ double2 red[4][64];
+  __shared__ int flag;
+  red[lane_r][threadIdx.x & 63] = make_double2(s, q);
+  __syncthreads();
+  if (lane_r == 0 && c < a.C) {
+    double2 t = red[0][threadIdx.x];
+    for (int i = 1; i < 4; ++i) { t.x += red[i][threadIdx.x].x; t.y += red[i][threadIdx.x].y; }
+    a.red[(size_t)g * a.C + c] = t;
+  }
+  if (!ticket_last(a.cnt + blockIdx.x, a.G, &flag)) return;
+  __syncthreads();
+  const double2 tot = merge_groups(a.red, a.G, a.C, c, red);
+  if (lane_r != 0 || c >= a.C) return;
+  const double S = tot.x, Tt = tot.y;
+  if (a.dgamma) a.dgamma[c] = (float)Tt;
+  if (a.dbeta) a.dbeta[c] = (float)S;
+  const double gi = (double)a.gamma[c] * a.invstd[c];
+  const double gi2 = gi * a.invstd[c];
+  a.ca[c] = (float)gi;
+  a.cb[c] = (float)(-gi2 * Tt / a.count);
+  a.cc[c] = (float)(-gi * S / a.count + gi2 * Tt / a.count * a.mean[c]);
 }
 
 template <typename T, bool DUAL>
@@ -484,7 +528,10 @@ using namespace argus;
 
 extern "C" {
 
-size_t argus_bn_workspace_bytes(int channels) { return (size_t)64 * channels * sizeof(double2); }
+// [0, kBnCounterBytes): one ticket counter per 64-channel block (zero at allocation, kept zero by the
+// kernels); then the fp64 group results double2[64][channels].
+static constexpr size_t kBnCounterBytes = 1024;
+size_t argus_bn_workspace_bytes(int channels) { return kBnCounterBytes + (size_t)64 * channels * sizeof(double2); }
 
 int argus_bn_finalize(int C, int rows, int tile_rows, const float* part, int64_t count, const float* gamma,
                       const float* beta, float eps, float momentum, float* rm, float* rv, int64_t* nbt, float* mean,
@@ -494,16 +541,21 @@ int argus_bn_finalize(int C, int rows, int tile_rows, const float* part, int64_t
     set_error("bn_finalize: bad arguments");
     return ARGUS_ERR_ARG;
   }
+  if ((C + 63) / 64 > (int)(kBnCounterBytes / 4)) {
+    set_error("bn_finalize: too many channels for the workspace counters");
+    return ARGUS_ERR_ARG;
+  }
   hipStream_t st = (hipStream_t)stream;
-  const int G = reduce_groups(rows);
-  const int rpg = (rows + G - 1) / G;
-  hipLaunchKernelGGL(stats_reduce_kernel, dim3((C + 63) / 64, G), dim3(256), 0, st,
-                     reinterpret_cast<const float2*>(part), rows, C, rpg, count, tile_rows, reinterpret_cast<double2*>(ws));
-  if (int e = check_launch("stats_reduce_kernel")) return e;
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st,
-                     reinterpret_cast<const double2*>(ws), G, C, (double)count, gamma, beta, eps, momentum, rm, rv,
-                     nbt, mean, invstd, scale, shift);
-  return check_launch("bn_finalize_kernel");
+  BnFinArgs a;
+  a.G = reduce_groups(rows);
+  a.part = reinterpret_cast<const float2*>(part); a.rows = rows; a.C = C; a.rpg = (rows + a.G - 1) / a.G;
+  a.tile_rows = tile_rows; a.count = count;
+  a.cnt = reinterpret_cast<unsigned*>(ws);
+  a.red = reinterpret_cast<double2*>(reinterpret_cast<char*>(ws) + kBnCounterBytes);
+  a.gamma = gamma; a.beta = beta; a.eps = eps; a.momentum = momentum; a.running_mean = rm; a.running_var = rv;
+  a.nbt = nbt; a.mean_o = mean; a.invstd_o = invstd; a.scale_o = scale; a.shift_o = shift;
+  hipLaunchKernelGGL(stats_finalize_kernel, dim3((C + 63) / 64, a.G), dim3(256), 0, st, a);
+  return check_launch("stats_finalize_kernel");
 }
 
 int argus_bn_eval_coeffs(int C, const float* gamma, const float* beta, const float* rm, const float* rv, float eps,
@@ -584,13 +636,21 @@ int argus_bn_bwd_reduce(int dtype, int64_t pixels, int C, const void* dz, int mo
 int argus_bn_bwd_finalize(int C, int rows, const float* part, int64_t count, const float* gamma, const float* mean,
                           const float* invstd, float* dgamma, float* dbeta, float* ca, float* cb, float* cc, void* ws,
                           argus_stream_t stream) {
+  if (C <= 0 || rows <= 0 || count <= 0 || !part || !gamma || !mean || !invstd || !ca || !cb || !cc || !ws ||
+      (C + 63) / 64 > (int)(kBnCounterBytes / 4)) {
+    set_error("bn_bwd_finalize: bad arguments");
+    return ARGUS_ERR_ARG;
+  }
   hipStream_t st = (hipStream_t)stream;
-  int G;
-  if (int e = colreduce(part, rows, C, ws, G, st)) return e;
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st,
-                     reinterpret_cast<const double2*>(ws), G, C, (double)count, gamma, mean, invstd, dgamma, dbeta,
-                     ca, cb, cc);
-  return check_launch("bn_bwd_finalize_kernel");
+  BnBwdFinArgs a;
+  a.G = reduce_groups(rows);
+  a.part = reinterpret_cast<const float2*>(part); a.rows = rows; a.C = C; a.rpg = (rows + a.G - 1) / a.G;
+  a.count = (double)count;
+  a.cnt = reinterpret_cast<unsigned*>(ws);
+  a.red = reinterpret_cast<double2*>(reinterpret_cast<char*>(ws) + kBnCounterBytes);
+  a.gamma = gamma; a.mean = mean; a.invstd = invstd; a.dgamma = dgamma; a.dbeta = dbeta; a.ca = ca; a.cb = cb; a.cc = cc;
+  hipLaunchKernelGGL(bwd_finalize_kernel, dim3((C + 63) / 64, a.G), dim3(256), 0, st, a);
+  return check_launch("bwd_finalize_kernel");
 }
 
 int argus_bn_bwd_apply(int dtype, int64_t pixels, int C, const void* dz, int mode, const void* mask, const void* y,

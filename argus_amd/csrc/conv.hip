@@ -1077,9 +1077,11 @@ int conv_wgrad(const argus_conv_desc& d, int dtype, const void* x, const float* 
   if (int e = check_desc(d)) return e;
   g_launch_work = 2.0 * d.n * d.ho * d.wo * d.k * d.r * d.s * d.c;  // algorithmic flops / bytes (ktimer)
   const WgPlan pl = wgrad_plan(d, dtype);
+  // algorithmic bytes: x + dy read once, the fp32 dW written once (the split partials and their
+  // reduction are this implementation's overhead, visible in the PMC traffic, not algorithmic work)
   g_launch_bytes = (double)(dtype == ARGUS_BF16 ? 2 : 4) *
                        ((double)d.n * d.h * d.w * (d.stem ? 4 : d.c) + (double)d.n * d.ho * d.wo * d.k) +
-                   4.0 * pl.splits * d.k * pl.N;
+                   4.0 * d.k * d.r * d.s * d.c;
   if (ws_bytes < (size_t)pl.splits * d.k * pl.N * sizeof(float)) {
     set_error("conv_wgrad: workspace too small");
     return ARGUS_ERR_ARG;

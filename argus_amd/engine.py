@@ -174,7 +174,7 @@ class ResNetEngine:
 
         max_stat = max(cv.stat_rows * cv.desc.k for cv in convs.values())
         self.stat_part = self._f(max_stat * 2)
-        self.bn_ws = torch.empty(L.dll.argus_bn_workspace_bytes(2048), dtype=torch.uint8, device=self.device)
+        self.bn_ws = torch.zeros(L.dll.argus_bn_workspace_bytes(2048), dtype=torch.uint8, device=self.device)
         max_bwd = 0
         for b, a in zip(self.blocks, act):
             for hw, c in ((a["hw_in"], b.width), (a["hw"], b.width), (a["hw"], b.cout)):

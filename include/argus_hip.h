@@ -125,6 +125,9 @@ int argus_ktimer_get(int index, char* name, int name_len, int64_t* launches, dou
                      double* work, double* bytes);
 
 /* ---- BatchNorm2d (train: batch stats, eps, momentum; eval: running stats) --------------------- */
+/* Workspace of argus_bn_finalize / argus_bn_bwd_finalize for up to `channels` channels. Its first
+ * 1 KiB holds inter-workgroup ticket counters: zero-fill the workspace ONCE when it is allocated;
+ * the kernels leave the counters zero (do not share one workspace between concurrent streams). */
 size_t argus_bn_workspace_bytes(int channels);
 /* From tile partials float2[rows][C] = {sum, M2 (sum of squared deviations from the tile mean)},
  * tile t holding min(tile_rows, count - t*tile_rows) elements per channel (as argus_conv_fwd

@@ -195,7 +195,7 @@ def test_bn_train_forward_backward(cuda, dt):
     rm, rv = torch.zeros(c, device=cuda), torch.ones(c, device=cuda)
     nbt = torch.zeros((), dtype=torch.int64, device=cuda)
     stt = torch.empty(4, c, device=cuda)
-    ws = torch.empty(L.dll.argus_bn_workspace_bytes(c), dtype=torch.uint8, device=cuda)
+    ws = torch.zeros(L.dll.argus_bn_workspace_bytes(c), dtype=torch.uint8, device=cuda)
     gd, bd = gamma.to(cuda), beta.to(cuda)
     partg = part.to(cuda)
     L.bn_finalize(c, rows, 5, ptr(partg), px, ptr(gd), ptr(bd), C.c_float(1e-5), C.c_float(0.1), ptr(rm), ptr(rv),
@@ -275,7 +275,7 @@ def test_bn_dual_branch_backward(cuda, dt):
     E = 8 if dt == "bf16" else 4
     ya, yb = _q(torch.randn(n, h, w, c) * 1.5 + 0.3, dt), _q(torch.randn(n, h, w, c) - 0.2, dt)
     gA, bA, gB, bB = torch.rand(c) + 0.5, torch.randn(c), torch.rand(c) + 0.5, torch.randn(c)
-    ws = torch.empty(L.dll.argus_bn_workspace_bytes(c), dtype=torch.uint8, device=cuda)
+    ws = torch.zeros(L.dll.argus_bn_workspace_bytes(c), dtype=torch.uint8, device=cuda)
 
     def finalize(yq, g, b):
         yy = yq.reshape(px, c).reshape(-1, 5, c)

@@ -108,3 +108,30 @@ def test_get_pose(cuda):
             want = se3.se3_exp(m(x).cpu().double())  # pp.se3(xi).Exp(), utils.py:179-189
         assert pose.shape == (b, 7)
         assert torch.allclose(pose.cpu().double(), want, atol=1e-5)
+
+
+def test_forward_latency_graph_replay(cuda):
+    """scripts/timing.py counterpart: the captured hipGraph of the native forward replays to the same
+    prediction as eager launches (train-mode BN, no_grad), and the benchmark reports finite times."""
+    from argus_amd.models import NCameraCNN
+    from argus_amd.timing import forward_latency
+
+    torch.manual_seed(3)
+    m = NCameraCNN().to(cuda)
+    x = torch.rand(2, 6, 64, 64, device=cuda)
+    with torch.no_grad():
+        eager = m(x).clone()
+    static_x = x.clone()
+    with torch.no_grad():
+        m(static_x)  # warm-up outside capture
+    g = torch.cuda.CUDAGraph()
+    with torch.no_grad(), torch.cuda.graph(g):
+        out = m(static_x)
+    static_x.copy_(torch.rand_like(x))
+    g.replay()
+    static_x.copy_(x)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, eager)
+    r = forward_latency(trials=3, hw=(64, 64))
+    assert r["mean_s"] > 0 and math.isfinite(r["mean_s"])

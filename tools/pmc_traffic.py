@@ -21,6 +21,8 @@ def demangle(name: str) -> str:
     """rocprof kernel name -> "argus::igemm_kernel<__bf16, 128, 128, false, false>" (no return type or
     argument list). Our template kernels are demangled here (binutils' c++filt predates DF16b);
     names rocprof already prints demangled are cut at their argument list."""
+    if name.startswith("void "):
+        name = name[5:]
     m = re.match(r"_ZN5argus(\d+)", name)
     if m:
         n = int(m.group(1))
