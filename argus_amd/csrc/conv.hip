@@ -375,9 +375,9 @@ __global__ __launch_bounds__(256, OCC == 1 ? 1 : 2) void wgrad_kernel(const WgPa
 
   const int mtiles = p.M / BM, ntiles = p.N / BN;
   const int nwg = mtiles * ntiles;
-  const int bid = xcd_remap(blockIdx.x, nwg);
+  int bid, split;
+  split_tile(nwg, (p.P + p.pps - 1) / p.pps, p.S == 1 && p.N == p.Cin, bid, split);
   const int mt = bid / ntiles, nt = bid - mt * ntiles;
-  const int split = blockIdx.y;
   const int pbeg = split * p.pps;
   const int pend = min(p.P, pbeg + p.pps);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1038,7 +1038,7 @@ static const char* wg_name() {
 
 template <typename T, int BM, int BN, bool STEM, bool PRO, bool FAST, int OCC = 2>
 static void launch_wg(const WgParams& p, const WgPlan& pl, hipStream_t st) {
-  dim3 grid(pl.mt * pl.nt, pl.splits);
+  dim3 grid(pl.mt * pl.nt * pl.splits);
   timed_launch(wg_name<T, BM, BN, STEM, PRO, FAST, OCC>(), wgrad_kernel<T, BM, BN, STEM, PRO, FAST, OCC>, grid,
                dim3(256), st, p);
 }

@@ -322,9 +322,10 @@ __global__ __launch_bounds__((BM / 64) * 2 * 64, 1) void wgrad_glds_kernel(const
 
   const int mtiles = p.M / BM, ntiles = p.N / 128;
   const int nwg = mtiles * ntiles;
-  const int bid = xcd_remap(blockIdx.x, nwg);
+  int bid, split;
+  split_tile(nwg, (p.P + p.pps - 1) / p.pps, p.S == 1 && p.N == p.Cin, bid, split);
   const int mt = bid / ntiles, nt = bid - mt * ntiles;
-  const int pbeg = blockIdx.y * p.pps;
+  const int pbeg = split * p.pps;
   const int pend = min(p.P, pbeg + p.pps);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -407,7 +408,7 @@ __global__ __launch_bounds__((BM / 64) * 2 * 64, 1) void wgrad_glds_kernel(const
     compute(kt % NSTAGE);
   }
 
-  float* out = p.part + (size_t)blockIdx.y * p.M * p.N;
+  float* out = p.part + (size_t)split * p.M * p.N;
 #pragma unroll
   for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
@@ -452,7 +453,7 @@ bool wgrad_glds_launch(const argus_conv_desc& d, const WgParams& base, int split
   WgParams p = base;
   p.pps = pps;
   const int bm = d.k % 256 == 0 ? 256 : 128;
-  dim3 grid((p.M / bm) * (p.N / 128), splits);
+  dim3 grid((p.M / bm) * (p.N / 128) * splits);
   if (bm == 256) timed_launch(wgg_name<256>(), wgrad_glds_kernel<256>, grid, dim3(512), st, p);
   else timed_launch(wgg_name<128>(), wgrad_glds_kernel<128>, grid, dim3(256), st, p);
   return true;

@@ -387,8 +387,9 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(const WgHaloParam
   __shared__ __attribute__((aligned(1024))) u32x4 lds[(2 * STG + 512) / 16];
 
   const int ctiles = p.C / 64;
-  const int kt = blockIdx.x / ctiles, ct = blockIdx.x - kt * ctiles;
-  const int split = blockIdx.y;
+  int tile, split;
+  split_tile((p.K / 64) * ctiles, (p.ptiles + p.tps - 1) / p.tps, false, tile, split);
+  const int kt = tile / ctiles, ct = tile - kt * ctiles;
   const int t0 = split * p.tps, t1 = min(p.ptiles, t0 + p.tps);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
@@ -579,7 +580,7 @@ bool wgrad3x3_halo_launch(const argus_conv_desc& d, int dtype, const void* x, co
   p.n = d.n; p.H = d.h; p.W = d.w; p.C = d.c; p.K = d.k;
   p.ptiles = d.n * d.h * d.w / 128;
   p.tps = tps;
-  dim3 grid((d.k / 64) * (d.c / 64), splits);
+  dim3 grid((d.k / 64) * (d.c / 64) * splits);
   if (sc) timed_launch(wg_halo_name<true>(), wgrad3x3_halo_kernel<true>, grid, dim3(512), st, p);
   else timed_launch(wg_halo_name<false>(), wgrad3x3_halo_kernel<false>, grid, dim3(512), st, p);
   *splits_out = splits;
