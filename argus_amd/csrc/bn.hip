@@ -26,16 +26,26 @@ static int reduce_groups(int rows) { return rows < 64 ? 1 : (rows < 512 ? 8 : (r
 // Grid (C/64, G): block (x, g) merges partial rows [g*rpg, (g+1)*rpg) of its 64 channels into
 // red[g][c] (fp64) exactly as the two-kernel form did, then takes a ticket on cnt[x]; the block that
 // draws G-1 merges the G group results in a fixed order (deterministic) and finalizes its 64 channels.
-// Hand-off: plain slab stores, every wave drains, agent-scope release, relaxed agent ticket; the
+// Hand-off: write-through (sc1) slab stores, every wave drains, relaxed agent-scope ticket; the
 // reducer's agent-scope acquire precedes its plain loads (cdna_hip_programming.md §6 Guideline 16,
-// counter form; correct for any workgroup -> XCD placement). The reducer resets cnt[x], so the
+// counter form with sc1 stores; correct for any workgroup -> XCD placement). The reducer resets cnt[x], so the
 // counters stay zero between calls; they are zeroed once when the workspace is allocated.
-ARGUS_DEV bool ticket_last(unsigned* cnt, int G, int* flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned gu32;
+
+// a group result, stored write-through (sc1: two 8-byte agent-scope atomic stores), so publishing it
+// needs no L2 write-back (release) fence — only the drain in ticket_last
+ARGUS_DEV void store_wt(double2* p, double2 v) {
+  gu64* q = (gu64*)p;
+  __hip_atomic_store(q, (unsigned long long)__double_as_longlong(v.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(q + 1, (unsigned long long)__double_as_longlong(v.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+ARGUS_DEV bool ticket_last(unsigned* cnt_, int G, int* flag) {
+  gu32* cnt = (gu32*)cnt_;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned t = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = t == (unsigned)(G - 1);
     if (last) {
@@ -102,7 +112,7 @@ __global__ __launch_bounds__(256) void stats_finalize_kernel(const BnFinArgs a) 
   if (lane_r == 0 && c < a.C) {
     double2 t = red[0][threadIdx.x];
     for (int i = 1; i < 4; ++i) { t.x += red[i][threadIdx.x].x; t.y += red[i][threadIdx.x].y; }
-    a.red[(size_t)g * a.C + c] = t;
+    store_wt(a.red + (size_t)g * a.C + c, t);
   }
   if (!ticket_last(a.cnt + blockIdx.x, a.G, &flag)) return;
   __syncthreads();
@@ -145,6 +155,9 @@ struct EwGeom {
   int CC, PL, cgroups, rows;
   int64_t ppb;
 };
+// geometry knobs (argus_conv_tuning keys 20-23; measured defaults)
+int g_bwd_min_px = 64, g_bwd_max_rows = 1024, g_ew_target = 512, g_ew_min_ppt = 16;
+
 static EwGeom ew_geom(int C, int E, int64_t pixels, int target_blocks) {
   EwGeom g;
   const int chunks = C / E;
@@ -152,7 +165,7 @@ static EwGeom ew_geom(int C, int E, int64_t pixels, int target_blocks) {
   g.PL = 256 / g.CC;
   g.cgroups = chunks / g.CC;
   int64_t rows = target_blocks / g.cgroups;
-  const int64_t maxrows = (pixels + 4 * g.PL - 1) / (4 * g.PL);  // >= 4 pixels per thread
+  const int64_t maxrows = (pixels + g_ew_min_ppt * g.PL - 1) / (g_ew_min_ppt * g.PL);  // min pixels per thread
   if (rows > maxrows) rows = maxrows;
   if (rows < 1) rows = 1;
   g.ppb = (pixels + rows - 1) / rows;
@@ -160,12 +173,17 @@ static EwGeom ew_geom(int C, int E, int64_t pixels, int target_blocks) {
   return g;
 }
 
+// Every elementwise kernel below walks its pixels U at a time: the U iterations' loads are issued
+// before any of their arithmetic or stores, so each thread keeps U x (tensors read) 16-byte loads in
+// flight (the memory-level parallelism an HBM stream needs at 4-8 waves per SIMD).
+constexpr int kEwU = 4;
+
 template <typename T>
 __global__ __launch_bounds__(256) void bn_apply_kernel(int64_t pixels, int C, int CC, int PL, int64_t ppb,
                                                        const T* __restrict__ y, const float* __restrict__ sc,
                                                        const float* __restrict__ sh, const T* __restrict__ res,
                                                        const float* __restrict__ rsc, const float* __restrict__ rsh,
-                                                       int relu, T* out, uint8_t* __restrict__ mask_out) {
+                                                       int relu, T* __restrict__ out, uint8_t* __restrict__ mask_out) {
   constexpr int E = Chunk<T>::E;
   const int cc = threadIdx.x % CC, pl = threadIdx.x / CC;
   const int c0 = (blockIdx.x * CC + cc) * E;
@@ -178,30 +196,42 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(int64_t pixels, int C, in
     ra[j] = rsc ? rsc[c0 + j] : 1.f;
     rb[j] = rsc ? rsh[c0 + j] : 0.f;
   }
-#pragma unroll 4
-  for (int64_t px = p0 + pl; px < p1; px += PL) {
-    const int64_t off = px * C + c0;
-    float f[E], r[E];
-    unpack(ld16(y + off), f);
-    if (res) unpack(ld16(res + off), r);
+  for (int64_t px0 = p0 + pl; px0 < p1; px0 += kEwU * PL) {
+    u32x4 yv[kEwU], rv[kEwU];
 #pragma unroll
-    for (int j = 0; j < E; ++j) {
-      float v = fmaf(f[j], a[j], b[j]);
-      if (res) v += fmaf(r[j], ra[j], rb[j]);
-      if (relu) v = fmaxf(v, 0.f);
-      f[j] = v;
+    for (int u = 0; u < kEwU; ++u) {
+      const int64_t px = px0 + u * PL;
+      const int64_t off = (px < p1 ? px : px0) * C + c0;
+      yv[u] = ld16(y + off);
+      if (res) rv[u] = ld16(res + off);
     }
-    const u32x4 o = pack(f);
-    st16(out + off, o);
-    if (mask_out) mask_out[off / E] = chunk_positive_bits<T>(o);
+#pragma unroll
+    for (int u = 0; u < kEwU; ++u) {
+      const int64_t px = px0 + u * PL;
+      if (px >= p1) break;
+      const int64_t off = px * C + c0;
+      float f[E], r[E];
+      unpack(yv[u], f);
+      if (res) unpack(rv[u], r);
+#pragma unroll
+      for (int j = 0; j < E; ++j) {
+        float v = fmaf(f[j], a[j], b[j]);
+        if (res) v += fmaf(r[j], ra[j], rb[j]);
+        if (relu) v = fmaxf(v, 0.f);
+        f[j] = v;
+      }
+      const u32x4 o = pack(f);
+      st16(out + off, o);
+      if (mask_out) mask_out[off / E] = chunk_positive_bits<T>(o);
+    }
   }
 }
 
 // ---- backward reduce ----------------------------------------------------------------------------
 // Grid: x = channel groups of CC chunks, y = pixel blocks. Block: CC chunk-columns x PL pixel lanes.
 static int bwd_rows(int64_t pixels) {
-  int64_t r = (pixels + 63) / 64;  // >= 64 pixels per block
-  return (int)(r > 1024 ? 1024 : (r < 1 ? 1 : r));
+  int64_t r = (pixels + g_bwd_min_px - 1) / g_bwd_min_px;  // >= g_bwd_min_px pixels per block
+  return (int)(r > g_bwd_max_rows ? g_bwd_max_rows : (r < 1 ? 1 : r));
 }
 static void bwd_geometry(int C, int E, int64_t pixels, int& CC, int& PL, int& cgroups, int& rows, int64_t& ppb) {
   const int chunks = C / E;
@@ -216,7 +246,7 @@ static void bwd_geometry(int C, int E, int64_t pixels, int& CC, int& PL, int& cg
 // Mask of the upstream ReLU for one 16-byte chunk (mode 0 none, 1 src>0, 2 y*S+H>0, 3 mask bits).
 template <typename T>
 ARGUS_DEV void apply_mask(int mode, float (&d)[Chunk<T>::E], const float (&yv)[Chunk<T>::E], const T* __restrict__ msrc,
-                          const uint8_t* __restrict__ mbits, int64_t off, const float* S, const float* H) {
+                          unsigned bits, int64_t off, const float* S, const float* H) {
   constexpr int E = Chunk<T>::E;
   if (mode == 1) {
     float m[E];
@@ -226,10 +256,9 @@ ARGUS_DEV void apply_mask(int mode, float (&d)[Chunk<T>::E], const float (&yv)[C
   } else if (mode == 2) {
 #pragma unroll
     for (int j = 0; j < E; ++j) d[j] = fmaf(yv[j], S[j], H[j]) > 0.f ? d[j] : 0.f;
-  } else if (mode == 3) {
-    const unsigned b = mbits[off / E];
+  } else if (mode == 3) {  // bits: the chunk's mask byte, loaded with the chunk
 #pragma unroll
-    for (int j = 0; j < E; ++j) d[j] = (b >> j) & 1u ? d[j] : 0.f;
+    for (int j = 0; j < E; ++j) d[j] = (bits >> j) & 1u ? d[j] : 0.f;
   }
 }
 
@@ -263,22 +292,38 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(int64_t pixels, int 
     is2[j] = DUAL ? invstd2[c0 + j] : 0.f;
     t2[j] = 0.f;
   }
-  for (int64_t px = p0 + pl; px < p1; px += PL) {
-    const int64_t off = px * C + c0;
-    float d[E], yv[E];
-    unpack(ld16(dz + off), d);
-    unpack(ld16(y + off), yv);
-    apply_mask<T>(mode, d, yv, mask_src, mbits, off, S, H);
+  for (int64_t px0 = p0 + pl; px0 < p1; px0 += kEwU * PL) {
+    u32x4 dv[kEwU], yr[kEwU], y2r[kEwU];
+    unsigned mb[kEwU];
 #pragma unroll
-    for (int j = 0; j < E; ++j) {
-      s[j] += d[j];
-      t[j] = fmaf(d[j], (yv[j] - mu[j]) * is[j], t[j]);
+    for (int u = 0; u < kEwU; ++u) {
+      const int64_t px = px0 + u * PL;
+      const int64_t off = (px < p1 ? px : px0) * C + c0;
+      dv[u] = ld16(dz + off);
+      yr[u] = ld16(y + off);
+      if constexpr (DUAL) y2r[u] = ld16(y2 + off);
+      mb[u] = mode == 3 ? mbits[off / E] : 0u;
     }
-    if constexpr (DUAL) {
-      float y2v[E];
-      unpack(ld16(y2 + off), y2v);
 #pragma unroll
-      for (int j = 0; j < E; ++j) t2[j] = fmaf(d[j], (y2v[j] - mu2[j]) * is2[j], t2[j]);
+    for (int u = 0; u < kEwU; ++u) {
+      const int64_t px = px0 + u * PL;
+      if (px >= p1) break;
+      const int64_t off = px * C + c0;
+      float d[E], yv[E];
+      unpack(dv[u], d);
+      unpack(yr[u], yv);
+      apply_mask<T>(mode, d, yv, mask_src, mb[u], off, S, H);
+#pragma unroll
+      for (int j = 0; j < E; ++j) {
+        s[j] += d[j];
+        t[j] = fmaf(d[j], (yv[j] - mu[j]) * is[j], t[j]);
+      }
+      if constexpr (DUAL) {
+        float y2v[E];
+        unpack(y2r[u], y2v);
+#pragma unroll
+        for (int j = 0; j < E; ++j) t2[j] = fmaf(d[j], (y2v[j] - mu2[j]) * is2[j], t2[j]);
+      }
     }
   }
   __shared__ float2 red[256 * 8];
@@ -330,7 +375,7 @@ __global__ __launch_bounds__(256) void bwd_finalize_kernel(const BnBwdFinArgs a)
   if (lane_r == 0 && c < a.C) {
     double2 t = red[0][threadIdx.x];
     for (int i = 1; i < 4; ++i) { t.x += red[i][threadIdx.x].x; t.y += red[i][threadIdx.x].y; }
-    a.red[(size_t)g * a.C + c] = t;
+    store_wt(a.red + (size_t)g * a.C + c, t);
   }
   if (!ticket_last(a.cnt + blockIdx.x, a.G, &flag)) return;
   __syncthreads();
@@ -373,24 +418,40 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(int64_t pixels, int C
     B2[j] = DUAL ? cb2[c0 + j] : 0.f;
     C2[j] = DUAL ? cc2[c0 + j] : 0.f;
   }
-  for (int64_t px = p0 + pl; px < p1; px += PL) {
-    const int64_t off = px * C + c0;
-    float d[E], yv[E];
-    unpack(ld16(dz + off), d);
-    unpack(ld16(y + off), yv);
-    apply_mask<T>(mode, d, yv, mask_src, mbits, off, S, H);
-    float o[E];
+  for (int64_t px0 = p0 + pl; px0 < p1; px0 += kEwU * PL) {
+    u32x4 dv[kEwU], yr[kEwU], y2r[kEwU];
+    unsigned mb[kEwU];
 #pragma unroll
-    for (int j = 0; j < E; ++j) o[j] = fmaf(A[j], d[j], fmaf(Bc[j], yv[j], Cc[j]));
-    st16(dy + off, pack(o));
-    if constexpr (DUAL) {
-      float y2v[E];
-      unpack(ld16(y2 + off), y2v);
-#pragma unroll
-      for (int j = 0; j < E; ++j) o[j] = fmaf(A2[j], d[j], fmaf(B2[j], y2v[j], C2[j]));
-      st16(dy2 + off, pack(o));
+    for (int u = 0; u < kEwU; ++u) {
+      const int64_t px = px0 + u * PL;
+      const int64_t off = (px < p1 ? px : px0) * C + c0;
+      dv[u] = ld16(dz + off);
+      yr[u] = ld16(y + off);
+      if constexpr (DUAL) y2r[u] = ld16(y2 + off);
+      mb[u] = mode == 3 ? mbits[off / E] : 0u;
     }
-    if (dm_out) st16(dm_out + off, pack(d));
+#pragma unroll
+    for (int u = 0; u < kEwU; ++u) {
+      const int64_t px = px0 + u * PL;
+      if (px >= p1) break;
+      const int64_t off = px * C + c0;
+      float d[E], yv[E];
+      unpack(dv[u], d);
+      unpack(yr[u], yv);
+      apply_mask<T>(mode, d, yv, mask_src, mb[u], off, S, H);
+      float o[E];
+#pragma unroll
+      for (int j = 0; j < E; ++j) o[j] = fmaf(A[j], d[j], fmaf(Bc[j], yv[j], Cc[j]));
+      st16(dy + off, pack(o));
+      if constexpr (DUAL) {
+        float y2v[E];
+        unpack(y2r[u], y2v);
+#pragma unroll
+        for (int j = 0; j < E; ++j) o[j] = fmaf(A2[j], d[j], fmaf(B2[j], y2v[j], C2[j]));
+        st16(dy2 + off, pack(o));
+      }
+      if (dm_out) st16(dm_out + off, pack(d));
+    }
   }
 }
 
@@ -574,7 +635,7 @@ int argus_bn_apply(int dtype, int64_t pixels, int C, const void* y, const float*
     set_error("bn_apply: bad arguments");
     return ARGUS_ERR_ARG;
   }
-  const EwGeom g = ew_geom(C, E, pixels, 2048);
+  const EwGeom g = ew_geom(C, E, pixels, g_ew_target);
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(g.cgroups, g.rows);
   const double pc = (double)pixels * C;
@@ -665,7 +726,7 @@ int argus_bn_bwd_apply(int dtype, int64_t pixels, int C, const void* dz, int mod
     set_error("bn_bwd_apply: bad arguments");
     return ARGUS_ERR_ARG;
   }
-  const EwGeom g = ew_geom(C, E, pixels, 2048);
+  const EwGeom g = ew_geom(C, E, pixels, g_ew_target);
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(g.cgroups, g.rows);
   const uint8_t* mb = mode == 3 ? (const uint8_t*)mask : nullptr;

@@ -827,6 +827,7 @@ static void dispatch_ig(const IgParams& p, int maxM, int bm, int bn, hipStream_t
 }
 
 extern int g_glds_min_k, g_glds_min_grid, g_wg_glds_enable, g_wg_glds_target;  // conv_glds.hip
+extern int g_bwd_min_px, g_bwd_max_rows, g_ew_target, g_ew_min_ppt;  // bn.hip
 static int g_wg_occ128 = 2;  // argus_conv_tuning key 15: workgroups/CU of the 128x128 wgrad tile (1 = with ring)
 extern int g_halo_enable, g_wg_halo_enable, g_wg_halo_target_blocks, g_halo_min_grid,
     g_wg_halo_max_tiles;  // conv_halo.hip
@@ -877,6 +878,10 @@ int conv_tuning(int key, int value) {
   if (key == 15) { g_wg_occ128 = value; return 0; }
   if (key == 16) { g_wg_glds_enable = value; return 0; }
   if (key == 17) { g_wg_glds_target = value; return 0; }
+  if (key == 20) { g_bwd_min_px = value; return 0; }   // bn.hip: BN-backward pixels per block (min)
+  if (key == 21) { g_bwd_max_rows = value; return 0; } //   ... and blocks per channel group (max)
+  if (key == 22) { g_ew_target = value; return 0; }    //   bn_apply / bwd_apply target blocks
+  if (key == 23) { g_ew_min_ppt = value; return 0; }   //   ... min pixels per thread
   return -1;
 }
 

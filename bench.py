@@ -29,6 +29,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import sys
 import math
 import os
 import time
@@ -50,6 +51,17 @@ def synthetic_batch(B, H, W, seed, device):
     xi = torch.randn(B, 6, generator=g, device=device) * 0.5
     targets = se3_exp(xi, canonical_w=True)
     return images, targets
+
+
+def _config_name(B: int, H: int, W: int, world: int) -> str:
+    """Which BASELINE.json config this run's shape is (configs[1] is the default bench line)."""
+    if (H, W) == (376, 672):
+        return "configs[3] cube_unity_data_large-shaped (2-cam 376x672)"
+    if (H, W) == (256, 256) and B == 256:
+        return "configs[2] cube_unity_data_medium-shaped"
+    if (H, W) == (256, 256) and B == 64:
+        return "configs[1] cube_unity_data_small-shaped"
+    return f"custom ({H}x{W}, batch {B} per rank)"
 
 
 def pmc_traffic(kernel: str, B: int, H: int, W: int, dtype: str):
@@ -109,6 +121,7 @@ def main() -> None:
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--kernels", action="store_true", help="print the probe step's per-kernel table to stderr")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -140,6 +153,11 @@ def main() -> None:
     summ = probe.summary()
     probe.stop()
     dom = max(summ, key=lambda k: summ[k]["total_ms"])
+    if args.kernels and rank == 0:
+        for k, v in sorted(summ.items(), key=lambda kv: -kv[1]["total_ms"]):
+            us = v["avg_us"]
+            print(f"{v['total_ms']:7.3f} ms {v['launches']:4d}x {us:8.1f} us {v['tflops']:7.1f} TF "
+                  f"{v['bytes_per_launch'] / us / 1e3:7.0f} GB/s  {k}", file=sys.stderr)
     timer = KernelTimer(dom)  # exact-name prefix: only this instantiation is timed
 
     torch.cuda.synchronize()
@@ -182,7 +200,7 @@ def main() -> None:
     eng = model._engine(dev)
     step_flops = sum((2 if n == "resnet.conv1" else 3) * c.flops for n, c in eng.convs.items())
     out = {
-        "metric": "train images/sec + val SE(3) geodesic err, 2x256x256 RGB",
+        "metric": f"train images/sec + val SE(3) geodesic err, 2x{H}x{W} RGB",
         "value": round(images_per_s, 2),
         "unit": "images/s",
         "n_gpus": world,
@@ -195,7 +213,7 @@ def main() -> None:
         "dtype": args.dtype,
         "data": "synthetic (uint8-uniform images, Exp(N(0,0.5^2)) SE(3) targets, seeded random-init weights)",
         "config": {
-            "workload": f"configs[1] cube_unity_data_small-shaped: fused train step, {B} samples "
+            "workload": f"{_config_name(B, H, W, world)}: fused train step, {B} samples "
                         f"({2 * B} images) of {H}x{W} per rank, 2 cams, ResNet-50 + MLP head, {args.dtype}",
             "batch_per_rank": B, "global_batch": B * world, "image_hw": [H, W], "parallelism": f"dp{world}",
         },

@@ -58,7 +58,9 @@ def main():
         for ps, fn in fns.items():
             with KernelTimer() as kt:
                 fn()
-            main_k = max(kt.summary().values(), key=lambda v: v["total_ms"])
+            ksum = kt.summary()
+            kname = max(ksum, key=lambda n: ksum[n]["total_ms"])
+            main_k = ksum[kname]
             roof_us = max(main_k["flops_per_launch"] / 2.5e15, main_k["bytes_per_launch"] / 8e12) * 1e6
             torch.cuda.synchronize()
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -69,7 +71,8 @@ def main():
             torch.cuda.synchronize()
             us = s.elapsed_time(e) * 1e3 / a.reps
             tot[ps] += us
-            row.append(f"p{ps}:{us:7.1f}us {cv.flops / us / 1e6:6.1f}TF {roof_us / us:4.0%}")
+            short = kname.replace("argus::", "").replace("_kernel", "").replace("__bf16, ", "").replace("false", "f").replace("true", "t")
+            row.append(f"p{ps}:{us:7.1f}us {cv.flops / us / 1e6:6.1f}TF {roof_us / us:4.0%} {short:24s}")
         totf += cv.flops * (2 if d.stem else 3)
         print(f"{name:32s} {d.h:3d}x{d.w:<3d} {d.c:4d}->{d.k:4d} k{d.r} s{d.stride}  " + "  ".join(row[1:]))
     allus = sum(tot.values())
