@@ -46,6 +46,7 @@ SIGNATURES = {
     "argus_conv_fwd_stat_rows": (_I, [_DESC, _I]),
     "argus_conv_fwd_stat_tile": (_I, [_DESC, _I]),
     "argus_conv_tuning": (_I, [_I, _I]),
+    "argus_conv_tuning_get": (_I, [_I]),
     "argus_conv_launch_info": (_I, [_DESC, _I, _I, C.POINTER(C.c_int64)]),
     "argus_conv_dgrad": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P]),
     "argus_conv_wgrad_workspace_bytes": (_SZ, [_DESC, _I]),

@@ -66,6 +66,7 @@ int argus_conv_fwd(const argus_conv_desc* d, int dtype, const void* x, const voi
 int argus_conv_fwd_stat_rows(const argus_conv_desc* d, int dtype) { return d ? conv_fwd_stat_rows(*d, dtype) : 0; }
 
 int argus_conv_tuning(int key, int value) { return conv_tuning(key, value); }
+int argus_conv_tuning_get(int key) { return conv_tuning_get(key); }
 
 int argus_conv_launch_info(const argus_conv_desc* d, int dtype, int pass, int64_t* flops) {
   return d ? conv_launch_info(*d, dtype, pass, flops) : -1;

@@ -863,26 +863,40 @@ static int run_ig(const IgParams& p, hipStream_t st, int bm, int bn) {
 static int g_force_bm[3] = {0, 0, 0}, g_force_bn[3] = {0, 0, 0};
 static int g_wgrad_target_blocks = 512;
 
+static int* tuning_slot(int key) {
+  if (key >= 0 && key < 3) return &g_force_bm[key];
+  if (key >= 3 && key < 6) return &g_force_bn[key - 3];
+  switch (key) {
+    case 6: return &g_wgrad_target_blocks;
+    case 7: return &g_smallk_max;
+    case 8: return &g_glds_min_k;
+    case 9: return &g_glds_min_grid;
+    case 10: return &g_halo_enable;
+    case 11: return &g_wg_halo_enable;
+    case 12: return &g_wg_halo_target_blocks;
+    case 13: return &g_halo_min_grid;
+    case 14: return &g_wg_halo_max_tiles;
+    case 15: return &g_wg_occ128;
+    case 16: return &g_wg_glds_enable;
+    case 17: return &g_wg_glds_target;
+    case 20: return &g_bwd_min_px;    // bn.hip: BN-backward pixels per block (min)
+    case 21: return &g_bwd_max_rows;  //   ... and blocks per channel group (max)
+    case 22: return &g_ew_target;     //   bn_apply / bwd_apply target blocks
+    case 23: return &g_ew_min_ppt;    //   ... min pixels per thread
+    default: return nullptr;
+  }
+}
+
 int conv_tuning(int key, int value) {
-  if (key >= 0 && key < 3) { g_force_bm[key] = value; return 0; }
-  if (key >= 3 && key < 6) { g_force_bn[key - 3] = value; return 0; }
-  if (key == 6) { g_wgrad_target_blocks = value; return 0; }
-  if (key == 7) { g_smallk_max = value; return 0; }
-  if (key == 8) { g_glds_min_k = value; return 0; }
-  if (key == 9) { g_glds_min_grid = value; return 0; }
-  if (key == 10) { g_halo_enable = value; return 0; }
-  if (key == 11) { g_wg_halo_enable = value; return 0; }
-  if (key == 12) { g_wg_halo_target_blocks = value; return 0; }
-  if (key == 13) { g_halo_min_grid = value; return 0; }
-  if (key == 14) { g_wg_halo_max_tiles = value; return 0; }
-  if (key == 15) { g_wg_occ128 = value; return 0; }
-  if (key == 16) { g_wg_glds_enable = value; return 0; }
-  if (key == 17) { g_wg_glds_target = value; return 0; }
-  if (key == 20) { g_bwd_min_px = value; return 0; }   // bn.hip: BN-backward pixels per block (min)
-  if (key == 21) { g_bwd_max_rows = value; return 0; } //   ... and blocks per channel group (max)
-  if (key == 22) { g_ew_target = value; return 0; }    //   bn_apply / bwd_apply target blocks
-  if (key == 23) { g_ew_min_ppt = value; return 0; }   //   ... min pixels per thread
-  return -1;
+  int* slot = tuning_slot(key);
+  if (!slot) return -1;
+  *slot = value;
+  return 0;
+}
+
+int conv_tuning_get(int key) {
+  const int* slot = tuning_slot(key);
+  return slot ? *slot : -1;
 }
 
 static int pick_bn(int pass, int n) {

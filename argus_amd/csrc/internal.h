@@ -17,6 +17,7 @@ int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, 
 int conv_fwd_stat_rows(const argus_conv_desc& d, int dtype);
 int conv_fwd_stat_tile(const argus_conv_desc& d, int dtype);
 int conv_tuning(int key, int value);
+int conv_tuning_get(int key);
 int conv_launch_info(const argus_conv_desc& d, int dtype, int pass, int64_t* flops);
 size_t conv_weight_prep_table_bytes(int count);
 int conv_weight_prep_table(int count, const argus_conv_desc* descs, const float* const* w, const int64_t* strides,

@@ -97,8 +97,12 @@ int argus_conv_dgrad(const argus_conv_desc* d, int dtype, const void* dy, const 
  * key 14 the most (64 x 64) channel tiles for the wgrad halo kernel (default 4), key 15 the
  * 128x128 register-staged wgrad variant (2 default, 1 / 3 with the prefetch ring), key 16 enables
  * (1, default) or disables the bf16 glds wgrad kernel, key 17 its split target (default 512).
+ * Keys 20-23 set the BatchNorm elementwise-kernel geometry (backward min pixels per block, max
+ * blocks per channel group; apply target blocks, min pixels per thread).
  * Returns 0, or -1 for an unknown key. */
 int argus_conv_tuning(int key, int value);
+/* Current value of a tuning key (-1 for an unknown key). */
+int argus_conv_tuning_get(int key);
 /* Which tile a pass launches and its algorithmic work: pass 0 fwd, 1 dgrad, 2 wgrad. Returns a
  * tag (kind*10^7 + dtype*10^6 + tile_m*1000 + tile_n; kind 1 igemm, 2 wgrad) and writes
  * 2*P*K*R*S*C flops (P = n*ho*wo output pixels). */

@@ -512,6 +512,7 @@ def test_conv_glds_kernel_parity(cuda):
     torch.manual_seed(11)
     L = lib()
     assert L.dll.argus_conv_tuning(8, 64) == 0 and L.dll.argus_conv_tuning(9, 1) == 0
+    defaults = (L.dll.argus_conv_tuning_get(8), L.dll.argus_conv_tuning_get(9))
     try:
         for cin, cout, k, s, hin, n in GLDS_SHAPES:
             d, p = _desc(n, hin, hin, cin, cout, k, s)
@@ -549,8 +550,8 @@ def test_conv_glds_kernel_parity(cuda):
             L.conv_dgrad(C.byref(d), BF16, ptr(dyd), ptr(wt), ptr(dx), ptr(resg), ptr(bits), stream())
             assert _rel(dx.permute(0, 3, 1, 2), refd + (res * keep).permute(0, 3, 1, 2)) < TOL["bf16"], ("dgrad mask", cin)
     finally:
-        L.dll.argus_conv_tuning(8, 512)
-        L.dll.argus_conv_tuning(9, 256)
+        L.dll.argus_conv_tuning(8, defaults[0])
+        L.dll.argus_conv_tuning(9, defaults[1])
 
 
 HALO_SHAPES = [  # (cin, cout, hw, n): 256-pixel tiles = 4 rows / 8 rows / 1 image / 4 images
