@@ -37,6 +37,7 @@ SIGNATURES = {
     "argus_abi_version": (_I, []),
     "argus_last_error": (C.c_char_p, []),
     "argus_images_to_nhwc4": (_I, [_I, _I64, _I, _I, _P, _P, _P]),
+    "argus_images_u8_to_nhwc4": (_I, [_I, _I64, _I, _I, _P, _P, _P]),
     "argus_conv_weight_prep": (_I, [_DESC, _I, _P, _P, _P, _P, _P]),
     "argus_conv_weight_prep_table_bytes": (_SZ, [_I]),
     "argus_conv_weight_prep_table": (_I, [_I, _DESC, C.POINTER(_P), C.POINTER(C.c_int64), C.POINTER(_P),

@@ -36,6 +36,12 @@ int argus_images_to_nhwc4(int dtype, int64_t nimg, int h, int w, const float* x,
   return images_to_nhwc4(dtype, nimg, h, w, x, out, (hipStream_t)stream);
 }
 
+int argus_images_u8_to_nhwc4(int dtype, int64_t nimg, int h, int w, const uint8_t* x, void* out,
+                             argus_stream_t stream) {
+  if (nimg <= 0 || h <= 0 || w <= 0 || !x || !out) { set_error("images_u8_to_nhwc4: bad arguments"); return ARGUS_ERR_ARG; }
+  return images_u8_to_nhwc4(dtype, nimg, h, w, x, out, (hipStream_t)stream);
+}
+
 int argus_conv_weight_prep(const argus_conv_desc* d, int dtype, const float* w, const int64_t* strides, void* wf,
                            void* wd, argus_stream_t stream) {
   if (!d || !w) { set_error("conv_weight_prep: null argument"); return ARGUS_ERR_ARG; }

@@ -640,17 +640,22 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
 // ------------------------------------------------------------------------------------------------
 // layout kernels
 // ------------------------------------------------------------------------------------------------
-template <typename T>
-__global__ __launch_bounds__(256) void images_to_nhwc4_kernel(const float* __restrict__ x, T* __restrict__ out,
+// Input pixel -> fp32: fp32 images pass through; uint8 images are divided by 255 exactly as the
+// reference's `.to(torch.float32) / 255.0` (argus/data.py:214-215), so both paths give equal bits.
+ARGUS_DEV float pixel_f32(float v) { return v; }
+ARGUS_DEV float pixel_f32(uint8_t v) { return (float)v / 255.0f; }
+
+template <typename T, typename In>
+__global__ __launch_bounds__(256) void images_to_nhwc4_kernel(const In* __restrict__ x, T* __restrict__ out,
                                                               int64_t nimg, int hw) {
   const int64_t total = nimg * hw;
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
     const int64_t img = i / hw, pix = i - img * hw;
-    const float* src = x + img * 3 * hw + pix;
+    const In* src = x + img * 3 * hw + pix;
     T* dst = out + i * 4;
-    dst[0] = from_f32<T>(src[0]);
-    dst[1] = from_f32<T>(src[hw]);
-    dst[2] = from_f32<T>(src[2 * hw]);
+    dst[0] = from_f32<T>(pixel_f32(src[0]));
+    dst[1] = from_f32<T>(pixel_f32(src[hw]));
+    dst[2] = from_f32<T>(pixel_f32(src[2 * hw]));
     dst[3] = from_f32<T>(0.f);
   }
 }
@@ -831,7 +836,10 @@ extern int g_bwd_min_px, g_bwd_max_rows, g_ew_target, g_ew_min_ppt;  // bn.hip
 static int g_wg_occ128 = 2;  // argus_conv_tuning key 15: workgroups/CU of the 128x128 wgrad tile (1 = with ring)
 extern int g_halo_enable, g_wg_halo_enable, g_wg_halo_target_blocks, g_halo_min_grid,
     g_wg_halo_max_tiles;  // conv_halo.hip
-static int g_smallk_max = 128;  // argus_conv_tuning key 7: largest K (elements) served by the OCC=4 kernel
+// argus_conv_tuning key 7: largest K (elements) served by the single-buffer OCC=3/4 kernel. Swept with
+// tools/convbench.py at B=64: 128 -> 1024 takes the fwd+dgrad conv time from 6.13 to 5.87 ms/step
+// (more resident workgroups hide the global-load latency better than the OCC=2 register ring).
+static int g_smallk_max = 1024;
 
 template <typename T>
 static int run_ig(const IgParams& p, hipStream_t st, int bm, int bn) {
@@ -919,10 +927,11 @@ int conv_fwd_stat_rows(const argus_conv_desc& d, int) {
 
 int conv_fwd_stat_tile(const argus_conv_desc& d, int) { return fwd_bm(d); }
 
-static int dgrad_bm(const argus_conv_desc& d) {
+// dgrad row tile: 64 (swept: 64-row tiles beat 128 on every non-glds/non-halo dgrad at B=64, the
+// extra workgroups outweigh the re-read weight tile; dgrad has no statistics partials to multiply)
+static int dgrad_bm(const argus_conv_desc&) {
   if (g_force_bm[1]) return g_force_bm[1];
-  const long M = (long)d.n * d.h * d.w / (d.stride * d.stride);
-  return M >= 16L * 1024 ? 128 : 64;
+  return 64;
 }
 
 int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, void* y,
@@ -1205,14 +1214,24 @@ int conv_weight_prep_batch(int dtype, int count, const void* device_table, int n
   return check_launch("weight_prep_batch_kernel");
 }
 
-int images_to_nhwc4(int dtype, int64_t nimg, int h, int w, const float* x, void* out, hipStream_t st) {
+template <typename In>
+static int launch_images(int dtype, int64_t nimg, int h, int w, const In* x, void* out, hipStream_t st) {
   const int64_t total = nimg * h * w;
   const int blocks = (int)std::min<int64_t>((total + 255) / 256, 8192);
   if (dtype == ARGUS_BF16)
-    hipLaunchKernelGGL(images_to_nhwc4_kernel<bf16>, dim3(blocks), dim3(256), 0, st, x, (bf16*)out, nimg, h * w);
+    hipLaunchKernelGGL((images_to_nhwc4_kernel<bf16, In>), dim3(blocks), dim3(256), 0, st, x, (bf16*)out, nimg, h * w);
   else
-    hipLaunchKernelGGL(images_to_nhwc4_kernel<float>, dim3(blocks), dim3(256), 0, st, x, (float*)out, nimg, h * w);
+    hipLaunchKernelGGL((images_to_nhwc4_kernel<float, In>), dim3(blocks), dim3(256), 0, st, x, (float*)out, nimg,
+                       h * w);
   return check_launch("images_to_nhwc4_kernel");
+}
+
+int images_to_nhwc4(int dtype, int64_t nimg, int h, int w, const float* x, void* out, hipStream_t st) {
+  return launch_images(dtype, nimg, h, w, x, out, st);
+}
+
+int images_u8_to_nhwc4(int dtype, int64_t nimg, int h, int w, const uint8_t* x, void* out, hipStream_t st) {
+  return launch_images(dtype, nimg, h, w, x, out, st);
 }
 
 }  // namespace argus

@@ -33,5 +33,7 @@ int conv_weight_prep(const argus_conv_desc& d, int dtype, const float* w, const 
                      void* wf, void* wd, hipStream_t st);
 int images_to_nhwc4(int dtype, int64_t nimg, int h, int w, const float* x, void* out,
                     hipStream_t st);
+int images_u8_to_nhwc4(int dtype, int64_t nimg, int h, int w, const uint8_t* x, void* out,
+                       hipStream_t st);
 
 }  // namespace argus

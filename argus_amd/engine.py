@@ -272,12 +272,15 @@ class ResNetEngine:
             raise ValueError(f"expected {3 * self.n_cams} input channels, got {Cn}")
         self.ensure(B, H, W)
         x = x.contiguous()
-        if x.dtype != torch.float32:
-            x = x.float()
         L, dt, s = self.L, self.dt, stream()
         N = self.N
         self.prepare_weights(P)
-        L.images_to_nhwc4(dt, N, H, W, ptr(x), ptr(self.x0), s)
+        if x.dtype == torch.uint8:  # CameraCubePoseDataset(uint8=True): /255 happens in the layout kernel
+            L.images_u8_to_nhwc4(dt, N, H, W, ptr(x), ptr(self.x0), s)
+        else:
+            if x.dtype != torch.float32:
+                x = x.float()
+            L.images_to_nhwc4(dt, N, H, W, ptr(x), ptr(self.x0), s)
         # stem
         self._conv_bn(P, Bf, "resnet.conv1", "resnet.bn1", self.x0, self.y0, None, training)
         st = self.bn_state["resnet.bn1"]

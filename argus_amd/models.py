@@ -149,7 +149,10 @@ class NCameraCNN(nn.Module):
         return P, Bf
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        """(B, 3*n_cams, H, W) fp32 images in [0, 1] -> (B, 6) se(3) poses."""
+        """(B, 3*n_cams, H, W) fp32 images in [0, 1] -> (B, 6) se(3) poses.
+
+        Extension: uint8 images in [0, 255] (``CameraCubePoseDataset(uint8=True)``) are accepted too;
+        the reference's ``/ 255.0`` (argus/data.py:214-215) then runs on the device, bit-identically."""
         assert len(x.shape) == 4, "The input images must be of shape (B, C, H, W)! If B=1, add a dummy dimension."
         if x.device.type != "cuda":
             raise RuntimeError("argus_amd.NCameraCNN runs only on the MI355X HIP path: move the model and the "

@@ -134,8 +134,9 @@ def initialize_training(cfg: TrainConfig, rank: int = 0, world: int = 1):
         device = torch.device("cuda", torch.cuda.current_device())
     torch.cuda.set_device(device)
 
-    train_ds = CameraCubePoseDataset(cfg.dataset_config, cfg_aug=cfg.augmentation_config, train=True)
-    val_ds = CameraCubePoseDataset(cfg.dataset_config, cfg_aug=cfg.augmentation_config, train=False)
+    # uint8 batches: 4x less host->device traffic; the /255 of argus/data.py:214-215 runs on the device
+    train_ds = CameraCubePoseDataset(cfg.dataset_config, cfg_aug=cfg.augmentation_config, train=True, uint8=True)
+    val_ds = CameraCubePoseDataset(cfg.dataset_config, cfg_aug=cfg.augmentation_config, train=False, uint8=True)
     distributed = world > 1
     train_sampler = DistributedSampler(train_ds, num_replicas=world, rank=rank, shuffle=True) if distributed else None
     val_sampler = DistributedSampler(val_ds, num_replicas=world, rank=rank, shuffle=False) if distributed else None

@@ -122,6 +122,7 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--kernels", action="store_true", help="print the probe step's per-kernel table to stderr")
+    ap.add_argument("--tune", nargs="*", default=[], help="dev: argus_conv_tuning key=value pairs")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -137,6 +138,11 @@ def main() -> None:
     from argus_amd.step import FusedTrainer
     from argus_amd.losses import geometric_loss_fn
 
+    from argus_amd._lib import lib
+
+    for kv in args.tune:
+        k, v = kv.split("=")
+        assert lib().dll.argus_conv_tuning(int(k), int(v)) == 0, kv
     B, (H, W) = args.batch, args.hw
     torch.manual_seed(42)
     model = NCameraCNN(compute_dtype=args.dtype).to(dev)

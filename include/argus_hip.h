@@ -49,6 +49,10 @@ const char* argus_last_error(void);
  * argus/models.py:81 plus the layout change cuDNN does internally. */
 int argus_images_to_nhwc4(int dtype, int64_t nimg, int h, int w, const float* x, void* out,
                           argus_stream_t stream);
+/* Same, from uint8 images (B,3*ncam,H,W) as CameraCubePoseDataset(uint8=True) yields them: the
+ * `.to(torch.float32) / 255.0` of argus/data.py:214-215 runs on the device (4x less H2D traffic). */
+int argus_images_u8_to_nhwc4(int dtype, int64_t nimg, int h, int w, const uint8_t* x, void* out,
+                             argus_stream_t stream);
 /* fp32 master weight -> compute copies: w_fwd[k][r][s][c] (dtype; padded [k][8][8][4] for the
  * stem) and w_dgrad[c][r][s][k] (dtype; ignored for the stem). The master is read with element
  * strides {sk, sc, sr, ss} (so an OIHW nn.Parameter or a channels-last view both work);

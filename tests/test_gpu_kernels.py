@@ -487,7 +487,9 @@ def test_kernel_timer_records_exact_instantiations(cuda):
     fl = C.c_int64()
     tag = L.dll.argus_conv_launch_info(C.byref(d), BF16, 0, C.byref(fl))
     bm, bn = divmod(tag % 1000000, 1000)
-    assert name == f"argus::igemm_kernel<__bf16, {bm}, {bn}, false, false, 2>"  # K = 576 > 128: OCC 2
+    # K = 576: the single-buffer kernel (OCC 4; 3 for the 128x128 tile) when K <= tuning key 7
+    occ = (3 if bm == bn == 128 else 4) if 576 <= L.dll.argus_conv_tuning_get(7) else 2
+    assert name == f"argus::igemm_kernel<__bf16, {bm}, {bn}, false, false, {occ}>"
     assert v["launches"] == 3 and v["flops_per_launch"] == fl.value and v["avg_us"] > 0
     assert v["bytes_per_launch"] == 2 * (4 * 32 * 32 * 64 + 128 * 9 * 64 + 4 * 32 * 32 * 128)
     with KernelTimer("argus::wgrad") as t:  # filtered out: nothing recorded
@@ -753,3 +755,25 @@ def _wgrad_glds_cases(cuda, L, KernelTimer):
         ref = torch.nn.grad.conv2d_weight(x.permute(0, 3, 1, 2).double(), (cout, cin, k, k),
                                           dy.permute(0, 3, 1, 2).double(), stride=s, padding=p)
         assert _rel(dw.permute(0, 3, 1, 2), ref) < 2e-3, ("wgrad glds", cin, cout, k, s, hw, n)
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+def test_images_u8_layout_matches_fp32_path(cuda, dt):
+    """uint8 input path (CameraCubePoseDataset(uint8=True)): the device-side /255 equals the
+    reference's host `.to(torch.float32) / 255.0` (argus/data.py:214-215) bit for bit, and the NHWC4
+    layout (camera fold of argus/models.py:81, zero 4th channel) matches the fp32 entry point."""
+    L = lib()
+    g = torch.Generator().manual_seed(5)
+    B, H, W = 3, 7, 11  # ragged sizes: the grid-stride loop's tail
+    u8 = torch.randint(0, 256, (B, 6, H, W), generator=g, dtype=torch.uint8)
+    f32 = u8.to(torch.float32) / 255.0
+    N = 2 * B
+    out_u8 = torch.full((N, H, W, 4), 7.0, dtype=TDT[dt], device=cuda)
+    out_f = torch.full((N, H, W, 4), 7.0, dtype=TDT[dt], device=cuda)
+    L.images_u8_to_nhwc4(DT[dt], N, H, W, ptr(u8.to(cuda)), ptr(out_u8), stream())
+    L.images_to_nhwc4(DT[dt], N, H, W, ptr(f32.to(cuda)), ptr(out_f), stream())
+    torch.cuda.synchronize()
+    want = torch.zeros(N, H, W, 4, dtype=torch.float32)
+    want[..., :3] = f32.reshape(N, 3, H, W).permute(0, 2, 3, 1)
+    assert torch.equal(out_u8.cpu(), want.to(TDT[dt]))
+    assert torch.equal(out_f.cpu(), want.to(TDT[dt]))

@@ -191,3 +191,19 @@ def test_forward_large_frame_matches_oracle(cuda, dtype, tol):
             got = m(x.to(cuda)).cpu()
             want = ref(x)
             assert (got - want).abs().max().item() < tol, (dtype, train, got, want)
+
+
+@pytest.mark.parametrize("compute_dtype", ["fp32", "bf16"])
+def test_uint8_images_give_identical_predictions(cuda, compute_dtype):
+    """The model accepts the uint8 batches of CameraCubePoseDataset(uint8=True) and predicts exactly
+    what it predicts on the reference's fp32 `/255` batch (argus/data.py:214-215)."""
+    from argus_amd.models import NCameraCNN
+
+    g = torch.Generator().manual_seed(11)
+    u8 = torch.randint(0, 256, (2, 6, 64, 64), generator=g, dtype=torch.uint8)
+    torch.manual_seed(42)
+    model = NCameraCNN(compute_dtype=compute_dtype).to(cuda).train()
+    with torch.no_grad():
+        a = model(u8.to(cuda))
+        b = model((u8.to(torch.float32) / 255.0).to(cuda))
+    assert torch.equal(a, b)
