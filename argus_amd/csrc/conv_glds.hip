@@ -428,7 +428,9 @@ static const char* wgg_name() {
   return s.c_str();
 }
 
-int g_wg_glds_enable = 1;     // argus_conv_tuning key 16
+// argus_conv_tuning key 16. Off by default since the single-buffer igemm change: swept at B=64 the
+// register-staged wgrad kernel is faster on every layer the glds one served (bench 7030 -> 7115 img/s).
+int g_wg_glds_enable = 0;
 int g_wg_glds_target = 512;   // key 17: split target (workgroups)
 
 bool wgrad_glds_plan(const argus_conv_desc& d, int dtype, bool pro, int* splits, int* pps) {

@@ -732,11 +732,14 @@ def test_wgrad_glds_kernel_parity(cuda):
 
     torch.manual_seed(29)
     L = lib()
+    halo, glds = L.dll.argus_conv_tuning_get(11), L.dll.argus_conv_tuning_get(16)
     assert L.dll.argus_conv_tuning(11, 0) == 0  # the 3x3 halo wgrad would take the 128-channel 3x3 case
+    assert L.dll.argus_conv_tuning(16, 1) == 0  # the glds wgrad is off by default (tuning key 16)
     try:
         _wgrad_glds_cases(cuda, L, KernelTimer)
     finally:
-        L.dll.argus_conv_tuning(11, 1)
+        L.dll.argus_conv_tuning(11, halo)
+        L.dll.argus_conv_tuning(16, glds)
 
 
 def _wgrad_glds_cases(cuda, L, KernelTimer):
