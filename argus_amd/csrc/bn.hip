@@ -456,43 +456,55 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(int64_t pixels, int C
 }
 
 // ---- max pool 3x3/2 p1 fused with the stem BN + ReLU ---------------------------------------------
+// One thread per (output pixel, 16-byte channel chunk). 32-bit index math (element counts < 2^31,
+// checked on the host); the E argmax bytes of a chunk move as one 8-byte (bf16) / 4-byte (fp32) access.
+template <int E> struct AmaxVec;
+template <> struct AmaxVec<8> { typedef uint2 type; };
+template <> struct AmaxVec<4> { typedef unsigned type; };
+
 template <typename T>
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(int n, int H, int W, int C, int Ho, int Wo,
                                                           const T* __restrict__ y, const float* __restrict__ sc,
                                                           const float* __restrict__ sh, T* __restrict__ out,
                                                           uint8_t* __restrict__ amax) {
   constexpr int E = Chunk<T>::E;
+  typedef typename AmaxVec<E>::type AV;
   const int CH = C / E;
-  const int64_t total = (int64_t)n * Ho * Wo * CH;
-  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int ch = (int)(i % CH);
-    const int64_t pix = i / CH;
-    const int ow = (int)(pix % Wo);
-    const int oh = (int)((pix / Wo) % Ho);
-    const int img = (int)(pix / ((int64_t)Wo * Ho));
+  const int total = n * Ho * Wo * CH;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int pix = i / CH, ch = i - pix * CH;
+    const int q = pix / Wo, ow = pix - q * Wo;
+    const int img = q / Ho, oh = q - img * Ho;
     const int c0 = ch * E;
-    float best[E];
-    uint8_t idx[E];
+    float s[E], h[E], best[E];
+    unsigned idx[E];
 #pragma unroll
-    for (int j = 0; j < E; ++j) { best[j] = -INFINITY; idx[j] = 0; }
+    for (int j = 0; j < E; ++j) { s[j] = sc[c0 + j]; h[j] = sh[c0 + j]; best[j] = -INFINITY; idx[j] = 0; }
+    const T* yb = y + (size_t)img * H * W * C + c0;
+#pragma unroll
     for (int r = 0; r < 3; ++r) {
       const int ih = 2 * oh - 1 + r;
       if ((unsigned)ih >= (unsigned)H) continue;
-      for (int s = 0; s < 3; ++s) {
-        const int iw = 2 * ow - 1 + s;
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+        const int iw = 2 * ow - 1 + t;
         if ((unsigned)iw >= (unsigned)W) continue;
         float v[E];
-        unpack(ld16(y + (((int64_t)img * H + ih) * W + iw) * C + c0), v);
+        unpack(ld16(yb + (ih * W + iw) * C), v);
 #pragma unroll
         for (int j = 0; j < E; ++j) {
-          const float z = fmaxf(fmaf(v[j], sc[c0 + j], sh[c0 + j]), 0.f);
-          if (z > best[j]) { best[j] = z; idx[j] = (uint8_t)(r * 3 + s); }
+          const float z = fmaxf(fmaf(v[j], s[j], h[j]), 0.f);
+          if (z > best[j]) { best[j] = z; idx[j] = (unsigned)(r * 3 + t); }
         }
       }
     }
-    st16(out + pix * C + c0, pack(best));
-#pragma unroll
-    for (int j = 0; j < E; ++j) amax[pix * C + c0 + j] = idx[j];
+    st16(out + (size_t)pix * C + c0, pack(best));
+    if constexpr (E == 8) {
+      const uint2 a = {idx[0] | idx[1] << 8 | idx[2] << 16 | idx[3] << 24, idx[4] | idx[5] << 8 | idx[6] << 16 | idx[7] << 24};
+      *reinterpret_cast<AV*>(amax + (size_t)pix * C + c0) = a;
+    } else {
+      *reinterpret_cast<AV*>(amax + (size_t)pix * C + c0) = idx[0] | idx[1] << 8 | idx[2] << 16 | idx[3] << 24;
+    }
   }
 }
 
@@ -501,36 +513,46 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(int n, int H, int W, i
                                                           const T* __restrict__ dout, const uint8_t* __restrict__ amax,
                                                           T* __restrict__ dz) {
   constexpr int E = Chunk<T>::E;
+  typedef typename AmaxVec<E>::type AV;
   const int CH = C / E;
-  const int64_t total = (int64_t)n * H * W * CH;
-  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int ch = (int)(i % CH);
-    const int64_t pix = i / CH;
-    const int iw = (int)(pix % W);
-    const int ih = (int)((pix / W) % H);
-    const int img = (int)(pix / ((int64_t)W * H));
+  const int total = n * H * W * CH;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int pix = i / CH, ch = i - pix * CH;
+    const int q = pix / W, iw = pix - q * W;
+    const int img = q / H, ih = q - img * H;
     const int c0 = ch * E;
     float acc[E];
 #pragma unroll
     for (int j = 0; j < E; ++j) acc[j] = 0.f;
+    // output rows/cols whose 3x3/2 window (offset -1) covers this input pixel: at most 2 x 2
     const int oh_lo = max(0, ih / 2), oh_hi = min(Ho - 1, (ih + 1) / 2);
     const int ow_lo = max(0, iw / 2), ow_hi = min(Wo - 1, (iw + 1) / 2);
     for (int oh = oh_lo; oh <= oh_hi; ++oh) {
       const int r = ih - (2 * oh - 1);
       if (r < 0 || r > 2) continue;
       for (int ow = ow_lo; ow <= ow_hi; ++ow) {
-        const int s = iw - (2 * ow - 1);
-        if (s < 0 || s > 2) continue;
-        const int64_t o = (((int64_t)img * Ho + oh) * Wo + ow) * C + c0;
+        const int t = iw - (2 * ow - 1);
+        if (t < 0 || t > 2) continue;
+        const size_t o = ((size_t)(img * Ho + oh) * Wo + ow) * C + c0;
         float g[E];
         unpack(ld16(dout + o), g);
-        const uint8_t want = (uint8_t)(r * 3 + s);
+        const unsigned want = (unsigned)(r * 3 + t);
+        unsigned a[E];
+        if constexpr (E == 8) {
+          const uint2 v = *reinterpret_cast<const AV*>(amax + o);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { a[j] = (v.x >> (8 * j)) & 0xffu; a[4 + j] = (v.y >> (8 * j)) & 0xffu; }
+        } else {
+          const unsigned v = *reinterpret_cast<const AV*>(amax + o);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) a[j] = (v >> (8 * j)) & 0xffu;
+        }
 #pragma unroll
         for (int j = 0; j < E; ++j)
-          if (amax[o + j] == want) acc[j] += g[j];
+          if (a[j] == want) acc[j] += g[j];
       }
     }
-    st16(dz + pix * C + c0, pack(acc));
+    st16(dz + (size_t)pix * C + c0, pack(acc));
   }
 }
 
@@ -755,6 +777,7 @@ int argus_maxpool_fwd(int dtype, int n, int h, int w, int c, const void* y, cons
                       void* out, uint8_t* amax, argus_stream_t stream) {
   const int E = dtype == ARGUS_BF16 ? 8 : 4;
   if (c % E) { set_error("maxpool_fwd: bad channels"); return ARGUS_ERR_SHAPE; }
+  if ((int64_t)n * h * w * c >= (1LL << 31)) { set_error("maxpool_fwd: tensor exceeds 2^31 elements"); return ARGUS_ERR_SHAPE; }
   const int ho = (h + 2 - 3) / 2 + 1, wo = (w + 2 - 3) / 2 + 1;
   const int64_t work = (int64_t)n * ho * wo * (c / E);
   hipStream_t st = (hipStream_t)stream;
@@ -771,6 +794,7 @@ int argus_maxpool_bwd(int dtype, int n, int h, int w, int c, const void* dout, c
                       argus_stream_t stream) {
   const int E = dtype == ARGUS_BF16 ? 8 : 4;
   if (c % E) { set_error("maxpool_bwd: bad channels"); return ARGUS_ERR_SHAPE; }
+  if ((int64_t)n * h * w * c >= (1LL << 31)) { set_error("maxpool_bwd: tensor exceeds 2^31 elements"); return ARGUS_ERR_SHAPE; }
   const int ho = (h + 2 - 3) / 2 + 1, wo = (w + 2 - 3) / 2 + 1;
   const int64_t work = (int64_t)n * h * w * (c / E);
   hipStream_t st = (hipStream_t)stream;
