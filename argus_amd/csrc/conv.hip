@@ -343,7 +343,7 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
           for (int j = 0; j < E; ++j) f[j] += (mb >> j) & 1u ? o[j] : 0.f;
           v = pack(f);
         }
-        st16(dst, v);
+        st16_nt(dst, v);
       }
     }
     if (EPASS > 1) __syncthreads();

@@ -244,7 +244,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) void igemm_glds_kern
       for (int j = 0; j < 8; ++j) f[j] += (mb >> j) & 1u ? o[j] : 0.f;
       v = pack(f);
     }
-    st16(dst, v);
+    st16_nt(dst, v);
   }
 }
 

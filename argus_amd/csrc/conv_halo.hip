@@ -285,7 +285,7 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, 1) void conv3x3_halo_kernel(con
       for (int j = 0; j < 8; ++j) f[j] += (mb >> j) & 1u ? o[j] : 0.f;
       v = pack(f);
     }
-    st16(Cg + off, v);
+    st16_nt(Cg + off, v);
   }
 }
 
