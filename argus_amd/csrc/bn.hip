@@ -552,7 +552,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(int n, int H, int W, i
           if (a[j] == want) acc[j] += g[j];
       }
     }
-    st16(dz + (size_t)pix * C + c0, pack(acc));
+    st16_nt(dz + (size_t)pix * C + c0, pack(acc));  // 268 MB written once, read by the stem wgrad later
   }
 }
 

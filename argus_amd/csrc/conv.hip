@@ -601,7 +601,7 @@ __global__ __launch_bounds__(256, OCC == 1 ? 1 : 2) void wgrad_kernel(const WgPa
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = mt * BM + wm * (BM / 2) + mi * 16 + g * 4 + r;
-        out[(size_t)m * p.N + n] = acc[mi][ni][r];
+        out[(size_t)m * p.N + n] = acc[mi][ni][r];  // cached: the split reduce reads it next
       }
     }
 }
