@@ -261,7 +261,9 @@ static void launch_glds(const IgParams& p, int maxM, hipStream_t st) {
   timed_launch(glds_name<BM, BN>(), igemm_glds_kernel<BM, BN>, grid, dim3((BM / 64) * (BN / 64) * 64), st, p);
 }
 
-int g_glds_min_k = 512;      // argus_conv_tuning key 8: smallest K (taps*C) served by the glds kernel (0 = off)
+// argus_conv_tuning key 8: smallest K (taps*C) served by the glds kernel (0 = off). 512 -> 1024 after
+// the non-temporal epilogue stores (convbench B=64: fwd+dgrad 5.32 -> 5.20 ms)
+int g_glds_min_k = 1024;
 int g_glds_min_grid = 256;  // key 9: fewest workgroups for which it is chosen
 
 bool igemm_glds_launch(const IgParams& p, int maxM, int maxK, hipStream_t st) {
