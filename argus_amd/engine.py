@@ -88,6 +88,14 @@ class ResNetEngine:
         self.shape = None
         self.saved = False
         self.debug: dict | None = None  # when a dict: clones of block outputs / block-input grads
+        # Weight gradients run on a side stream, overlapped with the dgrad -> BN-backward chain of the
+        # main stream (they only feed the gradient buffer). Events order them after their dy and
+        # before any main-stream overwrite of that dy buffer; backward() joins the side stream at every
+        # on_ready() and at its end. ARGUS_WGRAD_STREAM=0 keeps everything on the caller's stream.
+        self.wgrad_overlap = os.environ.get("ARGUS_WGRAD_STREAM", "1") != "0"
+        self._side: torch.cuda.Stream | None = None
+        self._pending: dict = {}  # dy data_ptr -> event of the last side-stream wgrad reading it
+        self._last_side = None
 
     # ------------------------------------------------------------------ allocation
     def _t(self, *shape, dtype=None):
@@ -365,6 +373,7 @@ class ResNetEngine:
         dh, dx = g[0], g[3]
         L.avgpool_bwd(dt, N, hf * wf, 2048, ptr(self.dfeat), ptr(dh), s)
         if on_ready is not None:
+            self._join()
             on_ready("resnet.fc.weight")
 
         for idx in range(len(self.blocks) - 1, -1, -1):
@@ -420,6 +429,7 @@ class ResNetEngine:
                 self._dgrad(pf + ".conv1", dyw, dx, addend=dh, mask=a["bits"])
             dh, dx = dx, dh
             if on_ready is not None:
+                self._join()
                 on_ready(pf + ".conv1.weight")
             if self.debug is not None:
                 n_in = N * hi * wi * b.cin
@@ -431,6 +441,7 @@ class ResNetEngine:
         L.maxpool_bwd(dt, N, H1, W1, 64, ptr(dh), ptr(self.amax), ptr(dz0), s)
         self._bn_bwd(P, G, "resnet.bn1", N * H1 * W1, 64, dz0, 2, None, self.y0, dy0, None)
         self._wgrad("resnet.conv1", self.x0, None, dy0, G)
+        self._join()
         if on_ready is not None:
             on_ready("resnet.conv1.weight")
 
@@ -440,6 +451,7 @@ class ResNetEngine:
         L.bn_bwd_reduce(dt, px, ch, ptr(dz), mode, ptr(mask_src), ptr(y), ptr(st[2]), ptr(st[3]), ptr(st[0]),
                         ptr(st[1]), ptr(self.bwd_part), None, None, None, None, s)
         self._bn_bwd_fin(P, G, name, px, ch, self.bwd_part)
+        self._guard(dy_out)
         L.bn_bwd_apply(dt, px, ch, ptr(dz), mode, ptr(mask_src), ptr(y), ptr(st[2]), ptr(st[3]), ptr(cf[0]),
                        ptr(cf[1]), ptr(cf[2]), ptr(dy_out), ptr(dm_out), None, None, None, None, None, s)
 
@@ -460,6 +472,8 @@ class ResNetEngine:
         self._bn_bwd_fin(P, G, name, px, ch, self.bwd_part)
         self._bn_bwd_fin(P, G, name2, px, ch, self.bwd_part2)
         cf, cf2 = self.bn_coef[name], self.bn_coef[name2]
+        self._guard(dy_out)
+        self._guard(dy2_out)
         L.bn_bwd_apply(dt, px, ch, ptr(dz), 3, ptr(bits), ptr(y), None, None, ptr(cf[0]), ptr(cf[1]), ptr(cf[2]),
                        ptr(dy_out), None, ptr(y2), ptr(cf2[0]), ptr(cf2[1]), ptr(cf2[2]), ptr(dy2_out), s)
 
@@ -468,9 +482,38 @@ class ResNetEngine:
         sc = sh = None
         if pro_state is not None:
             sc, sh = pro_state[2], pro_state[3]
-        self._launch(cv, 2, lambda: self.L.conv_wgrad(C.byref(cv.desc), self.dt, ptr(x), ptr(sc), ptr(sh), ptr(dy),
-                                                       ptr(G[conv + ".weight"]), ptr(self.wg_ws), self.wg_ws_bytes,
-                                                       stream()))
+        fn = lambda: self.L.conv_wgrad(C.byref(cv.desc), self.dt, ptr(x), ptr(sc), ptr(sh), ptr(dy),  # noqa: E731
+                                       ptr(G[conv + ".weight"]), ptr(self.wg_ws), self.wg_ws_bytes, stream())
+        if not self.wgrad_overlap:
+            self._launch(cv, 2, fn)
+            return
+        main = torch.cuda.current_stream()
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        ready = torch.cuda.Event()
+        ready.record(main)
+        self._side.wait_event(ready)  # dy (and x) are complete on the main stream
+        with torch.cuda.stream(self._side):
+            self._launch(cv, 2, fn)  # all wgrads share one side stream, so wg_ws is never shared
+        done = torch.cuda.Event()
+        done.record(self._side)
+        self._pending[dy.data_ptr()] = done
+        self._last_side = done
+
+    def _guard(self, buf) -> None:
+        """Before the main stream overwrites ``buf``: wait for the side-stream wgrad still reading it."""
+        if buf is None:
+            return
+        ev = self._pending.pop(buf.data_ptr(), None)
+        if ev is not None:
+            torch.cuda.current_stream().wait_event(ev)
+
+    def _join(self) -> None:
+        """Main stream waits for every weight gradient issued so far."""
+        if self._last_side is not None:
+            torch.cuda.current_stream().wait_event(self._last_side)
+            self._pending.clear()
+            self._last_side = None
 
     def _dgrad(self, conv, dy, dx, addend=None, mask=None):
         cv = self.convs[conv]
