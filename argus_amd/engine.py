@@ -183,6 +183,10 @@ class ResNetEngine:
         max_stat = max(cv.stat_rows * cv.desc.k for cv in convs.values())
         self.stat_part = self._f(max_stat * 2)
         self.bn_ws = torch.zeros(L.dll.argus_bn_workspace_bytes(2048), dtype=torch.uint8, device=self.device)
+        # the downsample branch's own statistics workspaces (it runs on the side stream in forward)
+        ds_stat = max([cv.stat_rows * cv.desc.k for n, cv in convs.items() if ".downsample." in n] or [1])
+        self.stat_part_ds = self._f(ds_stat * 2)
+        self.bn_ws_ds = torch.zeros(L.dll.argus_bn_workspace_bytes(2048), dtype=torch.uint8, device=self.device)
         max_bwd = 0
         for b, a in zip(self.blocks, act):
             for hw, c in ((a["hw_in"], b.width), (a["hw"], b.width), (a["hw"], b.cout)):
@@ -213,14 +217,16 @@ class ResNetEngine:
         self.gemm_ws = torch.empty(max(hws, 16), dtype=torch.uint8, device=self.device)
 
     # ------------------------------------------------------------------ helpers
-    def _bn_train(self, P, Bf, name, rows, tile, count):
+    def _bn_train(self, P, Bf, name, rows, tile, count, part=None, ws=None):
         st = self.bn_state[name]
         mom = Bf.get(name + ".momentum", 0.1)
-        self.L.bn_finalize(self.bn_ch[name], rows, tile, ptr(self.stat_part), count, ptr(P[name + ".weight"]),
+        part = self.stat_part if part is None else part
+        ws = self.bn_ws if ws is None else ws
+        self.L.bn_finalize(self.bn_ch[name], rows, tile, ptr(part), count, ptr(P[name + ".weight"]),
                            ptr(P[name + ".bias"]), C.c_float(Bf.get(name + ".eps", 1e-5)), C.c_float(mom),
                            ptr(Bf[name + ".running_mean"]), ptr(Bf[name + ".running_var"]),
                            ptr(Bf[name + ".num_batches_tracked"]), ptr(st[0]), ptr(st[1]), ptr(st[2]), ptr(st[3]),
-                           ptr(self.bn_ws), stream())
+                           ptr(ws), stream())
 
     def _bn_eval(self, P, Bf, name):
         st = self.bn_state[name]
@@ -228,16 +234,17 @@ class ResNetEngine:
                               ptr(Bf[name + ".running_mean"]), ptr(Bf[name + ".running_var"]),
                               C.c_float(Bf.get(name + ".eps", 1e-5)), ptr(st[2]), ptr(st[3]), stream())
 
-    def _conv_bn(self, P, Bf, conv, bn, x, y, pro, training):
+    def _conv_bn(self, P, Bf, conv, bn, x, y, pro, training, part=None, ws=None):
         cv = self.convs[conv]
         sc = sh = None
         if pro is not None:
             sc, sh = self.bn_state[pro][2], self.bn_state[pro][3]
+        part = self.stat_part if part is None else part
         self._launch(cv, 0, lambda: self.L.conv_fwd(C.byref(cv.desc), self.dt, ptr(x), ptr(cv.wf), ptr(y), ptr(sc),
-                                                     ptr(sh), ptr(self.stat_part) if training else None, stream()))
+                                                     ptr(sh), ptr(part) if training else None, stream()))
         if training:
             count = cv.desc.n * cv.desc.ho * cv.desc.wo
-            self._bn_train(P, Bf, bn, cv.stat_rows, cv.stat_tile, count)
+            self._bn_train(P, Bf, bn, cv.stat_rows, cv.stat_tile, count, part, ws)
         else:
             self._bn_eval(P, Bf, bn)
 
@@ -297,6 +304,13 @@ class ResNetEngine:
         h = self.p0
         for b, a in zip(self.blocks, self.act):
             pf = b.prefix
+            ds_done = None
+            if b.has_ds and self.wgrad_overlap:
+                # downsample conv + its BN statistics on the side stream, beside conv1..conv3 (joined
+                # before the block's bn_apply); own partial / ticket workspaces
+                ds_done = self._on_side(lambda: self._conv_bn(P, Bf, pf + ".downsample.0", pf + ".downsample.1", h,
+                                                              a["yd"], None, training, self.stat_part_ds,
+                                                              self.bn_ws_ds))
             self._conv_bn(P, Bf, pf + ".conv1", pf + ".bn1", h, a["y1"], None, training)
             if self.materialize:
                 self._act(pf + ".bn1", a["y1"], a["a1"], N * a["hw_in"][0] * a["hw_in"][1], b.width)
@@ -309,7 +323,10 @@ class ResNetEngine:
             s3 = self.bn_state[pf + ".bn3"]
             px = N * a["hw"][0] * a["hw"][1]
             if b.has_ds:
-                self._conv_bn(P, Bf, pf + ".downsample.0", pf + ".downsample.1", h, a["yd"], None, training)
+                if ds_done is None:
+                    self._conv_bn(P, Bf, pf + ".downsample.0", pf + ".downsample.1", h, a["yd"], None, training)
+                else:
+                    torch.cuda.current_stream().wait_event(ds_done)
                 sd = self.bn_state[pf + ".downsample.1"]
                 L.bn_apply(dt, px, b.cout, ptr(a["y3"]), ptr(s3[2]), ptr(s3[3]), ptr(a["yd"]), ptr(sd[2]),
                            ptr(sd[3]), 1, ptr(a["out"]), ptr(a["bits"]), s)
@@ -487,18 +504,26 @@ class ResNetEngine:
         if not self.wgrad_overlap:
             self._launch(cv, 2, fn)
             return
+        # after dy (and x) are complete on the main stream; all wgrads share the one side stream, so
+        # wg_ws is never shared
+        done = self._on_side(lambda: self._launch(cv, 2, fn))
+        self._pending[dy.data_ptr()] = done
+        self._last_side = done
+
+    def _on_side(self, fn):
+        """Run ``fn``'s launches on the side stream after the main stream's work so far; returns the
+        side-stream event that marks their completion."""
         main = torch.cuda.current_stream()
         if self._side is None:
             self._side = torch.cuda.Stream(device=self.device)
         ready = torch.cuda.Event()
         ready.record(main)
-        self._side.wait_event(ready)  # dy (and x) are complete on the main stream
+        self._side.wait_event(ready)
         with torch.cuda.stream(self._side):
-            self._launch(cv, 2, fn)  # all wgrads share one side stream, so wg_ws is never shared
+            fn()
         done = torch.cuda.Event()
         done.record(self._side)
-        self._pending[dy.data_ptr()] = done
-        self._last_side = done
+        return done
 
     def _guard(self, buf) -> None:
         """Before the main stream overwrites ``buf``: wait for the side-stream wgrad still reading it."""
