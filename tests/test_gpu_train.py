@@ -135,3 +135,29 @@ def test_forward_latency_graph_replay(cuda):
     assert torch.equal(out, eager)
     r = forward_latency(trials=3, hw=(64, 64))
     assert r["mean_s"] > 0 and math.isfinite(r["mean_s"])
+
+
+def test_side_stream_overlap_is_bit_identical(cuda):
+    """The weight-gradient / downsample side stream (engine.wgrad_overlap) only reorders independent
+    launches: three bf16 training steps with and without it must give bitwise-identical parameters,
+    Adam moments, BN running statistics and losses (a missed event would show up as a race here)."""
+    from argus_amd.models import NCameraCNN
+    from argus_amd.step import FusedTrainer
+    from oracle import se3
+
+    g = torch.Generator().manual_seed(3)
+    x = (torch.randint(0, 256, (8, 6, 128, 128), generator=g, dtype=torch.uint8).float() / 255.0).to(cuda)
+    T = se3.random_targets(8, generator=g).float().to(cuda)
+    runs = []
+    for overlap in (True, False):
+        torch.manual_seed(42)
+        model = NCameraCNN(compute_dtype="bf16").to(cuda).train()
+        tr = FusedTrainer(model, lr=1e-3, max_grad_norm=1.0)
+        model._engine(cuda).wgrad_overlap = overlap
+        losses = [tr.step(x, T).clone() for _ in range(3)]
+        torch.cuda.synchronize()
+        runs.append((torch.stack(losses).cpu(), tr.flat.param.cpu(), tr.exp_avg_sq.cpu(),
+                     {k: v.cpu() for k, v in model.state_dict().items()}))
+    (l1, p1, v1, s1), (l0, p0, v0, s0) = runs
+    assert torch.equal(l1, l0) and torch.equal(p1, p0) and torch.equal(v1, v0)
+    assert all(torch.equal(s1[k], s0[k]) for k in s1)
