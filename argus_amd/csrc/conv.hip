@@ -840,6 +840,9 @@ extern int g_halo_enable, g_wg_halo_enable, g_wg_halo_target_blocks, g_halo_min_
 // tools/convbench.py at B=64: 128 -> 1024 takes the fwd+dgrad conv time from 6.13 to 5.87 ms/step
 // (more resident workgroups hide the global-load latency better than the OCC=2 register ring).
 static int g_smallk_max = 1024;
+// argus_conv_tuning key 18: stem forward kernel, 2 (ring) or 4 (single buffer; convbench B=64:
+// 214 -> 179 us)
+static int g_stem_occ = 4;
 
 template <typename T>
 static int run_ig(const IgParams& p, hipStream_t st, int bm, int bn) {
@@ -855,7 +858,8 @@ static int run_ig(const IgParams& p, hipStream_t st, int bm, int bn) {
   }
   if (p.stem) {
     if (p.N != 64 || bm != 128) { set_error("igemm: stem expects 64 output channels"); return ARGUS_ERR_SHAPE; }
-    launch_ig<T, 128, 64, true, false, 2>(p, maxM, st);
+    if (g_stem_occ == 4) launch_ig<T, 128, 64, true, false, 4>(p, maxM, st);
+    else launch_ig<T, 128, 64, true, false, 2>(p, maxM, st);
   } else if (p.pro_scale) {
     if (smallk) dispatch_ig<T, true, 4>(p, maxM, bm, bn, st);
     else dispatch_ig<T, true, 2>(p, maxM, bm, bn, st);
@@ -887,6 +891,7 @@ static int* tuning_slot(int key) {
     case 15: return &g_wg_occ128;
     case 16: return &g_wg_glds_enable;
     case 17: return &g_wg_glds_target;
+    case 18: return &g_stem_occ;
     case 20: return &g_bwd_min_px;    // bn.hip: BN-backward pixels per block (min)
     case 21: return &g_bwd_max_rows;  //   ... and blocks per channel group (max)
     case 22: return &g_ew_target;     //   bn_apply / bwd_apply target blocks
