@@ -90,8 +90,9 @@ class ResNetEngine:
         self.debug: dict | None = None  # when a dict: clones of block outputs / block-input grads
         # Weight gradients run on a side stream, overlapped with the dgrad -> BN-backward chain of the
         # main stream (they only feed the gradient buffer). Events order them after their dy and
-        # before any main-stream overwrite of that dy buffer; backward() joins the side stream at every
-        # on_ready() and at its end. ARGUS_WGRAD_STREAM=0 keeps everything on the caller's stream.
+        # before any main-stream overwrite of that dy buffer; the trainer joins the side stream before
+        # each bucket all-reduce (on_ready's join) and backward() joins it at its end.
+        # ARGUS_WGRAD_STREAM=0 keeps everything on the caller's stream.
         self.wgrad_overlap = os.environ.get("ARGUS_WGRAD_STREAM", "1") != "0"
         self._side: torch.cuda.Stream | None = None
         self._pending: dict = {}  # dy data_ptr -> event of the last side-stream wgrad reading it
@@ -357,10 +358,13 @@ class ResNetEngine:
     def backward(self, dpred: torch.Tensor, P: dict, G: dict, on_ready=None) -> None:
         """Write every parameter gradient into G[name] (fp32; conv weights OHWI-contiguous).
 
-        ``on_ready(name)`` (optional) is called, in stream order, as soon as the gradients of parameter
-        ``name`` and of every parameter registered after it are complete: after the head
+        ``on_ready(name, join)`` (optional) is called, in stream order, as soon as the gradients of
+        parameter ``name`` and of every parameter registered after it have been issued: after the head
         ("resnet.fc.weight"), after each block ("<block>.conv1.weight"), after the stem
-        ("resnet.conv1.weight"). The trainer uses it to start bucketed all-reduces during backward."""
+        ("resnet.conv1.weight"). Weight gradients may still be running on the side stream then:
+        ``join()`` makes the current stream wait for them, and must be called before anything on the
+        current stream reads those gradients (the trainer calls it right before it issues a bucket's
+        all-reduce, so blocks that do not close a bucket keep their overlap)."""
         if not self.saved:
             raise RuntimeError("backward without a saved train-mode forward")
         L, dt, s = self.L, self.dt, stream()
@@ -390,8 +394,7 @@ class ResNetEngine:
         dh, dx = g[0], g[3]
         L.avgpool_bwd(dt, N, hf * wf, 2048, ptr(self.dfeat), ptr(dh), s)
         if on_ready is not None:
-            self._join()
-            on_ready("resnet.fc.weight")
+            on_ready("resnet.fc.weight", self._join)
 
         for idx in range(len(self.blocks) - 1, -1, -1):
             b, a = self.blocks[idx], self.act[idx]
@@ -446,8 +449,7 @@ class ResNetEngine:
                 self._dgrad(pf + ".conv1", dyw, dx, addend=dh, mask=a["bits"])
             dh, dx = dx, dh
             if on_ready is not None:
-                self._join()
-                on_ready(pf + ".conv1.weight")
+                on_ready(pf + ".conv1.weight", self._join)
             if self.debug is not None:
                 n_in = N * hi * wi * b.cin
                 self.debug["bwd." + pf] = dh[:n_in].view(N, hi, wi, b.cin).clone()
@@ -460,7 +462,7 @@ class ResNetEngine:
         self._wgrad("resnet.conv1", self.x0, None, dy0, G)
         self._join()
         if on_ready is not None:
-            on_ready("resnet.conv1.weight")
+            on_ready("resnet.conv1.weight", self._join)
 
     def _bn_bwd(self, P, G, name, px, ch, dz, mode, mask_src, y, dy_out, dm_out):
         L, dt, s = self.L, self.dt, stream()

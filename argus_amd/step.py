@@ -77,9 +77,13 @@ class GradBucketer:
         self.works = []
         self.pending_end = self.grad.numel()
 
-    def ready(self, name: str) -> None:
+    def ready(self, name: str, join=None) -> None:
+        """Gradients of ``name`` and everything after it are issued; ``join()`` (optional) makes the
+        current stream wait until they are written. Issues a bucket when the suffix is big enough."""
         start = self.offsets[name]
         if self.pending_end - start >= self.bucket or start == 0:
+            if join is not None:
+                join()
             self._issue(start)
 
     def _issue(self, start: int) -> None:
