@@ -128,10 +128,18 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knob (dev only): ARGUS_BENCH_REHEARSE=1 puts every rank on cuda:0 and exchanges over
+    # gloo, so the N>1 code path can be exercised on a one-GPU box (RCCL refuses two ranks per device)
+    rehearse = os.environ.get("ARGUS_BENCH_REHEARSE", "0") == "1"
+    if rehearse:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from argus_amd.models import NCameraCNN
     from argus_amd.profiling import KernelTimer
