@@ -533,7 +533,9 @@ static const char* wg_halo_name() {
 }
 
 int g_wg_halo_enable = 1;          // argus_conv_tuning key 11
-int g_wg_halo_target_blocks = 512;  // key 12
+// key 12: split target of the 3x3 halo wgrad. 512 -> 256 once it runs on the side stream beside the
+// main-stream chain (bench B=64: +0.6-0.9 %, two paired runs)
+int g_wg_halo_target_blocks = 256;
 int g_wg_halo_max_tiles = 4;        // key 14
 
 // Plan for a 3x3 / stride 1 / pad 1 bf16 weight gradient: false when not served. splits * K * 9C
