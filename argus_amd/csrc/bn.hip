@@ -20,7 +20,11 @@ namespace argus {
 // (= sum_t M2_t + sum_t n_t (mean_t - mean)^2, the exact parallel-variance merge; the within-tile
 // M2_t carry the large part, so fp64 leaves no cancellation problem).
 // Backward partials {sum dm, sum dm*xhat} are plain column sums.
-static int reduce_groups(int rows) { return rows < 64 ? 1 : (rows < 512 ? 8 : (rows < 4096 ? 32 : 64)); }
+int g_fin_div = 1;  // argus_conv_tuning key 24: divide the finalize group count (fewer, longer groups)
+static int reduce_groups(int rows) {
+  const int g = (rows < 64 ? 1 : (rows < 512 ? 8 : (rows < 4096 ? 32 : 64))) / (g_fin_div > 0 ? g_fin_div : 1);
+  return g < 1 ? 1 : g;
+}
 
 // ---- one-launch statistics merge + finalize ---------------------------------------------------------
 // Grid (C/64, G): block (x, g) merges partial rows [g*rpg, (g+1)*rpg) of its 64 channels into

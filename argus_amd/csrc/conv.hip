@@ -832,7 +832,7 @@ static void dispatch_ig(const IgParams& p, int maxM, int bm, int bn, hipStream_t
 }
 
 extern int g_glds_min_k, g_glds_min_grid, g_wg_glds_enable, g_wg_glds_target;  // conv_glds.hip
-extern int g_bwd_min_px, g_bwd_max_rows, g_ew_target, g_ew_min_ppt;  // bn.hip
+extern int g_bwd_min_px, g_bwd_max_rows, g_ew_target, g_ew_min_ppt, g_fin_div;  // bn.hip
 static int g_wg_occ128 = 2;  // argus_conv_tuning key 15: workgroups/CU of the 128x128 wgrad tile (1 = with ring)
 extern int g_halo_enable, g_wg_halo_enable, g_wg_halo_target_blocks, g_halo_min_grid,
     g_wg_halo_max_tiles;  // conv_halo.hip
@@ -896,6 +896,7 @@ static int* tuning_slot(int key) {
     case 21: return &g_bwd_max_rows;  //   ... and blocks per channel group (max)
     case 22: return &g_ew_target;     //   bn_apply / bwd_apply target blocks
     case 23: return &g_ew_min_ppt;    //   ... min pixels per thread
+    case 24: return &g_fin_div;       //   BN finalize group-count divisor
     default: return nullptr;
   }
 }
