@@ -80,6 +80,37 @@ def synthetic_targets(b: int, seed: int) -> torch.Tensor:
     return oracle_se3.random_targets(b, generator=g)
 
 
+def damp_residual(model, factor: float = 0.1):
+    """Scale every Bottleneck's last BN gamma (``*.bn3.weight``) by ``factor``, in place.
+
+    Why: at seeded init the train-mode gradient of this 16-block network is chaotic — the reference's
+    OWN fp32 gradient differs from its fp64 gradient by 2.2 % (global, any batch size tried), and its
+    bf16-autocast gradient is uncorrelated with fp64 (cosine 0.13). Damping the residual branches
+    gives a well-conditioned point of the SAME function (weights are data: a checkpoint could hold
+    them) where the reference's fp32 gradient is within 1e-3 of fp64, so gradient parity can be
+    pinned tightly there."""
+    with torch.no_grad():
+        for n, p in model.named_parameters():
+            if n.endswith("bn3.weight"):
+                p.mul_(factor)
+    return model
+
+
+DAMPED = {"batch": 8, "hw": [128, 128], "image_seed": 4321, "target_seed": 4000, "damp": 0.1}
+
+
+def flat_grads(model) -> dict:
+    return {n: p.grad.detach().double().clone() for n, p in model.named_parameters()}
+
+
+def grad_errors(g: dict, ref: dict):
+    """Global relative L2 error of the flat gradient vector and per-tensor relative L2 errors."""
+    fl = lambda d: torch.cat([v.flatten() for v in d.values()])  # noqa: E731
+    e = ((fl(g) - fl(ref)).norm() / fl(ref).norm()).item()
+    per = {n: ((g[n] - ref[n]).norm() / ref[n].norm().clamp_min(1e-30)).item() for n in ref}
+    return e, per
+
+
 def ref_train_step(model, x, T, lr=1e-4, max_norm=1.0):
     """argus/train.py:298-321 with amp off: fwd, fp32 loss, mean, zero_grad, backward, clip, Adam."""
     opt = torch.optim.Adam(model.parameters(), lr=lr)
@@ -182,6 +213,66 @@ def main() -> None:
     with open(OUT / "golden_b2.json", "w") as f:
         json.dump(golden, f, indent=1)
     print("wrote", OUT / "golden_b2.json", "pred_train", pred_train.tolist())
+    damped_golden(ref_models)
+
+
+def damped_golden(ref_models) -> None:
+    """golden_b8_damped.json: the reference's train step at a well-conditioned point (damp_residual),
+    B=8 at 128x128, with the reference's own fp32 / bf16-autocast gradient errors against fp64."""
+    cfg = DAMPED
+    B, (H, W) = cfg["batch"], cfg["hw"]
+    x = synthetic_images(B, H, W, seed=cfg["image_seed"])
+    T = synthetic_targets(B, seed=cfg["target_seed"])
+
+    def fresh(dt=torch.float32):
+        torch.manual_seed(42)
+        m = ref_models.NCameraCNN(ref_models.NCameraCNNConfig(n_cams=2))
+        return damp_residual(m, cfg["damp"]).to(dt).train()
+
+    grads, preds = {}, {}
+    for mode in ("fp64", "fp32", "bf16_autocast"):
+        dt = torch.float64 if mode == "fp64" else torch.float32
+        m = fresh(dt)
+        with torch.autocast("cpu", dtype=torch.bfloat16, enabled=mode == "bf16_autocast"):
+            pred = m(x.to(dt))
+        pred = pred.to(dt)
+        oracle_se3.geometric_loss(pred, T.to(dt)).mean().backward()
+        grads[mode], preds[mode] = flat_grads(m), pred.detach()
+    e32, per32 = grad_errors(grads["fp32"], grads["fp64"])
+    e16, per16 = grad_errors(grads["bf16_autocast"], grads["fp64"])
+    norm = lambda d: torch.cat([v.flatten() for v in d.values()]).norm().item()  # noqa: E731
+
+    m = fresh()
+    p0, l0, gnorm = ref_train_step(m, x, T)
+    with torch.no_grad():
+        pred_after = m(x)
+    sd_after = m.state_dict()
+    out = {
+        "generator": "tests/golden/make_golden.py::damped_golden",
+        "pinned_against": "reference argus/models.py executed with oracle.resnet as torchvision.models",
+        "config": cfg,
+        "images_sum": float(x.double().sum()),
+        "targets": T.tolist(),
+        "pred_train_fp32": preds["fp32"].tolist(),
+        "pred_train_fp64": preds["fp64"].tolist(),
+        "grad_norm_fp64": norm(grads["fp64"]),
+        "grad_norm_fp32": norm(grads["fp32"]),
+        "ref_fp32_vs_fp64": {"global": e32, "per_tensor": per32},
+        "ref_bf16_autocast_vs_fp64": {"global": e16, "per_tensor": per16},
+        "tensor_grad_norms_fp64": {n: v.norm().item() for n, v in grads["fp64"].items()},
+        "step": {
+            "loss": l0.tolist(),
+            "grad_norm": float(gnorm),
+            "pred_after_step_train": pred_after.tolist(),
+            "bn_running_sums": {k: [float(v.double().sum()), float(v.double().abs().sum())]
+                                for k, v in sd_after.items() if k.endswith(("running_mean", "running_var"))},
+            "param_sums": {k: [float(v.double().sum()), float(v.double().abs().sum())]
+                           for k, v in sd_after.items() if k.endswith(("weight", "bias"))},
+        },
+    }
+    with open(OUT / "golden_b8_damped.json", "w") as f:
+        json.dump(out, f, indent=1)
+    print("wrote", OUT / "golden_b8_damped.json", "fp32 vs fp64", e32, "bf16 autocast vs fp64", e16)
 
 
 if __name__ == "__main__":

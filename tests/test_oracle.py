@@ -72,3 +72,29 @@ def test_pose_order_kats(golden):
     assert torch.allclose(xyzwxyz_to_xyzxyzw_SE3(a[0]), b[0])
     r = torch.randn(2, 7)
     assert torch.allclose(xyzxyzw_to_xyzwxyz_SE3(xyzwxyz_to_xyzxyzw_SE3(r)), r)
+
+
+def test_damped_golden_pins_oracle():
+    """golden_b8_damped.json (reference models.py at damp_residual(0.1), B=8 at 128x128): the oracle
+    reproduces the reference's fp32 and fp64 predictions and its fp32-vs-fp64 gradient error."""
+    import json
+
+    import tests.golden.make_golden as mg
+
+    with open(mg.OUT / "golden_b8_damped.json") as f:
+        g = json.load(f)
+    c = g["config"]
+    x = mg.synthetic_images(c["batch"], *c["hw"], seed=c["image_seed"])
+    T = mg.synthetic_targets(c["batch"], seed=c["target_seed"])
+    assert torch.allclose(T, torch.tensor(g["targets"]))
+    grads = {}
+    for dt in (torch.float32, torch.float64):
+        m = mg.damp_residual(build_reference_model(42), c["damp"]).to(dt).train()
+        pred = m(x.to(dt))
+        want = torch.tensor(g["pred_train_fp32" if dt == torch.float32 else "pred_train_fp64"], dtype=dt)
+        assert (pred.detach() - want).abs().max().item() < (1e-6 if dt == torch.float32 else 1e-12)
+        se3.geometric_loss(pred, T.to(dt)).mean().backward()
+        grads[dt] = mg.flat_grads(m)
+    e, _ = mg.grad_errors(grads[torch.float32], grads[torch.float64])
+    assert abs(e - g["ref_fp32_vs_fp64"]["global"]) < 0.2 * g["ref_fp32_vs_fp64"]["global"]
+    assert e < 2e-3  # the point is well conditioned (vs 2.2e-2 at seeded init)
