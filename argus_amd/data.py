@@ -10,9 +10,10 @@ bytes like b"img/img3") and ``D/<stem>_a.png``, ``D/<stem>_b.png`` (uint8 RGB) p
 integer offsets is exact slicing). The HDF5 file is read by ``argus_amd.h5lite`` (h5py is not
 installed here).
 
-Deliberate differences: the kornia photometric augmentations and the random
-"spaghetti" arcs (data.py:41-103,213-215) are CPU-worker data augmentation, out of scope for the
-hot path — an ``AugmentationConfig`` is accepted for signature compatibility but not applied, and
+Augmentation: the "spaghetti" occluder arcs (data.py:212-215, utils.py:252-275) are drawn exactly
+as the reference does (same PIL calls and np.random draws; train and val). The kornia photometric
+augmentations (data.py:41-103: Planckian jitter, ColorJiggle, Gaussian / motion blur, plasma
+shadow) are not applied: a warning says so once whenever an ``AugmentationConfig`` enables them.
 ``cfg_aug=None`` works (the reference crashes on it, data.py:213). ``CameraCubePoseDatasetConfig``
 resolves ROOT-relative paths without tripping its own ``frozen=True`` (data.py:126-130).
 ``uint8=True`` keeps images as uint8 (4x less host->device traffic; the engine converts on device).
@@ -20,6 +21,7 @@ resolves ROOT-relative paths without tripping its own ``frozen=True`` (data.py:1
 from __future__ import annotations
 
 import os
+import warnings
 from dataclasses import dataclass
 from pathlib import Path
 from typing import Optional, Union
@@ -31,12 +33,18 @@ from torch.utils.data import Dataset
 
 from argus_amd import ROOT
 from argus_amd import h5lite
-from argus_amd.utils import xyzwxyz_to_xyzxyzw_SE3
+from argus_amd.utils import draw_spaghetti, xyzwxyz_to_xyzxyzw_SE3
+
+# the kornia photometric augmentations of argus/data.py:41-103 (not applied here)
+PHOTOMETRIC_FLAGS = ("random_erasing", "planckian_jitter", "color_jiggle", "blur", "motion_blur", "plasma_shadow",
+                     "salt_and_pepper")
+_warned = False
 
 
 @dataclass(frozen=True)
 class AugmentationConfig:
-    """Same fields as argus/data.py:18-39 (accepted; augmentations are out of scope, not applied)."""
+    """Same fields as argus/data.py:18-39. ``num_spaghetti`` is applied; the photometric flags are
+    accepted but not applied (warned once)."""
 
     brightness: Union[float, tuple] = (0.8, 1.0)
     contrast: Union[float, tuple] = (0.5, 1.2)
@@ -97,7 +105,14 @@ class CameraCubePoseDataset(Dataset):
             self.q_leap = torch.from_numpy(np.asarray(ds["q_leap"][()]))
             self.img_stems = [s.decode("utf-8") for s in ds["img_stems"][()]]
         self.cfg_aug = cfg_aug
-        self.augmentation = None  # kornia augmentations: out of scope (see module docstring)
+        self.augmentation = None  # kornia photometric augmentations: not applied (module docstring)
+        enabled = [k for k in PHOTOMETRIC_FLAGS if cfg_aug is not None and getattr(cfg_aug, k)]
+        global _warned
+        if enabled and train and not _warned:
+            _warned = True
+            warnings.warn(f"argus_amd: kornia photometric augmentations {enabled} are not applied (the "
+                          "spaghetti occluders are); pass an AugmentationConfig with them off to silence this",
+                          stacklevel=2)
         self.dataset_path = dataset_path
         self.center_crop = cfg_dataset.center_crop
         self.uint8 = uint8
@@ -109,7 +124,10 @@ class CameraCubePoseDataset(Dataset):
     def __getitem__(self, idx: int) -> dict:
         stem = self.img_stems[idx]
         suffixes = "abcdefghijklmnopqrstuvwxyz"[: self.n_cams]
-        imgs = [np.asarray(Image.open(f"{self.dataset_path}/{stem}_{s}.png").convert("RGB")) for s in suffixes]
+        pil = [Image.open(f"{self.dataset_path}/{stem}_{s}.png").convert("RGB") for s in suffixes]
+        if self.cfg_aug is not None and self.cfg_aug.num_spaghetti > 0:  # data.py:212-215, train and val
+            pil = [draw_spaghetti(im, self.cfg_aug.num_spaghetti) for im in pil]
+        imgs = [np.asarray(im) for im in pil]
         arr = np.concatenate(imgs, axis=-1).transpose(2, 0, 1)  # (3*n_cams, H, W) uint8
         if self.center_crop and tuple(arr.shape[-2:]) != tuple(self.center_crop):
             ys, xs = center_crop_slices(arr.shape[-2:], self.center_crop)

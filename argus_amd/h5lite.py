@@ -4,9 +4,11 @@ Covers what h5py writes for argus (argus/data_generation.py:247,313-314; tests/c
 superblock v0/v1 (h5py's default "earliest" libver) and v2/v3; object headers v1 and v2 (with
 continuation blocks); groups as old-style symbol tables (v1 B-tree + local heap) or link messages;
 datasets with contiguous or compact layout (data layout message v1-v4); datatypes fixed-point,
-IEEE float and fixed-length string; simple dataspaces; attributes (v1-v3). Chunked/compressed
-datasets, dense (fractal-heap) link storage, variable-length strings and references are rejected
-with a clear error. Pure Python + numpy, read via mmap.
+IEEE float, fixed-length string and variable-length string (the form h5py>=3 gives a list of str,
+as argus/data_generation.py:256,264 writes ``img_stems``; elements resolved through the global heap
+collections, returned as bytes like h5py's ``[()]``); simple dataspaces; attributes (v1-v3).
+Chunked/compressed datasets, dense (fractal-heap) link storage, variable-length sequences and
+references are rejected with a clear error. Pure Python + numpy, read via mmap.
 """
 from __future__ import annotations
 
@@ -17,6 +19,15 @@ from typing import Any
 import numpy as np
 
 _SIG = b"\x89HDF\r\n\x1a\n"
+
+
+class VlenStr:
+    """Variable-length string datatype (HDF5 class 9, type 1): each stored element is a 4-byte byte
+    count + a global heap ID (collection address, 4-byte object index)."""
+
+    def __init__(self, so: int):
+        self.itemsize = 4 + so + 4
+        self.record = np.dtype([("len", "<u4"), ("addr", f"<u{so}"), ("idx", "<u4")])
 
 
 class H5Error(ValueError):
@@ -141,7 +152,36 @@ class _Reader:
             return np.dtype(f"{be}f{size}")
         if cls == 3:
             return np.dtype(f"S{size}")
+        if cls == 9:
+            if bits & 0x0F != 1:
+                raise H5Error("variable-length sequences are not supported (only variable-length strings)")
+            if size != 4 + self.so + 4:
+                raise H5Error(f"unexpected variable-length string element size {size}")
+            return VlenStr(self.so)
         raise H5Error(f"unsupported HDF5 datatype class {cls}")
+
+    def global_heap_object(self, addr: int, idx: int) -> bytes:
+        """Object ``idx`` of the global heap collection at ``addr`` (collections are cached)."""
+        cache = self.__dict__.setdefault("_gcol", {})
+        objs = cache.get(addr)
+        if objs is None:
+            b = self.buf
+            if b[addr:addr + 4] != b"GCOL":
+                raise H5Error(f"bad global heap collection at {addr}")
+            end = addr + self.length(addr + 8)
+            p = addr + 8 + self.sl
+            objs = {}
+            while p + 8 + self.sl <= end:
+                oid = self.u(p, 2)
+                n = self.length(p + 8)
+                if oid == 0:  # free space: the rest of the collection
+                    break
+                objs[oid] = bytes(b[p + 8 + self.sl:p + 8 + self.sl + n])
+                p += 8 + self.sl + ((n + 7) & ~7)
+            cache[addr] = objs
+        if idx not in objs:
+            raise H5Error(f"global heap object {idx} missing in collection {addr}")
+        return objs[idx]
 
     def layout(self, p: int, shape: tuple, dt: np.dtype):
         ver = self.buf[p]
@@ -180,8 +220,19 @@ class _Reader:
         shape = self.dataspace(q)
         q += pad(slen)
         n = int(np.prod(shape)) if shape else 1
-        arr = np.frombuffer(self.buf, dtype=dt, count=n, offset=q).copy()
+        arr = self.elements(dt, n, q)
         return name, (arr.reshape(shape) if shape else arr[0])
+
+    def elements(self, dt, n: int, offset: int) -> np.ndarray:
+        """``n`` stored elements of type ``dt`` at ``offset`` (variable-length strings resolved to
+        bytes objects, as h5py returns them)."""
+        if isinstance(dt, VlenStr):
+            rec = np.frombuffer(self.buf, dtype=dt.record, count=n, offset=offset)
+            out = np.empty(n, dtype=object)
+            for i, (ln, addr, idx) in enumerate(rec):
+                out[i] = self.global_heap_object(int(addr), int(idx))[:int(ln)] if addr else b""
+            return out
+        return np.frombuffer(self.buf, dtype=dt, count=n, offset=offset).copy()
 
     # ---------------------------------------------------------------- groups
     def children(self, addr: int) -> dict:
@@ -265,9 +316,9 @@ class Dataset:
         kind, off, size = self._layout
         n = int(np.prod(self.shape)) if self.shape else 1
         if off == (1 << (8 * self._r.so)) - 1:  # never written -> fill value 0
-            arr = np.zeros(n, dtype=self.dtype)
+            arr = np.full(n, b"", dtype=object) if isinstance(self.dtype, VlenStr) else np.zeros(n, dtype=self.dtype)
         else:
-            arr = np.frombuffer(self._r.buf, dtype=self.dtype, count=n, offset=off).copy()
+            arr = self._r.elements(self.dtype, n, off)
         arr = arr.reshape(self.shape) if self.shape else arr[0]
         return arr if key == () or key is Ellipsis else arr[key]
 

@@ -105,6 +105,24 @@ class _NetFn(torch.autograd.Function):
         return (None, None, *grads)
 
 
+def strip_checkpoint_prefixes(state_dict):
+    """Remove leading ``module.`` / ``_orig_mod.`` (in any nesting) from every key."""
+    out = type(state_dict)() if isinstance(state_dict, dict) else {}
+    for k, v in state_dict.items():
+        while True:
+            for p in ("module.", "_orig_mod."):
+                if k.startswith(p):
+                    k = k[len(p):]
+                    break
+            else:
+                break
+        out[k] = v
+    if hasattr(state_dict, "_metadata"):
+        out._metadata = {strip_checkpoint_prefixes({m: None}).popitem()[0] if m else m: v
+                         for m, v in state_dict._metadata.items()}
+    return out
+
+
 class NCameraCNN(nn.Module):
     """A CNN which assumes N cameras are available in the scene (argus/models.py:26-90)."""
 
@@ -142,11 +160,24 @@ class NCameraCNN(nn.Module):
     def _maps(self):
         P = dict(self.named_parameters())
         Bf = dict(self.named_buffers())
+        cma = [(name, m) for name, m in self.named_modules() if isinstance(m, nn.BatchNorm2d) and m.momentum is None]
+        # momentum=None is torch's cumulative moving average: factor 1 / num_batches_tracked after the
+        # increment. The counters live on the device: one host read per forward, only in that mode.
+        counts = {}
+        if cma and self.training:
+            nbt = torch.stack([m.num_batches_tracked for _, m in cma]).cpu().tolist()
+            counts = {name: n for (name, _), n in zip(cma, nbt)}
         for name, m in self.named_modules():
             if isinstance(m, nn.BatchNorm2d):
                 Bf[name + ".eps"] = m.eps
-                Bf[name + ".momentum"] = m.momentum if m.momentum is not None else 0.1
+                Bf[name + ".momentum"] = m.momentum if m.momentum is not None else 1.0 / (counts.get(name, 0) + 1)
         return P, Bf
+
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        """``nn.Module.load_state_dict`` that also takes the reference's wrapped checkpoints: keys
+        prefixed ``module.`` (a DDP model's state_dict, argus/train.py:199,358) or ``_orig_mod.``
+        (a ``torch.compile``d model, train.py:61) are stripped first."""
+        return super().load_state_dict(strip_checkpoint_prefixes(state_dict), strict=strict, assign=assign)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         """(B, 3*n_cams, H, W) fp32 images in [0, 1] -> (B, 6) se(3) poses.

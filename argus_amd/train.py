@@ -15,9 +15,15 @@ reference's fp16 autocast; no GradScaler is needed in bf16). ``--multigpu``: one
 either launched by torch.distributed.run (env RANK/WORLD_SIZE) or spawned here like the reference's
 mp.spawn (train.py:376). Rendezvous on 127.0.0.1.
 
+Multi-GPU buffers: before every validation pass the BN running statistics (and counters) of rank 0
+are broadcast to every rank (``sync_bn_buffers``) — what DDP's ``broadcast_buffers=True`` makes the
+reference's ranks validate with (train.py:199; its first no-grad forward after training syncs
+buffers from rank 0). Rank 0's own buffers, the checkpointed ones, are never changed by it.
+
 Documented deviations: validation loss is averaged over ALL ranks (the reference's is rank-local,
 train.py:342-348, so its per-rank LR schedules can diverge); DDP checkpoints' ``module.`` key prefix
-is not produced (the keys are the plain model keys); ``TrainConfig`` does not require a GPU at
+is not produced (the keys are the plain model keys; ``NCameraCNN.load_state_dict`` accepts
+``module.`` / ``_orig_mod.`` prefixed checkpoints); ``TrainConfig`` does not require a GPU at
 construction time (the reference asserts >= 1 GPU, train.py:99-102).
 """
 from __future__ import annotations
@@ -43,7 +49,8 @@ from argus_amd.data import AugmentationConfig, CameraCubePoseDataset, CameraCube
 from argus_amd.losses import geometric_loss_fn
 from argus_amd.models import NCameraCNN, NCameraCNNConfig
 
-__all__ = ["TrainConfig", "geometric_loss_fn", "initialize_training", "train", "PlateauScheduler", "main"]
+__all__ = ["TrainConfig", "geometric_loss_fn", "initialize_training", "train", "PlateauScheduler", "main",
+           "sync_bn_buffers"]
 
 
 def _gpu_count() -> int:
@@ -119,6 +126,25 @@ def rank_print(msg: str, rank: int = 0) -> None:
         print(msg, flush=True)
 
 
+def sync_bn_buffers(model: torch.nn.Module, src: int = 0, group=None) -> None:
+    """Broadcast every buffer (BN running_mean / running_var / num_batches_tracked) from rank ``src``
+    to all ranks (DDP broadcast_buffers semantics, argus/train.py:199). No-op when not distributed."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return
+    for b in model.buffers():
+        dist.broadcast(b.data, src=src, group=group)
+
+
+def _device_for(cfg: TrainConfig, rank: int) -> torch.device:
+    """cuda:LOCAL_RANK under torch.distributed.run (multi-node safe), else the reference's
+    cuda:rank for mp.spawn (train.py:131); ``cfg.device`` single-process."""
+    if not cfg.multigpu:
+        return torch.device(cfg.device)
+    n = max(1, torch.cuda.device_count())
+    local = int(os.environ.get("LOCAL_RANK", rank % n))
+    return torch.device("cuda", local)
+
+
 def initialize_training(cfg: TrainConfig, rank: int = 0, world: int = 1):
     """Seeds, device, datasets/loaders, model, fused trainer, LR schedule (train.py:122-255)."""
     from argus_amd.step import FusedTrainer
@@ -127,7 +153,7 @@ def initialize_training(cfg: TrainConfig, rank: int = 0, world: int = 1):
     np.random.seed(cfg.random_seed)
     if torch.cuda.is_available():
         torch.cuda.manual_seed_all(cfg.random_seed)
-    device = torch.device("cuda", rank % max(1, torch.cuda.device_count())) if cfg.multigpu else torch.device(cfg.device)
+    device = _device_for(cfg, rank)
     if device.type != "cuda":
         raise RuntimeError("argus_amd trains on the MI355X HIP path only (device must be cuda)")
     if device.index is None:
@@ -197,6 +223,7 @@ def train(cfg: TrainConfig, rank: int = 0) -> str:
         if epoch % cfg.print_epochs == 0 and epoch_losses:
             rank_print(f"    Avg. Loss in Epoch: {torch.mean(torch.cat(epoch_losses)).item()}", rank)
         if epoch % cfg.val_epochs == 0:
+            sync_bn_buffers(model)  # every rank validates with rank 0's running statistics
             model.eval()
             tot = torch.zeros(2, dtype=torch.float64, device=device)
             with torch.no_grad():

@@ -23,7 +23,11 @@ Also reported:
   cpu_baseline - the CPU oracle (the reference's torch.nn ops on CPU, fp32, B=8) train step timed on
                  this host (rank 0, N=1), a bounded sample of ~15 s.
   val_loss     - mean SE(3) loss (argus/train.py:342) of the trained model in eval mode on a
-                 synthetic validation batch, and its sqrt (geodesic error).
+                 synthetic validation batch; val_se3_log_rms = sqrt(val_loss) (the RMS norm of the
+                 full se(3) log, translation included); val_rot_err_deg = mean rotation-angle
+                 component |phi| of the geodesic.
+Batch: 64 samples per rank on one GPU (configs[1]); 256 per rank when launched with N > 1 ranks
+(configs[2], cube_unity_data_medium-shaped); --batch overrides.
 """
 from __future__ import annotations
 
@@ -116,7 +120,9 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=64, help="samples (camera pairs) per rank")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="samples (camera pairs) per rank (default 64 on one GPU = configs[1], 256 per rank "
+                         "for N > 1 = configs[2])")
     ap.add_argument("--hw", type=int, nargs=2, default=(256, 256))
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -151,7 +157,7 @@ def main() -> None:
     for kv in args.tune:
         k, v = kv.split("=")
         assert lib().dll.argus_conv_tuning(int(k), int(v)) == 0, kv
-    B, (H, W) = args.batch, args.hw
+    B, (H, W) = (args.batch or (64 if world == 1 else 256)), args.hw
     torch.manual_seed(42)
     model = NCameraCNN(compute_dtype=args.dtype).to(dev)
     model.train()
@@ -209,12 +215,17 @@ def main() -> None:
     # validation SE(3) error (eval mode, running BN statistics), synthetic held-out batch
     model.eval()
     vimg, vtgt = synthetic_batch(B, H, W, 5000 + rank, dev)
+    from argus_amd.utils import rotation_angle_error
+
     with torch.no_grad():
-        vloss = geometric_loss_fn(model(vimg), vtgt)
-    vsum = torch.stack([vloss.sum(), torch.tensor(float(vloss.numel()), device=dev)])
+        vpred = model(vimg)
+        vloss = geometric_loss_fn(vpred, vtgt)
+        vrot = rotation_angle_error(vpred, vtgt)
+    vsum = torch.stack([vloss.sum(), vrot.sum(), torch.tensor(float(vloss.numel()), device=dev)])
     if world > 1:
         dist.all_reduce(vsum)
-    val_loss = (vsum[0] / vsum[1]).item()
+    val_loss = (vsum[0] / vsum[2]).item()
+    val_rot = (vsum[1] / vsum[2]).item()
 
     peak_flops = BF16_DENSE_PEAK_TFLOPS if args.dtype == "bf16" else F32_MFMA_PEAK_TFLOPS
     tflops = ks["flops_per_launch"] / (ks["avg_us"] * 1e-6) / 1e12
@@ -268,7 +279,8 @@ def main() -> None:
         "step_conv_frac_of_bf16_peak": round(step_flops / (ms * 1e-3) / 1e12 / BF16_DENSE_PEAK_TFLOPS, 4),
         "train_loss": round(train_loss, 6),
         "val_loss": round(val_loss, 6),
-        "val_geodesic_err": round(math.sqrt(max(val_loss, 0.0)), 6),
+        "val_se3_log_rms": round(math.sqrt(max(val_loss, 0.0)), 6),
+        "val_rot_err_deg": round(math.degrees(val_rot), 4),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(8, H, W, args.cpu_seconds)

@@ -27,10 +27,13 @@ def main():
     data = {"train": poses(rng, 10), "test": poses(rng, 5)}
     qleap = {"train": rng.normal(size=(10, 23)), "test": rng.normal(size=(5, 23))}
     stems = {"train": [f"img/img{i}" for i in range(10)], "test": [f"img/img{i}" for i in range(10, 15)]}
-    for libver in ("earliest", "latest"):
-        d = OUT / f"ds_{libver}"
+    # "vlen_*": img_stems written exactly as argus/data_generation.py:256,264 does (a plain list of
+    # str, which h5py>=3 stores as variable-length UTF-8 strings in the global heap)
+    for name, libver in (("earliest", "earliest"), ("latest", "latest"), ("vlen_earliest", "earliest"),
+                         ("vlen_latest", "latest")):
+        d = OUT / f"ds_{name}"
         d.mkdir(parents=True, exist_ok=True)
-        with h5py.File(d / f"ds_{libver}.hdf5", "w", libver=libver) as f:
+        with h5py.File(d / f"ds_{name}.hdf5", "w", libver=libver) as f:
             f.attrs["n_cams"] = 2
             f.attrs["W"] = 256
             f.attrs["H"] = 256
@@ -38,7 +41,11 @@ def main():
                 grp = f.create_group(g)
                 grp.create_dataset("cube_poses", data=data[g])
                 grp.create_dataset("q_leap", data=qleap[g])
-                grp.create_dataset("img_stems", data=np.array([s.encode("utf-8") for s in stems[g]]))
+                if name.startswith("vlen"):
+                    grp.create_dataset("img_stems", data=list(stems[g]))
+                    assert h5py.check_string_dtype(grp["img_stems"].dtype).length is None
+                else:
+                    grp.create_dataset("img_stems", data=np.array([s.encode("utf-8") for s in stems[g]]))
     with open(OUT / "fixtures.json", "w") as f:
         json.dump({"cube_poses": {k: v.tolist() for k, v in data.items()},
                    "q_leap": {k: v.tolist() for k, v in qleap.items()}, "img_stems": stems,

@@ -12,8 +12,10 @@ from argus_amd import h5lite
 GOLD = Path(__file__).resolve().parent / "golden" / "h5"
 
 
-@pytest.mark.parametrize("libver", ["earliest", "latest"])
+@pytest.mark.parametrize("libver", ["earliest", "latest", "vlen_earliest", "vlen_latest"])
 def test_h5lite_reads_h5py_files(libver):
+    """vlen_*: img_stems written as a plain list of str (argus/data_generation.py:256,264), which
+    h5py>=3 stores as variable-length strings (global heap); read back as bytes like h5py's [()]."""
     fx = json.loads((GOLD / "fixtures.json").read_text())
     with h5lite.File(str(GOLD / f"ds_{libver}" / f"ds_{libver}.hdf5")) as f:
         assert {k: int(v) for k, v in f.attrs.items()} == fx["attrs"]
@@ -49,6 +51,15 @@ def test_dataset_items(tmp_path):
 
     a = np.array(Image.open(d / "img" / "img3_a.png"))
     assert torch.equal(ex["images"][:3], torch.from_numpy(a).permute(2, 0, 1).float() / 255.0)
+
+
+def test_dataset_reads_datagen_vlen_stems(tmp_path):
+    from argus_amd.data import CameraCubePoseDataset, CameraCubePoseDatasetConfig
+
+    d = _make_dataset(tmp_path, "vlen_latest")
+    ds = CameraCubePoseDataset(CameraCubePoseDatasetConfig(str(d)), train=False)
+    assert ds.img_stems == [f"img/img{i}" for i in range(10, 15)]
+    assert ds[4]["images"].shape == (6, 256, 256)
 
 
 def test_center_crop(tmp_path):

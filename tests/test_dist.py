@@ -48,3 +48,40 @@ def test_bucketed_allreduce_world2():
         p.join(timeout=60)
     assert all(ok for _, ok, _ in res), res
     assert all(nw >= 3 for _, _, nw in res), res  # really bucketed, not one monolithic all-reduce
+
+
+def _bn_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from argus_amd.models import NCameraCNN
+    from argus_amd.train import sync_bn_buffers
+
+    torch.manual_seed(0)
+    m = NCameraCNN()
+    with torch.no_grad():  # per-rank running statistics, as after rank-local train-mode steps
+        for b in m.buffers():
+            b.add_(rank + 1 if b.dtype != torch.int64 else 7 * (rank + 1))
+    mine = {k: v.clone() for k, v in m.state_dict().items() if "running" in k or "num_batches" in k}
+    sync_bn_buffers(m)
+    synced = {k: v for k, v in m.state_dict().items() if k in mine}
+    rank0 = {k: v - 0 for k, v in mine.items()} if rank == 0 else None
+    q.put((rank, {k: v.double().sum().item() for k, v in synced.items()},
+           None if rank0 is None else {k: v.double().sum().item() for k, v in rank0.items()}))
+    dist.destroy_process_group()
+
+
+def test_bn_buffers_broadcast_from_rank0_before_validation():
+    """Every rank validates with rank 0's BN running statistics (DDP broadcast_buffers semantics,
+    argus/train.py:199); rank 0's own buffers are unchanged."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bn_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (s, r0)) for r, s, r0 in (q.get(timeout=120) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+    rank0_before = res[0][1]
+    assert res[0][0] == rank0_before and res[1][0] == rank0_before

@@ -138,7 +138,7 @@ def test_damped_fp32_fused_step_tight(cuda):
         assert abs(v.sum().item() - s) <= tol and abs(v.abs().sum().item() - a) <= tol, k
     for k, (s, a) in gs["bn_running_sums"].items():
         v = sd[k].double().cpu()
-        assert abs(v.sum().item() - s) <= 1e-5 * a + 1e-6, k
+        assert abs(v.sum().item() - s) <= 1e-4 * a + 1e-6, k  # fp32 batch statistics of deep layers
 
 
 # ------------------------------------------------------------------------------------------------ bf16

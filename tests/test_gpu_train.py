@@ -161,3 +161,70 @@ def test_side_stream_overlap_is_bit_identical(cuda):
     (l1, p1, v1, s1), (l0, p0, v0, s0) = runs
     assert torch.equal(l1, l0) and torch.equal(p1, p0) and torch.equal(v1, v0)
     assert all(torch.equal(s1[k], s0[k]) for k in s1)
+
+
+def test_rotation_angle_error_matches_oracle(cuda):
+    """|phi| of Log(Exp(pred) @ T^-1) (SURVEY §8d rotation component of the geodesic) vs the oracle."""
+    from argus_amd.utils import rotation_angle_error
+    from oracle import se3
+
+    g = torch.Generator().manual_seed(9)
+    pred = torch.randn(64, 6, generator=g, dtype=torch.float64)
+    pred[:, 3:] *= 1.3  # angles up to and beyond pi
+    T = se3.random_targets(64, generator=g)
+    want = se3.se3_log(se3.se3_mul(se3.se3_exp(pred), se3.se3_inv(T.double())))[:, 3:].norm(dim=-1)
+    got = rotation_angle_error(pred.float().to(cuda), T.to(cuda)).cpu().double()
+    assert (got - want).abs().max().item() < 1e-5, (got - want).abs().max()
+
+
+def test_validate_per_example_with_reference_checkpoint(cuda, dummy_data_path, tmp_path):
+    """argus/validate.py:100-128 counterpart: a DDP-prefixed (``module.``) reference-format .pth loads,
+    and the per-example eval losses equal the model's batched eval losses."""
+    from argus_amd.data import AugmentationConfig, CameraCubePoseDataset, CameraCubePoseDatasetConfig
+    from argus_amd.losses import geometric_loss_fn
+    from argus_amd.models import NCameraCNN
+    from argus_amd.validate import ValConfig, validate
+
+    torch.manual_seed(4)
+    src = NCameraCNN()
+    path = tmp_path / "ddp.pth"
+    torch.save({"module." + k: v for k, v in src.state_dict().items()}, path)
+    noaug = AugmentationConfig(num_spaghetti=0)
+    cfg = ValConfig(model_path=str(path), dataset_config=CameraCubePoseDatasetConfig(dummy_data_path),
+                    aug_config=noaug)
+    losses = validate(cfg)
+    ds = CameraCubePoseDataset(CameraCubePoseDatasetConfig(dummy_data_path), cfg_aug=noaug, train=False)
+    assert len(losses) == len(ds) == 5
+    m = src.to(cuda).eval()
+    x = torch.stack([ds[i]["images"] for i in range(5)]).to(cuda)
+    T = torch.stack([ds[i]["cube_pose"] for i in range(5)]).to(cuda)
+    with torch.no_grad():
+        want = geometric_loss_fn(m(x), T).cpu()
+    assert torch.allclose(torch.tensor(losses), want, atol=1e-5), (losses, want)
+
+
+def test_bn_momentum_none_running_stats(cuda):
+    """BatchNorm momentum=None (cumulative moving average) gives torch's running statistics."""
+    from argus_amd.models import NCameraCNN
+    from oracle.ncamera import build_reference_model
+
+    torch.manual_seed(42)
+    m = NCameraCNN().to(cuda).train()
+    ref = build_reference_model(42).train()
+    for mod in (m, ref):
+        for x in mod.modules():
+            if isinstance(x, torch.nn.BatchNorm2d):
+                x.momentum = None
+    g = torch.Generator().manual_seed(2)
+    with torch.no_grad():
+        for _ in range(3):
+            x = torch.rand(2, 6, 64, 64, generator=g)
+            m(x.to(cuda))
+            ref(x)
+    sd, sr = m.state_dict(), ref.state_dict()
+    for k in sd:
+        if "running" in k:
+            d = (sd[k].cpu() - sr[k]).abs().max() / sr[k].abs().max()
+            assert d < 1e-4, (k, d)
+        if "num_batches" in k:
+            assert int(sd[k]) == 3

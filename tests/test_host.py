@@ -64,3 +64,73 @@ def test_cli_flag_names(tmp_path):
     assert cfg.batch_size == 10 and cfg.learning_rate == 1e-3 and cfg.amp and not cfg.wandb_log
     assert cfg.dataset_config.center_crop == (128, 128) and cfg.model_config.n_cams == 2
     assert cfg.max_grad_norm == 1.0 and cfg.random_seed == 42 and not cfg.multigpu
+
+
+def test_load_state_dict_strips_ddp_and_compile_prefixes(tmp_path):
+    """Reference checkpoints saved from a DDP model (``module.``, argus/train.py:199,358) or a compiled
+    one (``_orig_mod.``, train.py:61) load into NCameraCNN, also through a .pth file."""
+    from argus_amd.models import strip_checkpoint_prefixes
+
+    torch.manual_seed(1)
+    src = NCameraCNN()
+    sd = src.state_dict()
+    for prefix in ("module.", "_orig_mod.", "module._orig_mod.", "_orig_mod.module."):
+        path = tmp_path / "ckpt.pth"
+        torch.save({prefix + k: v for k, v in sd.items()}, path)
+        dst = NCameraCNN()
+        res = dst.load_state_dict(torch.load(path, weights_only=True))
+        assert not res.missing_keys and not res.unexpected_keys
+        assert all(torch.equal(dst.state_dict()[k], sd[k]) for k in sd), prefix
+    assert list(strip_checkpoint_prefixes({"module.resnet.fc.bias": 1})) == ["resnet.fc.bias"]
+
+
+def test_bn_momentum_none_is_cumulative_average():
+    """momentum=None -> torch's cumulative moving average factor 1/num_batches_tracked (after the
+    increment), handed to the kernels per layer."""
+    m = NCameraCNN()
+    m.resnet.bn1.momentum = None
+    m.resnet.bn1.num_batches_tracked.fill_(3)
+    m.train()
+    _, Bf = m._maps()
+    assert Bf["resnet.bn1.momentum"] == 0.25
+    assert Bf["resnet.layer1.0.bn1.momentum"] == 0.1
+
+
+def test_spaghetti_draws_reference_arcs():
+    """draw_spaghetti (argus/utils.py:252-275): black arcs only, deterministic under the np seed, and
+    it consumes exactly six draws per arc (so a seeded worker stays in step with the reference)."""
+    import numpy as np
+    from PIL import Image
+
+    from argus_amd.utils import draw_spaghetti
+
+    base = Image.new("RGB", (64, 48), (200, 150, 100))
+    np.random.seed(5)
+    a = np.asarray(draw_spaghetti(base.copy(), 10))
+    after_a = np.random.rand()
+    np.random.seed(5)
+    b = np.asarray(draw_spaghetti(base.copy(), 10))
+    assert np.array_equal(a, b)
+    changed = (a != np.asarray(base)).any(-1)
+    assert changed.any() and (a[changed] == 0).all()
+    np.random.seed(5)
+    for _ in range(10):
+        x0, y0 = np.random.randint(0, 64), np.random.randint(0, 48)
+        np.random.randint(x0, 64), np.random.randint(y0, 48), np.random.randint(0, 360), np.random.randint(0, 360)
+        np.random.uniform(1.0, 5.0)
+    assert np.random.rand() == after_a
+    assert np.array_equal(np.asarray(draw_spaghetti(base.copy(), 0)), np.asarray(base))
+
+
+def test_validate_config_checks(tmp_path):
+    import pytest
+
+    from argus_amd.data import CameraCubePoseDatasetConfig
+    from argus_amd.validate import ValConfig
+    from tests.conftest import make_dummy_dataset
+
+    d = make_dummy_dataset(tmp_path)
+    with pytest.raises(AssertionError):
+        ValConfig(model_path=str(tmp_path / "x.pt"), dataset_config=CameraCubePoseDatasetConfig(d))
+    with pytest.raises(FileNotFoundError):
+        ValConfig(model_path=str(tmp_path / "missing.pth"), dataset_config=CameraCubePoseDatasetConfig(d))
