@@ -18,11 +18,20 @@ import torch  # noqa: F401  (must precede the CDLL, see module docstring)
 LIB_PATH = Path(os.environ.get("ARGUS_HIP_LIB", Path(__file__).resolve().parent / "libargus_hip.so"))
 
 F32, BF16 = 0, 1
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 
 class ConvDesc(C.Structure):
     _fields_ = [(n, C.c_int32) for n in ("n", "h", "w", "c", "k", "r", "s", "stride", "pad", "ho", "wo", "stem")]
+
+
+class BnBwdEpilogue(C.Structure):
+    """argus_bn_bwd_epilogue (include/argus_hip.h)."""
+
+    _fields_ = [("y", C.c_void_p), ("mean", C.c_void_p), ("invstd", C.c_void_p), ("mask_mode", C.c_int32),
+                ("reserved", C.c_int32), ("scale", C.c_void_p), ("shift", C.c_void_p), ("mask_bits", C.c_void_p),
+                ("y2", C.c_void_p), ("mean2", C.c_void_p), ("invstd2", C.c_void_p), ("part", C.c_void_p),
+                ("part2", C.c_void_p)]
 
 
 _P = C.c_void_p
@@ -50,6 +59,8 @@ SIGNATURES = {
     "argus_conv_tuning_get": (_I, [_I]),
     "argus_conv_launch_info": (_I, [_DESC, _I, _I, C.POINTER(C.c_int64)]),
     "argus_conv_dgrad": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P]),
+    "argus_conv_dgrad_bn_rows": (_I, [_DESC, _I]),
+    "argus_conv_dgrad_bn": (_I, [_DESC, _I, _P, _P, _P, _P, C.POINTER(BnBwdEpilogue), _P]),
     "argus_conv_wgrad_workspace_bytes": (_SZ, [_DESC, _I]),
     "argus_conv_wgrad": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     "argus_ktimer_enable": (_I, [C.c_char_p]),

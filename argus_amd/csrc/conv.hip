@@ -66,7 +66,7 @@ template <typename T, int BN> constexpr int epi_ld() { return BN + 16 / (int)siz
 // OCC = workgroups per CU the kernel is built for: 2 -> double-buffered LDS + 2-deep register
 // prefetch ring (deep-K GEMMs); 3 or 4 -> one LDS buffer, no ring, <= 168 / 128 VGPRs (K <= 2
 // k-steps: the 1x1 convs whose time is load/epilogue latency, hidden by more resident workgroups).
-template <typename T, int BM, int BN, bool STEM, bool PRO, int OCC>
+template <typename T, int BM, int BN, bool STEM, bool PRO, int OCC, int BW>
 __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
   constexpr int E = Chunk<T>::E;
   constexpr int BKE = 8 * E;  // K elements per k-step (8 chunks of 16 B per LDS row)
@@ -74,15 +74,20 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
   constexpr int AR = BM / 32, BR = BN / 32;
   constexpr int NBUF = OCC >= 3 ? 1 : 2;
   constexpr int HALF_C = (BM / 2) * (BN + 16 / (int)sizeof(T)) * (int)sizeof(T);  // epilogue pass of BM/2 rows
-  constexpr int LDS_BYTES = NBUF * (BM + BN) * 128 > HALF_C ? NBUF * (BM + BN) * 128 : HALF_C;
+  constexpr int RED_B = (256 / (BN * (int)sizeof(T) / 16)) * BN * 8;            // BN-backward column sums
+  constexpr int LDS0 = NBUF * (BM + BN) * 128 > HALF_C ? NBUF * (BM + BN) * 128 : HALF_C;
+  constexpr int LDS_BYTES = LDS0 > RED_B ? LDS0 : RED_B;
   __shared__ __attribute__((aligned(16))) u32x4 lds[LDS_BYTES / 16];
 
   const IgPhase& ph = p.ph[blockIdx.z];
   const int mtiles = (ph.M + BM - 1) / BM;
   const int ntiles = p.N / BN;
   const int nwg = mtiles * ntiles;
-  if ((int)blockIdx.x >= nwg) return;
-  if (ph.K == 0 && p.addend == p.c && !p.addend_mask) return;  // in-place += 0
+  if ((int)blockIdx.x >= nwg) {
+    if constexpr (BW != 0) bwd_epi_zero_rows<BN, 256>(p.bb, blockIdx.x - nwg, mtiles, ntiles, p.N);
+    return;
+  }
+  if (ph.K == 0 && p.addend == p.c && !p.addend_mask && BW == 0) return;  // in-place += 0
   const int bid = xcd_remap(blockIdx.x, nwg);
   const int mt = bid / ntiles, nt = bid - mt * ntiles;
 
@@ -308,6 +313,8 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
   constexpr int RPP = 256 / CPR;                  // rows per store pass
   T* Cs = reinterpret_cast<T*>(lds);
   T* __restrict__ Cg = reinterpret_cast<T*>(p.c);
+  BwdEpiAcc<T, BW> bwd;
+  if constexpr (BW != 0) bwd.init(p.bb, nt * BN + (tid % CPR) * E);
 #pragma unroll
   for (int q = 0; q < EPASS; ++q) {
     if (EPASS == 1 || wm == q) {
@@ -343,10 +350,16 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
           for (int j = 0; j < E; ++j) f[j] += (mb >> j) & 1u ? o[j] : 0.f;
           v = pack(f);
         }
+        if constexpr (BW != 0) v = bwd.step(p.bb, v, (size_t)(dst - Cg));
         st16_nt(dst, v);
       }
     }
     if (EPASS > 1) __syncthreads();
+  }
+  if constexpr (BW != 0) {
+    __syncthreads();  // the C staging area becomes the reduction buffer
+    bwd.template reduce<BN, 256>(p.bb, reinterpret_cast<float2*>(lds), tid / CPR, RPP, tid % CPR,
+                                 (size_t)blockIdx.z * p.bb.prow + mt, p.N, nt * BN);
   }
 }
 
@@ -802,32 +815,43 @@ static int check_desc(const argus_conv_desc& d) {
   return ARGUS_OK;
 }
 
-template <typename T, int BM, int BN, bool STEM, bool PRO, int OCC>
+template <typename T, int BM, int BN, bool STEM, bool PRO, int OCC, int BW>
 static const char* ig_name() {
   static const std::string s = std::string("argus::igemm_kernel<") + type_name<T>() + ", " + std::to_string(BM) +
                                ", " + std::to_string(BN) + ", " + bool_name(STEM) + ", " + bool_name(PRO) + ", " +
-                               std::to_string(OCC) + ">";
+                               std::to_string(OCC) + ", " + std::to_string(BW) + ">";
   return s.c_str();
 }
 
-template <typename T, int BM, int BN, bool STEM, bool PRO, int OCC>
+template <typename T, int BM, int BN, bool STEM, bool PRO, int OCC, int BW = 0>
 static void launch_ig(const IgParams& p, int maxM, hipStream_t st) {
   const int ntiles = p.N / BN;
   dim3 grid(cdiv(maxM, BM) * ntiles, 1, p.nphase);
-  timed_launch(ig_name<T, BM, BN, STEM, PRO, OCC>(), igemm_kernel<T, BM, BN, STEM, PRO, OCC>, grid, dim3(256), st,
-               p);
+  timed_launch(ig_name<T, BM, BN, STEM, PRO, OCC, BW>(), igemm_kernel<T, BM, BN, STEM, PRO, OCC, BW>, grid,
+               dim3(256), st, p);
 }
 
-template <typename T, bool PRO, int OCC>
+template <typename T, bool PRO, int OCC, int BW = 0>
 static void dispatch_ig(const IgParams& p, int maxM, int bm, int bn, hipStream_t st) {
   const bool bn128 = bn == 128;
   if (bm == 128) {
     // the single-buffer 128x128 tile needs > 128 VGPRs: 3 workgroups per CU instead of 4
-    if (bn128) launch_ig<T, 128, 128, false, PRO, (OCC == 4 ? 3 : OCC)>(p, maxM, st);
-    else launch_ig<T, 128, 64, false, PRO, OCC>(p, maxM, st);
+    if (bn128) launch_ig<T, 128, 128, false, PRO, (OCC == 4 ? 3 : OCC), BW>(p, maxM, st);
+    else launch_ig<T, 128, 64, false, PRO, OCC, BW>(p, maxM, st);
   } else {
-    if (bn128) launch_ig<T, 64, 128, false, PRO, OCC>(p, maxM, st);
-    else launch_ig<T, 64, 64, false, PRO, OCC>(p, maxM, st);
+    if (bn128) launch_ig<T, 64, 128, false, PRO, OCC, BW>(p, maxM, st);
+    else launch_ig<T, 64, 64, false, PRO, OCC, BW>(p, maxM, st);
+  }
+}
+
+// BN-backward epilogue variants (dgrad only: no stem, no prologue)
+template <typename T, int OCC>
+static void dispatch_ig_bwd(const IgParams& p, int maxM, int bm, int bn, hipStream_t st) {
+  switch (bwd_variant(p.bb)) {
+    case 2: dispatch_ig<T, false, OCC, 2>(p, maxM, bm, bn, st); break;
+    case 3: dispatch_ig<T, false, OCC, 3>(p, maxM, bm, bn, st); break;
+    case 4: dispatch_ig<T, false, OCC, 4>(p, maxM, bm, bn, st); break;
+    default: dispatch_ig<T, false, OCC>(p, maxM, bm, bn, st);
   }
 }
 
@@ -863,6 +887,9 @@ static int run_ig(const IgParams& p, hipStream_t st, int bm, int bn) {
   } else if (p.pro_scale) {
     if (smallk) dispatch_ig<T, true, 4>(p, maxM, bm, bn, st);
     else dispatch_ig<T, true, 2>(p, maxM, bm, bn, st);
+  } else if (p.bb.mode) {
+    if (smallk) dispatch_ig_bwd<T, 4>(p, maxM, bm, bn, st);
+    else dispatch_ig_bwd<T, 2>(p, maxM, bm, bn, st);
   } else {
     if (smallk) dispatch_ig<T, false, 4>(p, maxM, bm, bn, st);
     else dispatch_ig<T, false, 2>(p, maxM, bm, bn, st);
@@ -973,16 +1000,9 @@ int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, 
   return dtype == ARGUS_BF16 ? run_ig<bf16>(p, st, bm, bn) : run_ig<float>(p, st, bm, bn);
 }
 
-int conv_dgrad(const argus_conv_desc& d, int dtype, const void* dy, const void* wt, void* dx,
-               const void* addend, const uint8_t* addend_mask, hipStream_t st) {
-  if (int e = check_desc(d)) return e;
-  g_launch_work = 2.0 * d.n * d.ho * d.wo * d.k * d.r * d.s * d.c;  // algorithmic flops / bytes (ktimer)
-  g_launch_bytes = (double)(dtype == ARGUS_BF16 ? 2 : 4) *
-                   ((double)d.n * d.ho * d.wo * d.k + (double)d.k * d.r * d.s * d.c +
-                    (addend ? 2.0 : 1.0) * d.n * d.h * d.w * d.c) +
-                   (addend_mask ? (double)d.n * d.h * d.w * d.c / (dtype == ARGUS_BF16 ? 8 : 4) : 0.0);
-  if (d.stem) { set_error("conv_dgrad: the stem input has no gradient"); return ARGUS_ERR_ARG; }
-  IgParams p = {};
+static void dgrad_params(const argus_conv_desc& d, const void* dy, const void* wt, void* dx, const void* addend,
+                         const uint8_t* addend_mask, IgParams& p) {
+  p = IgParams{};
   p.a = dy; p.b = wt; p.c = dx;
   p.N = d.c; p.Cin = d.k; p.lda = d.k; p.H = d.ho; p.W = d.wo; p.ish = 1; p.isw = 1;
   p.Ho = d.h; p.Wo = d.w; p.osh = d.stride; p.osw = d.stride; p.ldc = d.c; p.ldb = d.r * d.s * d.k;
@@ -1009,8 +1029,71 @@ int conv_dgrad(const argus_conv_desc& d, int dtype, const void* dy, const void* 
       ph.K = t * d.k;
     }
   p.nphase = np;
+}
+
+// BN-backward partial rows per phase of the kernel run_ig will choose for these dgrad params
+static int dgrad_prow(const IgParams& p, int dtype, const argus_conv_desc& d) {
+  int maxM = 0, maxK = 0;
+  for (int i = 0; i < p.nphase; ++i) {
+    maxM = p.ph[i].M > maxM ? p.ph[i].M : maxM;
+    maxK = p.ph[i].K > maxK ? p.ph[i].K : maxK;
+  }
+  if (dtype == ARGUS_BF16) {
+    if (conv3x3_halo_ok(p)) return p.ph[0].M / 256;
+    if (igemm_glds_ok(p, maxM, maxK)) return cdiv(maxM, 256);
+  }
+  return cdiv(maxM, dgrad_bm(d));
+}
+
+static void dgrad_work(const argus_conv_desc& d, int dtype, bool addend, bool mask, bool bn, bool dual) {
+  const double E = dtype == ARGUS_BF16 ? 2.0 : 4.0;
+  const double px_in = (double)d.n * d.h * d.w * d.c;
+  g_launch_work = 2.0 * d.n * d.ho * d.wo * d.k * d.r * d.s * d.c;  // algorithmic flops / bytes (ktimer)
+  g_launch_bytes = E * ((double)d.n * d.ho * d.wo * d.k + (double)d.k * d.r * d.s * d.c +
+                        (addend ? 2.0 : 1.0) * px_in) +
+                   (mask ? px_in / (dtype == ARGUS_BF16 ? 8 : 4) : 0.0) +
+                   (bn ? E * px_in * (dual ? 2.0 : 1.0) : 0.0);  // BN input(s) y read by the epilogue
+}
+
+int conv_dgrad(const argus_conv_desc& d, int dtype, const void* dy, const void* wt, void* dx,
+               const void* addend, const uint8_t* addend_mask, hipStream_t st) {
+  if (int e = check_desc(d)) return e;
+  dgrad_work(d, dtype, addend != nullptr, addend_mask != nullptr, false, false);
+  if (d.stem) { set_error("conv_dgrad: the stem input has no gradient"); return ARGUS_ERR_ARG; }
+  IgParams p;
+  dgrad_params(d, dy, wt, dx, addend, addend_mask, p);
   const int bm = dgrad_bm(d), bn = pick_bn(1, d.c);
   return dtype == ARGUS_BF16 ? run_ig<bf16>(p, st, bm, bn) : run_ig<float>(p, st, bm, bn);
+}
+
+int conv_dgrad_bn_rows(const argus_conv_desc& d, int dtype) {
+  if (check_desc(d) || d.stem) return -1;
+  IgParams p;
+  dgrad_params(d, nullptr, nullptr, nullptr, nullptr, nullptr, p);
+  return p.nphase * dgrad_prow(p, dtype, d);
+}
+
+int conv_dgrad_bn(const argus_conv_desc& d, int dtype, const void* dy, const void* wt, void* dm,
+                  const void* addend, const argus_bn_bwd_epilogue* bn, hipStream_t st) {
+  if (int e = check_desc(d)) return e;
+  if (d.stem) { set_error("conv_dgrad_bn: the stem input has no gradient"); return ARGUS_ERR_ARG; }
+  if (!bn || !bn->y || !bn->mean || !bn->invstd || !bn->part || (bn->mask_mode != 2 && bn->mask_mode != 3) ||
+      (bn->mask_mode == 2 && (!bn->scale || !bn->shift || bn->y2)) || (bn->mask_mode == 3 && !bn->mask_bits) ||
+      (bn->y2 && (!bn->mean2 || !bn->invstd2 || !bn->part2)) || bn->y == dm) {
+    set_error("conv_dgrad_bn: bad BN-backward epilogue arguments");
+    return ARGUS_ERR_ARG;
+  }
+  dgrad_work(d, dtype, addend != nullptr, bn->mask_mode == 3, true, bn->y2 != nullptr);
+  IgParams p;
+  dgrad_params(d, dy, wt, dm, addend, nullptr, p);
+  BnBwdEpi& b = p.bb;
+  b.y = bn->y; b.mean = bn->mean; b.invstd = bn->invstd; b.sc = bn->scale; b.sh = bn->shift;
+  b.bits = bn->mask_bits; b.y2 = bn->y2; b.mean2 = bn->mean2; b.invstd2 = bn->invstd2;
+  b.part = reinterpret_cast<float2*>(bn->part); b.part2 = reinterpret_cast<float2*>(bn->part2);
+  b.mode = bn->mask_mode;
+  b.prow = dgrad_prow(p, dtype, d);
+  const int bm = dgrad_bm(d), bn_ = pick_bn(1, d.c);
+  return dtype == ARGUS_BF16 ? run_ig<bf16>(p, st, bm, bn_) : run_ig<float>(p, st, bm, bn_);
 }
 
 struct WgPlan {

@@ -41,14 +41,16 @@ ARGUS_DEV void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int BW>
 __global__ __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) void igemm_glds_kernel(const IgParams p) {
   constexpr int WM = BM / 64, WN = BN / 64, NW = WM * WN, NT = NW * 64;
   constexpr int STAGE = (BM + BN) * 128;      // bytes per pipeline stage (A image, then B image)
   constexpr int NSTAGE = 3;
   constexpr int LD = BN + 8;                   // epilogue C row stride (elements)
   constexpr int EPI = BM * LD * 2;
-  constexpr int LDS_BYTES = NSTAGE * STAGE > EPI ? NSTAGE * STAGE : EPI;
+  constexpr int LDS0 = NSTAGE * STAGE > EPI ? NSTAGE * STAGE : EPI;
+  constexpr int RED_B = (NT / (BN / 8)) * BN * 8;  // BN-backward column sums
+  constexpr int LDS_BYTES = LDS0 > RED_B ? LDS0 : RED_B;
   constexpr int AI = BM * 8 / NT;              // A glds per thread per stage
   constexpr int BI = BN * 8 / NT;              // B glds per thread per stage
   constexpr int GPS = AI + BI;                 // glds per wave per stage (vmcnt unit)
@@ -59,8 +61,11 @@ __global__ __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) void igemm_glds_kern
   const int mtiles = (ph.M + BM - 1) / BM;
   const int ntiles = p.N / BN;
   const int nwg = mtiles * ntiles;
-  if ((int)blockIdx.x >= nwg) return;
-  if (ph.K == 0 && p.addend == p.c && !p.addend_mask) return;  // in-place += 0
+  if ((int)blockIdx.x >= nwg) {
+    if constexpr (BW != 0) bwd_epi_zero_rows<BN, NT>(p.bb, blockIdx.x - nwg, mtiles, ntiles, p.N);
+    return;
+  }
+  if (ph.K == 0 && p.addend == p.c && !p.addend_mask && BW == 0) return;  // in-place += 0
   const int bid = xcd_remap(blockIdx.x, nwg);
   const int mt = bid / ntiles, nt = bid - mt * ntiles;
 
@@ -225,6 +230,8 @@ __global__ __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) void igemm_glds_kern
   constexpr int RPP = NT / CPR;  // rows per store pass
   bf16* __restrict__ Cg = reinterpret_cast<bf16*>(p.c);
   const int c = tid % CPR;
+  BwdEpiAcc<bf16, BW> bwd;
+  if constexpr (BW != 0) bwd.init(p.bb, nt * BN + c * 8);
 #pragma unroll 4
   for (int rr = tid / CPR; rr < BM; rr += RPP) {
     const int m = mt * BM + rr;
@@ -244,21 +251,38 @@ __global__ __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) void igemm_glds_kern
       for (int j = 0; j < 8; ++j) f[j] += (mb >> j) & 1u ? o[j] : 0.f;
       v = pack(f);
     }
+    if constexpr (BW != 0) v = bwd.step(p.bb, v, (size_t)(dst - Cg));
     st16_nt(dst, v);
+  }
+  if constexpr (BW != 0) {
+    __syncthreads();
+    bwd.template reduce<BN, NT>(p.bb, reinterpret_cast<float2*>(lds), tid / CPR, RPP, c,
+                                (size_t)blockIdx.z * p.bb.prow + mt, p.N, nt * BN);
   }
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int BW>
 static const char* glds_name() {
-  static const std::string s =
-      std::string("argus::igemm_glds_kernel<") + std::to_string(BM) + ", " + std::to_string(BN) + ">";
+  static const std::string s = std::string("argus::igemm_glds_kernel<") + std::to_string(BM) + ", " +
+                               std::to_string(BN) + ", " + std::to_string(BW) + ">";
   return s.c_str();
+}
+
+template <int BM, int BN, int BW>
+static void launch_glds1(const IgParams& p, int maxM, hipStream_t st) {
+  dim3 grid(cdiv(maxM, BM) * (p.N / BN), 1, p.nphase);
+  timed_launch(glds_name<BM, BN, BW>(), igemm_glds_kernel<BM, BN, BW>, grid, dim3((BM / 64) * (BN / 64) * 64), st,
+               p);
 }
 
 template <int BM, int BN>
 static void launch_glds(const IgParams& p, int maxM, hipStream_t st) {
-  dim3 grid(cdiv(maxM, BM) * (p.N / BN), 1, p.nphase);
-  timed_launch(glds_name<BM, BN>(), igemm_glds_kernel<BM, BN>, grid, dim3((BM / 64) * (BN / 64) * 64), st, p);
+  switch (bwd_variant(p.bb)) {
+    case 2: launch_glds1<BM, BN, 2>(p, maxM, st); break;
+    case 3: launch_glds1<BM, BN, 3>(p, maxM, st); break;
+    case 4: launch_glds1<BM, BN, 4>(p, maxM, st); break;
+    default: launch_glds1<BM, BN, 0>(p, maxM, st);
+  }
 }
 
 // argus_conv_tuning key 8: smallest K (taps*C) served by the glds kernel (0 = off). 512 -> 1024 after
@@ -266,7 +290,7 @@ static void launch_glds(const IgParams& p, int maxM, hipStream_t st) {
 int g_glds_min_k = 1024;
 int g_glds_min_grid = 256;  // key 9: fewest workgroups for which it is chosen
 
-bool igemm_glds_launch(const IgParams& p, int maxM, int maxK, hipStream_t st) {
+bool igemm_glds_ok(const IgParams& p, int maxM, int maxK) {
   if (g_glds_min_k <= 0 || p.stem || p.pro_scale || maxK < g_glds_min_k || p.Cin % 64 || p.lda % 8 ||
       p.ldb % 8 || maxM < 4 * 256)
     return false;
@@ -275,7 +299,11 @@ bool igemm_glds_launch(const IgParams& p, int maxM, int maxK, hipStream_t st) {
     if (p.ph[i].K % 64) return false;
   // measured (tools/convbench.py): a win only with >= one 8-wave workgroup per CU; the 4-wave
   // 256x64 tile and sub-CU-count grids lose to the register-staged kernel
-  if (p.N % 128 || cdiv(maxM, 256) * (p.N / 128) < g_glds_min_grid) return false;
+  return !(p.N % 128 || cdiv(maxM, 256) * (p.N / 128) < g_glds_min_grid);
+}
+
+bool igemm_glds_launch(const IgParams& p, int maxM, int maxK, hipStream_t st) {
+  if (!igemm_glds_ok(p, maxM, maxK)) return false;
   launch_glds<256, 128>(p, maxM, st);
   return true;
 }

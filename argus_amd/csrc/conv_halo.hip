@@ -47,7 +47,7 @@ ARGUS_DEV void sbar() {
 
 constexpr int kHaloPos = 448;  // halo positions per image buffer (max (rows+2)*(W+2) over the shapes served)
 
-template <int BN, bool PRO>
+template <int BN, bool PRO, int BW>
 __global__ __launch_bounds__(4 * (BN / 64) * 64, 1) void conv3x3_halo_kernel(const IgParams p) {
   constexpr int WN = BN / 64, NW = 4 * WN, NT = NW * 64;
   constexpr int HALO = kHaloPos * 128;          // bytes per halo image
@@ -56,7 +56,9 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, 1) void conv3x3_halo_kernel(con
   constexpr int LD = BN + 8;
   constexpr int EPI = 256 * LD * 2;
   constexpr int MAIN = 2 * HALO + NBS * BST;
-  constexpr int LDS_BYTES = MAIN > EPI ? MAIN : EPI;
+  constexpr int LDS0 = MAIN > EPI ? MAIN : EPI;
+  constexpr int RED_B = (NT / (BN / 8)) * BN * 8;  // BN-backward column sums
+  constexpr int LDS_BYTES = LDS0 > RED_B ? LDS0 : RED_B;
   constexpr int HG = kHaloPos / (8 * NW);       // halo glds per wave per chunk
   constexpr int BG = BN * 8 / NT;               // weight glds per wave per tap
   static_assert(HG * 8 * NW == kHaloPos && BG * NT == BN * 8, "halo / tile partition");
@@ -272,6 +274,8 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, 1) void conv3x3_halo_kernel(con
   constexpr int CPR = BN / 8, RPP = NT / CPR;
   bf16* __restrict__ Cg = reinterpret_cast<bf16*>(p.c);
   const int c = tid % CPR;
+  BwdEpiAcc<bf16, BW> bwd;
+  if constexpr (BW != 0) bwd.init(p.bb, nt * BN + c * 8);
 #pragma unroll 4
   for (int rr = tid / CPR; rr < 256; rr += RPP) {
     const size_t off = (size_t)(mt * 256 + rr) * p.ldc + nt * BN + c * 8;
@@ -285,56 +289,79 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, 1) void conv3x3_halo_kernel(con
       for (int j = 0; j < 8; ++j) f[j] += (mb >> j) & 1u ? o[j] : 0.f;
       v = pack(f);
     }
+    if constexpr (BW != 0) v = bwd.step(p.bb, v, off);
     st16_nt(Cg + off, v);
+  }
+  if constexpr (BW != 0) {
+    __syncthreads();
+    bwd.template reduce<BN, NT>(p.bb, reinterpret_cast<float2*>(lds), tid / CPR, RPP, c, (size_t)mt, p.N, nt * BN);
   }
 }
 
-template <int BN, bool PRO>
+template <int BN, bool PRO, int BW>
 static const char* halo_name() {
   static const std::string s = std::string("argus::conv3x3_halo_kernel<") + std::to_string(BN) + ", " +
-                               bool_name(PRO) + ">";
+                               bool_name(PRO) + ", " + std::to_string(BW) + ">";
   return s.c_str();
+}
+
+template <int BN, bool PRO, int BW>
+static void launch_halo1(const IgParams& p, hipStream_t st) {
+  dim3 grid((p.ph[0].M / 256) * (p.N / BN));
+  timed_launch(halo_name<BN, PRO, BW>(), conv3x3_halo_kernel<BN, PRO, BW>, grid, dim3(4 * (BN / 64) * 64), st, p);
 }
 
 template <int BN, bool PRO>
 static void launch_halo(const IgParams& p, hipStream_t st) {
-  dim3 grid((p.ph[0].M / 256) * (p.N / BN));
-  timed_launch(halo_name<BN, PRO>(), conv3x3_halo_kernel<BN, PRO>, grid, dim3(4 * (BN / 64) * 64), st, p);
+  if constexpr (PRO) {
+    launch_halo1<BN, true, 0>(p, st);  // forward (prologue) never carries the backward epilogue
+  } else {
+    switch (bwd_variant(p.bb)) {
+      case 2: launch_halo1<BN, false, 2>(p, st); break;
+      case 3: launch_halo1<BN, false, 3>(p, st); break;
+      case 4: launch_halo1<BN, false, 4>(p, st); break;
+      default: launch_halo1<BN, false, 0>(p, st);
+    }
+  }
 }
 
 int g_halo_enable = 1;      // argus_conv_tuning key 10
 int g_halo_min_grid = 256;  // key 13: fewest workgroups for which the fwd/dgrad halo kernel is chosen
 
 // 3x3 / stride 1 / pad 1, same input and output grid, one phase, whole-row / whole-image 256-pixel tiles
-bool conv3x3_halo_launch(const IgParams& p, hipStream_t st) {
-  if (!g_halo_enable || p.stem || p.nphase != 1 || p.ish != 1 || p.isw != 1 || p.osh != 1 || p.osw != 1) return false;
+int conv3x3_halo_ok(const IgParams& p) {
+  if (!g_halo_enable || p.stem || p.nphase != 1 || p.ish != 1 || p.isw != 1 || p.osh != 1 || p.osw != 1) return 0;
   const IgPhase& ph = p.ph[0];
-  if (ph.K != 9 * p.Cin || p.Cin % 64 || p.lda % 8 || p.ldb % 8 || p.H != p.Ho || p.W != p.Wo) return false;
+  if (ph.K != 9 * p.Cin || p.Cin % 64 || p.lda % 8 || p.ldb % 8 || p.H != p.Ho || p.W != p.Wo) return 0;
   for (int t = 0; t < 9; ++t)
-    if (ph.dh[t] < -1 || ph.dh[t] > 1 || ph.dw[t] < -1 || ph.dw[t] > 1) return false;
+    if (ph.dh[t] < -1 || ph.dh[t] > 1 || ph.dw[t] < -1 || ph.dw[t] > 1) return 0;
   const int HWi = p.H * p.W;
-  if (ph.M % 256) return false;
+  if (ph.M % 256) return 0;
   int npos;
   if (HWi >= 256) {
-    if (256 % p.W || HWi % 256) return false;
+    if (256 % p.W || HWi % 256) return 0;
     npos = (256 / p.W + 2) * (p.W + 2);
   } else {
-    if (256 % HWi) return false;
+    if (256 % HWi) return 0;
     npos = (256 / HWi) * (p.H + 2) * (p.W + 2);
   }
-  if (npos > kHaloPos) return false;
-  if (p.stats && p.stat_tile != 64 && p.stat_tile != 128) return false;
+  if (npos > kHaloPos) return 0;
+  if (p.stats && p.stat_tile != 64 && p.stat_tile != 128) return 0;
   // measured (tools/convbench.py, B=64): wins only with 8-wave workgroups (N % 128) filling every CU;
   // the 4-wave BN=64 tile and sub-CU-count grids lose to the register-staged kernel
-  if (p.N % 128 == 0 && (ph.M / 256) * (p.N / 128) >= g_halo_min_grid) {
+  if (p.N % 128 == 0 && (ph.M / 256) * (p.N / 128) >= g_halo_min_grid) return 128;
+  if (g_halo_min_grid <= 1 && p.N % 64 == 0) return 64;  // forced (tests): the 4-wave variant
+  return 0;
+}
+
+bool conv3x3_halo_launch(const IgParams& p, hipStream_t st) {
+  const int bn = conv3x3_halo_ok(p);
+  if (bn == 128) {
     if (p.pro_scale) launch_halo<128, true>(p, st); else launch_halo<128, false>(p, st);
-    return true;
-  }
-  if (g_halo_min_grid <= 1 && p.N % 64 == 0) {  // forced (tests): the 4-wave variant
+  } else if (bn == 64) {
     if (p.pro_scale) launch_halo<64, true>(p, st); else launch_halo<64, false>(p, st);
-    return true;
   }
-  return false;
+  return bn != 0;
 }
 
 

@@ -14,6 +14,24 @@ struct IgPhase {
   int dh[9], dw[9], boff[9];  // per tap: input offset (input = q*is + d) and B-row element offset
 };
 
+// BatchNorm-backward epilogue of a dgrad whose output feeds BN backward (argus_bn_bwd_epilogue):
+// store dm = output * relu-mask and emit per-(row tile, channel) {sum dm, sum dm*(y-mean)*invstd}.
+struct BnBwdEpi {
+  const void* y;
+  const float* mean;
+  const float* invstd;
+  const float* sc;        // mode 2: mask = y*sc+sh > 0
+  const float* sh;
+  const uint8_t* bits;    // mode 3: argus_bn_apply mask bits of y's block output
+  const void* y2;         // optional second branch (mode 3): the downsample BN
+  const float* mean2;
+  const float* invstd2;
+  float2* part;           // [nphase * prow][N]
+  float2* part2;
+  int mode;               // 0 = off, 2, 3
+  int prow;               // partial rows per dgrad phase
+};
+
 struct IgParams {
   const void* a;
   const void* b;
@@ -27,6 +45,7 @@ struct IgParams {
   int stem, nphase;
   int stat_tile;  // rows per BN-statistics partial (forward with stats)
   IgPhase ph[4];
+  BnBwdEpi bb;    // dgrad only
 };
 
 struct WgParams {
@@ -60,6 +79,111 @@ template <> struct Mma<float> {
 
 ARGUS_DEV int swz8(int row) { return (row >> 1) & 7; }
 
+// Per-thread state of the BN-backward epilogue: a thread owns one 16-byte channel chunk (fixed
+// across the rows it stores), keeps that chunk's coefficients and its column sums in registers.
+// BW (compile time, so the plain forward / dgrad kernels keep their register budget): 2 = mask from
+// y*scale+shift > 0; 3 = mask bits; 4 = mask bits + the second (downsample) BN branch.
+template <int BW> struct BwdMode {
+  static constexpr bool ON = BW != 0, RECOMPUTE = BW == 2, DUAL = BW == 4;
+};
+
+template <typename T, int BW>
+struct BwdEpiAcc {
+  static constexpr int E = Chunk<T>::E;
+  static constexpr int EM = BwdMode<BW>::RECOMPUTE ? E : 1;  // mask coefficients
+  static constexpr int ED = BwdMode<BW>::DUAL ? E : 1;       // second branch
+  float s[E], t[E], mu[E], is[E], S[EM], H[EM], t2[ED], mu2[ED], is2[ED];
+
+  ARGUS_DEV static void ld(float* dst, const float* src) {
+#pragma unroll
+    for (int j = 0; j < E; j += 4) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(src + j);
+      dst[j] = v.x; dst[j + 1] = v.y; dst[j + 2] = v.z; dst[j + 3] = v.w;
+    }
+  }
+
+  ARGUS_DEV void init(const BnBwdEpi& b, int ch) {
+    ld(mu, b.mean + ch);
+    ld(is, b.invstd + ch);
+    if constexpr (BwdMode<BW>::RECOMPUTE) { ld(S, b.sc + ch); ld(H, b.sh + ch); }
+    if constexpr (BwdMode<BW>::DUAL) {
+      ld(mu2, b.mean2 + ch);
+      ld(is2, b.invstd2 + ch);
+#pragma unroll
+      for (int j = 0; j < E; ++j) t2[j] = 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < E; ++j) { s[j] = 0.f; t[j] = 0.f; }
+  }
+
+  // v = the output chunk as it would be stored (rounded to T), at element offset off of the output
+  // (the BN input y has the same layout): returns the masked chunk dm and accumulates the sums.
+  ARGUS_DEV u32x4 step(const BnBwdEpi& b, u32x4 v, size_t off) {
+    float d[E], yv[E];
+    unpack(v, d);
+    unpack(ld16(reinterpret_cast<const T*>(b.y) + off), yv);
+    if constexpr (BwdMode<BW>::RECOMPUTE) {
+#pragma unroll
+      for (int j = 0; j < E; ++j) d[j] = fmaf(yv[j], S[j], H[j]) > 0.f ? d[j] : 0.f;
+    } else {
+      const unsigned mb = b.bits[off / E];
+#pragma unroll
+      for (int j = 0; j < E; ++j) d[j] = (mb >> j) & 1u ? d[j] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      s[j] += d[j];
+      t[j] = fmaf(d[j], (yv[j] - mu[j]) * is[j], t[j]);
+    }
+    if constexpr (BwdMode<BW>::DUAL) {
+      float y2v[E];
+      unpack(ld16(reinterpret_cast<const T*>(b.y2) + off), y2v);
+#pragma unroll
+      for (int j = 0; j < E; ++j) t2[j] = fmaf(d[j], (y2v[j] - mu2[j]) * is2[j], t2[j]);
+    }
+    return pack(d);
+  }
+
+  // Fixed-order reduction over the RG row groups of the workgroup (thread = (row group rg, chunk c))
+  // through LDS red[RG][COLS] (float2), written as partial row `row` of columns col0..col0+COLS.
+  template <int COLS, int NT>
+  ARGUS_DEV void reduce(const BnBwdEpi& b, float2* red, int rg, int RG, int c, size_t row, int N, int col0) {
+#pragma unroll
+    for (int br = 0; br < (BwdMode<BW>::DUAL ? 2 : 1); ++br) {
+#pragma unroll
+      for (int j = 0; j < E; ++j) {
+        float tv = t[j];
+        if constexpr (BwdMode<BW>::DUAL) tv = br == 0 ? t[j] : t2[j];
+        red[rg * COLS + c * E + j] = make_float2(s[j], tv);
+      }
+      __syncthreads();
+      float2* out = (br == 0 ? b.part : b.part2) + row * N + col0;
+      for (int idx = threadIdx.x; idx < COLS; idx += NT) {
+        float2 a = red[idx];
+        for (int g = 1; g < RG; ++g) { a.x += red[g * COLS + idx].x; a.y += red[g * COLS + idx].y; }
+        out[idx] = a;
+      }
+      __syncthreads();
+    }
+  }
+};
+
+// host: the epilogue variant of a BnBwdEpi (0 when off)
+inline int bwd_variant(const BnBwdEpi& b) { return b.mode == 0 ? 0 : (b.mode == 2 ? 2 : (b.y2 ? 4 : 3)); }
+
+// Partial rows of tiles that do not exist in a smaller dgrad phase (grid sized for the largest):
+// workgroup e past the phase's tiles zeroes row (mtiles + e / ntiles), columns of tile e % ntiles.
+template <int COLS, int NT>
+ARGUS_DEV void bwd_epi_zero_rows(const BnBwdEpi& b, int e, int mtiles, int ntiles, int N) {
+  const int mt = mtiles + e / ntiles, nt = e - (e / ntiles) * ntiles;
+  if (mt >= b.prow) return;
+  const size_t row = (size_t)blockIdx.z * b.prow + mt;
+  for (int idx = threadIdx.x; idx < COLS; idx += NT) {
+    b.part[row * N + nt * COLS + idx] = make_float2(0.f, 0.f);
+    if (b.y2) b.part2[row * N + nt * COLS + idx] = make_float2(0.f, 0.f);
+  }
+}
+
 ARGUS_DEV u32x4 sel(bool ok, u32x4 v) {
   const u32x4 z = {0u, 0u, 0u, 0u};
   return ok ? v : z;
@@ -67,9 +191,12 @@ ARGUS_DEV u32x4 sel(bool ok, u32x4 v) {
 
 
 // forward / dgrad launchers of the glds kernel (conv_glds.hip); return false when the shape is not
-// served by it (then conv.hip's kernel runs)
+// served by it (then conv.hip's kernel runs). _ok: the same choice without launching.
+bool igemm_glds_ok(const IgParams& p, int maxM, int maxK);
 bool igemm_glds_launch(const IgParams& p, int maxM, int maxK, hipStream_t st);
-// 3x3 stride-1 forward / dgrad with an LDS-resident halo tile (conv_halo.hip); false = not served
+// 3x3 stride-1 forward / dgrad with an LDS-resident halo tile (conv_halo.hip); false = not served.
+// _ok returns the column tile it would launch (128 / 64) or 0.
+int conv3x3_halo_ok(const IgParams& p);
 bool conv3x3_halo_launch(const IgParams& p, hipStream_t st);
 // 3x3 stride-1 weight gradient with an LDS-resident halo tile (conv_halo.hip): plan / launch of the
 // split partials (fp32 [splits][K][9C]); false = not served

@@ -25,6 +25,9 @@ int conv_weight_prep_table(int count, const argus_conv_desc* descs, const float*
 int conv_weight_prep_batch(int dtype, int count, const void* device_table, int nblocks, hipStream_t st);
 int conv_dgrad(const argus_conv_desc& d, int dtype, const void* dy, const void* wt, void* dx,
                const void* addend, const uint8_t* addend_mask, hipStream_t st);
+int conv_dgrad_bn_rows(const argus_conv_desc& d, int dtype);
+int conv_dgrad_bn(const argus_conv_desc& d, int dtype, const void* dy, const void* wt, void* dm,
+                  const void* addend, const argus_bn_bwd_epilogue* bn, hipStream_t st);
 size_t conv_wgrad_ws(const argus_conv_desc& d, int dtype);
 int conv_wgrad(const argus_conv_desc& d, int dtype, const void* x, const float* sc,
                const float* sh, const void* dy, float* dw, void* ws, size_t ws_bytes,

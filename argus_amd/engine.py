@@ -27,7 +27,7 @@ from dataclasses import dataclass
 
 import torch
 
-from argus_amd._lib import BF16, F32, ConvDesc, lib, ptr, stream
+from argus_amd._lib import BF16, F32, BnBwdEpilogue, ConvDesc, lib, ptr, stream
 
 
 @dataclass(frozen=True)
@@ -194,6 +194,9 @@ class ResNetEngine:
                 px = N * hw[0] * hw[1]
                 max_bwd = max(max_bwd, L.dll.argus_bn_bwd_rows(px, c) * c)
         max_bwd = max(max_bwd, L.dll.argus_bn_bwd_rows(N * H1 * W1, 64) * 64)
+        for cv in convs.values():  # BN-backward partials written by dgrad epilogues (rows x C_in)
+            if not cv.desc.stem:
+                max_bwd = max(max_bwd, L.dll.argus_conv_dgrad_bn_rows(C.byref(cv.desc), dt) * cv.desc.c)
         self.bwd_part = self._f(max_bwd * 2)
         self.bwd_part2 = self._f(max_bwd * 2)  # second branch (downsample BN) of a dual reduce
         ws = max(L.dll.argus_conv_wgrad_workspace_bytes(C.byref(cv.desc), dt) for cv in convs.values())
@@ -396,7 +399,15 @@ class ResNetEngine:
         if on_ready is not None:
             on_ready("resnet.fc.weight", self._join)
 
-        for idx in range(len(self.blocks) - 1, -1, -1):
+        # BN backward: the reduction over dz = d(BN output) runs in the epilogue of the dgrad that
+        # produces dz (argus_conv_dgrad_bn), which stores the ReLU-masked dm and the partial column
+        # sums; only finalize + apply (dy = ca*dm + cb*y + cc) remain as passes. Invariant at the top
+        # of each block: dh holds dm3 = relu'(out) * dout (bn3's masked input gradient) and bwd_part
+        # (bwd_part2: the downsample BN) its partials, rows3 rows - except for the last block, whose
+        # dout comes from the average pool unmasked.
+        nb = len(self.blocks)
+        rows3 = None
+        for idx in range(nb - 1, -1, -1):
             b, a = self.blocks[idx], self.act[idx]
             pf = b.prefix
             h_in = self.act[idx - 1]["out"] if idx > 0 else self.p0
@@ -412,48 +423,67 @@ class ResNetEngine:
                     dbg[key + "." + pf] = t[:n].view(*shape).clone()
 
             cap("b_dout", dh, px_o * b.cout, (N, ho, wo, b.cout))
-            # bn3 (+ downsample BN, one dual pass) backward; ReLU mask bits of the block output
-            if b.has_ds:
-                self._bn_bwd_dual(P, G, pf + ".bn3", pf + ".downsample.1", px_o, b.cout, dh, a["bits"], a["y3"],
-                                  a["yd"], dy3, dyd)
+            # bn3 (+ downsample BN) backward
+            if rows3 is None:  # last block: mask + reduce pass over the pooled gradient
+                L.bn_bwd_reduce(dt, px_o, b.cout, ptr(dh), 3, ptr(a["bits"]), ptr(a["y3"]), None, None,
+                                ptr(self.bn_state[pf + ".bn3"][0]), ptr(self.bn_state[pf + ".bn3"][1]),
+                                ptr(self.bwd_part), None, None, None, None, s)
+                rows3 = L.dll.argus_bn_bwd_rows(px_o, b.cout)
+                self._bn_bwd_fin(P, G, pf + ".bn3", px_o, b.cout, self.bwd_part, rows3)
+                cf, st3 = self.bn_coef[pf + ".bn3"], self.bn_state[pf + ".bn3"]
+                self._guard(dy3)
+                L.bn_bwd_apply(dt, px_o, b.cout, ptr(dh), 3, ptr(a["bits"]), ptr(a["y3"]), None, None, ptr(cf[0]),
+                               ptr(cf[1]), ptr(cf[2]), ptr(dy3), ptr(dh), None, None, None, None, None, s)
             else:
-                self._bn_bwd(P, G, pf + ".bn3", px_o, b.cout, dh, 3, a["bits"], a["y3"], dy3, None)
+                self._bn_bwd_fin(P, G, pf + ".bn3", px_o, b.cout, self.bwd_part, rows3)
+                if b.has_ds:
+                    self._bn_bwd_fin(P, G, pf + ".downsample.1", px_o, b.cout, self.bwd_part2, rows3)
+                self._bn_apply_bwd(pf + ".bn3", px_o, b.cout, dh, a["y3"], dy3,
+                                   (pf + ".downsample.1", a["yd"], dyd) if b.has_ds else None)
             cap("b_dy3", dy3, px_o * b.cout, (N, ho, wo, b.cout))
-            # conv3
+            if b.has_ds:
+                cap("b_dyd", dyd, px_o * b.cout, (N, ho, wo, b.cout))
+            # conv3 -> bn2
             s2 = self.bn_state[pf + ".bn2"]
             if self.materialize:
                 self._wgrad(pf + ".conv3", a["a2"], None, dy3, G)
             else:
                 self._wgrad(pf + ".conv3", a["y2"], s2, dy3, G)
-            self._dgrad(pf + ".conv3", dy3, dz)
+            r2 = self._dgrad_bn(pf + ".conv3", dy3, dz, None, pf + ".bn2", a["y2"], 2)
             cap("b_dz2", dz, px_o * b.width, (N, ho, wo, b.width))
-            self._bn_bwd(P, G, pf + ".bn2", px_o, b.width, dz, 2, None, a["y2"], dyw, None)
+            self._bn_bwd_fin(P, G, pf + ".bn2", px_o, b.width, self.bwd_part, r2)
+            self._bn_apply_bwd(pf + ".bn2", px_o, b.width, dz, a["y2"], dyw)
             cap("b_dy2", dyw, px_o * b.width, (N, ho, wo, b.width))
-            # conv2
+            # conv2 -> bn1
             s1 = self.bn_state[pf + ".bn1"]
             if self.materialize:
                 self._wgrad(pf + ".conv2", a["a1"], None, dyw, G)
             else:
                 self._wgrad(pf + ".conv2", a["y1"], s1, dyw, G)
-            self._dgrad(pf + ".conv2", dyw, dz)
+            r1 = self._dgrad_bn(pf + ".conv2", dyw, dz, None, pf + ".bn1", a["y1"], 2)
             cap("b_dz1", dz, px_i * b.width, (N, hi, wi, b.width))
-            self._bn_bwd(P, G, pf + ".bn1", px_i, b.width, dz, 2, None, a["y1"], dyw, None)
+            self._bn_bwd_fin(P, G, pf + ".bn1", px_i, b.width, self.bwd_part, r1)
+            self._bn_apply_bwd(pf + ".bn1", px_i, b.width, dz, a["y1"], dyw)
             cap("b_dy1", dyw, px_i * b.width, (N, hi, wi, b.width))
-            # conv1 (+ downsample)
+            # conv1 (+ downsample) -> the previous block's bn3 (+ its downsample BN): dm3 of block idx-1
             self._wgrad(pf + ".conv1", h_in, None, dyw, G)
+            last_conv, last_dy, addend = pf + ".conv1", dyw, (None if b.has_ds else dh)
             if b.has_ds:
-                self._dgrad(pf + ".conv1", dyw, dx)
                 self._wgrad(pf + ".downsample.0", h_in, None, dyd, G)
-                self._dgrad(pf + ".downsample.0", dyd, dx, addend=dx)
-            else:  # identity skip: dx = dgrad(conv1) + relu'(out) * dout, added in the dgrad epilogue
-                self._dgrad(pf + ".conv1", dyw, dx, addend=dh, mask=a["bits"])
+                self._dgrad(pf + ".conv1", dyw, dx)
+                last_conv, last_dy, addend = pf + ".downsample.0", dyd, dx
+            if idx > 0:
+                pb, pa = self.blocks[idx - 1], self.act[idx - 1]
+                rows3 = self._dgrad_bn(last_conv, last_dy, dx, addend, pb.prefix + ".bn3", pa["y3"], 3, pa["bits"],
+                                       (pb.prefix + ".downsample.1", pa["yd"]) if pb.has_ds else None)
+            else:
+                self._dgrad(last_conv, last_dy, dx, addend=addend)
             dh, dx = dx, dh
             if on_ready is not None:
                 on_ready(pf + ".conv1.weight", self._join)
             if self.debug is not None:
                 n_in = N * hi * wi * b.cin
                 self.debug["bwd." + pf] = dh[:n_in].view(N, hi, wi, b.cin).clone()
-                self.debug["bwd_dh." + pf] = dy3[:px_o * b.cout].view(N, ho, wo, b.cout).clone()
         # stem: maxpool -> relu/bn1 -> conv1 wgrad
         H1, W1 = self.stem_hw
         dz0, dy0 = g[4], g[5]
@@ -464,37 +494,54 @@ class ResNetEngine:
         if on_ready is not None:
             on_ready("resnet.conv1.weight", self._join)
 
+    def _dgrad_bn(self, conv, dy, dm, addend, bn, y, mode, bits=None, second=None):
+        """dgrad of ``conv`` whose output feeds BN ``bn`` (input ``y``) backward: stores the masked dm
+        and writes bwd_part (+ bwd_part2 for ``second`` = (bn name, y) of a downsample BN); returns the
+        partial row count."""
+        cv = self.convs[conv]
+        st = self.bn_state[bn]
+        e = BnBwdEpilogue()
+        e.y, e.mean, e.invstd, e.mask_mode = ptr(y), ptr(st[0]), ptr(st[1]), mode
+        if mode == 2:
+            e.scale, e.shift = ptr(st[2]), ptr(st[3])
+        else:
+            e.mask_bits = ptr(bits)
+        e.part = ptr(self.bwd_part)
+        if second is not None:
+            st2 = self.bn_state[second[0]]
+            e.y2, e.mean2, e.invstd2, e.part2 = ptr(second[1]), ptr(st2[0]), ptr(st2[1]), ptr(self.bwd_part2)
+        self._launch(cv, 1, lambda: self.L.conv_dgrad_bn(C.byref(cv.desc), self.dt, ptr(dy), ptr(cv.wd), ptr(dm),
+                                                          ptr(addend), C.byref(e), stream()))
+        return self.L.dll.argus_conv_dgrad_bn_rows(C.byref(cv.desc), self.dt)
+
+    def _bn_apply_bwd(self, name, px, ch, dm, y, dy_out, second=None):
+        """dy = ca*dm + cb*y + cc from an already-masked dm (+ the downsample BN's dy2 from the same dm)."""
+        cf = self.bn_coef[name]
+        self._guard(dy_out)
+        y2 = ca2 = cb2 = cc2 = dy2 = None
+        if second is not None:
+            cf2 = self.bn_coef[second[0]]
+            y2, dy2 = second[1], second[2]
+            ca2, cb2, cc2 = cf2[0], cf2[1], cf2[2]
+            self._guard(dy2)
+        self.L.bn_bwd_apply(self.dt, px, ch, ptr(dm), 0, None, ptr(y), None, None, ptr(cf[0]), ptr(cf[1]), ptr(cf[2]),
+                            ptr(dy_out), None, ptr(y2), ptr(ca2), ptr(cb2), ptr(cc2), ptr(dy2), stream())
+
     def _bn_bwd(self, P, G, name, px, ch, dz, mode, mask_src, y, dy_out, dm_out):
         L, dt, s = self.L, self.dt, stream()
         st, cf = self.bn_state[name], self.bn_coef[name]
         L.bn_bwd_reduce(dt, px, ch, ptr(dz), mode, ptr(mask_src), ptr(y), ptr(st[2]), ptr(st[3]), ptr(st[0]),
                         ptr(st[1]), ptr(self.bwd_part), None, None, None, None, s)
-        self._bn_bwd_fin(P, G, name, px, ch, self.bwd_part)
+        self._bn_bwd_fin(P, G, name, px, ch, self.bwd_part, L.dll.argus_bn_bwd_rows(px, ch))
         self._guard(dy_out)
         L.bn_bwd_apply(dt, px, ch, ptr(dz), mode, ptr(mask_src), ptr(y), ptr(st[2]), ptr(st[3]), ptr(cf[0]),
                        ptr(cf[1]), ptr(cf[2]), ptr(dy_out), ptr(dm_out), None, None, None, None, None, s)
 
-    def _bn_bwd_fin(self, P, G, name, px, ch, part):
+    def _bn_bwd_fin(self, P, G, name, px, ch, part, rows):
         st, cf = self.bn_state[name], self.bn_coef[name]
-        rows = self.L.dll.argus_bn_bwd_rows(px, ch)
         self.L.bn_bwd_finalize(ch, rows, ptr(part), px, ptr(P[name + ".weight"]), ptr(st[0]), ptr(st[1]),
                                ptr(G[name + ".weight"]), ptr(G[name + ".bias"]), ptr(cf[0]), ptr(cf[1]), ptr(cf[2]),
                                ptr(self.bn_ws), stream())
-
-    def _bn_bwd_dual(self, P, G, name, name2, px, ch, dz, bits, y, y2, dy_out, dy2_out):
-        """bn3 and the downsample BN of a bottleneck: both outputs were summed before the block ReLU,
-        so they share dm = relu'(out) * dout; one reduce pass and one apply pass serve both."""
-        L, dt, s = self.L, self.dt, stream()
-        st, st2 = self.bn_state[name], self.bn_state[name2]
-        L.bn_bwd_reduce(dt, px, ch, ptr(dz), 3, ptr(bits), ptr(y), None, None, ptr(st[0]), ptr(st[1]),
-                        ptr(self.bwd_part), ptr(y2), ptr(st2[0]), ptr(st2[1]), ptr(self.bwd_part2), s)
-        self._bn_bwd_fin(P, G, name, px, ch, self.bwd_part)
-        self._bn_bwd_fin(P, G, name2, px, ch, self.bwd_part2)
-        cf, cf2 = self.bn_coef[name], self.bn_coef[name2]
-        self._guard(dy_out)
-        self._guard(dy2_out)
-        L.bn_bwd_apply(dt, px, ch, ptr(dz), 3, ptr(bits), ptr(y), None, None, ptr(cf[0]), ptr(cf[1]), ptr(cf[2]),
-                       ptr(dy_out), None, ptr(y2), ptr(cf2[0]), ptr(cf2[1]), ptr(cf2[2]), ptr(dy2_out), s)
 
     def _wgrad(self, conv, x, pro_state, dy, G):
         cv = self.convs[conv]

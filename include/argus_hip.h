@@ -89,6 +89,33 @@ int argus_conv_fwd_stat_tile(const argus_conv_desc* d, int dtype);
  * (the bn_apply ReLU mask: the residual path of a bottleneck, dx += relu'(out) * dout). */
 int argus_conv_dgrad(const argus_conv_desc* d, int dtype, const void* dy, const void* w_dgrad,
                      void* dx, const void* addend, const uint8_t* addend_mask, argus_stream_t stream);
+/* dgrad whose output feeds the backward of a BatchNorm (+ReLU): the BN-backward reduction
+ * (argus_bn_bwd_reduce) runs in the dgrad epilogue instead of as its own pass over dz.
+ * With v = dgrad(dy, w_dgrad) [+ addend] (addend unmasked, may alias dm), the kernel stores
+ * dm = v * mask (mask_mode 2: y*scale+shift > 0, the BN's own ReLU; 3: mask_bits of argus_bn_apply,
+ * a block output) and writes part float2[rows][C] = {sum dm, sum dm*(y-mean)*invstd}, rows =
+ * argus_conv_dgrad_bn_rows(d, dtype) (C = d->c) — the input of argus_bn_bwd_finalize. Optional second
+ * branch (mask_mode 3): y2/mean2/invstd2 -> part2 (the downsample BN of a bottleneck sharing dm).
+ * Replaces the ATen batch_norm_backward reduction behind loss.backward() (argus/train.py:316). */
+typedef struct {
+  const void* y;
+  const float* mean;
+  const float* invstd;
+  int32_t mask_mode;
+  int32_t reserved;
+  const float* scale;
+  const float* shift;
+  const uint8_t* mask_bits;
+  const void* y2;
+  const float* mean2;
+  const float* invstd2;
+  float* part;
+  float* part2;
+} argus_bn_bwd_epilogue;
+int argus_conv_dgrad_bn_rows(const argus_conv_desc* d, int dtype);
+int argus_conv_dgrad_bn(const argus_conv_desc* d, int dtype, const void* dy, const void* w_dgrad,
+                        void* dm, const void* addend, const argus_bn_bwd_epilogue* bn,
+                        argus_stream_t stream);
 /* Tuning knobs (process-wide; for autotuning / experiments): key 0..2 force the row tile (64|128,
  * 0 = heuristic) of pass fwd/dgrad/wgrad, key 3..5 force the column tile, key 6 sets the wgrad
  * split target (workgroups), key 7 the largest K (= taps*C) served by the 4-workgroups-per-CU

@@ -780,3 +780,112 @@ def test_images_u8_layout_matches_fp32_path(cuda, dt):
     want[..., :3] = f32.reshape(N, 3, H, W).permute(0, 2, 3, 1)
     assert torch.equal(out_u8.cpu(), want.to(TDT[dt]))
     assert torch.equal(out_f.cpu(), want.to(TDT[dt]))
+
+
+def _tuned(settings):
+    """Context: set argus_conv_tuning keys, restore the defaults after."""
+    import contextlib
+
+    @contextlib.contextmanager
+    def cm():
+        L = lib()
+        old = {k: L.dll.argus_conv_tuning_get(k) for k in settings}
+        for k, v in settings.items():
+            assert L.dll.argus_conv_tuning(k, v) == 0
+        try:
+            yield
+        finally:
+            for k, v in old.items():
+                L.dll.argus_conv_tuning(k, v)
+    return cm()
+
+
+# (cin, cout, k, stride, hin, n, tuning, kernel the dgrad lands on)
+DGRAD_BN_CASES = [
+    (64, 64, 3, 1, 16, 2, {13: 1}, "conv3x3_halo_kernel<64"),
+    (128, 128, 3, 1, 16, 2, {13: 1}, "conv3x3_halo_kernel<128"),
+    (128, 256, 1, 1, 32, 2, {8: 64, 9: 1}, "igemm_glds_kernel"),
+    (128, 128, 3, 2, 11, 2, {}, "igemm_kernel"),
+    (256, 512, 1, 2, 9, 2, {}, "igemm_kernel"),     # stride-2 1x1: three phases with no taps
+    (64, 256, 1, 1, 12, 3, {}, "igemm_kernel"),
+]
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+def test_conv_dgrad_bn_epilogue(cuda, dt):
+    """argus_conv_dgrad_bn: dm = (dgrad + addend) * relu-mask and the BN-backward column partials
+    {sum dm, sum dm*xhat} (+ the second, downsample branch) vs fp64 torch, on every kernel family the
+    dgrad can land on (halo, glds, register-staged with strided phases and empty phases)."""
+    from argus_amd._lib import BnBwdEpilogue
+    from argus_amd.profiling import KernelTimer
+
+    torch.manual_seed(5)
+    L = lib()
+    for cin, cout, k, s, hin, n, tune, kname in DGRAD_BN_CASES:
+        if dt == "fp32" and kname != "igemm_kernel":
+            continue  # halo / glds are bf16 kernels
+        d, p = _desc(n, hin, hin, cin, cout, k, s)
+        w = torch.randn(cout, k, k, cin) * (2.0 / (k * k * cin)) ** 0.5
+        wf, wt = _prep(d, dt, w.to(cuda), cuda)
+        dy = torch.randn(n, d.ho, d.wo, cout)
+        y = torch.randn(n, hin, hin, cin) * 2 + 0.3
+        y2 = torch.randn(n, hin, hin, cin)
+        mean, invstd = torch.randn(cin) * 0.1 + 0.3, torch.rand(cin) + 0.5
+        mean2, invstd2 = torch.randn(cin) * 0.1, torch.rand(cin) + 0.5
+        sc, sh = torch.randn(cin), torch.randn(cin) * 0.5
+        for mode, dual, with_add in ((2, False, False), (3, False, True), (3, True, True)):
+            add = torch.randn(n, hin, hin, cin)
+            bits_t = torch.randint(0, 256, (n * hin * hin * cin // (8 if dt == "bf16" else 4),), dtype=torch.uint8)
+            g = {t: v.to(cuda) for t, v in dict(mean=mean, invstd=invstd, sc=sc, sh=sh, mean2=mean2,
+                                                 invstd2=invstd2).items()}
+            yg, y2g = y.to(cuda, TDT[dt]), y2.to(cuda, TDT[dt])
+            dm = add.to(cuda, TDT[dt]) if with_add else torch.empty(n, hin, hin, cin, dtype=TDT[dt], device=cuda)
+            bitsg = bits_t.to(cuda)
+            with _tuned(tune):  # the row count depends on the kernel the tuning selects
+                rows = L.dll.argus_conv_dgrad_bn_rows(C.byref(d), DT[dt])
+            part = torch.full((rows, cin, 2), float("nan"), device=cuda)
+            part2 = torch.full((rows, cin, 2), float("nan"), device=cuda)
+            e = BnBwdEpilogue()
+            e.y, e.mean, e.invstd, e.mask_mode, e.part = ptr(yg), ptr(g["mean"]), ptr(g["invstd"]), mode, ptr(part)
+            if mode == 2:
+                e.scale, e.shift = ptr(g["sc"]), ptr(g["sh"])
+            else:
+                e.mask_bits = ptr(bitsg)
+            if dual:
+                e.y2, e.mean2, e.invstd2, e.part2 = ptr(y2g), ptr(g["mean2"]), ptr(g["invstd2"]), ptr(part2)
+            dyg = dy.to(cuda, TDT[dt])
+            with _tuned(tune), KernelTimer() as kt:
+                L.conv_dgrad_bn(C.byref(d), DT[dt], ptr(dyg), ptr(wt), ptr(dm), ptr(dm) if with_add else None,
+                                C.byref(e), stream())
+            torch.cuda.synchronize()
+            assert any(kname in nm for nm in kt.summary()), (kname, list(kt.summary()))
+            # reference
+            v = torch.nn.grad.conv2d_input((n, cin, hin, hin), _q(w, dt).permute(0, 3, 1, 2),
+                                           _q(dy, dt).permute(0, 3, 1, 2), stride=s, padding=p).permute(0, 2, 3, 1)
+            if with_add:
+                v = v + _q(add, dt)
+            yq, y2q = _q(y, dt), _q(y2, dt)
+            if mode == 2:
+                mask = (yq * sc.double() + sh.double()) > 0
+            else:
+                E = 8 if dt == "bf16" else 4
+                bb = bits_t.long().repeat_interleave(E).reshape(n, hin, hin, cin)
+                shift = torch.arange(cin) % E
+                mask = ((bb >> shift) & 1).bool()
+            ref = v * mask
+            got = dm.double().cpu()
+            err = _rel(got, ref)
+            assert err < TOL[dt], (cin, cout, k, s, mode, dt, err)
+            # partials, from the stored dm (what the apply pass will read)
+            xh = (yq - mean.double()) * invstd.double()
+            S, T_ = got.sum((0, 1, 2)), (got * xh).sum((0, 1, 2))
+            pc = part.double().cpu().sum(0)
+            scale = got.abs().sum((0, 1, 2)).max()
+            tol = 1e-5 if dt == "fp32" else 1e-4
+            assert (pc[:, 0] - S).abs().max() <= tol * scale and (pc[:, 1] - T_).abs().max() <= tol * scale * 4, \
+                (cin, cout, mode, dt)
+            if dual:
+                xh2 = (y2q - mean2.double()) * invstd2.double()
+                pc2 = part2.double().cpu().sum(0)
+                assert (pc2[:, 1] - (got * xh2).sum((0, 1, 2))).abs().max() <= tol * scale * 4
+                assert (pc2[:, 0] - S).abs().max() <= tol * scale

@@ -19,6 +19,7 @@ import torch
 
 from oracle import se3
 from oracle.ncamera import build_reference_model
+from tests.stage_checks import stage_checks
 
 pytestmark = pytest.mark.gpu
 
@@ -122,39 +123,8 @@ def test_block_backward_stages_exact(cuda, golden, shape):
     m.train()
     geometric_loss_fn(m(x.to(cuda)), T.to(cuda)).mean().backward()
     eng_debug, eng.debug = eng.debug, None
-    P = dict(m.named_parameters())
-    nchw = lambda t: t.detach().double().cpu().permute(0, 3, 1, 2)  # noqa: E731
-    col = lambda v: v[None, :, None, None]  # noqa: E731
-
-    def bn_bwd(dm, y, mean, invstd, gamma):
-        xh = (y - col(mean)) * col(invstd)
-        n = dm.shape[0] * dm.shape[2] * dm.shape[3]
-        S, Tt = dm.sum((0, 2, 3)), (dm * xh).sum((0, 2, 3))
-        return col(gamma * invstd) * (dm - col(S) / n - xh * col(Tt) / n)
-
-    for idx, (b, a) in enumerate(zip(eng.blocks, eng.act)):
-        pf = b.prefix
-        st = {k: eng.bn_state[pf + k].double().cpu() for k in (".bn1", ".bn2", ".bn3")}
-        gm = {k: P[pf + k + ".weight"].double().cpu() for k in (".bn1", ".bn2", ".bn3")}
-        D = {k: nchw(eng_debug[k + "." + pf]) for k in ("b_dout", "b_dy3", "b_dz2", "b_dy2", "b_dz1", "b_dy1")}
-        out, y3, y2, y1 = nchw(a["out"]), nchw(a["y3"]), nchw(a["y2"]), nchw(a["y1"])
-        checks = {}
-        checks["dy3"] = (D["b_dy3"], bn_bwd(D["b_dout"] * (out > 0), y3, st[".bn3"][0], st[".bn3"][1], gm[".bn3"]))
-        w3 = P[pf + ".conv3.weight"].double().cpu()
-        checks["dz2"] = (D["b_dz2"], torch.nn.grad.conv2d_input(y2.shape, w3, D["b_dy3"]))
-        mask2 = (y2 * col(st[".bn2"][2]) + col(st[".bn2"][3])) > 0
-        checks["dy2"] = (D["b_dy2"], bn_bwd(D["b_dz2"] * mask2, y2, st[".bn2"][0], st[".bn2"][1], gm[".bn2"]))
-        w2 = P[pf + ".conv2.weight"].double().cpu()
-        checks["dz1"] = (D["b_dz1"], torch.nn.grad.conv2d_input(y1.shape, w2, D["b_dy2"], stride=b.stride, padding=1))
-        mask1 = (y1 * col(st[".bn1"][2]) + col(st[".bn1"][3])) > 0
-        checks["dy1"] = (D["b_dy1"], bn_bwd(D["b_dz1"] * mask1, y1, st[".bn1"][0], st[".bn1"][1], gm[".bn1"]))
-        z1 = torch.relu(y1 * col(st[".bn1"][2]) + col(st[".bn1"][3]))
-        z2 = torch.relu(y2 * col(st[".bn2"][2]) + col(st[".bn2"][3]))
-        checks["dW3"] = (P[pf + ".conv3.weight"].grad, torch.nn.grad.conv2d_weight(z2, w3.shape, D["b_dy3"]))
-        checks["dW2"] = (P[pf + ".conv2.weight"].grad,
-                         torch.nn.grad.conv2d_weight(z1, w2.shape, D["b_dy2"], stride=b.stride, padding=1))
-        for k, (got, want) in checks.items():
-            assert _rel(got, want) < 2e-5, (pf, k, _rel(got, want))
+    worst = stage_checks(eng, dict(m.named_parameters()), eng_debug, 2e-5)
+    print("fp32 worst max-relative error per stage:", {k: f"{v:.2e}" for k, v in worst.items()})
 
 
 def test_bf16_forward_tolerance(cuda, golden):

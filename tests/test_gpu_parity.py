@@ -25,6 +25,7 @@ import torch
 import tests.golden.make_golden as mg
 from oracle import se3
 from oracle.ncamera import build_reference_model
+from tests.stage_checks import stage_checks
 
 pytestmark = pytest.mark.gpu
 
@@ -70,11 +71,6 @@ def _oracle_grads(model, x, T, autocast=False):
 
 def _ours(model):
     return {n: p.grad.detach().double().cpu() for n, p in model.named_parameters()}
-
-
-def _rel_max(a, b):
-    a, b = a.detach().double().cpu(), b.detach().double().cpu()
-    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
 
 
 def _rel_l2(a, b):
@@ -142,51 +138,6 @@ def test_damped_fp32_fused_step_tight(cuda):
 
 
 # ------------------------------------------------------------------------------------------------ bf16
-def _stage_checks(eng, P, debug, tol_max):
-    """Re-derive every backward stage of every Bottleneck in fp64 from the engine's own tensors (the
-    ones the kernels consumed) and compare with what the kernels produced."""
-    nchw = lambda t: t.detach().double().cpu().permute(0, 3, 1, 2)  # noqa: E731
-    col = lambda v: v[None, :, None, None]  # noqa: E731
-
-    def bn_bwd(dm, y, mean, invstd, gamma):
-        xh = (y - col(mean)) * col(invstd)
-        n = dm.shape[0] * dm.shape[2] * dm.shape[3]
-        S, Tt = dm.sum((0, 2, 3)), (dm * xh).sum((0, 2, 3))
-        return col(gamma * invstd) * (dm - col(S) / n - xh * col(Tt) / n)
-
-    worst = {}
-    for b, a in zip(eng.blocks, eng.act):
-        pf = b.prefix
-        st = {k: eng.bn_state[pf + k].double().cpu() for k in (".bn1", ".bn2", ".bn3")}
-        gm = {k: P[pf + k + ".weight"].double().cpu() for k in (".bn1", ".bn2", ".bn3")}
-        D = {k: nchw(debug[k + "." + pf]) for k in ("b_dout", "b_dy3", "b_dz2", "b_dy2", "b_dz1", "b_dy1")}
-        out, y3, y2, y1 = nchw(a["out"]), nchw(a["y3"]), nchw(a["y2"]), nchw(a["y1"])
-        z1 = torch.relu(y1 * col(st[".bn1"][2]) + col(st[".bn1"][3]))
-        z2 = torch.relu(y2 * col(st[".bn2"][2]) + col(st[".bn2"][3]))
-        checks = {}
-        if eng.materialize:  # the materialised relu(bn(y)) the conv2/conv3 kernels consumed
-            checks["a1"] = (nchw(a["a1"]), z1)
-            checks["a2"] = (nchw(a["a2"]), z2)
-            z1, z2 = nchw(a["a1"]), nchw(a["a2"])
-        checks["dy3"] = (D["b_dy3"], bn_bwd(D["b_dout"] * (out > 0), y3, st[".bn3"][0], st[".bn3"][1], gm[".bn3"]))
-        w3 = P[pf + ".conv3.weight"].double().cpu()
-        checks["dz2"] = (D["b_dz2"], torch.nn.grad.conv2d_input(y2.shape, w3, D["b_dy3"]))
-        mask2 = (y2 * col(st[".bn2"][2]) + col(st[".bn2"][3])) > 0
-        checks["dy2"] = (D["b_dy2"], bn_bwd(D["b_dz2"] * mask2, y2, st[".bn2"][0], st[".bn2"][1], gm[".bn2"]))
-        w2 = P[pf + ".conv2.weight"].double().cpu()
-        checks["dz1"] = (D["b_dz1"], torch.nn.grad.conv2d_input(y1.shape, w2, D["b_dy2"], stride=b.stride, padding=1))
-        mask1 = (y1 * col(st[".bn1"][2]) + col(st[".bn1"][3])) > 0
-        checks["dy1"] = (D["b_dy1"], bn_bwd(D["b_dz1"] * mask1, y1, st[".bn1"][0], st[".bn1"][1], gm[".bn1"]))
-        checks["dW3"] = (P[pf + ".conv3.weight"].grad, torch.nn.grad.conv2d_weight(z2, w3.shape, D["b_dy3"]))
-        checks["dW2"] = (P[pf + ".conv2.weight"].grad,
-                         torch.nn.grad.conv2d_weight(z1, w2.shape, D["b_dy2"], stride=b.stride, padding=1))
-        for k, (got, want) in checks.items():
-            r = _rel_max(got, want)
-            worst[k] = max(worst.get(k, 0.0), r)
-            assert r < tol_max, (pf, k, r)
-    return worst
-
-
 @pytest.mark.parametrize("shape", ["golden_256", "large_376x672"])
 def test_bf16_block_backward_stages(cuda, golden, shape):
     """The benched bf16 schedule (engine defaults: materialize on, default kernel selection), every
@@ -206,7 +157,7 @@ def test_bf16_block_backward_stages(cuda, golden, shape):
     eng.debug = {}
     geometric_loss_fn(m(x.to(cuda)), T.to(cuda)).mean().backward()
     debug, eng.debug = eng.debug, None
-    worst = _stage_checks(eng, dict(m.named_parameters()), debug, 1e-2)
+    worst = stage_checks(eng, dict(m.named_parameters()), debug, 1e-2)
     print("bf16 worst max-relative error per stage:", {k: f"{v:.2e}" for k, v in worst.items()})
 
 
