@@ -18,7 +18,7 @@ import torch  # noqa: F401  (must precede the CDLL, see module docstring)
 LIB_PATH = Path(os.environ.get("ARGUS_HIP_LIB", Path(__file__).resolve().parent / "libargus_hip.so"))
 
 F32, BF16 = 0, 1
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class ConvDesc(C.Structure):
@@ -31,7 +31,19 @@ class BnBwdEpilogue(C.Structure):
     _fields_ = [("y", C.c_void_p), ("mean", C.c_void_p), ("invstd", C.c_void_p), ("mask_mode", C.c_int32),
                 ("reserved", C.c_int32), ("scale", C.c_void_p), ("shift", C.c_void_p), ("mask_bits", C.c_void_p),
                 ("y2", C.c_void_p), ("mean2", C.c_void_p), ("invstd2", C.c_void_p), ("part", C.c_void_p),
-                ("part2", C.c_void_p)]
+                ("part2", C.c_void_p), ("workspace", C.c_void_p), ("gamma", C.c_void_p), ("dgamma", C.c_void_p),
+                ("dbeta", C.c_void_p), ("ca", C.c_void_p), ("cb", C.c_void_p), ("cc", C.c_void_p),
+                ("gamma2", C.c_void_p), ("dgamma2", C.c_void_p), ("dbeta2", C.c_void_p), ("ca2", C.c_void_p),
+                ("cb2", C.c_void_p), ("cc2", C.c_void_p)]
+
+
+class BnFwdFin(C.Structure):
+    """argus_bn_fwd_fin (include/argus_hip.h)."""
+
+    _fields_ = [("part", C.c_void_p), ("gamma", C.c_void_p), ("beta", C.c_void_p), ("eps", C.c_float),
+                ("momentum", C.c_float), ("running_mean", C.c_void_p), ("running_var", C.c_void_p),
+                ("num_batches_tracked", C.c_void_p), ("mean", C.c_void_p), ("invstd", C.c_void_p),
+                ("scale", C.c_void_p), ("shift", C.c_void_p), ("workspace", C.c_void_p)]
 
 
 _P = C.c_void_p
@@ -54,6 +66,7 @@ SIGNATURES = {
     "argus_conv_weight_prep_batch": (_I, [_I, _I, _P, _I, _P]),
     "argus_conv_fwd": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P, _P]),
     "argus_conv_fwd_stat_rows": (_I, [_DESC, _I]),
+    "argus_conv_fwd_bn": (_I, [_DESC, _I, _P, _P, _P, _P, _P, C.POINTER(BnFwdFin), _P]),
     "argus_conv_fwd_stat_tile": (_I, [_DESC, _I]),
     "argus_conv_tuning": (_I, [_I, _I]),
     "argus_conv_tuning_get": (_I, [_I]),

@@ -615,10 +615,10 @@ using namespace argus;
 
 extern "C" {
 
-// [0, kBnCounterBytes): one ticket counter per 64-channel block (zero at allocation, kept zero by the
-// kernels); then the fp64 group results double2[64][channels].
-static constexpr size_t kBnCounterBytes = 1024;
-size_t argus_bn_workspace_bytes(int channels) { return kBnCounterBytes + (size_t)64 * channels * sizeof(double2); }
+// [0, kBnCounterBytes): ticket counters (zero at allocation, kept zero by the kernels): one per
+// 64-channel block for the finalize kernels, [column tile][65] for the finalize folded into the conv
+// kernels (bnfin.h); then the fp64 group results double2[2 branches][64][channels].
+size_t argus_bn_workspace_bytes(int channels) { return kBnCounterBytes + (size_t)2 * 64 * channels * sizeof(double2); }
 
 int argus_bn_finalize(int C, int rows, int tile_rows, const float* part, int64_t count, const float* gamma,
                       const float* beta, float eps, float momentum, float* rm, float* rv, int64_t* nbt, float* mean,

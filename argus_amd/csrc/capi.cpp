@@ -27,7 +27,7 @@ using namespace argus;
 
 extern "C" {
 
-int argus_abi_version(void) { return 2; }
+int argus_abi_version(void) { return 3; }
 
 const char* argus_last_error(void) { return g_last_error.c_str(); }
 
@@ -70,6 +70,15 @@ int argus_conv_fwd(const argus_conv_desc* d, int dtype, const void* x, const voi
 }
 
 int argus_conv_fwd_stat_rows(const argus_conv_desc* d, int dtype) { return d ? conv_fwd_stat_rows(*d, dtype) : 0; }
+
+int argus_conv_fwd_bn(const argus_conv_desc* d, int dtype, const void* x, const void* w, void* y, const float* sc,
+                      const float* sh, const argus_bn_fwd_fin* fin, argus_stream_t stream) {
+  if (!d || !x || !w || !y || !fin || (sc == nullptr) != (sh == nullptr)) {
+    set_error("conv_fwd_bn: bad arguments");
+    return ARGUS_ERR_ARG;
+  }
+  return conv_fwd_bn(*d, dtype, x, w, y, sc, sh, *fin, (hipStream_t)stream);
+}
 
 int argus_conv_tuning(int key, int value) { return conv_tuning(key, value); }
 int argus_conv_tuning_get(int key) { return conv_tuning_get(key); }

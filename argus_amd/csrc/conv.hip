@@ -83,8 +83,15 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
   const int mtiles = (ph.M + BM - 1) / BM;
   const int ntiles = p.N / BN;
   const int nwg = mtiles * ntiles;
+  __shared__ int fin_flag;
   if ((int)blockIdx.x >= nwg) {
-    if constexpr (BW != 0) bwd_epi_zero_rows<BN, 256>(p.bb, blockIdx.x - nwg, mtiles, ntiles, p.N);
+    if constexpr (BW != 0) {
+      const int e = blockIdx.x - nwg;
+      bwd_epi_zero_rows<BN, 256>(p.bb, e, mtiles, ntiles, p.N);
+      if (p.fin.mode && mtiles + e / ntiles < p.bb.prow)
+        bn_fin_arrive<256, BN>(p.fin, blockIdx.z * p.bb.prow + mtiles + e / ntiles, e % ntiles,
+                               reinterpret_cast<double2*>(lds), &fin_flag);
+    }
     return;
   }
   if (ph.K == 0 && p.addend == p.c && !p.addend_mask && BW == 0) return;  // in-place += 0
@@ -299,9 +306,15 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
         const float d = a0.x / (float)na - a1.x / (float)nb;
         m2 += d * d * ((float)na * (float)nb / (float)(na + nb));
       }
-      p.stats[(size_t)mt * p.N + nt * BN + tid] = make_float2(a0.x + a1.x, m2);
+      store_part(p.stats + (size_t)mt * p.N + nt * BN + tid, make_float2(a0.x + a1.x, m2));
     }
     __syncthreads();
+    // forward finalize: ticket taken before the output stores, so its drain waits only for the
+    // partial row just written
+    if (p.fin.mode == 1) {
+      bn_fin_arrive<256, BN>(p.fin, mt, nt, reinterpret_cast<double2*>(lds), &fin_flag);
+      __syncthreads();
+    }
   }
 
   // ---- epilogue: stage the C tile in LDS, then 16-byte coalesced (+accumulating) stores ----
@@ -331,27 +344,31 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
     }
     __syncthreads();
     const int c = tid % CPR;
+    constexpr int NIT = ROWS / RPP, U = NIT < 4 ? NIT : 4;
+    static_assert(NIT * RPP == ROWS && NIT % U == 0, "epilogue row partition");
 #pragma unroll
-    for (int rr = tid / CPR; rr < ROWS; rr += RPP) {
-      const int m = mt * BM + q * ROWS + rr;
-      if (m < ph.M) {
-        const int nimg = m / HWq, rem = m - nimg * HWq;
+    for (int i0 = 0; i0 < NIT; i0 += U) {
+      size_t off[U];
+      bool ok[U];
+      EpiIn in[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int rr = tid / CPR + RPP * (i0 + u);
+        const int m = mt * BM + q * ROWS + rr;
+        ok[u] = m < ph.M;
+        const int mm = ok[u] ? m : 0;
+        const int nimg = mm / HWq, rem = mm - nimg * HWq;
         const int qh = rem / ph.Wq, qw = rem - qh * ph.Wq;
         const int oh = qh * p.osh + ph.oh0, ow = qw * p.osw + ph.ow0;
-        T* dst = Cg + (((size_t)nimg * p.Ho + oh) * p.Wo + ow) * p.ldc + nt * BN + c * E;
-        u32x4 v = *reinterpret_cast<const u32x4*>(Cs + rr * LD + c * E);
-        if (p.addend) {
-          const size_t off = (size_t)(dst - Cg);
-          float f[E], o[E];
-          unpack(v, f);
-          unpack(ld16(reinterpret_cast<const T*>(p.addend) + off), o);
-          const unsigned mb = p.addend_mask ? p.addend_mask[off / E] : 0xffu;
+        off[u] = (((size_t)nimg * p.Ho + oh) * p.Wo + ow) * p.ldc + nt * BN + c * E;
+        if (ok[u]) epi_load<T, BW>(p, off[u], in[u]);
+      }
 #pragma unroll
-          for (int j = 0; j < E; ++j) f[j] += (mb >> j) & 1u ? o[j] : 0.f;
-          v = pack(f);
-        }
-        if constexpr (BW != 0) v = bwd.step(p.bb, v, (size_t)(dst - Cg));
-        st16_nt(dst, v);
+      for (int u = 0; u < U; ++u) {
+        if (!ok[u]) continue;
+        const int rr = tid / CPR + RPP * (i0 + u);
+        const u32x4 v = *reinterpret_cast<const u32x4*>(Cs + rr * LD + c * E);
+        st16_nt(Cg + off[u], epi_apply<T, BW>(p, v, in[u], bwd));
       }
     }
     if (EPASS > 1) __syncthreads();
@@ -360,6 +377,12 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
     __syncthreads();  // the C staging area becomes the reduction buffer
     bwd.template reduce<BN, 256>(p.bb, reinterpret_cast<float2*>(lds), tid / CPR, RPP, tid % CPR,
                                  (size_t)blockIdx.z * p.bb.prow + mt, p.N, nt * BN);
+  }
+  if constexpr (BW != 0) {
+    if (p.fin.mode == 2) {
+      __syncthreads();
+      bn_fin_arrive<256, BN>(p.fin, blockIdx.z * p.bb.prow + mt, nt, reinterpret_cast<double2*>(lds), &fin_flag);
+    }
   }
 }
 
@@ -790,6 +813,10 @@ __global__ __launch_bounds__(256) void weight_prep_batch_kernel(const WpEntry* _
 // host launchers
 // ------------------------------------------------------------------------------------------------
 
+// argus_conv_fwd_bn hands its finalize arguments to conv_fwd through this (host, one thread per
+// process: the library's contract)
+static const argus_bn_fwd_fin* g_fwd_fin = nullptr;
+
 static int check_desc(const argus_conv_desc& d) {
   if (d.n <= 0 || d.h <= 0 || d.w <= 0 || d.k <= 0 || d.r <= 0 || d.s <= 0 || d.stride <= 0) {
     set_error("conv: non-positive dimension in descriptor");
@@ -824,7 +851,9 @@ static const char* ig_name() {
 }
 
 template <typename T, int BM, int BN, bool STEM, bool PRO, int OCC, int BW = 0>
-static void launch_ig(const IgParams& p, int maxM, hipStream_t st) {
+static void launch_ig(const IgParams& p0, int maxM, hipStream_t st) {
+  IgParams p = p0;
+  plan_fin(p, BM);
   const int ntiles = p.N / BN;
   dim3 grid(cdiv(maxM, BM) * ntiles, 1, p.nphase);
   timed_launch(ig_name<T, BM, BN, STEM, PRO, OCC, BW>(), igemm_kernel<T, BM, BN, STEM, PRO, OCC, BW>, grid,
@@ -997,6 +1026,17 @@ int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, 
   }
   const int bm = fwd_bm(d), bn = d.stem ? 64 : pick_bn(0, d.k);
   p.stat_tile = bm;
+  if (g_fwd_fin && stats) {  // argus_conv_fwd_bn: the statistics finalize folded into this launch
+    const argus_bn_fwd_fin& f = *g_fwd_fin;
+    BnFin& b = p.fin;
+    b.mode = 1; b.C = d.k; b.count = (long long)d.n * d.ho * d.wo; b.tile_rows = bm;
+    b.cnt = reinterpret_cast<unsigned*>(f.workspace);
+    b.red = reinterpret_cast<double2*>(reinterpret_cast<char*>(f.workspace) + kBnCounterBytes);
+    b.part = reinterpret_cast<const float2*>(f.part);
+    b.gamma = f.gamma; b.beta = f.beta; b.eps = f.eps; b.momentum = f.momentum;
+    b.rm = f.running_mean; b.rv = f.running_var; b.nbt = reinterpret_cast<long long*>(f.num_batches_tracked);
+    b.mean = f.mean; b.invstd = f.invstd; b.scale = f.scale; b.shift = f.shift;
+  }
   return dtype == ARGUS_BF16 ? run_ig<bf16>(p, st, bm, bn) : run_ig<float>(p, st, bm, bn);
 }
 
@@ -1055,6 +1095,19 @@ static void dgrad_work(const argus_conv_desc& d, int dtype, bool addend, bool ma
                    (bn ? E * px_in * (dual ? 2.0 : 1.0) : 0.0);  // BN input(s) y read by the epilogue
 }
 
+int conv_fwd_bn(const argus_conv_desc& d, int dtype, const void* x, const void* w, void* y, const float* sc,
+                const float* sh, const argus_bn_fwd_fin& f, hipStream_t st) {
+  if (!f.part || !f.gamma || !f.beta || !f.mean || !f.invstd || !f.scale || !f.shift || !f.workspace) {
+    set_error("conv_fwd_bn: bad finalize arguments");
+    return ARGUS_ERR_ARG;
+  }
+  if (d.k / 64 * 65 * 4 > (int)kBnCounterBytes) { set_error("conv_fwd_bn: too many channels"); return ARGUS_ERR_ARG; }
+  g_fwd_fin = &f;
+  const int rc = conv_fwd(d, dtype, x, w, y, sc, sh, f.part, st);
+  g_fwd_fin = nullptr;
+  return rc;
+}
+
 int conv_dgrad(const argus_conv_desc& d, int dtype, const void* dy, const void* wt, void* dx,
                const void* addend, const uint8_t* addend_mask, hipStream_t st) {
   if (int e = check_desc(d)) return e;
@@ -1092,6 +1145,22 @@ int conv_dgrad_bn(const argus_conv_desc& d, int dtype, const void* dy, const voi
   b.part = reinterpret_cast<float2*>(bn->part); b.part2 = reinterpret_cast<float2*>(bn->part2);
   b.mode = bn->mask_mode;
   b.prow = dgrad_prow(p, dtype, d);
+  if (bn->workspace) {  // the BN-backward finalize folded into this launch
+    if (!bn->gamma || !bn->ca || !bn->cb || !bn->cc || (bn->y2 && (!bn->gamma2 || !bn->ca2 || !bn->cb2 || !bn->cc2)) ||
+        d.c / 64 * 65 * 4 > (int)kBnCounterBytes) {
+      set_error("conv_dgrad_bn: bad finalize arguments");
+      return ARGUS_ERR_ARG;
+    }
+    BnFin& f = p.fin;
+    f.mode = 2; f.C = d.c; f.count = (long long)d.n * d.h * d.w;
+    f.cnt = reinterpret_cast<unsigned*>(bn->workspace);
+    f.red = reinterpret_cast<double2*>(reinterpret_cast<char*>(bn->workspace) + kBnCounterBytes);
+    f.part = reinterpret_cast<const float2*>(bn->part); f.part2 = reinterpret_cast<const float2*>(bn->part2);
+    f.gamma = bn->gamma; f.bmean = bn->mean; f.binvstd = bn->invstd;
+    f.dgamma = bn->dgamma; f.dbeta = bn->dbeta; f.ca = bn->ca; f.cb = bn->cb; f.cc = bn->cc;
+    f.gamma2 = bn->gamma2; f.bmean2 = bn->mean2; f.binvstd2 = bn->invstd2;
+    f.dgamma2 = bn->dgamma2; f.dbeta2 = bn->dbeta2; f.ca2 = bn->ca2; f.cb2 = bn->cb2; f.cc2 = bn->cc2;
+  }
   const int bm = dgrad_bm(d), bn_ = pick_bn(1, d.c);
   return dtype == ARGUS_BF16 ? run_ig<bf16>(p, st, bm, bn_) : run_ig<float>(p, st, bm, bn_);
 }

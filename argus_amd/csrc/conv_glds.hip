@@ -61,8 +61,15 @@ __global__ __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) void igemm_glds_kern
   const int mtiles = (ph.M + BM - 1) / BM;
   const int ntiles = p.N / BN;
   const int nwg = mtiles * ntiles;
+  __shared__ int fin_flag;
   if ((int)blockIdx.x >= nwg) {
-    if constexpr (BW != 0) bwd_epi_zero_rows<BN, NT>(p.bb, blockIdx.x - nwg, mtiles, ntiles, p.N);
+    if constexpr (BW != 0) {
+      const int e = blockIdx.x - nwg;
+      bwd_epi_zero_rows<BN, NT>(p.bb, e, mtiles, ntiles, p.N);
+      if (p.fin.mode && mtiles + e / ntiles < p.bb.prow)
+        bn_fin_arrive<NT, BN>(p.fin, blockIdx.z * p.bb.prow + mtiles + e / ntiles, e % ntiles,
+                              reinterpret_cast<double2*>(lds), &fin_flag);
+    }
     return;
   }
   if (ph.K == 0 && p.addend == p.c && !p.addend_mask && BW == 0) return;  // in-place += 0
@@ -186,7 +193,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) void igemm_glds_kern
       q += __shfl_xor(q, 32, 64);
       if (p.stat_tile == 64) {  // a wave's 64 rows are one partial row
         if (lane < 16 && nvalid_w > 0)
-          p.stats[(size_t)(mt * WM + wm) * p.N + nt * BN + wn * 64 + ni * 16 + lane] = make_float2(s, q);
+          store_part(p.stats + (size_t)(mt * WM + wm) * p.N + nt * BN + wn * 64 + ni * 16 + lane, make_float2(s, q));
       } else if (lane < 16) {
         red[wm * BN + wn * 64 + ni * 16 + lane] = make_float2(s, q);
       }
@@ -208,9 +215,13 @@ __global__ __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) void igemm_glds_kern
         const float d = a0.x / (float)na - a1.x / (float)nb;
         m2 += d * d * ((float)na * (float)nb / (float)(na + nb));
       }
-      p.stats[(size_t)(mt * HALVES + h) * p.N + nt * BN + col] = make_float2(a0.x + a1.x, m2);
+      store_part(p.stats + (size_t)(mt * HALVES + h) * p.N + nt * BN + col, make_float2(a0.x + a1.x, m2));
     }
     __syncthreads();
+    if (p.fin.mode == 1) {  // before the output stores (see conv.hip)
+      bn_fin_arrive<NT, BN>(p.fin, mt, nt, reinterpret_cast<double2*>(lds), &fin_flag);
+      __syncthreads();
+    }
   }
 
   // ---- epilogue: stage the C tile in LDS, then 16-byte coalesced (+addend) stores ----
@@ -232,32 +243,42 @@ __global__ __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) void igemm_glds_kern
   const int c = tid % CPR;
   BwdEpiAcc<bf16, BW> bwd;
   if constexpr (BW != 0) bwd.init(p.bb, nt * BN + c * 8);
-#pragma unroll 4
-  for (int rr = tid / CPR; rr < BM; rr += RPP) {
-    const int m = mt * BM + rr;
-    if (m >= ph.M) continue;
-    const int nimg = m / HWq, rem = m - nimg * HWq;
-    const int qh = rem / ph.Wq, qw = rem - qh * ph.Wq;
-    const int oh = qh * p.osh + ph.oh0, ow = qw * p.osw + ph.ow0;
-    bf16* dst = Cg + (((size_t)nimg * p.Ho + oh) * p.Wo + ow) * p.ldc + nt * BN + c * 8;
-    u32x4 v = *reinterpret_cast<const u32x4*>(Cs + rr * LD + c * 8);
-    if (p.addend) {
-      const size_t off = (size_t)(dst - Cg);
-      float f[8], o[8];
-      unpack(v, f);
-      unpack(ld16(reinterpret_cast<const bf16*>(p.addend) + off), o);
-      const unsigned mb = p.addend_mask ? p.addend_mask[off / 8] : 0xffu;
+  constexpr int NIT = BM / RPP, U = 4;
+  static_assert(NIT * RPP == BM && NIT % U == 0, "epilogue row partition");
+  for (int i0 = 0; i0 < NIT; i0 += U) {
+    size_t off[U];
+    bool ok[U];
+    EpiIn in[U];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] += (mb >> j) & 1u ? o[j] : 0.f;
-      v = pack(f);
+    for (int u = 0; u < U; ++u) {
+      const int rr = tid / CPR + RPP * (i0 + u);
+      const int m = mt * BM + rr;
+      ok[u] = m < ph.M;
+      const int mm = ok[u] ? m : 0;
+      const int nimg = mm / HWq, rem = mm - nimg * HWq;
+      const int qh = rem / ph.Wq, qw = rem - qh * ph.Wq;
+      const int oh = qh * p.osh + ph.oh0, ow = qw * p.osw + ph.ow0;
+      off[u] = (((size_t)nimg * p.Ho + oh) * p.Wo + ow) * p.ldc + nt * BN + c * 8;
+      if (ok[u]) epi_load<bf16, BW>(p, off[u], in[u]);
     }
-    if constexpr (BW != 0) v = bwd.step(p.bb, v, (size_t)(dst - Cg));
-    st16_nt(dst, v);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (!ok[u]) continue;
+      const int rr = tid / CPR + RPP * (i0 + u);
+      const u32x4 v = *reinterpret_cast<const u32x4*>(Cs + rr * LD + c * 8);
+      st16_nt(Cg + off[u], epi_apply<bf16, BW>(p, v, in[u], bwd));
+    }
   }
   if constexpr (BW != 0) {
     __syncthreads();
     bwd.template reduce<BN, NT>(p.bb, reinterpret_cast<float2*>(lds), tid / CPR, RPP, c,
                                 (size_t)blockIdx.z * p.bb.prow + mt, p.N, nt * BN);
+  }
+  if constexpr (BW != 0) {
+    if (p.fin.mode == 2) {
+      __syncthreads();
+      bn_fin_arrive<NT, BN>(p.fin, blockIdx.z * p.bb.prow + mt, nt, reinterpret_cast<double2*>(lds), &fin_flag);
+    }
   }
 }
 
@@ -269,7 +290,9 @@ static const char* glds_name() {
 }
 
 template <int BM, int BN, int BW>
-static void launch_glds1(const IgParams& p, int maxM, hipStream_t st) {
+static void launch_glds1(const IgParams& p0, int maxM, hipStream_t st) {
+  IgParams p = p0;
+  plan_fin(p, BM);
   dim3 grid(cdiv(maxM, BM) * (p.N / BN), 1, p.nphase);
   timed_launch(glds_name<BM, BN, BW>(), igemm_glds_kernel<BM, BN, BW>, grid, dim3((BM / 64) * (BN / 64) * 64), st,
                p);

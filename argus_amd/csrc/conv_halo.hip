@@ -244,7 +244,7 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, 1) void conv3x3_halo_kernel(con
       q += __shfl_xor(q, 32, 64);
       const int col = wn * 64 + ni * 16 + lane;
       if (p.stat_tile == 64) {
-        if (lane < 16) p.stats[(size_t)(mt * 4 + wm) * p.N + nt * BN + col] = make_float2(s, q);
+        if (lane < 16) store_part(p.stats + (size_t)(mt * 4 + wm) * p.N + nt * BN + col, make_float2(s, q));
       } else if (lane < 16) {
         red[wm * BN + col] = make_float2(s, q);
       }
@@ -255,10 +255,16 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, 1) void conv3x3_halo_kernel(con
         const int h = idx / BN, col = idx - h * BN;
         const float2 a0 = red[(2 * h) * BN + col], a1 = red[(2 * h + 1) * BN + col];
         const float d = (a0.x - a1.x) * (1.f / 64.f);
-        p.stats[(size_t)(mt * 2 + h) * p.N + nt * BN + col] = make_float2(a0.x + a1.x, a0.y + a1.y + d * d * 32.f);
+        store_part(p.stats + (size_t)(mt * 2 + h) * p.N + nt * BN + col,
+                   make_float2(a0.x + a1.x, a0.y + a1.y + d * d * 32.f));
       }
     }
     __syncthreads();
+    if (p.fin.mode == 1) {  // before the output stores (see conv.hip)
+      bn_fin_arrive<NT, BN>(p.fin, mt, nt, reinterpret_cast<double2*>(lds),
+                            reinterpret_cast<int*>(reinterpret_cast<char*>(lds) + NT * 32));
+      __syncthreads();
+    }
   }
 
   // ---- epilogue: LDS-staged C tile, 16-byte coalesced (+addend) stores; output pixels are contiguous ----
@@ -276,25 +282,32 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, 1) void conv3x3_halo_kernel(con
   const int c = tid % CPR;
   BwdEpiAcc<bf16, BW> bwd;
   if constexpr (BW != 0) bwd.init(p.bb, nt * BN + c * 8);
-#pragma unroll 4
-  for (int rr = tid / CPR; rr < 256; rr += RPP) {
-    const size_t off = (size_t)(mt * 256 + rr) * p.ldc + nt * BN + c * 8;
-    u32x4 v = *reinterpret_cast<const u32x4*>(Cs + rr * LD + c * 8);
-    if (p.addend) {
-      float f[8], o[8];
-      unpack(v, f);
-      unpack(ld16(reinterpret_cast<const bf16*>(p.addend) + off), o);
-      const unsigned mb = p.addend_mask ? p.addend_mask[off / 8] : 0xffu;
+  constexpr int NIT = 256 / RPP, U = 4;
+  static_assert(NIT * RPP == 256 && NIT % U == 0, "epilogue row partition");
+  for (int i0 = 0; i0 < NIT; i0 += U) {
+    size_t off[U];
+    EpiIn in[U];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] += (mb >> j) & 1u ? o[j] : 0.f;
-      v = pack(f);
+    for (int u = 0; u < U; ++u) {
+      const int rr = tid / CPR + RPP * (i0 + u);
+      off[u] = (size_t)(mt * 256 + rr) * p.ldc + nt * BN + c * 8;
+      epi_load<bf16, BW>(p, off[u], in[u]);
     }
-    if constexpr (BW != 0) v = bwd.step(p.bb, v, off);
-    st16_nt(Cg + off, v);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int rr = tid / CPR + RPP * (i0 + u);
+      const u32x4 v = *reinterpret_cast<const u32x4*>(Cs + rr * LD + c * 8);
+      st16_nt(Cg + off[u], epi_apply<bf16, BW>(p, v, in[u], bwd));
+    }
   }
   if constexpr (BW != 0) {
     __syncthreads();
     bwd.template reduce<BN, NT>(p.bb, reinterpret_cast<float2*>(lds), tid / CPR, RPP, c, (size_t)mt, p.N, nt * BN);
+  }
+  if (p.fin.mode == 2) {  // LDS is free now: scratch [2 NT] double2, then the ticket flag
+    __syncthreads();
+    bn_fin_arrive<NT, BN>(p.fin, mt, nt, reinterpret_cast<double2*>(lds),
+                          reinterpret_cast<int*>(reinterpret_cast<char*>(lds) + NT * 32));
   }
 }
 
@@ -306,7 +319,9 @@ static const char* halo_name() {
 }
 
 template <int BN, bool PRO, int BW>
-static void launch_halo1(const IgParams& p, hipStream_t st) {
+static void launch_halo1(const IgParams& p0, hipStream_t st) {
+  IgParams p = p0;
+  plan_fin(p, 256);
   dim3 grid((p.ph[0].M / 256) * (p.N / BN));
   timed_launch(halo_name<BN, PRO, BW>(), conv3x3_halo_kernel<BN, PRO, BW>, grid, dim3(4 * (BN / 64) * 64), st, p);
 }

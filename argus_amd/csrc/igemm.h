@@ -2,6 +2,7 @@
 // global->LDS (glds) kernel (conv_glds.hip).
 #pragma once
 #include "common.h"
+#include "bnfin.h"
 #include "../../include/argus_hip.h"
 
 namespace argus {
@@ -46,6 +47,7 @@ struct IgParams {
   int stat_tile;  // rows per BN-statistics partial (forward with stats)
   IgPhase ph[4];
   BnBwdEpi bb;    // dgrad only
+  BnFin fin;      // BN finalize folded into this launch (fin.mode != 0)
 };
 
 struct WgParams {
@@ -116,17 +118,17 @@ struct BwdEpiAcc {
     for (int j = 0; j < E; ++j) { s[j] = 0.f; t[j] = 0.f; }
   }
 
-  // v = the output chunk as it would be stored (rounded to T), at element offset off of the output
-  // (the BN input y has the same layout): returns the masked chunk dm and accumulates the sums.
-  ARGUS_DEV u32x4 step(const BnBwdEpi& b, u32x4 v, size_t off) {
+  // v = the output chunk as it would be stored (rounded to T); yv / y2v / mb = the BN input chunk(s)
+  // and mask byte at the same element offset (loaded by epi_load): returns the masked chunk dm and
+  // accumulates the column sums.
+  ARGUS_DEV u32x4 step(u32x4 v, u32x4 yraw, u32x4 y2raw, unsigned mb) {
     float d[E], yv[E];
     unpack(v, d);
-    unpack(ld16(reinterpret_cast<const T*>(b.y) + off), yv);
+    unpack(yraw, yv);
     if constexpr (BwdMode<BW>::RECOMPUTE) {
 #pragma unroll
       for (int j = 0; j < E; ++j) d[j] = fmaf(yv[j], S[j], H[j]) > 0.f ? d[j] : 0.f;
     } else {
-      const unsigned mb = b.bits[off / E];
 #pragma unroll
       for (int j = 0; j < E; ++j) d[j] = (mb >> j) & 1u ? d[j] : 0.f;
     }
@@ -137,7 +139,7 @@ struct BwdEpiAcc {
     }
     if constexpr (BwdMode<BW>::DUAL) {
       float y2v[E];
-      unpack(ld16(reinterpret_cast<const T*>(b.y2) + off), y2v);
+      unpack(y2raw, y2v);
 #pragma unroll
       for (int j = 0; j < E; ++j) t2[j] = fmaf(d[j], (y2v[j] - mu2[j]) * is2[j], t2[j]);
     }
@@ -161,12 +163,63 @@ struct BwdEpiAcc {
       for (int idx = threadIdx.x; idx < COLS; idx += NT) {
         float2 a = red[idx];
         for (int g = 1; g < RG; ++g) { a.x += red[g * COLS + idx].x; a.y += red[g * COLS + idx].y; }
-        out[idx] = a;
+        store_part(out + idx, a);  // write-through: the folded finalize (bnfin.h) reads it cross-CU
       }
       __syncthreads();
     }
   }
 };
+
+// Global operands of one epilogue output chunk (addend, BN-backward inputs). The conv epilogues load
+// them for a batch of rows before storing any (epi_load, then epi_apply): the addend may alias the
+// output, so loads could not otherwise be hoisted above earlier rows' stores, and one dependent HBM
+// round trip per row left the epilogue latency-bound.
+struct EpiIn {
+  u32x4 add, y, y2;
+  unsigned amask, bits;
+};
+
+template <typename T, int BW>
+ARGUS_DEV void epi_load(const IgParams& p, size_t off, EpiIn& in) {
+  constexpr int E = Chunk<T>::E;
+  if (p.addend) {
+    in.add = ld16(reinterpret_cast<const T*>(p.addend) + off);
+    in.amask = p.addend_mask ? p.addend_mask[off / E] : 0xffu;
+  }
+  if constexpr (BW != 0) {
+    in.y = ld16(reinterpret_cast<const T*>(p.bb.y) + off);
+    if constexpr (!BwdMode<BW>::RECOMPUTE) in.bits = p.bb.bits[off / E];
+    if constexpr (BwdMode<BW>::DUAL) in.y2 = ld16(reinterpret_cast<const T*>(p.bb.y2) + off);
+  }
+}
+
+template <typename T, int BW>
+ARGUS_DEV u32x4 epi_apply(const IgParams& p, u32x4 v, const EpiIn& in, BwdEpiAcc<T, BW>& bwd) {
+  constexpr int E = Chunk<T>::E;
+  if (p.addend) {
+    float f[E], o[E];
+    unpack(v, f);
+    unpack(in.add, o);
+#pragma unroll
+    for (int j = 0; j < E; ++j) f[j] += (in.amask >> j) & 1u ? o[j] : 0.f;
+    v = pack(f);
+  }
+  if constexpr (BW != 0) v = bwd.step(v, in.y, in.y2, in.bits);
+  return v;
+}
+
+// host: group plan of a folded BN finalize for a launch whose row tile is tile_m pixels
+inline void plan_fin(IgParams& p, int tile_m) {
+  if (!p.fin.mode) return;
+  if (p.fin.mode == 1) {  // forward: one phase; partial rows of stat_tile pixels
+    const int M = p.ph[0].M;
+    bn_fin_plan(p.fin, (M + tile_m - 1) / tile_m, tile_m / p.stat_tile);
+    p.fin.rows = (M + p.stat_tile - 1) / p.stat_tile;
+  } else {  // backward: one partial row per (phase, row tile)
+    bn_fin_plan(p.fin, p.nphase * p.bb.prow, 1);
+    p.fin.rows = p.fin.T;
+  }
+}
 
 // host: the epilogue variant of a BnBwdEpi (0 when off)
 inline int bwd_variant(const BnBwdEpi& b) { return b.mode == 0 ? 0 : (b.mode == 2 ? 2 : (b.y2 ? 4 : 3)); }
@@ -179,8 +232,8 @@ ARGUS_DEV void bwd_epi_zero_rows(const BnBwdEpi& b, int e, int mtiles, int ntile
   if (mt >= b.prow) return;
   const size_t row = (size_t)blockIdx.z * b.prow + mt;
   for (int idx = threadIdx.x; idx < COLS; idx += NT) {
-    b.part[row * N + nt * COLS + idx] = make_float2(0.f, 0.f);
-    if (b.y2) b.part2[row * N + nt * COLS + idx] = make_float2(0.f, 0.f);
+    store_part(b.part + row * N + nt * COLS + idx, make_float2(0.f, 0.f));  // write-through (bnfin.h)
+    if (b.y2) store_part(b.part2 + row * N + nt * COLS + idx, make_float2(0.f, 0.f));
   }
 }
 

@@ -15,6 +15,10 @@ int check_launch(const char* what);
 int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, void* y,
              const float* sc, const float* sh, float* stats, hipStream_t st);
 int conv_fwd_stat_rows(const argus_conv_desc& d, int dtype);
+int conv_fwd_bn(const argus_conv_desc& d, int dtype, const void* x, const void* w, void* y, const float* sc,
+                const float* sh, const argus_bn_fwd_fin& fin, hipStream_t st);
+// BN workspace layout (bn.hip): [0, kBnCounterBytes) ticket counters, then double2 group results
+constexpr size_t kBnCounterBytes = 16384;
 int conv_fwd_stat_tile(const argus_conv_desc& d, int dtype);
 int conv_tuning(int key, int value);
 int conv_tuning_get(int key);

@@ -27,7 +27,7 @@ from dataclasses import dataclass
 
 import torch
 
-from argus_amd._lib import BF16, F32, BnBwdEpilogue, ConvDesc, lib, ptr, stream
+from argus_amd._lib import BF16, F32, BnBwdEpilogue, BnFwdFin, ConvDesc, lib, ptr, stream
 
 
 @dataclass(frozen=True)
@@ -94,6 +94,12 @@ class ResNetEngine:
         # each bucket all-reduce (on_ready's join) and backward() joins it at its end.
         # ARGUS_WGRAD_STREAM=0 keeps everything on the caller's stream.
         self.wgrad_overlap = os.environ.get("ARGUS_WGRAD_STREAM", "1") != "0"
+        # BN finalize (forward statistics and backward coefficients) folded into the producing conv
+        # launch (argus_conv_fwd_bn / argus_conv_dgrad_bn with a workspace); ARGUS_FOLD_FIN=0 keeps the
+        # separate finalize kernels (A/B measurements, tests)
+        fold = os.environ.get("ARGUS_FOLD_FIN", "bwd")  # A/B at B=64: fwd fold neutral, bwd +0.3 %
+        self.fold_fin_fwd = fold in ("1", "fwd")
+        self.fold_fin = fold in ("1", "bwd")  # backward
         self._side: torch.cuda.Stream | None = None
         self._pending: dict = {}  # dy data_ptr -> event of the last side-stream wgrad reading it
         self._last_side = None
@@ -202,7 +208,13 @@ class ResNetEngine:
         ws = max(L.dll.argus_conv_wgrad_workspace_bytes(C.byref(cv.desc), dt) for cv in convs.values())
         self.wg_ws = torch.empty(ws, dtype=torch.uint8, device=self.device)
         self.wg_ws_bytes = ws
-        self.gbuf = [self._t(max_elems) for _ in range(6)]
+        self.gbuf = [self._t(max_elems) for _ in range(3)]  # dh / dx ping-pong, dz
+        # dy operands of the side-stream weight gradients come from a ring, so the main stream can
+        # run ahead of the wgrad stream by several layers before it must wait to reuse a buffer
+        # (ARGUS_DY_RING buffers; a reuse waits on the event of the wgrad that last read it)
+        nring = max(2, int(os.environ.get("ARGUS_DY_RING", "8")))
+        self.dyring = [self._t(max_elems) for _ in range(nring)]
+        self._ring_i = 0
 
         Fd = 512 * 4
         self.feat = self._f(N, Fd)
@@ -244,6 +256,15 @@ class ResNetEngine:
         if pro is not None:
             sc, sh = self.bn_state[pro][2], self.bn_state[pro][3]
         part = self.stat_part if part is None else part
+        ws = self.bn_ws if ws is None else ws
+        if training and self.fold_fin_fwd:  # BN statistics finalize folded into the conv launch
+            st = self.bn_state[bn]
+            f = BnFwdFin(ptr(part), ptr(P[bn + ".weight"]), ptr(P[bn + ".bias"]), Bf.get(bn + ".eps", 1e-5),
+                         Bf.get(bn + ".momentum", 0.1), ptr(Bf[bn + ".running_mean"]), ptr(Bf[bn + ".running_var"]),
+                         ptr(Bf[bn + ".num_batches_tracked"]), ptr(st[0]), ptr(st[1]), ptr(st[2]), ptr(st[3]), ptr(ws))
+            self._launch(cv, 0, lambda: self.L.conv_fwd_bn(C.byref(cv.desc), self.dt, ptr(x), ptr(cv.wf), ptr(y),
+                                                            ptr(sc), ptr(sh), C.byref(f), stream()))
+            return
         self._launch(cv, 0, lambda: self.L.conv_fwd(C.byref(cv.desc), self.dt, ptr(x), ptr(cv.wf), ptr(y), ptr(sc),
                                                      ptr(sh), ptr(part) if training else None, stream()))
         if training:
@@ -394,7 +415,7 @@ class ResNetEngine:
         L.gemm_f32(N, 2048, R, ptr(self.dh0), R, 0, ptr(fcw), 2048, 0, ptr(self.dfeat), 2048, None, 0, None, ptr(self.gemm_ws), self.gemm_ws.numel(), s)
         hf, wf = self.final_hw
         g = self.gbuf
-        dh, dx = g[0], g[3]
+        dh, dx = g[0], g[1]
         L.avgpool_bwd(dt, N, hf * wf, 2048, ptr(self.dfeat), ptr(dh), s)
         if on_ready is not None:
             on_ready("resnet.fc.weight", self._join)
@@ -415,7 +436,9 @@ class ResNetEngine:
             ho, wo = a["hw"]
             px_o = N * ho * wo
             px_i = N * hi * wi
-            dy3, dyd, dz, dyw = g[1], g[2], g[4], g[5]
+            dz = g[2]
+            dy3 = self._next_dy()
+            dyd = self._next_dy() if b.has_ds else None
             dbg = self.debug
 
             def cap(key, t, n, shape):
@@ -435,9 +458,10 @@ class ResNetEngine:
                 L.bn_bwd_apply(dt, px_o, b.cout, ptr(dh), 3, ptr(a["bits"]), ptr(a["y3"]), None, None, ptr(cf[0]),
                                ptr(cf[1]), ptr(cf[2]), ptr(dy3), ptr(dh), None, None, None, None, None, s)
             else:
-                self._bn_bwd_fin(P, G, pf + ".bn3", px_o, b.cout, self.bwd_part, rows3)
-                if b.has_ds:
-                    self._bn_bwd_fin(P, G, pf + ".downsample.1", px_o, b.cout, self.bwd_part2, rows3)
+                if rows3:  # not folded into the producing dgrad
+                    self._bn_bwd_fin(P, G, pf + ".bn3", px_o, b.cout, self.bwd_part, rows3)
+                    if b.has_ds:
+                        self._bn_bwd_fin(P, G, pf + ".downsample.1", px_o, b.cout, self.bwd_part2, rows3)
                 self._bn_apply_bwd(pf + ".bn3", px_o, b.cout, dh, a["y3"], dy3,
                                    (pf + ".downsample.1", a["yd"], dyd) if b.has_ds else None)
             cap("b_dy3", dy3, px_o * b.cout, (N, ho, wo, b.cout))
@@ -449,9 +473,11 @@ class ResNetEngine:
                 self._wgrad(pf + ".conv3", a["a2"], None, dy3, G)
             else:
                 self._wgrad(pf + ".conv3", a["y2"], s2, dy3, G)
-            r2 = self._dgrad_bn(pf + ".conv3", dy3, dz, None, pf + ".bn2", a["y2"], 2)
+            r2 = self._dgrad_bn(pf + ".conv3", dy3, dz, None, pf + ".bn2", a["y2"], 2, P=P, G=G)
             cap("b_dz2", dz, px_o * b.width, (N, ho, wo, b.width))
-            self._bn_bwd_fin(P, G, pf + ".bn2", px_o, b.width, self.bwd_part, r2)
+            if r2:
+                self._bn_bwd_fin(P, G, pf + ".bn2", px_o, b.width, self.bwd_part, r2)
+            dyw = self._next_dy()
             self._bn_apply_bwd(pf + ".bn2", px_o, b.width, dz, a["y2"], dyw)
             cap("b_dy2", dyw, px_o * b.width, (N, ho, wo, b.width))
             # conv2 -> bn1
@@ -460,9 +486,11 @@ class ResNetEngine:
                 self._wgrad(pf + ".conv2", a["a1"], None, dyw, G)
             else:
                 self._wgrad(pf + ".conv2", a["y1"], s1, dyw, G)
-            r1 = self._dgrad_bn(pf + ".conv2", dyw, dz, None, pf + ".bn1", a["y1"], 2)
+            r1 = self._dgrad_bn(pf + ".conv2", dyw, dz, None, pf + ".bn1", a["y1"], 2, P=P, G=G)
             cap("b_dz1", dz, px_i * b.width, (N, hi, wi, b.width))
-            self._bn_bwd_fin(P, G, pf + ".bn1", px_i, b.width, self.bwd_part, r1)
+            if r1:
+                self._bn_bwd_fin(P, G, pf + ".bn1", px_i, b.width, self.bwd_part, r1)
+            dyw = self._next_dy()
             self._bn_apply_bwd(pf + ".bn1", px_i, b.width, dz, a["y1"], dyw)
             cap("b_dy1", dyw, px_i * b.width, (N, hi, wi, b.width))
             # conv1 (+ downsample) -> the previous block's bn3 (+ its downsample BN): dm3 of block idx-1
@@ -475,7 +503,7 @@ class ResNetEngine:
             if idx > 0:
                 pb, pa = self.blocks[idx - 1], self.act[idx - 1]
                 rows3 = self._dgrad_bn(last_conv, last_dy, dx, addend, pb.prefix + ".bn3", pa["y3"], 3, pa["bits"],
-                                       (pb.prefix + ".downsample.1", pa["yd"]) if pb.has_ds else None)
+                                       (pb.prefix + ".downsample.1", pa["yd"]) if pb.has_ds else None, P=P, G=G)
             else:
                 self._dgrad(last_conv, last_dy, dx, addend=addend)
             dh, dx = dx, dh
@@ -486,7 +514,7 @@ class ResNetEngine:
                 self.debug["bwd." + pf] = dh[:n_in].view(N, hi, wi, b.cin).clone()
         # stem: maxpool -> relu/bn1 -> conv1 wgrad
         H1, W1 = self.stem_hw
-        dz0, dy0 = g[4], g[5]
+        dz0, dy0 = g[2], self._next_dy()
         L.maxpool_bwd(dt, N, H1, W1, 64, ptr(dh), ptr(self.amax), ptr(dz0), s)
         self._bn_bwd(P, G, "resnet.bn1", N * H1 * W1, 64, dz0, 2, None, self.y0, dy0, None)
         self._wgrad("resnet.conv1", self.x0, None, dy0, G)
@@ -494,13 +522,24 @@ class ResNetEngine:
         if on_ready is not None:
             on_ready("resnet.conv1.weight", self._join)
 
-    def _dgrad_bn(self, conv, dy, dm, addend, bn, y, mode, bits=None, second=None):
+    def _dgrad_bn(self, conv, dy, dm, addend, bn, y, mode, bits=None, second=None, P=None, G=None):
         """dgrad of ``conv`` whose output feeds BN ``bn`` (input ``y``) backward: stores the masked dm
         and writes bwd_part (+ bwd_part2 for ``second`` = (bn name, y) of a downsample BN); returns the
-        partial row count."""
+        partial row count. With ``fold_fin`` the BN-backward finalize (dgamma, dbeta, ca/cb/cc) runs in
+        the same launch and 0 is returned (nothing left to finalize)."""
         cv = self.convs[conv]
         st = self.bn_state[bn]
         e = BnBwdEpilogue()
+        if self.fold_fin:
+            cf = self.bn_coef[bn]
+            e.workspace, e.gamma, e.dgamma, e.dbeta = ptr(self.bn_ws), ptr(P[bn + ".weight"]), ptr(G[bn + ".weight"]), \
+                ptr(G[bn + ".bias"])
+            e.ca, e.cb, e.cc = ptr(cf[0]), ptr(cf[1]), ptr(cf[2])
+            if second is not None:
+                cf2 = self.bn_coef[second[0]]
+                e.gamma2, e.dgamma2, e.dbeta2 = ptr(P[second[0] + ".weight"]), ptr(G[second[0] + ".weight"]), \
+                    ptr(G[second[0] + ".bias"])
+                e.ca2, e.cb2, e.cc2 = ptr(cf2[0]), ptr(cf2[1]), ptr(cf2[2])
         e.y, e.mean, e.invstd, e.mask_mode = ptr(y), ptr(st[0]), ptr(st[1]), mode
         if mode == 2:
             e.scale, e.shift = ptr(st[2]), ptr(st[3])
@@ -512,7 +551,7 @@ class ResNetEngine:
             e.y2, e.mean2, e.invstd2, e.part2 = ptr(second[1]), ptr(st2[0]), ptr(st2[1]), ptr(self.bwd_part2)
         self._launch(cv, 1, lambda: self.L.conv_dgrad_bn(C.byref(cv.desc), self.dt, ptr(dy), ptr(cv.wd), ptr(dm),
                                                           ptr(addend), C.byref(e), stream()))
-        return self.L.dll.argus_conv_dgrad_bn_rows(C.byref(cv.desc), self.dt)
+        return 0 if self.fold_fin else self.L.dll.argus_conv_dgrad_bn_rows(C.byref(cv.desc), self.dt)
 
     def _bn_apply_bwd(self, name, px, ch, dm, y, dy_out, second=None):
         """dy = ca*dm + cb*y + cc from an already-masked dm (+ the downsample BN's dy2 from the same dm)."""
@@ -573,6 +612,11 @@ class ResNetEngine:
         done = torch.cuda.Event()
         done.record(self._side)
         return done
+
+    def _next_dy(self) -> torch.Tensor:
+        buf = self.dyring[self._ring_i % len(self.dyring)]
+        self._ring_i += 1
+        return buf
 
     def _guard(self, buf) -> None:
         """Before the main stream overwrites ``buf``: wait for the side-stream wgrad still reading it."""

@@ -128,6 +128,8 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--kernels", action="store_true", help="print the probe step's per-kernel table to stderr")
+    ap.add_argument("--no-isolated", action="store_true",
+                    help="skip the two untimed no-overlap steps that measure the dominant kernel alone")
     ap.add_argument("--tune", nargs="*", default=[], help="dev: argus_conv_tuning key=value pairs")
     args = ap.parse_args()
 
@@ -203,14 +205,16 @@ def main() -> None:
     # the same kernel without the side-stream overlap (untimed, after the timed region): its duration
     # when it has the GPU to itself, reported beside the concurrent figure
     eng = model._engine(dev)
-    iso = KernelTimer(dom)
-    eng.wgrad_overlap = False
-    iso.start()
-    for _ in range(2):
-        trainer.step(images, targets)
-    iso_s = iso.summary().get(dom)
-    iso.stop()
-    eng.wgrad_overlap = True
+    iso_s = None
+    if not args.no_isolated:
+        iso = KernelTimer(dom)
+        eng.wgrad_overlap = False
+        iso.start()
+        for _ in range(2):
+            trainer.step(images, targets)
+        iso_s = iso.summary().get(dom)
+        iso.stop()
+        eng.wgrad_overlap = True
 
     # validation SE(3) error (eval mode, running BN statistics), synthetic held-out batch
     model.eval()

@@ -83,6 +83,30 @@ int argus_conv_fwd(const argus_conv_desc* d, int dtype, const void* x, const voi
                    const float* pro_scale, const float* pro_shift, float* stat_part,
                    argus_stream_t stream);
 int argus_conv_fwd_stat_rows(const argus_conv_desc* d, int dtype);
+/* conv_fwd with the train-mode BatchNorm statistics finalize of its output folded into the launch
+ * (replaces argus_conv_fwd(..stat_part..) + argus_bn_finalize): `part` is the partial scratch
+ * (float2[argus_conv_fwd_stat_rows(d)][k]), the last workgroups merge it (fp64, fixed order) and
+ * write mean / invstd / scale / shift, update running_mean / running_var (momentum, unbiased
+ * variance; NULL = skip) and num_batches_tracked (+1; NULL = skip). workspace: argus_bn_workspace_bytes(k),
+ * zero-filled once, not shared by concurrent launches. */
+typedef struct {
+  float* part;
+  const float* gamma;
+  const float* beta;
+  float eps;
+  float momentum;
+  float* running_mean;
+  float* running_var;
+  int64_t* num_batches_tracked;
+  float* mean;
+  float* invstd;
+  float* scale;
+  float* shift;
+  void* workspace;
+} argus_bn_fwd_fin;
+int argus_conv_fwd_bn(const argus_conv_desc* d, int dtype, const void* x, const void* w_fwd, void* y,
+                      const float* pro_scale, const float* pro_shift, const argus_bn_fwd_fin* fin,
+                      argus_stream_t stream);
 int argus_conv_fwd_stat_tile(const argus_conv_desc* d, int dtype);
 /* dx = dgrad(dy, w_dgrad) [+ addend]: when addend != NULL (same NHWC layout as dx; may be dx itself
  * for in-place accumulation) it is added, element-wise masked by addend_mask when that is non-NULL
@@ -111,6 +135,22 @@ typedef struct {
   const float* invstd2;
   float* part;
   float* part2;
+  /* Optional: with workspace != NULL (argus_bn_workspace_bytes(c), zero-filled once) the BN-backward
+   * finalize (argus_bn_bwd_finalize) is folded into the same launch: the last workgroups merge the
+   * partials and write dgamma/dbeta (may be NULL) and ca/cb/cc with gamma (+ the second branch). */
+  void* workspace;
+  const float* gamma;
+  float* dgamma;
+  float* dbeta;
+  float* ca;
+  float* cb;
+  float* cc;
+  const float* gamma2;
+  float* dgamma2;
+  float* dbeta2;
+  float* ca2;
+  float* cb2;
+  float* cc2;
 } argus_bn_bwd_epilogue;
 int argus_conv_dgrad_bn_rows(const argus_conv_desc* d, int dtype);
 int argus_conv_dgrad_bn(const argus_conv_desc* d, int dtype, const void* dy, const void* w_dgrad,
@@ -160,8 +200,8 @@ int argus_ktimer_get(int index, char* name, int name_len, int64_t* launches, dou
                      double* work, double* bytes);
 
 /* ---- BatchNorm2d (train: batch stats, eps, momentum; eval: running stats) --------------------- */
-/* Workspace of argus_bn_finalize / argus_bn_bwd_finalize for up to `channels` channels. Its first
- * 1 KiB holds inter-workgroup ticket counters: zero-fill the workspace ONCE when it is allocated;
+/* Workspace of argus_bn_finalize / argus_bn_bwd_finalize / the folded finalize of argus_conv_fwd_bn and
+ * argus_conv_dgrad_bn for up to `channels` channels. Its first 16 KiB hold inter-workgroup ticket counters: zero-fill the workspace ONCE when it is allocated;
  * the kernels leave the counters zero (do not share one workspace between concurrent streams). */
 size_t argus_bn_workspace_bytes(int channels);
 /* From tile partials float2[rows][C] = {sum, M2 (sum of squared deviations from the tile mean)},

@@ -489,7 +489,7 @@ def test_kernel_timer_records_exact_instantiations(cuda):
     bm, bn = divmod(tag % 1000000, 1000)
     # K = 576: the single-buffer kernel (OCC 4; 3 for the 128x128 tile) when K <= tuning key 7
     occ = (3 if bm == bn == 128 else 4) if 576 <= L.dll.argus_conv_tuning_get(7) else 2
-    assert name == f"argus::igemm_kernel<__bf16, {bm}, {bn}, false, false, {occ}>"
+    assert name == f"argus::igemm_kernel<__bf16, {bm}, {bn}, false, false, {occ}, 0>"
     assert v["launches"] == 3 and v["flops_per_launch"] == fl.value and v["avg_us"] > 0
     assert v["bytes_per_launch"] == 2 * (4 * 32 * 32 * 64 + 128 * 9 * 64 + 4 * 32 * 32 * 128)
     with KernelTimer("argus::wgrad") as t:  # filtered out: nothing recorded
@@ -889,3 +889,87 @@ def test_conv_dgrad_bn_epilogue(cuda, dt):
                 pc2 = part2.double().cpu().sum(0)
                 assert (pc2[:, 1] - (got * xh2).sum((0, 1, 2))).abs().max() <= tol * scale * 4
                 assert (pc2[:, 0] - S).abs().max() <= tol * scale
+
+
+FOLD_CASES = [  # (cin, cout, k, stride, hin, n, tuning): forward kernels igemm / halo / glds / stem
+    (64, 256, 1, 1, 40, 4, {}),
+    (128, 128, 3, 1, 16, 4, {13: 1}),
+    (256, 256, 1, 1, 32, 2, {8: 64, 9: 1}),
+    (128, 128, 3, 2, 21, 3, {}),
+]
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+def test_folded_bn_finalize_matches_separate_kernels(cuda, dt):
+    """argus_conv_fwd_bn / argus_conv_dgrad_bn(workspace): the BN finalize folded into the producing
+    conv launch (two-level ticket merge) gives what argus_bn_finalize / argus_bn_bwd_finalize give from
+    the same partials, up to fp64 summation order (1e-6 relative), and leaves its counters at zero."""
+    from argus_amd._lib import BnBwdEpilogue, BnFwdFin
+
+    torch.manual_seed(9)
+    L = lib()
+    ws_bytes = L.dll.argus_bn_workspace_bytes(2048)
+    for cin, cout, k, s, hin, n, tune in FOLD_CASES:
+        if dt == "fp32" and tune:
+            continue
+        d, p = _desc(n, hin, hin, cin, cout, k, s)
+        w = torch.randn(cout, k, k, cin) * (2.0 / (k * k * cin)) ** 0.5
+        wf, wt = _prep(d, dt, w.to(cuda), cuda)
+        x = torch.randn(n, hin, hin, cin, device=cuda).to(TDT[dt])
+        gamma, beta = torch.rand(cout, device=cuda) + 0.5, torch.randn(cout, device=cuda)
+        outs = []
+        with _tuned(tune):
+            rows = L.dll.argus_conv_fwd_stat_rows(C.byref(d), DT[dt])
+            tile = L.dll.argus_conv_fwd_stat_tile(C.byref(d), DT[dt])
+            for folded in (False, True):
+                ws = torch.zeros(ws_bytes, dtype=torch.uint8, device=cuda)
+                part = torch.empty(rows, cout, 2, device=cuda)
+                y = torch.empty(n, d.ho, d.wo, cout, dtype=TDT[dt], device=cuda)
+                st = torch.zeros(4, cout, device=cuda)
+                rm, rv = torch.zeros(cout, device=cuda), torch.ones(cout, device=cuda)
+                nbt = torch.zeros((), dtype=torch.int64, device=cuda)
+                if folded:
+                    f = BnFwdFin(ptr(part), ptr(gamma), ptr(beta), 1e-5, 0.1, ptr(rm), ptr(rv), ptr(nbt),
+                                 ptr(st[0]), ptr(st[1]), ptr(st[2]), ptr(st[3]), ptr(ws))
+                    L.conv_fwd_bn(C.byref(d), DT[dt], ptr(x), ptr(wf), ptr(y), None, None, C.byref(f), stream())
+                else:
+                    L.conv_fwd(C.byref(d), DT[dt], ptr(x), ptr(wf), ptr(y), None, None, ptr(part), stream())
+                    L.bn_finalize(cout, rows, tile, ptr(part), n * d.ho * d.wo, ptr(gamma), ptr(beta),
+                                  C.c_float(1e-5), C.c_float(0.1), ptr(rm), ptr(rv), ptr(nbt), ptr(st[0]),
+                                  ptr(st[1]), ptr(st[2]), ptr(st[3]), ptr(ws), stream())
+                torch.cuda.synchronize()
+                assert int(ws[:16384].view(torch.int32).abs().sum()) == 0  # counters back at zero
+                outs.append((y.cpu(), st.cpu(), rm.cpu(), rv.cpu(), int(nbt)))
+        (y0, s0, m0, v0, n0), (y1, s1, m1, v1, n1) = outs
+        assert torch.equal(y0, y1) and n0 == n1 == 1
+        for a_, b_ in ((s0, s1), (m0, m1), (v0, v1)):
+            assert _rel(a_, b_) < 1e-6, (cin, cout, k, s, dt)
+        # backward: dgrad_bn with the finalize folded vs bn_bwd_finalize on its partials
+        dy = torch.randn(n, d.ho, d.wo, cout, device=cuda).to(TDT[dt])
+        yb = torch.randn(n, hin, hin, cin, device=cuda).to(TDT[dt])
+        mean, invstd = torch.randn(cin, device=cuda) * 0.1, torch.rand(cin, device=cuda) + 0.5
+        sc, sh = torch.randn(cin, device=cuda), torch.randn(cin, device=cuda)
+        g_in = torch.rand(cin, device=cuda) + 0.5
+        res = []
+        with _tuned(tune):
+            brows = L.dll.argus_conv_dgrad_bn_rows(C.byref(d), DT[dt])
+            for folded in (False, True):
+                ws = torch.zeros(ws_bytes, dtype=torch.uint8, device=cuda)
+                part = torch.empty(brows, cin, 2, device=cuda)
+                dm = torch.empty(n, hin, hin, cin, dtype=TDT[dt], device=cuda)
+                co = torch.zeros(5, cin, device=cuda)
+                e = BnBwdEpilogue()
+                e.y, e.mean, e.invstd, e.mask_mode, e.scale, e.shift, e.part = ptr(yb), ptr(mean), ptr(invstd), 2, \
+                    ptr(sc), ptr(sh), ptr(part)
+                if folded:
+                    e.workspace, e.gamma, e.dgamma, e.dbeta = ptr(ws), ptr(g_in), ptr(co[3]), ptr(co[4])
+                    e.ca, e.cb, e.cc = ptr(co[0]), ptr(co[1]), ptr(co[2])
+                L.conv_dgrad_bn(C.byref(d), DT[dt], ptr(dy), ptr(wt), ptr(dm), None, C.byref(e), stream())
+                if not folded:
+                    L.bn_bwd_finalize(cin, brows, ptr(part), n * hin * hin, ptr(g_in), ptr(mean), ptr(invstd),
+                                      ptr(co[3]), ptr(co[4]), ptr(co[0]), ptr(co[1]), ptr(co[2]), ptr(ws), stream())
+                torch.cuda.synchronize()
+                assert int(ws[:16384].view(torch.int32).abs().sum()) == 0
+                res.append((dm.cpu(), co.cpu()))
+        assert torch.equal(res[0][0], res[1][0])
+        assert _rel(res[0][1], res[1][1]) < 1e-6, (cin, cout, k, s, dt)
