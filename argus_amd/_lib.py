@@ -18,7 +18,7 @@ import torch  # noqa: F401  (must precede the CDLL, see module docstring)
 LIB_PATH = Path(os.environ.get("ARGUS_HIP_LIB", Path(__file__).resolve().parent / "libargus_hip.so"))
 
 F32, BF16 = 0, 1
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 class ConvDesc(C.Structure):
@@ -35,6 +35,13 @@ class BnBwdEpilogue(C.Structure):
                 ("dbeta", C.c_void_p), ("ca", C.c_void_p), ("cb", C.c_void_p), ("cc", C.c_void_p),
                 ("gamma2", C.c_void_p), ("dgamma2", C.c_void_p), ("dbeta2", C.c_void_p), ("ca2", C.c_void_p),
                 ("cb2", C.c_void_p), ("cc2", C.c_void_p)]
+
+
+class BnBwdPrologue(C.Structure):
+    """argus_bn_bwd_prologue (include/argus_hip.h)."""
+
+    _fields_ = [("y", C.c_void_p), ("ca", C.c_void_p), ("cb", C.c_void_p), ("cc", C.c_void_p),
+                ("dy_out", C.c_void_p)]
 
 
 class BnFwdFin(C.Structure):
@@ -73,7 +80,7 @@ SIGNATURES = {
     "argus_conv_launch_info": (_I, [_DESC, _I, _I, C.POINTER(C.c_int64)]),
     "argus_conv_dgrad": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P]),
     "argus_conv_dgrad_bn_rows": (_I, [_DESC, _I]),
-    "argus_conv_dgrad_bn": (_I, [_DESC, _I, _P, _P, _P, _P, C.POINTER(BnBwdEpilogue), _P]),
+    "argus_conv_dgrad_bn": (_I, [_DESC, _I, _P, _P, _P, _P, C.POINTER(BnBwdEpilogue), C.POINTER(BnBwdPrologue), _P]),
     "argus_conv_wgrad_workspace_bytes": (_SZ, [_DESC, _I]),
     "argus_conv_wgrad": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     "argus_ktimer_enable": (_I, [C.c_char_p]),

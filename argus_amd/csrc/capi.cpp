@@ -27,7 +27,7 @@ using namespace argus;
 
 extern "C" {
 
-int argus_abi_version(void) { return 3; }
+int argus_abi_version(void) { return 4; }
 
 const char* argus_last_error(void) { return g_last_error.c_str(); }
 
@@ -99,9 +99,10 @@ int argus_conv_dgrad(const argus_conv_desc* d, int dtype, const void* dy, const 
 int argus_conv_dgrad_bn_rows(const argus_conv_desc* d, int dtype) { return d ? conv_dgrad_bn_rows(*d, dtype) : -1; }
 
 int argus_conv_dgrad_bn(const argus_conv_desc* d, int dtype, const void* dy, const void* wt, void* dm,
-                        const void* addend, const argus_bn_bwd_epilogue* bn, argus_stream_t stream) {
+                        const void* addend, const argus_bn_bwd_epilogue* bn, const argus_bn_bwd_prologue* pro,
+                        argus_stream_t stream) {
   if (!d || !dy || !wt || !dm) { set_error("conv_dgrad_bn: bad arguments"); return ARGUS_ERR_ARG; }
-  return conv_dgrad_bn(*d, dtype, dy, wt, dm, addend, bn, (hipStream_t)stream);
+  return conv_dgrad_bn(*d, dtype, dy, wt, dm, addend, bn, pro, (hipStream_t)stream);
 }
 
 size_t argus_conv_wgrad_workspace_bytes(const argus_conv_desc* d, int dtype) { return d ? conv_wgrad_ws(*d, dtype) : 0; }

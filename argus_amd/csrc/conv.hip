@@ -66,8 +66,10 @@ template <typename T, int BN> constexpr int epi_ld() { return BN + 16 / (int)siz
 // OCC = workgroups per CU the kernel is built for: 2 -> double-buffered LDS + 2-deep register
 // prefetch ring (deep-K GEMMs); 3 or 4 -> one LDS buffer, no ring, <= 168 / 128 VGPRs (K <= 2
 // k-steps: the 1x1 convs whose time is load/epilogue latency, hidden by more resident workgroups).
-template <typename T, int BM, int BN, bool STEM, bool PRO, int OCC, int BW>
+template <typename T, int BM, int BN, bool STEM, bool PRO, int OCC, int BWX>
 __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
+  constexpr int BW = BWX & 7;                   // BN-backward epilogue variant
+  constexpr bool AP = (BWX & kApplyBit) != 0;   // BN-backward apply prologue
   constexpr int E = Chunk<T>::E;
   constexpr int BKE = 8 * E;  // K elements per k-step (8 chunks of 16 B per LDS row)
   constexpr int MI = BM / 32, NI = BN / 32;
@@ -134,8 +136,9 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
   // one k-step of staged operands (two named copies form the 2-deep prefetch ring)
   struct Stage {
     u32x4 a[AR], b[BR];
+    u32x4 y[AP ? AR : 1];  // apply prologue: the BN input rows beside the dm rows
     bool ok[AR];
-    int ch;
+    int ch, tap0;  // tap0: this k-step is the center tap of phase 0 (the dy store)
   };
 
   auto load = [&](int kt, Stage& S) {
@@ -174,12 +177,14 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
         const int ih = a_ih[i] + dh, iw = a_iw[i] + dw;
         const bool ok = a_ok[i] && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
         S.a[i] = ld16(A + (ok ? a_off[i] + tap : ch));
-        if constexpr (!PRO) S.a[i] = sel(ok, S.a[i]);
+        if constexpr (AP) S.y[i] = ld16(reinterpret_cast<const T*>(p.ap.y) + (ok ? a_off[i] + tap : ch));
+        if constexpr (!PRO && !AP) S.a[i] = sel(ok, S.a[i]);
         S.ok[i] = ok;
       }
 #pragma unroll
       for (int i = 0; i < BR; ++i) S.b[i] = ld16(b_row[i] + boff + ci0);
       S.ch = ch;
+      if constexpr (AP) S.tap0 = dh == 0 && dw == 0 && blockIdx.z == 0 && nt == 0;
     }
   };
 
@@ -190,6 +195,22 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
       pc.load(p.pro_scale, p.pro_shift, S.ch);
 #pragma unroll
       for (int i = 0; i < AR; ++i) S.a[i] = sel(S.ok[i], pc.apply(S.a[i]));
+    }
+    if constexpr (AP) {  // dy = ca*dm + cb*y + cc; zero outside the image (dgrad's zero padding of dy)
+      float ca[E], cb[E], cc[E];
+      BwdEpiAcc<T, 3>::ld(ca, p.ap.ca + S.ch);
+      BwdEpiAcc<T, 3>::ld(cb, p.ap.cb + S.ch);
+      BwdEpiAcc<T, 3>::ld(cc, p.ap.cc + S.ch);
+#pragma unroll
+      for (int i = 0; i < AR; ++i) {
+        float d[E], yv[E];
+        unpack(S.a[i], d);
+        unpack(S.y[i], yv);
+#pragma unroll
+        for (int j = 0; j < E; ++j) d[j] = fmaf(ca[j], d[j], fmaf(cb[j], yv[j], cc[j]));
+        S.a[i] = sel(S.ok[i], pack(d));
+        if (S.tap0 && S.ok[i]) st16(reinterpret_cast<T*>(p.ap.out) + a_off[i] + S.ch, S.a[i]);
+      }
     }
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
@@ -873,15 +894,21 @@ static void dispatch_ig(const IgParams& p, int maxM, int bm, int bn, hipStream_t
   }
 }
 
-// BN-backward epilogue variants (dgrad only: no stem, no prologue)
+// BN-backward epilogue (+ apply prologue) variants (dgrad only: no stem, no BN+ReLU prologue)
+template <typename T, int OCC, int APB>
+static void dispatch_ig_bwd1(const IgParams& p, int maxM, int bm, int bn, hipStream_t st) {
+  switch (bwd_variant(p.bb)) {
+    case 2: dispatch_ig<T, false, OCC, 2 | APB>(p, maxM, bm, bn, st); break;
+    case 3: dispatch_ig<T, false, OCC, 3 | APB>(p, maxM, bm, bn, st); break;
+    case 4: dispatch_ig<T, false, OCC, 4 | APB>(p, maxM, bm, bn, st); break;
+    default: dispatch_ig<T, false, OCC, APB>(p, maxM, bm, bn, st);
+  }
+}
+
 template <typename T, int OCC>
 static void dispatch_ig_bwd(const IgParams& p, int maxM, int bm, int bn, hipStream_t st) {
-  switch (bwd_variant(p.bb)) {
-    case 2: dispatch_ig<T, false, OCC, 2>(p, maxM, bm, bn, st); break;
-    case 3: dispatch_ig<T, false, OCC, 3>(p, maxM, bm, bn, st); break;
-    case 4: dispatch_ig<T, false, OCC, 4>(p, maxM, bm, bn, st); break;
-    default: dispatch_ig<T, false, OCC>(p, maxM, bm, bn, st);
-  }
+  if (p.ap.y) dispatch_ig_bwd1<T, OCC, kApplyBit>(p, maxM, bm, bn, st);
+  else dispatch_ig_bwd1<T, OCC, 0>(p, maxM, bm, bn, st);
 }
 
 extern int g_glds_min_k, g_glds_min_grid, g_wg_glds_enable, g_wg_glds_target;  // conv_glds.hip
@@ -916,7 +943,7 @@ static int run_ig(const IgParams& p, hipStream_t st, int bm, int bn) {
   } else if (p.pro_scale) {
     if (smallk) dispatch_ig<T, true, 4>(p, maxM, bm, bn, st);
     else dispatch_ig<T, true, 2>(p, maxM, bm, bn, st);
-  } else if (p.bb.mode) {
+  } else if (p.bb.mode || p.ap.y) {
     if (smallk) dispatch_ig_bwd<T, 4>(p, maxM, bm, bn, st);
     else dispatch_ig_bwd<T, 2>(p, maxM, bm, bn, st);
   } else {
@@ -1127,18 +1154,48 @@ int conv_dgrad_bn_rows(const argus_conv_desc& d, int dtype) {
 }
 
 int conv_dgrad_bn(const argus_conv_desc& d, int dtype, const void* dy, const void* wt, void* dm,
-                  const void* addend, const argus_bn_bwd_epilogue* bn, hipStream_t st) {
+                  const void* addend, const argus_bn_bwd_epilogue* bn, const argus_bn_bwd_prologue* pro,
+                  hipStream_t st) {
   if (int e = check_desc(d)) return e;
   if (d.stem) { set_error("conv_dgrad_bn: the stem input has no gradient"); return ARGUS_ERR_ARG; }
-  if (!bn || !bn->y || !bn->mean || !bn->invstd || !bn->part || (bn->mask_mode != 2 && bn->mask_mode != 3) ||
+  static const argus_bn_bwd_epilogue no_epilogue = {};
+  const bool epi = bn != nullptr;
+  if (!epi) bn = &no_epilogue;
+  if (epi && (!bn->y || !bn->mean || !bn->invstd || !bn->part || (bn->mask_mode != 2 && bn->mask_mode != 3)) ||
       (bn->mask_mode == 2 && (!bn->scale || !bn->shift || bn->y2)) || (bn->mask_mode == 3 && !bn->mask_bits) ||
       (bn->y2 && (!bn->mean2 || !bn->invstd2 || !bn->part2)) || bn->y == dm) {
     set_error("conv_dgrad_bn: bad BN-backward epilogue arguments");
     return ARGUS_ERR_ARG;
   }
-  dgrad_work(d, dtype, addend != nullptr, bn->mask_mode == 3, true, bn->y2 != nullptr);
+  if (pro && (!pro->y || !pro->ca || !pro->cb || !pro->cc || !pro->dy_out || pro->dy_out == dy || pro->dy_out == dm)) {
+    set_error("conv_dgrad_bn: bad apply-prologue arguments");
+    return ARGUS_ERR_ARG;
+  }
   IgParams p;
   dgrad_params(d, dy, wt, dm, addend, nullptr, p);
+  if (pro) {
+    // the register-staged kernel stages dy = ca*dm + cb*y + cc itself; the halo / glds kernels (LDS
+    // DMA, no staging transform) get it materialised by the apply kernel first
+    int maxM = 0, maxK = 0;
+    for (int i = 0; i < p.nphase; ++i) {
+      maxM = p.ph[i].M > maxM ? p.ph[i].M : maxM;
+      maxK = p.ph[i].K > maxK ? p.ph[i].K : maxK;
+    }
+    const bool lds_dma = dtype == ARGUS_BF16 && (conv3x3_halo_ok(p) || igemm_glds_ok(p, maxM, maxK));
+    // a 3x3 dgrad would stage each dy element once per tap (9x the apply work, measured slower than
+    // the separate pass): fused for the 1x1 dgrads only
+    if (lds_dma || d.r != 1 || d.s != 1) {
+      if (int e = argus_bn_bwd_apply(dtype, (int64_t)d.n * d.ho * d.wo, d.k, dy, 0, nullptr, pro->y, nullptr,
+                                     nullptr, pro->ca, pro->cb, pro->cc, pro->dy_out, nullptr, nullptr, nullptr,
+                                     nullptr, nullptr, nullptr, st))
+        return e;
+      p.a = pro->dy_out;
+    } else {
+      p.ap.y = pro->y; p.ap.ca = pro->ca; p.ap.cb = pro->cb; p.ap.cc = pro->cc; p.ap.out = pro->dy_out;
+    }
+  }
+  dgrad_work(d, dtype, addend != nullptr, bn->mask_mode == 3, epi, bn->y2 != nullptr);
+  if (p.ap.y) g_launch_bytes += (dtype == ARGUS_BF16 ? 2.0 : 4.0) * 2.0 * d.n * d.ho * d.wo * d.k;  // y in, dy out
   BnBwdEpi& b = p.bb;
   b.y = bn->y; b.mean = bn->mean; b.invstd = bn->invstd; b.sc = bn->scale; b.sh = bn->shift;
   b.bits = bn->mask_bits; b.y2 = bn->y2; b.mean2 = bn->mean2; b.invstd2 = bn->invstd2;

@@ -33,6 +33,18 @@ struct BnBwdEpi {
   int prow;               // partial rows per dgrad phase
 };
 
+// BN-backward apply folded into the A-operand staging of a dgrad (argus_bn_bwd_prologue): the A
+// operand `a` holds dm; the kernel consumes dy = ca*dm + cb*y + cc (per channel of A) and the
+// workgroups of column tile 0 also store that dy (center tap, phase 0: each element once) to `out`
+// for the weight gradient.
+struct BnApplyPro {
+  const void* y;
+  const float* ca;
+  const float* cb;
+  const float* cc;
+  void* out;
+};
+
 struct IgParams {
   const void* a;
   const void* b;
@@ -48,7 +60,12 @@ struct IgParams {
   IgPhase ph[4];
   BnBwdEpi bb;    // dgrad only
   BnFin fin;      // BN finalize folded into this launch (fin.mode != 0)
+  BnApplyPro ap;  // dgrad only: the A operand is dm (ap.y != nullptr)
 };
+
+// compile-time epilogue/prologue variant of the dgrad kernels: low 3 bits = BN-backward epilogue
+// (BwdMode), bit 4 = BN-backward apply prologue (BnApplyPro)
+constexpr int kApplyBit = 16;
 
 struct WgParams {
   const void* x;

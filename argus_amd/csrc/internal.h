@@ -31,7 +31,8 @@ int conv_dgrad(const argus_conv_desc& d, int dtype, const void* dy, const void* 
                const void* addend, const uint8_t* addend_mask, hipStream_t st);
 int conv_dgrad_bn_rows(const argus_conv_desc& d, int dtype);
 int conv_dgrad_bn(const argus_conv_desc& d, int dtype, const void* dy, const void* wt, void* dm,
-                  const void* addend, const argus_bn_bwd_epilogue* bn, hipStream_t st);
+                  const void* addend, const argus_bn_bwd_epilogue* bn, const argus_bn_bwd_prologue* pro,
+                  hipStream_t st);
 size_t conv_wgrad_ws(const argus_conv_desc& d, int dtype);
 int conv_wgrad(const argus_conv_desc& d, int dtype, const void* x, const float* sc,
                const float* sh, const void* dy, float* dw, void* ws, size_t ws_bytes,

@@ -27,7 +27,7 @@ from dataclasses import dataclass
 
 import torch
 
-from argus_amd._lib import BF16, F32, BnBwdEpilogue, BnFwdFin, ConvDesc, lib, ptr, stream
+from argus_amd._lib import BF16, F32, BnBwdEpilogue, BnBwdPrologue, BnFwdFin, ConvDesc, lib, ptr, stream
 
 
 @dataclass(frozen=True)
@@ -97,6 +97,9 @@ class ResNetEngine:
         # BN finalize (forward statistics and backward coefficients) folded into the producing conv
         # launch (argus_conv_fwd_bn / argus_conv_dgrad_bn with a workspace); ARGUS_FOLD_FIN=0 keeps the
         # separate finalize kernels (A/B measurements, tests)
+        # BN-backward apply (dy = ca*dm + cb*y + cc) staged by the consuming dgrad, which also stores dy for
+        # the weight gradient (argus_conv_dgrad_bn with a prologue); ARGUS_FUSE_APPLY=0 runs the apply pass
+        self.fuse_apply = os.environ.get("ARGUS_FUSE_APPLY", "1") != "0"
         fold = os.environ.get("ARGUS_FOLD_FIN", "bwd")  # A/B at B=64: fwd fold neutral, bwd +0.3 %
         self.fold_fin_fwd = fold in ("1", "fwd")
         self.fold_fin = fold in ("1", "bwd")  # backward
@@ -208,7 +211,7 @@ class ResNetEngine:
         ws = max(L.dll.argus_conv_wgrad_workspace_bytes(C.byref(cv.desc), dt) for cv in convs.values())
         self.wg_ws = torch.empty(ws, dtype=torch.uint8, device=self.device)
         self.wg_ws_bytes = ws
-        self.gbuf = [self._t(max_elems) for _ in range(3)]  # dh / dx ping-pong, dz
+        self.gbuf = [self._t(max_elems) for _ in range(4)]  # dh / dx ping-pong, dz ping-pong
         # dy operands of the side-stream weight gradients come from a ring, so the main stream can
         # run ahead of the wgrad stream by several layers before it must wait to reuse a buffer
         # (ARGUS_DY_RING buffers; a reuse waits on the event of the wgrad that last read it)
@@ -436,7 +439,6 @@ class ResNetEngine:
             ho, wo = a["hw"]
             px_o = N * ho * wo
             px_i = N * hi * wi
-            dz = g[2]
             dy3 = self._next_dy()
             dyd = self._next_dy() if b.has_ds else None
             dbg = self.debug
@@ -446,6 +448,8 @@ class ResNetEngine:
                     dbg[key + "." + pf] = t[:n].view(*shape).clone()
 
             cap("b_dout", dh, px_o * b.cout, (N, ho, wo, b.cout))
+            fuse = self.fuse_apply
+            dza, dzb = g[2], g[3]
             # bn3 (+ downsample BN) backward
             if rows3 is None:  # last block: mask + reduce pass over the pooled gradient
                 L.bn_bwd_reduce(dt, px_o, b.cout, ptr(dh), 3, ptr(a["bits"]), ptr(a["y3"]), None, None,
@@ -457,55 +461,79 @@ class ResNetEngine:
                 self._guard(dy3)
                 L.bn_bwd_apply(dt, px_o, b.cout, ptr(dh), 3, ptr(a["bits"]), ptr(a["y3"]), None, None, ptr(cf[0]),
                                ptr(cf[1]), ptr(cf[2]), ptr(dy3), ptr(dh), None, None, None, None, None, s)
+                pro3 = None  # dy3 materialised above
             else:
                 if rows3:  # not folded into the producing dgrad
                     self._bn_bwd_fin(P, G, pf + ".bn3", px_o, b.cout, self.bwd_part, rows3)
                     if b.has_ds:
                         self._bn_bwd_fin(P, G, pf + ".downsample.1", px_o, b.cout, self.bwd_part2, rows3)
-                self._bn_apply_bwd(pf + ".bn3", px_o, b.cout, dh, a["y3"], dy3,
-                                   (pf + ".downsample.1", a["yd"], dyd) if b.has_ds else None)
-            cap("b_dy3", dy3, px_o * b.cout, (N, ho, wo, b.cout))
-            if b.has_ds:
-                cap("b_dyd", dyd, px_o * b.cout, (N, ho, wo, b.cout))
+                if fuse:  # dy3 (and dyd) are staged by the conv3 (downsample) dgrad from dm3 = dh
+                    pro3 = (pf + ".bn3", a["y3"], dy3)
+                    if b.has_ds and idx == 0:  # block 0's downsample dgrad is a plain dgrad: materialise dyd
+                        self._bn_apply_bwd(pf + ".downsample.1", px_o, b.cout, dh, a["yd"], dyd)
+                else:
+                    pro3 = None
+                    self._bn_apply_bwd(pf + ".bn3", px_o, b.cout, dh, a["y3"], dy3,
+                                       (pf + ".downsample.1", a["yd"], dyd) if b.has_ds else None)
             # conv3 -> bn2
+            r2 = self._dgrad_bn(pf + ".conv3", dh if pro3 else dy3, dza, None, pf + ".bn2", a["y2"], 2, P=P, G=G,
+                                pro=pro3)
+            cap("b_dy3", dy3, px_o * b.cout, (N, ho, wo, b.cout))
+            cap("b_dz2", dza, px_o * b.width, (N, ho, wo, b.width))
             s2 = self.bn_state[pf + ".bn2"]
             if self.materialize:
                 self._wgrad(pf + ".conv3", a["a2"], None, dy3, G)
             else:
                 self._wgrad(pf + ".conv3", a["y2"], s2, dy3, G)
-            r2 = self._dgrad_bn(pf + ".conv3", dy3, dz, None, pf + ".bn2", a["y2"], 2, P=P, G=G)
-            cap("b_dz2", dz, px_o * b.width, (N, ho, wo, b.width))
             if r2:
                 self._bn_bwd_fin(P, G, pf + ".bn2", px_o, b.width, self.bwd_part, r2)
-            dyw = self._next_dy()
-            self._bn_apply_bwd(pf + ".bn2", px_o, b.width, dz, a["y2"], dyw)
-            cap("b_dy2", dyw, px_o * b.width, (N, ho, wo, b.width))
+            dy2 = self._next_dy()
+            if fuse:
+                pro2 = (pf + ".bn2", a["y2"], dy2)
+            else:
+                pro2 = None
+                self._bn_apply_bwd(pf + ".bn2", px_o, b.width, dza, a["y2"], dy2)
             # conv2 -> bn1
+            r1 = self._dgrad_bn(pf + ".conv2", dza if pro2 else dy2, dzb, None, pf + ".bn1", a["y1"], 2, P=P, G=G,
+                                pro=pro2)
+            cap("b_dy2", dy2, px_o * b.width, (N, ho, wo, b.width))
+            cap("b_dz1", dzb, px_i * b.width, (N, hi, wi, b.width))
             s1 = self.bn_state[pf + ".bn1"]
             if self.materialize:
-                self._wgrad(pf + ".conv2", a["a1"], None, dyw, G)
+                self._wgrad(pf + ".conv2", a["a1"], None, dy2, G)
             else:
-                self._wgrad(pf + ".conv2", a["y1"], s1, dyw, G)
-            r1 = self._dgrad_bn(pf + ".conv2", dyw, dz, None, pf + ".bn1", a["y1"], 2, P=P, G=G)
-            cap("b_dz1", dz, px_i * b.width, (N, hi, wi, b.width))
+                self._wgrad(pf + ".conv2", a["y1"], s1, dy2, G)
             if r1:
                 self._bn_bwd_fin(P, G, pf + ".bn1", px_i, b.width, self.bwd_part, r1)
-            dyw = self._next_dy()
-            self._bn_apply_bwd(pf + ".bn1", px_i, b.width, dz, a["y1"], dyw)
-            cap("b_dy1", dyw, px_i * b.width, (N, hi, wi, b.width))
+            dy1 = self._next_dy()
+            pro1 = None
+            if fuse and idx > 0:
+                pro1 = (pf + ".bn1", a["y1"], dy1)
+            else:
+                self._bn_apply_bwd(pf + ".bn1", px_i, b.width, dzb, a["y1"], dy1)
             # conv1 (+ downsample) -> the previous block's bn3 (+ its downsample BN): dm3 of block idx-1
-            self._wgrad(pf + ".conv1", h_in, None, dyw, G)
-            last_conv, last_dy, addend = pf + ".conv1", dyw, (None if b.has_ds else dh)
-            if b.has_ds:
-                self._wgrad(pf + ".downsample.0", h_in, None, dyd, G)
-                self._dgrad(pf + ".conv1", dyw, dx)
-                last_conv, last_dy, addend = pf + ".downsample.0", dyd, dx
+            c1_in = dzb if pro1 else dy1
             if idx > 0:
                 pb, pa = self.blocks[idx - 1], self.act[idx - 1]
-                rows3 = self._dgrad_bn(last_conv, last_dy, dx, addend, pb.prefix + ".bn3", pa["y3"], 3, pa["bits"],
-                                       (pb.prefix + ".downsample.1", pa["yd"]) if pb.has_ds else None, P=P, G=G)
+                second = (pb.prefix + ".downsample.1", pa["yd"]) if pb.has_ds else None
+                if b.has_ds:
+                    self._dgrad_plain_or_pro(pf + ".conv1", c1_in, dx, pro1)
+                    rows3 = self._dgrad_bn(pf + ".downsample.0", dh if fuse else dyd, dx, dx, pb.prefix + ".bn3",
+                                           pa["y3"], 3, pa["bits"], second, P=P, G=G,
+                                           pro=(pf + ".downsample.1", a["yd"], dyd) if fuse else None)
+                else:
+                    rows3 = self._dgrad_bn(pf + ".conv1", c1_in, dx, dh, pb.prefix + ".bn3", pa["y3"], 3, pa["bits"],
+                                           second, P=P, G=G, pro=pro1)
             else:
-                self._dgrad(last_conv, last_dy, dx, addend=addend)
+                self._dgrad(pf + ".conv1", dy1, dx)
+                if b.has_ds:
+                    self._dgrad(pf + ".downsample.0", dyd, dx, addend=dx)
+            cap("b_dy1", dy1, px_i * b.width, (N, hi, wi, b.width))
+            if b.has_ds:
+                cap("b_dyd", dyd, px_o * b.cout, (N, ho, wo, b.cout))
+            self._wgrad(pf + ".conv1", h_in, None, dy1, G)
+            if b.has_ds:
+                self._wgrad(pf + ".downsample.0", h_in, None, dyd, G)
             dh, dx = dx, dh
             if on_ready is not None:
                 on_ready(pf + ".conv1.weight", self._join)
@@ -522,7 +550,7 @@ class ResNetEngine:
         if on_ready is not None:
             on_ready("resnet.conv1.weight", self._join)
 
-    def _dgrad_bn(self, conv, dy, dm, addend, bn, y, mode, bits=None, second=None, P=None, G=None):
+    def _dgrad_bn(self, conv, dy, dm, addend, bn, y, mode, bits=None, second=None, P=None, G=None, pro=None):
         """dgrad of ``conv`` whose output feeds BN ``bn`` (input ``y``) backward: stores the masked dm
         and writes bwd_part (+ bwd_part2 for ``second`` = (bn name, y) of a downsample BN); returns the
         partial row count. With ``fold_fin`` the BN-backward finalize (dgamma, dbeta, ca/cb/cc) runs in
@@ -549,9 +577,30 @@ class ResNetEngine:
         if second is not None:
             st2 = self.bn_state[second[0]]
             e.y2, e.mean2, e.invstd2, e.part2 = ptr(second[1]), ptr(st2[0]), ptr(st2[1]), ptr(self.bwd_part2)
+        pp = self._prologue(pro)
         self._launch(cv, 1, lambda: self.L.conv_dgrad_bn(C.byref(cv.desc), self.dt, ptr(dy), ptr(cv.wd), ptr(dm),
-                                                          ptr(addend), C.byref(e), stream()))
+                                                          ptr(addend), C.byref(e), pp, stream()))
         return 0 if self.fold_fin else self.L.dll.argus_conv_dgrad_bn_rows(C.byref(cv.desc), self.dt)
+
+    def _prologue(self, pro):
+        """argus_bn_bwd_prologue for ``pro`` = (bn name, y, dy_out): the dgrad stages dy = ca*dm + cb*y + cc
+        from its dm operand and stores dy to dy_out (for the weight gradient)."""
+        if pro is None:
+            return None
+        cf = self.bn_coef[pro[0]]
+        self._guard(pro[2])
+        return C.byref(BnBwdPrologue(ptr(pro[1]), ptr(cf[0]), ptr(cf[1]), ptr(cf[2]), ptr(pro[2])))
+
+    def _dgrad_plain_or_pro(self, conv, dy, dx, pro):
+        """dgrad without a BN epilogue (the conv1 dgrad of a downsample block, accumulated into by the
+        downsample dgrad) - with the apply prologue when ``pro`` is given."""
+        if pro is None:
+            self._dgrad(conv, dy, dx)
+            return
+        cv = self.convs[conv]
+        pp = self._prologue(pro)
+        self._launch(cv, 1, lambda: self.L.conv_dgrad_bn(C.byref(cv.desc), self.dt, ptr(dy), ptr(cv.wd), ptr(dx),
+                                                          None, None, pp, stream()))
 
     def _bn_apply_bwd(self, name, px, ch, dm, y, dy_out, second=None):
         """dy = ca*dm + cb*y + cc from an already-masked dm (+ the downsample BN's dy2 from the same dm)."""

@@ -152,10 +152,22 @@ typedef struct {
   float* cb2;
   float* cc2;
 } argus_bn_bwd_epilogue;
+/* Optional BN-backward apply folded into the dgrad's operand staging: with `pro` != NULL the `dy`
+ * argument of argus_conv_dgrad_bn holds dm (the masked gradient of a BN output) and the dgrad consumes
+ * dy = ca*dm + cb*y + cc (per channel; argus_bn_bwd_apply's formula), which it also stores to dy_out
+ * for the weight gradient. Kernels that cannot stage it run argus_bn_bwd_apply first (same result).
+ * `bn` may be NULL with a prologue: a plain dgrad (no BN-backward epilogue) of the applied dy. */
+typedef struct {
+  const void* y;
+  const float* ca;
+  const float* cb;
+  const float* cc;
+  void* dy_out;
+} argus_bn_bwd_prologue;
 int argus_conv_dgrad_bn_rows(const argus_conv_desc* d, int dtype);
 int argus_conv_dgrad_bn(const argus_conv_desc* d, int dtype, const void* dy, const void* w_dgrad,
                         void* dm, const void* addend, const argus_bn_bwd_epilogue* bn,
-                        argus_stream_t stream);
+                        const argus_bn_bwd_prologue* pro, argus_stream_t stream);
 /* Tuning knobs (process-wide; for autotuning / experiments): key 0..2 force the row tile (64|128,
  * 0 = heuristic) of pass fwd/dgrad/wgrad, key 3..5 force the column tile, key 6 sets the wgrad
  * split target (workgroups), key 7 the largest K (= taps*C) served by the 4-workgroups-per-CU

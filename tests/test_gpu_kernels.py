@@ -856,7 +856,7 @@ def test_conv_dgrad_bn_epilogue(cuda, dt):
             dyg = dy.to(cuda, TDT[dt])
             with _tuned(tune), KernelTimer() as kt:
                 L.conv_dgrad_bn(C.byref(d), DT[dt], ptr(dyg), ptr(wt), ptr(dm), ptr(dm) if with_add else None,
-                                C.byref(e), stream())
+                                C.byref(e), None, stream())
             torch.cuda.synchronize()
             assert any(kname in nm for nm in kt.summary()), (kname, list(kt.summary()))
             # reference
@@ -964,7 +964,7 @@ def test_folded_bn_finalize_matches_separate_kernels(cuda, dt):
                 if folded:
                     e.workspace, e.gamma, e.dgamma, e.dbeta = ptr(ws), ptr(g_in), ptr(co[3]), ptr(co[4])
                     e.ca, e.cb, e.cc = ptr(co[0]), ptr(co[1]), ptr(co[2])
-                L.conv_dgrad_bn(C.byref(d), DT[dt], ptr(dy), ptr(wt), ptr(dm), None, C.byref(e), stream())
+                L.conv_dgrad_bn(C.byref(d), DT[dt], ptr(dy), ptr(wt), ptr(dm), None, C.byref(e), None, stream())
                 if not folded:
                     L.bn_bwd_finalize(cin, brows, ptr(part), n * hin * hin, ptr(g_in), ptr(mean), ptr(invstd),
                                       ptr(co[3]), ptr(co[4]), ptr(co[0]), ptr(co[1]), ptr(co[2]), ptr(ws), stream())
@@ -973,3 +973,58 @@ def test_folded_bn_finalize_matches_separate_kernels(cuda, dt):
                 res.append((dm.cpu(), co.cpu()))
         assert torch.equal(res[0][0], res[1][0])
         assert _rel(res[0][1], res[1][1]) < 1e-6, (cin, cout, k, s, dt)
+
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+def test_dgrad_apply_prologue_matches_apply_pass(cuda, dt):
+    """argus_conv_dgrad_bn with an argus_bn_bwd_prologue (the dgrad stages dy = ca*dm + cb*y + cc from
+    dm and stores dy): bit-identical dy and dgrad output to argus_bn_bwd_apply + a plain dgrad, on the
+    register-staged kernel (strided phases included) and on the LDS-DMA kernels (library fallback),
+    with and without a BN-backward epilogue."""
+    from argus_amd._lib import BnBwdEpilogue, BnBwdPrologue
+
+    torch.manual_seed(12)
+    L = lib()
+    for cin, cout, k, s, hin, n, tune, kname in DGRAD_BN_CASES:
+        if dt == "fp32" and kname != "igemm_kernel":
+            continue
+        d, p = _desc(n, hin, hin, cin, cout, k, s)
+        w = torch.randn(cout, k, k, cin) * (2.0 / (k * k * cin)) ** 0.5
+        _, wt = _prep(d, dt, w.to(cuda), cuda)
+        dm = torch.randn(n, d.ho, d.wo, cout, device=cuda).to(TDT[dt])
+        yb = torch.randn(n, d.ho, d.wo, cout, device=cuda).to(TDT[dt])
+        ca, cb, cc = (torch.randn(cout, device=cuda) * 0.3 for _ in range(3))
+        yin = torch.randn(n, hin, hin, cin, device=cuda).to(TDT[dt])
+        mean, invstd = torch.randn(cin, device=cuda) * 0.1, torch.rand(cin, device=cuda) + 0.5
+        sc, sh = torch.randn(cin, device=cuda), torch.randn(cin, device=cuda)
+        for with_epi in (False, True):
+            outs = []
+            for fused in (False, True):
+                with _tuned(tune):
+                    rows = L.dll.argus_conv_dgrad_bn_rows(C.byref(d), DT[dt])
+                    part = torch.zeros(rows, cin, 2, device=cuda)
+                    e = BnBwdEpilogue()
+                    e.y, e.mean, e.invstd, e.mask_mode, e.scale, e.shift, e.part = ptr(yin), ptr(mean), ptr(invstd), \
+                        2, ptr(sc), ptr(sh), ptr(part)
+                    dy = torch.zeros(n, d.ho, d.wo, cout, device=cuda, dtype=TDT[dt])
+                    dx = torch.empty(n, hin, hin, cin, device=cuda, dtype=TDT[dt])
+                    if fused:
+                        pro = BnBwdPrologue(ptr(yb), ptr(ca), ptr(cb), ptr(cc), ptr(dy))
+                        L.conv_dgrad_bn(C.byref(d), DT[dt], ptr(dm), ptr(wt), ptr(dx), None,
+                                        C.byref(e) if with_epi else None, C.byref(pro), stream())
+                    else:
+                        L.bn_bwd_apply(DT[dt], n * d.ho * d.wo, cout, ptr(dm), 0, None, ptr(yb), None, None, ptr(ca),
+                                       ptr(cb), ptr(cc), ptr(dy), None, None, None, None, None, None, stream())
+                        if with_epi:
+                            L.conv_dgrad_bn(C.byref(d), DT[dt], ptr(dy), ptr(wt), ptr(dx), None, C.byref(e), None,
+                                            stream())
+                        else:
+                            L.conv_dgrad(C.byref(d), DT[dt], ptr(dy), ptr(wt), ptr(dx), None, None, stream())
+                torch.cuda.synchronize()
+                outs.append((dy.cpu(), dx.cpu(), part.cpu()))
+            (y0, x0, p0), (y1, x1, p1) = outs
+            assert torch.equal(y0, y1), (cin, cout, k, s, dt, "dy")
+            assert torch.equal(x0, x1), (cin, cout, k, s, dt, "dx")
+            if with_epi:
+                assert torch.equal(p0, p1), (cin, cout, k, s, dt, "partials")

@@ -11,12 +11,17 @@ import argparse
 import csv
 import re
 import subprocess
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent))
+from pmc_traffic import demangle as _dm  # noqa: E402
 from collections import defaultdict
 
 
 def demangle(names):
     out = subprocess.run(["c++filt"], input="\n".join(names), capture_output=True, text=True).stdout.split("\n")
-    return dict(zip(names, out))
+    return {n: (_dm(n) if n.startswith("_ZN5argus") else o) for n, o in zip(names, out)}
 
 
 def family(name: str) -> str:
@@ -51,6 +56,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--list", action="store_true", help="also list the last step's main-stream kernels in order "
+                                                        "(start offset, gap before, duration)")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     skey = "Stream_Id" if "Stream_Id" in rows[0] else "Queue_Id"
@@ -80,6 +87,14 @@ def main():
         tag = "main" if st == main_stream else "side"
         print(f"  stream {st} ({tag}): busy {busy:.3f} ms/step ({busy / wall:.0%}), idle {wall - busy:.3f} ms, "
               f"{launches:.0f} kernels/step")
+    if a.list:
+        t0, t1 = bounds[-2], bounds[-1]
+        sel = [k for k in ks if k[0] >= t0 and k[1] <= t1 and k[2] == main_stream]
+        prev = t0
+        print("last step, main stream: offset_us gap_us dur_us kernel")
+        for st_, en, _, nm in sel:
+            print(f"  {(st_ - t0) / 1e3:9.1f} {(st_ - prev) / 1e3:7.1f} {(en - st_) / 1e3:8.1f}  {nm[:110]}")
+            prev = en
     for title, fam in (("main-stream kernel time by family (ms/step)", fam_main),
                        ("other-stream kernel time by family (ms/step)", fam_side)):
         print(title)
