@@ -18,7 +18,7 @@ import torch  # noqa: F401  (must precede the CDLL, see module docstring)
 LIB_PATH = Path(os.environ.get("ARGUS_HIP_LIB", Path(__file__).resolve().parent / "libargus_hip.so"))
 
 F32, BF16 = 0, 1
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 class ConvDesc(C.Structure):
@@ -83,6 +83,7 @@ SIGNATURES = {
     "argus_conv_dgrad_bn": (_I, [_DESC, _I, _P, _P, _P, _P, C.POINTER(BnBwdEpilogue), C.POINTER(BnBwdPrologue), _P]),
     "argus_conv_wgrad_workspace_bytes": (_SZ, [_DESC, _I]),
     "argus_conv_wgrad": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P, _SZ, _P]),
+    "argus_conv_wgrad_apply": (_I, [_DESC, _I, _P, _P, C.POINTER(BnBwdPrologue), _P, _P, _SZ, _P]),
     "argus_ktimer_enable": (_I, [C.c_char_p]),
     "argus_ktimer_disable": (_I, []),
     "argus_ktimer_count": (_I, []),
@@ -98,6 +99,8 @@ SIGNATURES = {
     "argus_bn_bwd_apply": (_I, [_I, _I64, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "argus_maxpool_fwd": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
     "argus_maxpool_bwd": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P]),
+    "argus_maxpool_bwd_bn_rows": (_I, [_I, _I, _I, _I, _I]),
+    "argus_maxpool_bwd_bn": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "argus_avgpool_fwd": (_I, [_I, _I, _I, _I, _P, _P, _P]),
     "argus_avgpool_bwd": (_I, [_I, _I, _I, _I, _P, _P, _P]),
     "argus_gemm_f32_workspace_bytes": (_SZ, [_I, _I, _I]),

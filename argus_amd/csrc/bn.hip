@@ -512,51 +512,100 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(int n, int H, int W, i
   }
 }
 
-template <typename T>
+// Gather form: one thread per (input pixel, 16-byte channel chunk) sums the gradients of the (at most
+// 2 x 2) output windows whose argmax is this pixel; the four candidates' loads are issued together.
+// BNE: the stem BatchNorm's backward reduction is fused in (the pooled input is relu(bn1(y0))):
+// dm = dz * (y0*scale+shift > 0) is stored instead of dz, and each block writes its column partials
+// {sum dm, sum dm*(y0-mean)*invstd} (a thread's channel chunk is fixed: the grid stride is a multiple
+// of the chunks per pixel) — one partial row per block, the input of argus_bn_bwd_finalize.
+template <typename T, bool BNE>
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(int n, int H, int W, int C, int Ho, int Wo,
                                                           const T* __restrict__ dout, const uint8_t* __restrict__ amax,
-                                                          T* __restrict__ dz) {
+                                                          T* __restrict__ dz, const T* __restrict__ y,
+                                                          const float* __restrict__ sc, const float* __restrict__ sh,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ invstd, float2* __restrict__ part) {
   constexpr int E = Chunk<T>::E;
   typedef typename AmaxVec<E>::type AV;
   const int CH = C / E;
   const int total = n * H * W * CH;
+  float S[E], Hs[E], mu[E], is[E], s[E], t[E];
+  const int ch0 = (int)(threadIdx.x % CH);
+  if constexpr (BNE) {
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      S[j] = sc[ch0 * E + j]; Hs[j] = sh[ch0 * E + j]; mu[j] = mean[ch0 * E + j]; is[j] = invstd[ch0 * E + j];
+      s[j] = 0.f; t[j] = 0.f;
+    }
+  }
   for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
     const int pix = i / CH, ch = i - pix * CH;
     const int q = pix / W, iw = pix - q * W;
     const int img = q / H, ih = q - img * H;
     const int c0 = ch * E;
+    // output rows/cols whose 3x3/2 window (offset -1) covers this input pixel: oh in {ih/2, (ih+1)/2}
+    const int oh0 = ih >> 1, oh1 = (ih + 1) >> 1, ow0 = iw >> 1, ow1 = (iw + 1) >> 1;
+    const int ohs[2] = {oh0, oh1}, ows[2] = {ow0, ow1};
+    u32x4 g[4];
+    AV av[4];
+    bool ok[4];
+    unsigned want[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int oh = ohs[k >> 1], ow = ows[k & 1];
+      const bool dup = ((k >> 1) && oh1 == oh0) || ((k & 1) && ow1 == ow0);
+      ok[k] = !dup && oh < Ho && ow < Wo;
+      want[k] = (unsigned)((ih - (2 * oh - 1)) * 3 + (iw - (2 * ow - 1)));
+      const int o = ok[k] ? ((img * Ho + oh) * Wo + ow) * C + c0 : 0;
+      g[k] = ld16(dout + o);
+      av[k] = *reinterpret_cast<const AV*>(amax + o);
+    }
     float acc[E];
 #pragma unroll
     for (int j = 0; j < E; ++j) acc[j] = 0.f;
-    // output rows/cols whose 3x3/2 window (offset -1) covers this input pixel: at most 2 x 2
-    const int oh_lo = max(0, ih / 2), oh_hi = min(Ho - 1, (ih + 1) / 2);
-    const int ow_lo = max(0, iw / 2), ow_hi = min(Wo - 1, (iw + 1) / 2);
-    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
-      const int r = ih - (2 * oh - 1);
-      if (r < 0 || r > 2) continue;
-      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
-        const int t = iw - (2 * ow - 1);
-        if (t < 0 || t > 2) continue;
-        const size_t o = ((size_t)(img * Ho + oh) * Wo + ow) * C + c0;
-        float g[E];
-        unpack(ld16(dout + o), g);
-        const unsigned want = (unsigned)(r * 3 + t);
-        unsigned a[E];
-        if constexpr (E == 8) {
-          const uint2 v = *reinterpret_cast<const AV*>(amax + o);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) { a[j] = (v.x >> (8 * j)) & 0xffu; a[4 + j] = (v.y >> (8 * j)) & 0xffu; }
-        } else {
-          const unsigned v = *reinterpret_cast<const AV*>(amax + o);
+    for (int k = 0; k < 4; ++k) {
+      if (!ok[k]) continue;
+      float gv[E];
+      unpack(g[k], gv);
+      unsigned a[E];
+      if constexpr (E == 8) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) a[j] = (v >> (8 * j)) & 0xffu;
-        }
+        for (int j = 0; j < 4; ++j) { a[j] = (av[k].x >> (8 * j)) & 0xffu; a[4 + j] = (av[k].y >> (8 * j)) & 0xffu; }
+      } else {
 #pragma unroll
-        for (int j = 0; j < E; ++j)
-          if (a[j] == want) acc[j] += g[j];
+        for (int j = 0; j < 4; ++j) a[j] = (av[k] >> (8 * j)) & 0xffu;
+      }
+#pragma unroll
+      for (int j = 0; j < E; ++j) acc[j] += a[j] == want[k] ? gv[j] : 0.f;
+    }
+    const size_t off = (size_t)pix * C + c0;
+    if constexpr (BNE) {
+      float yv[E];
+      unpack(ld16(y + off), yv);
+      const u32x4 r = pack(acc);  // the dz value as stored by the plain kernel (rounded to T)
+      unpack(r, acc);
+#pragma unroll
+      for (int j = 0; j < E; ++j) {
+        const float d = fmaf(yv[j], S[j], Hs[j]) > 0.f ? acc[j] : 0.f;
+        acc[j] = d;
+        s[j] += d;
+        t[j] = fmaf(d, (yv[j] - mu[j]) * is[j], t[j]);
       }
     }
-    st16_nt(dz + (size_t)pix * C + c0, pack(acc));  // 268 MB written once, read by the stem wgrad later
+    st16_nt(dz + off, pack(acc));  // 268 MB written once, read by the stem BN backward / wgrad later
+  }
+  if constexpr (BNE) {
+    __shared__ float2 red[256 * E];
+    const int lanes = 256 / CH, ln = threadIdx.x / CH;
+#pragma unroll
+    for (int j = 0; j < E; ++j) red[ln * C + ch0 * E + j] = make_float2(s[j], t[j]);
+    __syncthreads();
+    for (int col = threadIdx.x; col < C; col += 256) {
+      float2 a = red[col];
+      for (int l = 1; l < lanes; ++l) { a.x += red[l * C + col].x; a.y += red[l * C + col].y; }
+      part[(size_t)blockIdx.x * C + col] = a;
+    }
   }
 }
 
@@ -796,18 +845,36 @@ int argus_maxpool_fwd(int dtype, int n, int h, int w, int c, const void* y, cons
 
 int argus_maxpool_bwd(int dtype, int n, int h, int w, int c, const void* dout, const uint8_t* amax, void* dz,
                       argus_stream_t stream) {
+  return argus_maxpool_bwd_bn(dtype, n, h, w, c, dout, amax, dz, nullptr, nullptr, nullptr, nullptr, nullptr,
+                              nullptr, stream);
+}
+
+int argus_maxpool_bwd_bn_rows(int dtype, int n, int h, int w, int c) {
   const int E = dtype == ARGUS_BF16 ? 8 : 4;
-  if (c % E) { set_error("maxpool_bwd: bad channels"); return ARGUS_ERR_SHAPE; }
+  return c % E ? -1 : grid_for((int64_t)n * h * w * (c / E));
+}
+
+int argus_maxpool_bwd_bn(int dtype, int n, int h, int w, int c, const void* dout, const uint8_t* amax, void* dm,
+                         const void* y, const float* scale, const float* shift, const float* mean,
+                         const float* invstd, float* part, argus_stream_t stream) {
+  const int E = dtype == ARGUS_BF16 ? 8 : 4;
+  if (c % E || 256 % (c / E) || c > 256) { set_error("maxpool_bwd: bad channels"); return ARGUS_ERR_SHAPE; }
   if ((int64_t)n * h * w * c >= (1LL << 31)) { set_error("maxpool_bwd: tensor exceeds 2^31 elements"); return ARGUS_ERR_SHAPE; }
+  const bool bne = y != nullptr;
+  if (bne && (!scale || !shift || !mean || !invstd || !part)) { set_error("maxpool_bwd_bn: bad arguments"); return ARGUS_ERR_ARG; }
   const int ho = (h + 2 - 3) / 2 + 1, wo = (w + 2 - 3) / 2 + 1;
   const int64_t work = (int64_t)n * h * w * (c / E);
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == ARGUS_BF16)
-    hipLaunchKernelGGL(maxpool_bwd_kernel<bf16>, dim3(grid_for(work)), dim3(256), 0, st, n, h, w, c, ho, wo,
-                       (const bf16*)dout, amax, (bf16*)dz);
-  else
-    hipLaunchKernelGGL(maxpool_bwd_kernel<float>, dim3(grid_for(work)), dim3(256), 0, st, n, h, w, c, ho, wo,
-                       (const float*)dout, amax, (float*)dz);
+  float2* pt = reinterpret_cast<float2*>(part);
+#define ARGUS_MPB(TT, B)                                                                                          \
+  hipLaunchKernelGGL((maxpool_bwd_kernel<TT, B>), dim3(grid_for(work)), dim3(256), 0, st, n, h, w, c, ho, wo,     \
+                     (const TT*)dout, amax, (TT*)dm, (const TT*)y, scale, shift, mean, invstd, pt)
+  if (dtype == ARGUS_BF16) {
+    if (bne) ARGUS_MPB(bf16, true); else ARGUS_MPB(bf16, false);
+  } else {
+    if (bne) ARGUS_MPB(float, true); else ARGUS_MPB(float, false);
+  }
+#undef ARGUS_MPB
   return check_launch("maxpool_bwd_kernel");
 }
 

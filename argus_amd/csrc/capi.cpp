@@ -27,7 +27,7 @@ using namespace argus;
 
 extern "C" {
 
-int argus_abi_version(void) { return 4; }
+int argus_abi_version(void) { return 5; }
 
 const char* argus_last_error(void) { return g_last_error.c_str(); }
 
@@ -103,6 +103,12 @@ int argus_conv_dgrad_bn(const argus_conv_desc* d, int dtype, const void* dy, con
                         argus_stream_t stream) {
   if (!d || !dy || !wt || !dm) { set_error("conv_dgrad_bn: bad arguments"); return ARGUS_ERR_ARG; }
   return conv_dgrad_bn(*d, dtype, dy, wt, dm, addend, bn, pro, (hipStream_t)stream);
+}
+
+int argus_conv_wgrad_apply(const argus_conv_desc* d, int dtype, const void* x, const void* dm,
+                           const argus_bn_bwd_prologue* ap, float* dw, void* ws, size_t ws_bytes, argus_stream_t stream) {
+  if (!d || !x || !dm || !ap || !dw || !ws) { set_error("conv_wgrad_apply: bad arguments"); return ARGUS_ERR_ARG; }
+  return conv_wgrad_apply(*d, dtype, x, dm, *ap, dw, ws, ws_bytes, (hipStream_t)stream);
 }
 
 size_t argus_conv_wgrad_workspace_bytes(const argus_conv_desc* d, int dtype) { return d ? conv_wgrad_ws(*d, dtype) : 0; }

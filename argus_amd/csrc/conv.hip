@@ -416,7 +416,7 @@ ARGUS_DEV int swz32(int row) { return (row & 3) | (((row >> 3) & 1) << 2); }
 
 // OCC: 2 = two workgroups per CU, no register prefetch ring on the 128x128 tile (historical default);
 // 1 = one per CU with the ring; 3 = two per CU with the ring (fits: ~220 VGPRs)
-template <typename T, int BM, int BN, bool STEM, bool PRO, bool FAST, int OCC = 2>
+template <typename T, int BM, int BN, bool STEM, bool PRO, bool FAST, int OCC = 2, bool AP = false>
 __global__ __launch_bounds__(256, OCC == 1 ? 1 : 2) void wgrad_kernel(const WgParams p) {
   constexpr int E = Chunk<T>::E;
   constexpr bool BF = (E == 8);
@@ -474,6 +474,14 @@ __global__ __launch_bounds__(256, OCC == 1 ? 1 : 2) void wgrad_kernel(const WgPa
 
   ProCoef<T> pc;
   if constexpr (PRO) pc.load(p.pro_scale, p.pro_shift, ci);
+  // apply prologue: this thread's A chunk is a fixed channel chunk -> coefficients in registers
+  float apa[AP ? E : 1], apb[AP ? E : 1], apc[AP ? E : 1];
+  if constexpr (AP) {
+    BwdEpiAcc<T, 3>::ld(apa, p.ap_ca + mt * BM + ca * E);
+    BwdEpiAcc<T, 3>::ld(apb, p.ap_cb + mt * BM + ca * E);
+    BwdEpiAcc<T, 3>::ld(apc, p.ap_cc + mt * BM + ca * E);
+  }
+  const T* ap_col = AP ? reinterpret_cast<const T*>(p.ap_y) + mt * BM + ca * E : nullptr;
 
   struct Stage {
     u32x4 a[PA], b[PB];
@@ -484,7 +492,16 @@ __global__ __launch_bounds__(256, OCC == 1 ? 1 : 2) void wgrad_kernel(const WgPa
     for (int i = 0; i < PA; ++i) {
       const int pix = p0 + ra0 + RPA * i;
       const bool ok = pix < pend;
-      S.a[i] = sel(ok, ld16(a_col + (size_t)(ok ? pix : pbeg) * p.M));
+      S.a[i] = ld16(a_col + (size_t)(ok ? pix : pbeg) * p.M);
+      if constexpr (AP) {  // dy = ca*dm + cb*y + cc (argus_bn_bwd_apply's formula, fp32, rounded to T)
+        float d[E], yv[E];
+        unpack(S.a[i], d);
+        unpack(ld16(ap_col + (size_t)(ok ? pix : pbeg) * p.M), yv);
+#pragma unroll
+        for (int j = 0; j < E; ++j) d[j] = fmaf(apa[j], d[j], fmaf(apb[j], yv[j], apc[j]));
+        S.a[i] = pack(d);
+      }
+      S.a[i] = sel(ok, S.a[i]);
     }
     int n0 = 0, oh0 = 0, ow0 = 0;
     if constexpr (FAST) {  // uniform: the k-step lies inside one image
@@ -834,9 +851,10 @@ __global__ __launch_bounds__(256) void weight_prep_batch_kernel(const WpEntry* _
 // host launchers
 // ------------------------------------------------------------------------------------------------
 
-// argus_conv_fwd_bn hands its finalize arguments to conv_fwd through this (host, one thread per
-// process: the library's contract)
+// argus_conv_fwd_bn / argus_conv_wgrad_apply hand their extra arguments to conv_fwd / conv_wgrad
+// through these (host, one thread per process: the library's contract)
 static const argus_bn_fwd_fin* g_fwd_fin = nullptr;
+static const argus_bn_bwd_prologue* g_wg_apply = nullptr;
 
 static int check_desc(const argus_conv_desc& d) {
   if (d.n <= 0 || d.h <= 0 || d.w <= 0 || d.k <= 0 || d.r <= 0 || d.s <= 0 || d.stride <= 0) {
@@ -1271,19 +1289,19 @@ size_t conv_wgrad_ws(const argus_conv_desc& d, int dtype) {
   return b;
 }
 
-template <typename T, int BM, int BN, bool STEM, bool PRO, bool FAST, int OCC>
+template <typename T, int BM, int BN, bool STEM, bool PRO, bool FAST, int OCC, bool AP>
 static const char* wg_name() {
   static const std::string s = std::string("argus::wgrad_kernel<") + type_name<T>() + ", " + std::to_string(BM) +
                                ", " + std::to_string(BN) + ", " + bool_name(STEM) + ", " + bool_name(PRO) + ", " +
-                               bool_name(FAST) + ", " + std::to_string(OCC) + ">";
+                               bool_name(FAST) + ", " + std::to_string(OCC) + ", " + bool_name(AP) + ">";
   return s.c_str();
 }
 
-template <typename T, int BM, int BN, bool STEM, bool PRO, bool FAST, int OCC = 2>
+template <typename T, int BM, int BN, bool STEM, bool PRO, bool FAST, int OCC = 2, bool AP = false>
 static void launch_wg(const WgParams& p, const WgPlan& pl, hipStream_t st) {
   dim3 grid(pl.mt * pl.nt * pl.splits);
-  timed_launch(wg_name<T, BM, BN, STEM, PRO, FAST, OCC>(), wgrad_kernel<T, BM, BN, STEM, PRO, FAST, OCC>, grid,
-               dim3(256), st, p);
+  timed_launch(wg_name<T, BM, BN, STEM, PRO, FAST, OCC, AP>(), wgrad_kernel<T, BM, BN, STEM, PRO, FAST, OCC, AP>,
+               grid, dim3(256), st, p);
 }
 
 template <typename T, bool PRO, bool FAST>
@@ -1303,9 +1321,14 @@ static void dispatch_wg(const WgParams& p, const WgPlan& pl, hipStream_t st) {
   // FAST pixel indexing: every k-step lies in one image and rows tile the k-step evenly
   const int bkp = pl.kstep;
   const bool fast = (p.Ho * p.Wo) % bkp == 0 && (p.Wo % bkp == 0 || bkp % p.Wo == 0);
-  if (p.stem) {
-    if (fast) launch_wg<T, 64, 128, true, false, true>(p, pl, st);  // stem: M = 64 channels, N = 256
-    else launch_wg<T, 64, 128, true, false, false>(p, pl, st);
+  if (p.stem) {  // stem: M = 64 channels, N = 256; with the BN-backward apply of dy staged (AP) or not
+    if (p.ap_y) {
+      if (fast) launch_wg<T, 64, 128, true, false, true, 2, true>(p, pl, st);
+      else launch_wg<T, 64, 128, true, false, false, 2, true>(p, pl, st);
+    } else {
+      if (fast) launch_wg<T, 64, 128, true, false, true>(p, pl, st);
+      else launch_wg<T, 64, 128, true, false, false>(p, pl, st);
+    }
   } else if (p.pro_scale) {
     if (fast) dispatch_wg_tiles<T, true, true>(p, pl, st);
     else dispatch_wg_tiles<T, true, false>(p, pl, st);
@@ -1331,6 +1354,10 @@ int conv_wgrad(const argus_conv_desc& d, int dtype, const void* x, const float* 
   }
   WgParams p = {};
   p.x = x; p.dy = dy; p.pro_scale = sc; p.pro_shift = sh; p.part = reinterpret_cast<float*>(ws);
+  if (g_wg_apply) {  // argus_conv_wgrad_apply (stem only)
+    p.ap_y = g_wg_apply->y; p.ap_ca = g_wg_apply->ca; p.ap_cb = g_wg_apply->cb; p.ap_cc = g_wg_apply->cc;
+    g_launch_bytes += (dtype == ARGUS_BF16 ? 2.0 : 4.0) * (double)d.n * d.ho * d.wo * d.k;  // y of the apply
+  }
   p.M = d.k; p.N = pl.N; p.Cin = d.stem ? 4 : d.c; p.lda = d.stem ? 4 : d.c;
   p.H = d.h; p.W = d.w; p.Ho = d.ho; p.Wo = d.wo; p.stride = d.stride; p.pad = d.pad; p.S = d.s;
   p.P = d.n * d.ho * d.wo; p.pps = pl.pps; p.stem = d.stem;
@@ -1356,6 +1383,19 @@ int conv_wgrad(const argus_conv_desc& d, int dtype, const void* x, const float* 
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, reinterpret_cast<const float*>(ws),
                      splits, d.k, pl.N, d.stem, cw, dw);
   return check_launch("wgrad_reduce_kernel");
+}
+
+int conv_wgrad_apply(const argus_conv_desc& d, int dtype, const void* x, const void* dm,
+                     const argus_bn_bwd_prologue& ap, float* dw, void* ws, size_t ws_bytes, hipStream_t st) {
+  if (!d.stem) {
+    set_error("conv_wgrad_apply: implemented for the stem (whose dy feeds nothing but its weight gradient)");
+    return ARGUS_ERR_ARG;
+  }
+  if (!ap.y || !ap.ca || !ap.cb || !ap.cc) { set_error("conv_wgrad_apply: bad apply arguments"); return ARGUS_ERR_ARG; }
+  g_wg_apply = &ap;
+  const int rc = conv_wgrad(d, dtype, x, nullptr, nullptr, dm, dw, ws, ws_bytes, st);
+  g_wg_apply = nullptr;
+  return rc;
 }
 
 int conv_launch_info(const argus_conv_desc& d, int dtype, int pass, int64_t* flops) {

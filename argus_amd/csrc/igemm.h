@@ -77,6 +77,9 @@ struct WgParams {
   int P;
   int pps;  // pixels per split (multiple of the k-step)
   int stem;
+  // BN-backward apply prologue (AP kernels): dy holds dm; the A operand is ca*dm + cb*ap_y + cc
+  const void* ap_y;
+  const float *ap_ca, *ap_cb, *ap_cc;
 };
 
 template <typename T> struct Mma;

@@ -34,6 +34,8 @@ int conv_dgrad_bn(const argus_conv_desc& d, int dtype, const void* dy, const voi
                   const void* addend, const argus_bn_bwd_epilogue* bn, const argus_bn_bwd_prologue* pro,
                   hipStream_t st);
 size_t conv_wgrad_ws(const argus_conv_desc& d, int dtype);
+int conv_wgrad_apply(const argus_conv_desc& d, int dtype, const void* x, const void* dm,
+                     const argus_bn_bwd_prologue& ap, float* dw, void* ws, size_t ws_bytes, hipStream_t st);
 int conv_wgrad(const argus_conv_desc& d, int dtype, const void* x, const float* sc,
                const float* sh, const void* dy, float* dw, void* ws, size_t ws_bytes,
                hipStream_t st);

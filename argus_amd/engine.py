@@ -202,7 +202,8 @@ class ResNetEngine:
             for hw, c in ((a["hw_in"], b.width), (a["hw"], b.width), (a["hw"], b.cout)):
                 px = N * hw[0] * hw[1]
                 max_bwd = max(max_bwd, L.dll.argus_bn_bwd_rows(px, c) * c)
-        max_bwd = max(max_bwd, L.dll.argus_bn_bwd_rows(N * H1 * W1, 64) * 64)
+        max_bwd = max(max_bwd, L.dll.argus_bn_bwd_rows(N * H1 * W1, 64) * 64,
+                      L.dll.argus_maxpool_bwd_bn_rows(dt, N, H1, W1, 64) * 64)
         for cv in convs.values():  # BN-backward partials written by dgrad epilogues (rows x C_in)
             if not cv.desc.stem:
                 max_bwd = max(max_bwd, L.dll.argus_conv_dgrad_bn_rows(C.byref(cv.desc), dt) * cv.desc.c)
@@ -543,9 +544,25 @@ class ResNetEngine:
         # stem: maxpool -> relu/bn1 -> conv1 wgrad
         H1, W1 = self.stem_hw
         dz0, dy0 = g[2], self._next_dy()
-        L.maxpool_bwd(dt, N, H1, W1, 64, ptr(dh), ptr(self.amax), ptr(dz0), s)
-        self._bn_bwd(P, G, "resnet.bn1", N * H1 * W1, 64, dz0, 2, None, self.y0, dy0, None)
-        self._wgrad("resnet.conv1", self.x0, None, dy0, G)
+        if self.fuse_apply:
+            # maxpool backward + the stem BN's backward reduction in one pass (stores dm0), finalize, then
+            # the stem weight gradient stages dy0 = ca*dm0 + cb*y0 + cc itself (dy0 is never written)
+            st, cf = self.bn_state["resnet.bn1"], self.bn_coef["resnet.bn1"]
+            L.maxpool_bwd_bn(dt, N, H1, W1, 64, ptr(dh), ptr(self.amax), ptr(dz0), ptr(self.y0), ptr(st[2]),
+                             ptr(st[3]), ptr(st[0]), ptr(st[1]), ptr(self.bwd_part), s)
+            self._bn_bwd_fin(P, G, "resnet.bn1", N * H1 * W1, 64, self.bwd_part,
+                             L.dll.argus_maxpool_bwd_bn_rows(dt, N, H1, W1, 64))
+            cv = self.convs["resnet.conv1"]
+            ap = BnBwdPrologue(ptr(self.y0), ptr(cf[0]), ptr(cf[1]), ptr(cf[2]), None)
+            fn = lambda: L.conv_wgrad_apply(C.byref(cv.desc), dt, ptr(self.x0), ptr(dz0), C.byref(ap),  # noqa: E731
+                                            ptr(G["resnet.conv1.weight"]), ptr(self.wg_ws), self.wg_ws_bytes, stream())
+            # on the main stream: it is the last work of the backward (the join would wait for it anyway)
+            self._join()
+            self._launch(cv, 2, fn)
+        else:
+            L.maxpool_bwd(dt, N, H1, W1, 64, ptr(dh), ptr(self.amax), ptr(dz0), s)
+            self._bn_bwd(P, G, "resnet.bn1", N * H1 * W1, 64, dz0, 2, None, self.y0, dy0, None)
+            self._wgrad("resnet.conv1", self.x0, None, dy0, G)
         self._join()
         if on_ready is not None:
             on_ready("resnet.conv1.weight", self._join)

@@ -195,6 +195,12 @@ size_t argus_conv_wgrad_workspace_bytes(const argus_conv_desc* d, int dtype);
 int argus_conv_wgrad(const argus_conv_desc* d, int dtype, const void* x, const float* pro_scale,
                      const float* pro_shift, const void* dy, float* dw, void* workspace,
                      size_t workspace_bytes, argus_stream_t stream);
+/* Weight gradient of the stem whose dy = ca*dm + cb*y + cc (BN-backward apply, argus_bn_bwd_apply's
+ * formula) is formed while staging its operand from dm (ap->dy_out is ignored: the stem's dy feeds
+ * nothing else, so it is never materialised). Stem descriptors only. */
+int argus_conv_wgrad_apply(const argus_conv_desc* d, int dtype, const void* x, const void* dm,
+                           const argus_bn_bwd_prologue* ap, float* dw, void* workspace,
+                           size_t workspace_bytes, argus_stream_t stream);
 
 /* ---- kernel timer (bench.py roofline) ------------------------------------------------------------
  * While enabled, conv and BN kernel launches whose demangled instantiation name (e.g.
@@ -267,6 +273,14 @@ int argus_maxpool_fwd(int dtype, int n, int h, int w, int c, const void* y, cons
                       const float* shift, void* out, uint8_t* argmax, argus_stream_t stream);
 int argus_maxpool_bwd(int dtype, int n, int h, int w, int c, const void* dout,
                       const uint8_t* argmax, void* dz, argus_stream_t stream);
+/* maxpool backward with the stem BatchNorm's backward reduction fused (the pooled tensor is
+ * relu(y*scale+shift), y the stem conv output): stores dm = dz * (y*scale+shift > 0) and
+ * part float2[argus_maxpool_bwd_bn_rows()][c] = {sum dm, sum dm*(y-mean)*invstd}, the input of
+ * argus_bn_bwd_finalize. y == NULL: plain argus_maxpool_bwd. */
+int argus_maxpool_bwd_bn_rows(int dtype, int n, int h, int w, int c);
+int argus_maxpool_bwd_bn(int dtype, int n, int h, int w, int c, const void* dout, const uint8_t* argmax,
+                         void* dm, const void* y, const float* scale, const float* shift,
+                         const float* mean, const float* invstd, float* part, argus_stream_t stream);
 int argus_avgpool_fwd(int dtype, int n, int hw, int c, const void* x, float* feat,
                       argus_stream_t stream);
 int argus_avgpool_bwd(int dtype, int n, int hw, int c, const float* dfeat, void* dx,

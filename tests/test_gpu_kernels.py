@@ -1028,3 +1028,58 @@ def test_dgrad_apply_prologue_matches_apply_pass(cuda, dt):
             assert torch.equal(x0, x1), (cin, cout, k, s, dt, "dx")
             if with_epi:
                 assert torch.equal(p0, p1), (cin, cout, k, s, dt, "partials")
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+def test_stem_backward_fusions(cuda, dt):
+    """argus_maxpool_bwd_bn (maxpool backward + the stem BN's backward reduction) against
+    argus_maxpool_bwd + argus_bn_bwd_reduce(mode 2), and argus_conv_wgrad_apply (the stem weight
+    gradient staging dy = ca*dm + cb*y + cc) against argus_bn_bwd_apply + argus_conv_wgrad: bitwise."""
+    from argus_amd._lib import BnBwdPrologue
+
+    torch.manual_seed(21)
+    L = lib()
+    n, H, W = 4, 34, 30  # odd pooled sizes (17 x 15)
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    y0 = torch.randn(n, H, W, 64, device=cuda).to(TDT[dt])
+    sc, sh = torch.rand(64, device=cuda) + 0.5, torch.randn(64, device=cuda) * 0.3
+    mean, invstd = torch.randn(64, device=cuda) * 0.1, torch.rand(64, device=cuda) + 0.5
+    pooled = torch.empty(n, Ho, Wo, 64, device=cuda, dtype=TDT[dt])
+    amax = torch.empty(n, Ho, Wo, 64, device=cuda, dtype=torch.uint8)
+    L.maxpool_fwd(DT[dt], n, H, W, 64, ptr(y0), ptr(sc), ptr(sh), ptr(pooled), ptr(amax), stream())
+    dout = torch.randn(n, Ho, Wo, 64, device=cuda).to(TDT[dt])
+    # reference path
+    dz = torch.empty(n, H, W, 64, device=cuda, dtype=TDT[dt])
+    L.maxpool_bwd(DT[dt], n, H, W, 64, ptr(dout), ptr(amax), ptr(dz), stream())
+    rows = L.dll.argus_bn_bwd_rows(n * H * W, 64)
+    part_ref = torch.empty(rows, 64, 2, device=cuda)
+    L.bn_bwd_reduce(DT[dt], n * H * W, 64, ptr(dz), 2, None, ptr(y0), ptr(sc), ptr(sh), ptr(mean), ptr(invstd),
+                    ptr(part_ref), None, None, None, None, stream())
+    # fused
+    rows2 = L.dll.argus_maxpool_bwd_bn_rows(DT[dt], n, H, W, 64)
+    part = torch.empty(rows2, 64, 2, device=cuda)
+    dm = torch.empty_like(dz)
+    L.maxpool_bwd_bn(DT[dt], n, H, W, 64, ptr(dout), ptr(amax), ptr(dm), ptr(y0), ptr(sc), ptr(sh), ptr(mean),
+                     ptr(invstd), ptr(part), stream())
+    torch.cuda.synchronize()
+    mask = (y0.double() * sc.double() + sh.double()) > 0
+    assert torch.equal(dm.cpu(), (dz.double() * mask).to(TDT[dt]).cpu())
+    a, b = part.double().sum(0).cpu(), part_ref.double().sum(0).cpu()
+    assert ((a - b).abs() <= 1e-5 * b.abs().max()).all()
+    # stem weight gradient with the apply staged
+    ca, cb, cc = (torch.randn(64, device=cuda) * 0.2 for _ in range(3))
+    x0 = torch.randn(n, 2 * H, 2 * W, 4, device=cuda).to(TDT[dt])
+    x0[..., 3] = 0
+    d, _ = _desc(n, 2 * H, 2 * W, 3, 64, 7, 2, stem=True)
+    assert (d.ho, d.wo) == (H, W)
+    ws = torch.empty(L.dll.argus_conv_wgrad_workspace_bytes(C.byref(d), DT[dt]), dtype=torch.uint8, device=cuda)
+    dy = torch.empty_like(dm)
+    L.bn_bwd_apply(DT[dt], n * H * W, 64, ptr(dm), 0, None, ptr(y0), None, None, ptr(ca), ptr(cb), ptr(cc), ptr(dy),
+                   None, None, None, None, None, None, stream())
+    dw_ref = torch.empty(64, 7, 7, 3, device=cuda)
+    L.conv_wgrad(C.byref(d), DT[dt], ptr(x0), None, None, ptr(dy), ptr(dw_ref), ptr(ws), ws.numel(), stream())
+    dw = torch.empty_like(dw_ref)
+    ap = BnBwdPrologue(ptr(y0), ptr(ca), ptr(cb), ptr(cc), None)
+    L.conv_wgrad_apply(C.byref(d), DT[dt], ptr(x0), ptr(dm), C.byref(ap), ptr(dw), ptr(ws), ws.numel(), stream())
+    torch.cuda.synchronize()
+    assert torch.equal(dw.cpu(), dw_ref.cpu())
