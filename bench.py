@@ -83,6 +83,23 @@ def pmc_traffic(kernel: str, B: int, H: int, W: int, dtype: str):
     return None
 
 
+def pmc_mfma(kernel: str, B: int, H: int, W: int, dtype: str):
+    """MFMA-pipe busy fraction of ``kernel`` (SQ_VALU_MFMA_BUSY_CYCLES over 4 SIMD x 256 CU x kernel
+    cycles) and its wave-state split, from the newest committed PMC summary of this workload
+    (profiles/*_pmc_mfma_summary.json, tools/prof_pmc.sh). None when no summary matches."""
+    prof = sorted(Path(__file__).resolve().parent.glob("profiles/*_pmc_mfma_summary.json"))
+    for p in reversed(prof):
+        d = json.loads(p.read_text())
+        if d.get("meta", {}).get("workload") != [B, H, W, dtype]:
+            continue
+        for name, v in d["kernels"].items():
+            if name == kernel and "mfma_busy" in v:
+                return {"mfma_busy": round(v["mfma_busy"], 4), "wait_frac": round(v.get("wait_frac", 0), 3),
+                        "issue_stall_frac": round(v.get("issue_stall_frac", 0), 3),
+                        "active_frac": round(v.get("active_frac", 0), 3), "source": p.name}
+    return None
+
+
 def cpu_baseline(batch: int, H: int, W: int, budget_s: float = 15.0) -> dict:
     """Oracle (CPU restatement of the reference model, same torch CPU ops) fwd+loss+bwd+clip+Adam."""
     from oracle import se3
@@ -270,6 +287,7 @@ def main() -> None:
             "achieved_tflops": round(tflops, 2), "frac_of_mfma_peak": round(tflops / peak_flops, 4),
             "achieved_gbs": round(gbs, 1), "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4),
             "traffic": pmc_traffic(dom, B, H, W, args.dtype),
+            "mfma_counters": pmc_mfma(dom, B, H, W, args.dtype),
             "concurrency": "weight-gradient kernels run on a side stream, overlapped with the main-stream "
                            "dgrad/BN chain; avg_launch_us is measured while sharing the GPU",
             "isolated_avg_launch_us": round(iso_s["avg_us"], 3) if iso_s else None,

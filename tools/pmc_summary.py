@@ -38,6 +38,8 @@ def main():
     ap.add_argument("out")
     ap.add_argument("dirs", nargs="+")
     ap.add_argument("--top", type=int, default=25)
+    ap.add_argument("--workload", nargs=4, default=["64", "256", "256", "bf16"],
+                    help="B H W dtype of the bench run (bench.py looks the summary up by it)")
     a = ap.parse_args()
     vals = load(a.dirs)
     res = {}
@@ -60,7 +62,9 @@ def main():
         if g:
             d["gpu_cycles"] = g / 8
         res[k] = d
-    Path(a.out).write_text(json.dumps({"derived_from": a.dirs, "kernels": res}, indent=1))
+    meta = {"workload": [int(a.workload[0]), int(a.workload[1]), int(a.workload[2]), a.workload[3]],
+            "derived_from": a.dirs}
+    Path(a.out).write_text(json.dumps({"meta": meta, "kernels": res}, indent=1))
     order = sorted(res.items(), key=lambda kv: -kv[1].get("gpu_cycles", 0) * kv[1]["dispatches"])
     print(f"{'cyc/disp':>9} {'n':>4} {'mfma':>5} {'wait':>5} {'stall':>5} {'act':>5} {'ldsc':>5}  kernel")
     for k, d in order[:a.top]:
