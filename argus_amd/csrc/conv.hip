@@ -416,8 +416,13 @@ ARGUS_DEV int swz32(int row) { return (row & 3) | (((row >> 3) & 1) << 2); }
 
 // OCC: 2 = two workgroups per CU, no register prefetch ring on the 128x128 tile (historical default);
 // 1 = one per CU with the ring; 3 = two per CU with the ring (fits: ~220 VGPRs)
-template <typename T, int BM, int BN, bool STEM, bool PRO, bool FAST, int OCC = 2, bool AP = false>
-__global__ __launch_bounds__(256, OCC == 1 ? 1 : 2) void wgrad_kernel(const WgParams p) {
+// SUB: independent 256-thread sub-pipelines per workgroup, each with its own LDS ring, splitting
+// the workgroup's pixel range in two contiguous halves; their accumulators are summed through LDS
+// (sub 0 + sub 1, fixed order) before the one fp32 partial is written. SUB = 2 keeps the
+// occupancy of two 256-thread workgroups per CU and halves the split partials (HBM traffic and
+// the reduce's input).
+template <typename T, int BM, int BN, bool STEM, bool PRO, bool FAST, int OCC = 2, bool AP = false, int SUB = 1>
+__global__ __launch_bounds__(256 * SUB, (OCC == 1 || SUB == 2) ? 1 : 2) void wgrad_kernel(const WgParams p) {
   constexpr int E = Chunk<T>::E;
   constexpr bool BF = (E == 8);
   constexpr int BKP = BF ? 64 : 32;               // pixels per k-step
@@ -428,16 +433,25 @@ __global__ __launch_bounds__(256, OCC == 1 ? 1 : 2) void wgrad_kernel(const WgPa
   constexpr int RPA = 256 / CA, RPB = 256 / CB;   // rows per staging pass
   constexpr int PA = BKP / RPA, PB = BKP / RPB;   // passes
   constexpr int MI = BM / 32, NI = BN / 32;
-  __shared__ __attribute__((aligned(16))) u32x4 lds[2][BKP * (RSA + RSB)];
+  __shared__ __attribute__((aligned(16))) u32x4 lds_all[SUB][2][BKP * (RSA + RSB)];
+  static_assert(SUB == 1 || (size_t)MI * NI * 256 * 16 <= sizeof(lds_all[0]), "sub-pipeline merge buffer");
+  const int sub = SUB == 1 ? 0 : (int)(threadIdx.x >> 8);
+  auto& lds = lds_all[sub];
 
   const int mtiles = p.M / BM, ntiles = p.N / BN;
   const int nwg = mtiles * ntiles;
   int bid, split;
   split_tile(nwg, (p.P + p.pps - 1) / p.pps, p.S == 1 && p.N == p.Cin, bid, split);
   const int mt = bid / ntiles, nt = bid - mt * ntiles;
-  const int pbeg = split * p.pps;
-  const int pend = min(p.P, pbeg + p.pps);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // this sub-pipeline's pixels: half (SUB = 2) of the split's k-steps; both halves run the same
+  // trip count (the shorter one loads zeros) so the workgroup barriers stay matched
+  const int sbeg = split * p.pps;
+  const int send = min(p.P, sbeg + p.pps);
+  const int nks = send > sbeg ? (send - sbeg + BKP - 1) / BKP : 0;
+  const int nkh = (nks + SUB - 1) / SUB;
+  const int pbeg = sbeg + sub * nkh * BKP;
+  const int pend = min(send, pbeg + nkh * BKP);
+  const int tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const T* __restrict__ X = reinterpret_cast<const T*>(p.x);
   const T* __restrict__ DY = reinterpret_cast<const T*>(p.dy);
@@ -492,11 +506,11 @@ __global__ __launch_bounds__(256, OCC == 1 ? 1 : 2) void wgrad_kernel(const WgPa
     for (int i = 0; i < PA; ++i) {
       const int pix = p0 + ra0 + RPA * i;
       const bool ok = pix < pend;
-      S.a[i] = ld16(a_col + (size_t)(ok ? pix : pbeg) * p.M);
+      S.a[i] = ld16(a_col + (size_t)(ok ? pix : sbeg) * p.M);  // sbeg < P: a safe clamp
       if constexpr (AP) {  // dy = ca*dm + cb*y + cc (argus_bn_bwd_apply's formula, fp32, rounded to T)
         float d[E], yv[E];
         unpack(S.a[i], d);
-        unpack(ld16(ap_col + (size_t)(ok ? pix : pbeg) * p.M), yv);
+        unpack(ld16(ap_col + (size_t)(ok ? pix : sbeg) * p.M), yv);
 #pragma unroll
         for (int j = 0; j < E; ++j) d[j] = fmaf(apa[j], d[j], fmaf(apb[j], yv[j], apc[j]));
         S.a[i] = pack(d);
@@ -518,7 +532,7 @@ __global__ __launch_bounds__(256, OCC == 1 ? 1 : 2) void wgrad_kernel(const WgPa
       if constexpr (FAST) {
         nimg = n0; oh = oh0 + dr[i]; ow = ow0 + dc[i];
       } else {
-        const int pp = pok ? pix : pbeg;
+        const int pp = pok ? pix : sbeg;
         nimg = pp / HWo;
         const int rem = pp - nimg * HWo;
         oh = rem / p.Wo;
@@ -630,7 +644,7 @@ __global__ __launch_bounds__(256, OCC == 1 ? 1 : 2) void wgrad_kernel(const WgPa
   // LDS double buffer + 2-deep register prefetch ring (as igemm_kernel); the 128x128 tile keeps a
   // single staged k-step (the ring would not fit two waves per SIMD without spilling)
   constexpr bool RING = !(BM == 128 && BN == 128) || OCC != 2;
-  const int nk = pend > pbeg ? (pend - pbeg + BKP - 1) / BKP : 0;
+  const int nk = nkh;
   if (!RING && nk > 0) {
     Stage S0;
     load(pbeg, S0);
@@ -666,6 +680,22 @@ __global__ __launch_bounds__(256, OCC == 1 ? 1 : 2) void wgrad_kernel(const WgPa
     if (kt < nk) compute(0);
   }
 
+  if constexpr (SUB == 2) {  // sub 1 hands its accumulators to sub 0 through (its own) LDS
+    f32x4* red = reinterpret_cast<f32x4*>(&lds_all[1][0][0]);
+    __syncthreads();
+    if (sub == 1) {
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) red[(mi * NI + ni) * 256 + tid] = acc[mi][ni];
+    }
+    __syncthreads();
+    if (sub == 1) return;
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) acc[mi][ni] += red[(mi * NI + ni) * 256 + tid];
+  }
   float* out = p.part + (size_t)split * p.M * p.N;
 #pragma unroll
   for (int mi = 0; mi < MI; ++mi)
@@ -931,6 +961,10 @@ static void dispatch_ig_bwd(const IgParams& p, int maxM, int bm, int bn, hipStre
 
 extern int g_glds_min_k, g_glds_min_grid, g_wg_glds_enable, g_wg_glds_target;  // conv_glds.hip
 extern int g_bwd_min_px, g_bwd_max_rows, g_ew_target, g_ew_min_ppt, g_fin_div;  // bn.hip
+// argus_conv_tuning key 26: wgrad_kernel sub-pipelines per workgroup (1 or 2). Measured on MI355X at
+// B=64: SUB = 2 halves the split partials but the shared barrier couples the two pipelines (both
+// load, then both compute): 128x128 alone 72 us vs 62 us, step 8000 vs 8100 img/s -> default 1
+static int g_wg_sub = 1;
 static int g_wg_occ128 = 2;  // argus_conv_tuning key 15: workgroups/CU of the 128x128 wgrad tile (1 = with ring)
 extern int g_halo_enable, g_wg_halo_enable, g_wg_halo_target_blocks, g_halo_min_grid,
     g_wg_halo_max_tiles;  // conv_halo.hip
@@ -998,6 +1032,7 @@ static int* tuning_slot(int key) {
     case 22: return &g_ew_target;     //   bn_apply / bwd_apply target blocks
     case 23: return &g_ew_min_ppt;    //   ... min pixels per thread
     case 24: return &g_fin_div;       //   BN finalize group-count divisor
+    case 26: return &g_wg_sub;
     default: return nullptr;
   }
 }
@@ -1243,6 +1278,7 @@ int conv_dgrad_bn(const argus_conv_desc& d, int dtype, const void* dy, const voi
 struct WgPlan {
   int bm, bn, mt, nt, splits, pps, kstep;
   int N;
+  int sub;  // sub-pipelines per workgroup (wgrad_kernel SUB)
 };
 
 static WgPlan wgrad_plan(const argus_conv_desc& d, int dtype) {
@@ -1260,8 +1296,13 @@ static WgPlan wgrad_plan(const argus_conv_desc& d, int dtype) {
   // (2048 when Cout = 64: one row tile, 9 column tiles)
   long target = g_wgrad_target_blocks;
   if (target == 512 && d.r == 3) target = d.k <= 64 ? 2048 : 1024;
+  // two sub-pipelines per workgroup (bf16 register-staged tiles): half the workgroups, each with
+  // twice the pixels, same wave count on the chip
+  pl.sub = (g_wg_sub == 2 && dtype == ARGUS_BF16 && !d.stem && !(pl.bm == 128 && pl.bn == 128 && g_wg_occ128 != 2))
+               ? 2 : 1;
+  target /= pl.sub;
   long splits = (target + tiles - 1) / tiles;
-  const long max_splits = (P + pl.kstep * 4 - 1) / (pl.kstep * 4);  // >= 4 k-steps per split
+  const long max_splits = (P + pl.kstep * 4 * pl.sub - 1) / (pl.kstep * 4 * pl.sub);  // >= 4 k-steps per sub
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
   long pps = (P + splits - 1) / splits;
@@ -1289,19 +1330,31 @@ size_t conv_wgrad_ws(const argus_conv_desc& d, int dtype) {
   return b;
 }
 
-template <typename T, int BM, int BN, bool STEM, bool PRO, bool FAST, int OCC, bool AP>
+template <typename T, int BM, int BN, bool STEM, bool PRO, bool FAST, int OCC, bool AP, int SUB>
 static const char* wg_name() {
   static const std::string s = std::string("argus::wgrad_kernel<") + type_name<T>() + ", " + std::to_string(BM) +
                                ", " + std::to_string(BN) + ", " + bool_name(STEM) + ", " + bool_name(PRO) + ", " +
-                               bool_name(FAST) + ", " + std::to_string(OCC) + ", " + bool_name(AP) + ">";
+                               bool_name(FAST) + ", " + std::to_string(OCC) + ", " + bool_name(AP) + ", " +
+                               std::to_string(SUB) + ">";
   return s.c_str();
 }
 
 template <typename T, int BM, int BN, bool STEM, bool PRO, bool FAST, int OCC = 2, bool AP = false>
 static void launch_wg(const WgParams& p, const WgPlan& pl, hipStream_t st) {
   dim3 grid(pl.mt * pl.nt * pl.splits);
-  timed_launch(wg_name<T, BM, BN, STEM, PRO, FAST, OCC, AP>(), wgrad_kernel<T, BM, BN, STEM, PRO, FAST, OCC, AP>,
-               grid, dim3(256), st, p);
+  constexpr bool kSub2 = std::is_same<T, bf16>::value && !STEM && OCC == 2;  // wgrad_plan's sub = 2 cases
+  if (pl.sub == 2 && !kSub2) { set_error("wgrad: no two-sub-pipeline variant"); return; }
+  if constexpr (kSub2) {
+    if (pl.sub == 2) {
+      timed_launch(wg_name<T, BM, BN, STEM, PRO, FAST, OCC, AP, 2>(),
+                   wgrad_kernel<T, BM, BN, STEM, PRO, FAST, OCC, AP, 2>, grid, dim3(512), st, p);
+      return;
+    }
+  }
+  {
+    timed_launch(wg_name<T, BM, BN, STEM, PRO, FAST, OCC, AP, 1>(), wgrad_kernel<T, BM, BN, STEM, PRO, FAST, OCC, AP, 1>,
+                 grid, dim3(256), st, p);
+  }
 }
 
 template <typename T, bool PRO, bool FAST>

@@ -181,7 +181,10 @@ int argus_conv_dgrad_bn(const argus_conv_desc* d, int dtype, const void* dy, con
  * 128x128 register-staged wgrad variant (2 default, 1 / 3 with the prefetch ring), key 16 enables
  * (1, default) or disables the bf16 glds wgrad kernel, key 17 its split target (default 512).
  * Keys 20-23 set the BatchNorm elementwise-kernel geometry (backward min pixels per block, max
- * blocks per channel group; apply target blocks, min pixels per thread).
+ * blocks per channel group; apply target blocks, min pixels per thread), key 24 the BN finalize
+ * group-count divisor, key 18 the stem forward occupancy, key 26 the sub-pipelines per workgroup of
+ * the bf16 register-staged weight gradient (1 default; 2 = 512-thread workgroups summing two pixel
+ * halves in LDS: half the split partials, but slower).
  * Returns 0, or -1 for an unknown key. */
 int argus_conv_tuning(int key, int value);
 /* Current value of a tuning key (-1 for an unknown key). */

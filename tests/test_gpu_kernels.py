@@ -760,6 +760,44 @@ def _wgrad_glds_cases(cuda, L, KernelTimer):
         assert _rel(dw.permute(0, 3, 1, 2), ref) < 2e-3, ("wgrad glds", cin, cout, k, s, hw, n)
 
 
+def test_wgrad_sub_pipelines(cuda):
+    """bf16 register-staged weight gradient with two sub-pipelines per workgroup (tuning key 26 = 2:
+    512 threads, the split's pixel range halved, the halves summed in LDS) and with one (key 26 = 1,
+    the default), vs torch fp64: FAST and ragged pixel indexing, odd k-step counts per split (the
+    second half runs a zero-filled tail step), a last split shorter than one half, every row/column
+    tile shape, stride 2. The kernel timer confirms which variant ran."""
+    from argus_amd.profiling import KernelTimer
+
+    torch.manual_seed(31)
+    L = lib()
+    cases = [  # (cin, cout, k, s, hw, n, split target)
+        (256, 256, 1, 1, 16, 4, 512), (64, 256, 1, 1, 13, 3, 512), (256, 64, 1, 1, 13, 3, 64),
+        (128, 128, 3, 2, 17, 2, 512), (256, 512, 1, 2, 16, 2, 512), (512, 128, 1, 1, 9, 5, 8),
+        (128, 128, 3, 1, 16, 2, 96), (64, 64, 1, 1, 64, 2, 2048),
+    ]
+    for cin, cout, k, s, hw, n, target in cases:
+        d, p = _desc(n, hw, hw, cin, cout, k, s)
+        x = _q(torch.randn(n, hw, hw, cin), "bf16")
+        dy = _q(torch.randn(n, d.ho, d.wo, cout), "bf16")
+        xg, dyg = x.to(cuda, torch.bfloat16), dy.to(cuda, torch.bfloat16)
+        ref = torch.nn.grad.conv2d_weight(x.permute(0, 3, 1, 2).double(), (cout, cin, k, k),
+                                          dy.permute(0, 3, 1, 2).double(), stride=s, padding=p)
+        out = {}
+        for sub in (1, 2):
+            with _tuned({26: sub, 6: target, 11: 0, 16: 0}):
+                wsb = L.dll.argus_conv_wgrad_workspace_bytes(C.byref(d), BF16)
+                ws = torch.full((wsb,), 255, dtype=torch.uint8, device=cuda)  # NaN-filled partials
+                dw = torch.empty(cout, k, k, cin, device=cuda)
+                with KernelTimer("argus::wgrad_kernel") as t:
+                    L.conv_wgrad(C.byref(d), BF16, ptr(xg), None, None, ptr(dyg), ptr(dw), ptr(ws), wsb, stream())
+                names = list(t.summary())
+            assert len(names) == 1 and names[0].endswith(f", {sub}>"), (names, sub)
+            e = _rel(dw.permute(0, 3, 1, 2), ref)
+            assert e < 2e-3, ("wgrad sub", sub, cin, cout, k, s, hw, n, target, e)
+            out[sub] = dw.cpu()
+        assert _rel(out[2], out[1]) < 1e-5, (cin, cout, k, s, hw, n)
+
+
 @pytest.mark.parametrize("dt", ["fp32", "bf16"])
 def test_images_u8_layout_matches_fp32_path(cuda, dt):
     """uint8 input path (CameraCubePoseDataset(uint8=True)): the device-side /255 equals the

@@ -17,7 +17,8 @@ timeout -k 10 240 python3 -u bench.py --hw 376 672 --batch 128 --no-cpu-baseline
 bash tools/profile_round.sh $TAG
 python3 tools/pmc_traffic.py gpurun_out/prof_$TAG/pmc_fetch gpurun_out/prof_$TAG/pmc_write $O/pmc_traffic.json 64 256 256 bf16
 python3 tools/profsum.py $(find gpurun_out/prof_$TAG/stats -name "*kernel_stats.csv" | head -1) 28 40 > $O/kernel_summary.txt
-python3 tools/timeline.py $(find gpurun_out/prof_$TAG/stats -name "*kernel_trace.csv" | head -1) --steps 8 --list > $O/timeline.txt
+bash tools/prof_timeline.sh $TAG
+cp gpurun_out/tl_$TAG/timeline.txt $O/timeline.txt
 WORKLOAD="64 256 256 bf16" bash tools/prof_pmc.sh $TAG
 bash tools/profile_round.sh ${TAG}_376 --hw 376 672 --batch 128 --steps 5 --warmup 2
 python3 tools/pmc_traffic.py gpurun_out/prof_${TAG}_376/pmc_fetch gpurun_out/prof_${TAG}_376/pmc_write $O/pmc_traffic_376x672.json 128 376 672 bf16

@@ -3,7 +3,8 @@
     python tools/timeline.py OUT/run_kernel_trace.csv [--steps K]
 
 Steps are delimited by the optimizer kernel (adam_kernel): one step = from the end of one Adam to the
-end of the next. For the last K steps it reports the step wall time, each HIP stream's busy time
+end of the next. Trace a bench run with --no-isolated (tools/prof_timeline.sh does): otherwise the
+last steps are bench.py's two untimed no-overlap steps. For the last K steps it reports the step wall time, each HIP stream's busy time
 (union of its kernel intervals) and idle gaps, and the main stream's (the one running Adam) busy time
 per kernel family — i.e. what the critical path is made of and how much the side stream overlaps.
 """
