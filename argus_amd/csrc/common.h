@@ -22,6 +22,28 @@ constexpr int kWave = 64;
 
 static inline __host__ __device__ int cdiv(int a, int b) { return (a + b - 1) / b; }
 
+// Division of a non-negative int (< 2^31) by a runtime-constant divisor without the ~40-instruction
+// integer division: q = umulhi(n, m) >> s with m = ceil(2^(31+l) / d), l = ceil(log2 d) (the
+// round-up method of Granlund & Montgomery, exact for 31-bit numerators); d = 1 passes through.
+struct FastDiv {
+  int d;
+  unsigned m;
+  int s;
+};
+static inline FastDiv make_fastdiv(int d) {
+  FastDiv f{d, 0u, 0};
+  if (d > 1) {
+    int l = 0;
+    while ((1LL << l) < d) ++l;
+    f.m = (unsigned)(((1ULL << (31 + l)) + (unsigned long long)d - 1) / (unsigned long long)d);
+    f.s = l - 1;
+  }
+  return f;
+}
+ARGUS_DEV int fdiv(int n, const FastDiv& f) {
+  return f.d == 1 ? n : (int)(__umulhi((unsigned)n, f.m) >> f.s);
+}
+
 ARGUS_DEV float to_f32(float x) { return x; }
 ARGUS_DEV float to_f32(bf16 x) { return (float)x; }
 template <typename T> ARGUS_DEV T from_f32(float x);

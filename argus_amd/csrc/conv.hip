@@ -209,7 +209,7 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
 #pragma unroll
         for (int j = 0; j < E; ++j) d[j] = fmaf(ca[j], d[j], fmaf(cb[j], yv[j], cc[j]));
         S.a[i] = sel(S.ok[i], pack(d));
-        if (S.tap0 && S.ok[i]) st16(reinterpret_cast<T*>(p.ap.out) + a_off[i] + S.ch, S.a[i]);
+        if (p.ap.out && S.tap0 && S.ok[i]) st16(reinterpret_cast<T*>(p.ap.out) + a_off[i] + S.ch, S.a[i]);
       }
     }
 #pragma unroll
@@ -519,9 +519,9 @@ __global__ __launch_bounds__(256 * SUB, (OCC == 1 || SUB == 2) ? 1 : 2) void wgr
     }
     int n0 = 0, oh0 = 0, ow0 = 0;
     if constexpr (FAST) {  // uniform: the k-step lies inside one image
-      n0 = p0 / HWo;
+      n0 = fdiv(p0, p.fd_hw);
       const int rem0 = p0 - n0 * HWo;
-      oh0 = rem0 / p.Wo;
+      oh0 = fdiv(rem0, p.fd_w);
       ow0 = rem0 - oh0 * p.Wo;
     }
 #pragma unroll
@@ -533,9 +533,9 @@ __global__ __launch_bounds__(256 * SUB, (OCC == 1 || SUB == 2) ? 1 : 2) void wgr
         nimg = n0; oh = oh0 + dr[i]; ow = ow0 + dc[i];
       } else {
         const int pp = pok ? pix : sbeg;
-        nimg = pp / HWo;
+        nimg = fdiv(pp, p.fd_hw);
         const int rem = pp - nimg * HWo;
-        oh = rem / p.Wo;
+        oh = fdiv(rem, p.fd_w);
         ow = rem - oh * p.Wo;
       }
       const int ih = oh * p.stride - p.pad + tap_r;
@@ -1206,6 +1206,27 @@ int conv_dgrad_bn_rows(const argus_conv_desc& d, int dtype) {
   return p.nphase * dgrad_prow(p, dtype, d);
 }
 
+// Whether argus_conv_dgrad_bn stages the apply prologue inside the (register-staged) dgrad kernel:
+// the halo / glds kernels (LDS DMA, no staging transform) get dy materialised by the apply kernel
+// first, and a 3x3 dgrad would stage each dy element once per tap (9x the apply work, measured slower
+// than the separate pass), so only 1x1 dgrads on the register-staged kernel stage it.
+static bool dgrad_stages_prologue(const argus_conv_desc& d, int dtype, IgParams& p) {
+  if (d.r != 1 || d.s != 1) return false;
+  int maxM = 0, maxK = 0;
+  for (int i = 0; i < p.nphase; ++i) {
+    maxM = p.ph[i].M > maxM ? p.ph[i].M : maxM;
+    maxK = p.ph[i].K > maxK ? p.ph[i].K : maxK;
+  }
+  return !(dtype == ARGUS_BF16 && (conv3x3_halo_ok(p) || igemm_glds_ok(p, maxM, maxK)));
+}
+
+int conv_dgrad_stages_prologue(const argus_conv_desc& d, int dtype) {
+  if (check_desc(d) || d.stem) return 0;
+  IgParams p;
+  dgrad_params(d, nullptr, nullptr, nullptr, nullptr, nullptr, p);
+  return dgrad_stages_prologue(d, dtype, p) ? 1 : 0;
+}
+
 int conv_dgrad_bn(const argus_conv_desc& d, int dtype, const void* dy, const void* wt, void* dm,
                   const void* addend, const argus_bn_bwd_epilogue* bn, const argus_bn_bwd_prologue* pro,
                   hipStream_t st) {
@@ -1220,7 +1241,7 @@ int conv_dgrad_bn(const argus_conv_desc& d, int dtype, const void* dy, const voi
     set_error("conv_dgrad_bn: bad BN-backward epilogue arguments");
     return ARGUS_ERR_ARG;
   }
-  if (pro && (!pro->y || !pro->ca || !pro->cb || !pro->cc || !pro->dy_out || pro->dy_out == dy || pro->dy_out == dm)) {
+  if (pro && (!pro->y || !pro->ca || !pro->cb || !pro->cc || (pro->dy_out && (pro->dy_out == dy || pro->dy_out == dm)))) {
     set_error("conv_dgrad_bn: bad apply-prologue arguments");
     return ARGUS_ERR_ARG;
   }
@@ -1229,15 +1250,11 @@ int conv_dgrad_bn(const argus_conv_desc& d, int dtype, const void* dy, const voi
   if (pro) {
     // the register-staged kernel stages dy = ca*dm + cb*y + cc itself; the halo / glds kernels (LDS
     // DMA, no staging transform) get it materialised by the apply kernel first
-    int maxM = 0, maxK = 0;
-    for (int i = 0; i < p.nphase; ++i) {
-      maxM = p.ph[i].M > maxM ? p.ph[i].M : maxM;
-      maxK = p.ph[i].K > maxK ? p.ph[i].K : maxK;
-    }
-    const bool lds_dma = dtype == ARGUS_BF16 && (conv3x3_halo_ok(p) || igemm_glds_ok(p, maxM, maxK));
-    // a 3x3 dgrad would stage each dy element once per tap (9x the apply work, measured slower than
-    // the separate pass): fused for the 1x1 dgrads only
-    if (lds_dma || d.r != 1 || d.s != 1) {
+    if (!dgrad_stages_prologue(d, dtype, p)) {
+      if (!pro->dy_out) {
+        set_error("conv_dgrad_bn: this dgrad cannot stage the apply prologue; dy_out is required");
+        return ARGUS_ERR_ARG;
+      }
       if (int e = argus_bn_bwd_apply(dtype, (int64_t)d.n * d.ho * d.wo, d.k, dy, 0, nullptr, pro->y, nullptr,
                                      nullptr, pro->ca, pro->cb, pro->cc, pro->dy_out, nullptr, nullptr, nullptr,
                                      nullptr, nullptr, nullptr, st))
@@ -1248,7 +1265,8 @@ int conv_dgrad_bn(const argus_conv_desc& d, int dtype, const void* dy, const voi
     }
   }
   dgrad_work(d, dtype, addend != nullptr, bn->mask_mode == 3, epi, bn->y2 != nullptr);
-  if (p.ap.y) g_launch_bytes += (dtype == ARGUS_BF16 ? 2.0 : 4.0) * 2.0 * d.n * d.ho * d.wo * d.k;  // y in, dy out
+  if (p.ap.y)  // y in (+ dy out)
+    g_launch_bytes += (dtype == ARGUS_BF16 ? 2.0 : 4.0) * (p.ap.out ? 2.0 : 1.0) * d.n * d.ho * d.wo * d.k;
   BnBwdEpi& b = p.bb;
   b.y = bn->y; b.mean = bn->mean; b.invstd = bn->invstd; b.sc = bn->scale; b.sh = bn->shift;
   b.bits = bn->mask_bits; b.y2 = bn->y2; b.mean2 = bn->mean2; b.invstd2 = bn->invstd2;
@@ -1357,16 +1375,16 @@ static void launch_wg(const WgParams& p, const WgPlan& pl, hipStream_t st) {
   }
 }
 
-template <typename T, bool PRO, bool FAST>
+template <typename T, bool PRO, bool FAST, bool AP = false>
 static void dispatch_wg_tiles(const WgParams& p, const WgPlan& pl, hipStream_t st) {
   if (pl.bm == 128 && pl.bn == 128) {
-    if (g_wg_occ128 == 1) launch_wg<T, 128, 128, false, PRO, FAST, 1>(p, pl, st);
-    else if (g_wg_occ128 == 3) launch_wg<T, 128, 128, false, PRO, FAST, 3>(p, pl, st);
-    else launch_wg<T, 128, 128, false, PRO, FAST, 2>(p, pl, st);
+    if (!AP && g_wg_occ128 == 1) launch_wg<T, 128, 128, false, PRO, FAST, 1>(p, pl, st);
+    else if (!AP && g_wg_occ128 == 3) launch_wg<T, 128, 128, false, PRO, FAST, 3>(p, pl, st);
+    else launch_wg<T, 128, 128, false, PRO, FAST, 2, AP>(p, pl, st);
   }
-  else if (pl.bm == 128) launch_wg<T, 128, 64, false, PRO, FAST>(p, pl, st);
-  else if (pl.bn == 128) launch_wg<T, 64, 128, false, PRO, FAST>(p, pl, st);
-  else launch_wg<T, 64, 64, false, PRO, FAST>(p, pl, st);
+  else if (pl.bm == 128) launch_wg<T, 128, 64, false, PRO, FAST, 2, AP>(p, pl, st);
+  else if (pl.bn == 128) launch_wg<T, 64, 128, false, PRO, FAST, 2, AP>(p, pl, st);
+  else launch_wg<T, 64, 64, false, PRO, FAST, 2, AP>(p, pl, st);
 }
 
 template <typename T>
@@ -1382,6 +1400,9 @@ static void dispatch_wg(const WgParams& p, const WgPlan& pl, hipStream_t st) {
       if (fast) launch_wg<T, 64, 128, true, false, true>(p, pl, st);
       else launch_wg<T, 64, 128, true, false, false>(p, pl, st);
     }
+  } else if (p.ap_y) {  // the BN-backward apply of dy staged from dm (argus_conv_wgrad_apply)
+    if (fast) dispatch_wg_tiles<T, false, true, true>(p, pl, st);
+    else dispatch_wg_tiles<T, false, false, true>(p, pl, st);
   } else if (p.pro_scale) {
     if (fast) dispatch_wg_tiles<T, true, true>(p, pl, st);
     else dispatch_wg_tiles<T, true, false>(p, pl, st);
@@ -1414,10 +1435,15 @@ int conv_wgrad(const argus_conv_desc& d, int dtype, const void* x, const float* 
   p.M = d.k; p.N = pl.N; p.Cin = d.stem ? 4 : d.c; p.lda = d.stem ? 4 : d.c;
   p.H = d.h; p.W = d.w; p.Ho = d.ho; p.Wo = d.wo; p.stride = d.stride; p.pad = d.pad; p.S = d.s;
   p.P = d.n * d.ho * d.wo; p.pps = pl.pps; p.stem = d.stem;
+  p.fd_hw = make_fastdiv(d.ho * d.wo); p.fd_w = make_fastdiv(d.wo);
   if (d.stem && sc) { set_error("conv_wgrad: stem has no prologue"); return ARGUS_ERR_ARG; }
   int splits = pl.splits;
   int gs, gpps;
-  if (wgrad3x3_halo_launch(d, dtype, x, sc, sh, dy, ws, ws_bytes, &splits, st)) {
+  if (g_wg_apply) {  // the register-staged kernel stages the apply; no halo / glds variant does
+    if (dtype == ARGUS_BF16) dispatch_wg<bf16>(p, pl, st);
+    else dispatch_wg<float>(p, pl, st);
+    if (int e = check_launch("wgrad_kernel")) return e;
+  } else if (wgrad3x3_halo_launch(d, dtype, x, sc, sh, dy, ws, ws_bytes, &splits, st)) {
     if (int e = check_launch("wgrad3x3_halo_kernel")) return e;
   } else if (wgrad_glds_plan(d, dtype, sc != nullptr, &gs, &gpps) &&
              ws_bytes >= (size_t)gs * d.k * pl.N * sizeof(float)) {
@@ -1440,10 +1466,7 @@ int conv_wgrad(const argus_conv_desc& d, int dtype, const void* x, const float* 
 
 int conv_wgrad_apply(const argus_conv_desc& d, int dtype, const void* x, const void* dm,
                      const argus_bn_bwd_prologue& ap, float* dw, void* ws, size_t ws_bytes, hipStream_t st) {
-  if (!d.stem) {
-    set_error("conv_wgrad_apply: implemented for the stem (whose dy feeds nothing but its weight gradient)");
-    return ARGUS_ERR_ARG;
-  }
+  if (int e = check_desc(d)) return e;
   if (!ap.y || !ap.ca || !ap.cb || !ap.cc) { set_error("conv_wgrad_apply: bad apply arguments"); return ARGUS_ERR_ARG; }
   g_wg_apply = &ap;
   const int rc = conv_wgrad(d, dtype, x, nullptr, nullptr, dm, dw, ws, ws_bytes, st);

@@ -408,8 +408,8 @@ __global__ __launch_bounds__((BM / 64) * 2 * 64, 1) void wgrad_glds_kernel(const
 
   auto issue = [&](int kt, int stage) {
     const int p0 = pbeg + kt * 64;
-    const int n0 = p0 / HWo, rem0 = p0 - n0 * HWo;
-    const int oh0 = rem0 / p.Wo, ow0 = rem0 - oh0 * p.Wo;
+    const int n0 = fdiv(p0, p.fd_hw), rem0 = p0 - n0 * HWo;
+    const int oh0 = fdiv(rem0, p.fd_w), ow0 = rem0 - oh0 * p.Wo;
     const uint32_t base = lds0 + stage * STAGE;
 #pragma unroll
     for (int i = 0; i < GPS; ++i) {

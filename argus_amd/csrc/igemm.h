@@ -80,6 +80,7 @@ struct WgParams {
   // BN-backward apply prologue (AP kernels): dy holds dm; the A operand is ca*dm + cb*ap_y + cc
   const void* ap_y;
   const float *ap_ca, *ap_cb, *ap_cc;
+  FastDiv fd_hw, fd_w;  // Ho*Wo and Wo (pixel -> (image, row, column) without integer division)
 };
 
 template <typename T> struct Mma;

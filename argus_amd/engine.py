@@ -100,6 +100,11 @@ class ResNetEngine:
         # BN-backward apply (dy = ca*dm + cb*y + cc) staged by the consuming dgrad, which also stores dy for
         # the weight gradient (argus_conv_dgrad_bn with a prologue); ARGUS_FUSE_APPLY=0 runs the apply pass
         self.fuse_apply = os.environ.get("ARGUS_FUSE_APPLY", "1") != "0"
+        # ... and where that dgrad stages the apply inside its kernel (1x1, register-staged:
+        # argus_conv_dgrad_stages_prologue), dy is not stored at all: the side-stream weight gradient
+        # stages the same apply from dm and y (argus_conv_wgrad_apply). Moves the dy write off the main
+        # stream (one more read on the side stream). ARGUS_WGRAD_APPLY=0 stores dy as before.
+        self.wgrad_apply = os.environ.get("ARGUS_WGRAD_APPLY", "1") != "0"
         fold = os.environ.get("ARGUS_FOLD_FIN", "bwd")  # A/B at B=64: fwd fold neutral, bwd +0.3 %
         self.fold_fin_fwd = fold in ("1", "fwd")
         self.fold_fin = fold in ("1", "bwd")  # backward
@@ -212,11 +217,13 @@ class ResNetEngine:
         ws = max(L.dll.argus_conv_wgrad_workspace_bytes(C.byref(cv.desc), dt) for cv in convs.values())
         self.wg_ws = torch.empty(ws, dtype=torch.uint8, device=self.device)
         self.wg_ws_bytes = ws
+        self.stages_pro = {n: bool(L.dll.argus_conv_dgrad_stages_prologue(C.byref(cv.desc), dt))
+                           for n, cv in convs.items() if not cv.desc.stem}
         self.gbuf = [self._t(max_elems) for _ in range(4)]  # dh / dx ping-pong, dz ping-pong
         # dy operands of the side-stream weight gradients come from a ring, so the main stream can
         # run ahead of the wgrad stream by several layers before it must wait to reuse a buffer
         # (ARGUS_DY_RING buffers; a reuse waits on the event of the wgrad that last read it)
-        nring = max(2, int(os.environ.get("ARGUS_DY_RING", "8")))
+        nring = max(8, int(os.environ.get("ARGUS_DY_RING", "12")))  # >= 2 blocks of takes
         self.dyring = [self._t(max_elems) for _ in range(nring)]
         self._ring_i = 0
 
@@ -419,7 +426,7 @@ class ResNetEngine:
         L.gemm_f32(N, 2048, R, ptr(self.dh0), R, 0, ptr(fcw), 2048, 0, ptr(self.dfeat), 2048, None, 0, None, ptr(self.gemm_ws), self.gemm_ws.numel(), s)
         hf, wf = self.final_hw
         g = self.gbuf
-        dh, dx = g[0], g[1]
+        dh = g[0]
         L.avgpool_bwd(dt, N, hf * wf, 2048, ptr(self.dfeat), ptr(dh), s)
         if on_ready is not None:
             on_ready("resnet.fc.weight", self._join)
@@ -440,9 +447,14 @@ class ResNetEngine:
             ho, wo = a["hw"]
             px_o = N * ho * wo
             px_i = N * hi * wi
-            dy3 = self._next_dy()
             dyd = self._next_dy() if b.has_ds else None
             dbg = self.debug
+            # weight gradients that stage the BN-backward apply from dm themselves (dy never stored;
+            # the debug capture keeps storing it for the stage checks)
+            wg3_apply = (rows3 is not None and self.fuse_apply and self.wgrad_apply and self.materialize
+                         and self.stages_pro[pf + ".conv3"])
+            wg1_apply = idx > 0 and self.fuse_apply and self.wgrad_apply and self.stages_pro[pf + ".conv1"]
+            dy3 = None if wg3_apply and dbg is None else self._next_dy()
 
             def cap(key, t, n, shape):
                 if dbg is not None:
@@ -479,10 +491,13 @@ class ResNetEngine:
             # conv3 -> bn2
             r2 = self._dgrad_bn(pf + ".conv3", dh if pro3 else dy3, dza, None, pf + ".bn2", a["y2"], 2, P=P, G=G,
                                 pro=pro3)
-            cap("b_dy3", dy3, px_o * b.cout, (N, ho, wo, b.cout))
+            if dy3 is not None:
+                cap("b_dy3", dy3, px_o * b.cout, (N, ho, wo, b.cout))
             cap("b_dz2", dza, px_o * b.width, (N, ho, wo, b.width))
             s2 = self.bn_state[pf + ".bn2"]
-            if self.materialize:
+            if wg3_apply:  # dh holds dm3 (read by the side stream until its event: dh is not reused)
+                self._wgrad_apply(pf + ".conv3", a["a2"], dh, pf + ".bn3", a["y3"], G)
+            elif self.materialize:
                 self._wgrad(pf + ".conv3", a["a2"], None, dy3, G)
             else:
                 self._wgrad(pf + ".conv3", a["y2"], s2, dy3, G)
@@ -494,7 +509,9 @@ class ResNetEngine:
             else:
                 pro2 = None
                 self._bn_apply_bwd(pf + ".bn2", px_o, b.width, dza, a["y2"], dy2)
-            # conv2 -> bn1
+            # conv2 -> bn1 (dm1 goes to a ring buffer when the side stream's conv1 wgrad reads it)
+            if wg1_apply:
+                dzb = self._next_dy()
             r1 = self._dgrad_bn(pf + ".conv2", dza if pro2 else dy2, dzb, None, pf + ".bn1", a["y1"], 2, P=P, G=G,
                                 pro=pro2)
             cap("b_dy2", dy2, px_o * b.width, (N, ho, wo, b.width))
@@ -506,12 +523,15 @@ class ResNetEngine:
                 self._wgrad(pf + ".conv2", a["y1"], s1, dy2, G)
             if r1:
                 self._bn_bwd_fin(P, G, pf + ".bn1", px_i, b.width, self.bwd_part, r1)
-            dy1 = self._next_dy()
+            dy1 = None if wg1_apply and dbg is None else self._next_dy()
             pro1 = None
             if fuse and idx > 0:
                 pro1 = (pf + ".bn1", a["y1"], dy1)
             else:
                 self._bn_apply_bwd(pf + ".bn1", px_i, b.width, dzb, a["y1"], dy1)
+            # the block-input gradient goes to a fresh ring buffer (dm3 / dm1 may still be read by the
+            # side stream; a buffer held across blocks must never be handed out again while live)
+            dx = self._next_dy()
             # conv1 (+ downsample) -> the previous block's bn3 (+ its downsample BN): dm3 of block idx-1
             c1_in = dzb if pro1 else dy1
             if idx > 0:
@@ -529,13 +549,17 @@ class ResNetEngine:
                 self._dgrad(pf + ".conv1", dy1, dx)
                 if b.has_ds:
                     self._dgrad(pf + ".downsample.0", dyd, dx, addend=dx)
-            cap("b_dy1", dy1, px_i * b.width, (N, hi, wi, b.width))
+            if dy1 is not None:
+                cap("b_dy1", dy1, px_i * b.width, (N, hi, wi, b.width))
             if b.has_ds:
                 cap("b_dyd", dyd, px_o * b.cout, (N, ho, wo, b.cout))
-            self._wgrad(pf + ".conv1", h_in, None, dy1, G)
+            if wg1_apply:
+                self._wgrad_apply(pf + ".conv1", h_in, dzb, pf + ".bn1", a["y1"], G)
+            else:
+                self._wgrad(pf + ".conv1", h_in, None, dy1, G)
             if b.has_ds:
                 self._wgrad(pf + ".downsample.0", h_in, None, dyd, G)
-            dh, dx = dx, dh
+            dh = dx
             if on_ready is not None:
                 on_ready(pf + ".conv1.weight", self._join)
             if self.debug is not None:
@@ -595,6 +619,7 @@ class ResNetEngine:
             st2 = self.bn_state[second[0]]
             e.y2, e.mean2, e.invstd2, e.part2 = ptr(second[1]), ptr(st2[0]), ptr(st2[1]), ptr(self.bwd_part2)
         pp = self._prologue(pro)
+        self._guard(dm)
         self._launch(cv, 1, lambda: self.L.conv_dgrad_bn(C.byref(cv.desc), self.dt, ptr(dy), ptr(cv.wd), ptr(dm),
                                                           ptr(addend), C.byref(e), pp, stream()))
         return 0 if self.fold_fin else self.L.dll.argus_conv_dgrad_bn_rows(C.byref(cv.desc), self.dt)
@@ -606,7 +631,8 @@ class ResNetEngine:
             return None
         cf = self.bn_coef[pro[0]]
         self._guard(pro[2])
-        return C.byref(BnBwdPrologue(ptr(pro[1]), ptr(cf[0]), ptr(cf[1]), ptr(cf[2]), ptr(pro[2])))
+        return C.byref(BnBwdPrologue(ptr(pro[1]), ptr(cf[0]), ptr(cf[1]), ptr(cf[2]), ptr(pro[2]) if pro[2] is not None
+                                     else None))
 
     def _dgrad_plain_or_pro(self, conv, dy, dx, pro):
         """dgrad without a BN epilogue (the conv1 dgrad of a downsample block, accumulated into by the
@@ -616,6 +642,7 @@ class ResNetEngine:
             return
         cv = self.convs[conv]
         pp = self._prologue(pro)
+        self._guard(dx)
         self._launch(cv, 1, lambda: self.L.conv_dgrad_bn(C.byref(cv.desc), self.dt, ptr(dy), ptr(cv.wd), ptr(dx),
                                                           None, None, pp, stream()))
 
@@ -664,6 +691,21 @@ class ResNetEngine:
         self._pending[dy.data_ptr()] = done
         self._last_side = done
 
+    def _wgrad_apply(self, conv, x, dm, bn, y, G):
+        """Weight gradient of ``conv`` whose dy = ca*dm + cb*y + cc (BN ``bn``'s backward apply) is staged
+        by the wgrad kernel from dm (argus_conv_wgrad_apply); same placement as _wgrad."""
+        cv = self.convs[conv]
+        cf = self.bn_coef[bn]
+        ap = BnBwdPrologue(ptr(y), ptr(cf[0]), ptr(cf[1]), ptr(cf[2]), None)
+        fn = lambda: self.L.conv_wgrad_apply(C.byref(cv.desc), self.dt, ptr(x), ptr(dm), C.byref(ap),  # noqa: E731
+                                             ptr(G[conv + ".weight"]), ptr(self.wg_ws), self.wg_ws_bytes, stream())
+        if not self.wgrad_overlap:
+            self._launch(cv, 2, fn)
+            return
+        done = self._on_side(lambda: self._launch(cv, 2, fn))
+        self._pending[dm.data_ptr()] = done
+        self._last_side = done
+
     def _on_side(self, fn):
         """Run ``fn``'s launches on the side stream after the main stream's work so far; returns the
         side-stream event that marks their completion."""
@@ -701,6 +743,7 @@ class ResNetEngine:
 
     def _dgrad(self, conv, dy, dx, addend=None, mask=None):
         cv = self.convs[conv]
+        self._guard(dx)
         self._launch(cv, 1, lambda: self.L.conv_dgrad(C.byref(cv.desc), self.dt, ptr(dy), ptr(cv.wd), ptr(dx),
                                                        ptr(addend), ptr(mask), stream()))
 

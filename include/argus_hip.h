@@ -156,7 +156,10 @@ typedef struct {
  * argument of argus_conv_dgrad_bn holds dm (the masked gradient of a BN output) and the dgrad consumes
  * dy = ca*dm + cb*y + cc (per channel; argus_bn_bwd_apply's formula), which it also stores to dy_out
  * for the weight gradient. Kernels that cannot stage it run argus_bn_bwd_apply first (same result).
- * `bn` may be NULL with a prologue: a plain dgrad (no BN-backward epilogue) of the applied dy. */
+ * `bn` may be NULL with a prologue: a plain dgrad (no BN-backward epilogue) of the applied dy.
+ * dy_out may be NULL when argus_conv_dgrad_stages_prologue(d, dtype) is 1 (1x1 dgrads on the
+ * register-staged kernel): dy is then never stored, and the weight gradient stages the same apply
+ * from dm itself (argus_conv_wgrad_apply). */
 typedef struct {
   const void* y;
   const float* ca;
@@ -165,6 +168,9 @@ typedef struct {
   void* dy_out;
 } argus_bn_bwd_prologue;
 int argus_conv_dgrad_bn_rows(const argus_conv_desc* d, int dtype);
+/* 1 when argus_conv_dgrad_bn stages an apply prologue inside the dgrad kernel for this conv (so
+ * dy_out may be NULL), 0 when it materialises dy with argus_bn_bwd_apply first. */
+int argus_conv_dgrad_stages_prologue(const argus_conv_desc* d, int dtype);
 int argus_conv_dgrad_bn(const argus_conv_desc* d, int dtype, const void* dy, const void* w_dgrad,
                         void* dm, const void* addend, const argus_bn_bwd_epilogue* bn,
                         const argus_bn_bwd_prologue* pro, argus_stream_t stream);
@@ -198,9 +204,11 @@ size_t argus_conv_wgrad_workspace_bytes(const argus_conv_desc* d, int dtype);
 int argus_conv_wgrad(const argus_conv_desc* d, int dtype, const void* x, const float* pro_scale,
                      const float* pro_shift, const void* dy, float* dw, void* workspace,
                      size_t workspace_bytes, argus_stream_t stream);
-/* Weight gradient of the stem whose dy = ca*dm + cb*y + cc (BN-backward apply, argus_bn_bwd_apply's
- * formula) is formed while staging its operand from dm (ap->dy_out is ignored: the stem's dy feeds
- * nothing else, so it is never materialised). Stem descriptors only. */
+/* Weight gradient whose dy = ca*dm + cb*y + cc (BN-backward apply, argus_bn_bwd_apply's formula) is
+ * formed while staging its operand from dm (ap->dy_out is ignored): dy is never materialised. Used
+ * for the stem (whose dy feeds nothing else) and for the 1x1 convs whose dgrad stages the same apply
+ * (argus_conv_dgrad_stages_prologue). Runs the register-staged wgrad kernel; the input x has no
+ * BN prologue. */
 int argus_conv_wgrad_apply(const argus_conv_desc* d, int dtype, const void* x, const void* dm,
                            const argus_bn_bwd_prologue* ap, float* dw, void* workspace,
                            size_t workspace_bytes, argus_stream_t stream);

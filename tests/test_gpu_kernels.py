@@ -513,8 +513,8 @@ def test_conv_glds_kernel_parity(cuda):
 
     torch.manual_seed(11)
     L = lib()
-    assert L.dll.argus_conv_tuning(8, 64) == 0 and L.dll.argus_conv_tuning(9, 1) == 0
     defaults = (L.dll.argus_conv_tuning_get(8), L.dll.argus_conv_tuning_get(9))
+    assert L.dll.argus_conv_tuning(8, 64) == 0 and L.dll.argus_conv_tuning(9, 1) == 0
     try:
         for cin, cout, k, s, hin, n in GLDS_SHAPES:
             d, p = _desc(n, hin, hin, cin, cout, k, s)
@@ -1066,6 +1066,68 @@ def test_dgrad_apply_prologue_matches_apply_pass(cuda, dt):
             assert torch.equal(x0, x1), (cin, cout, k, s, dt, "dx")
             if with_epi:
                 assert torch.equal(p0, p1), (cin, cout, k, s, dt, "partials")
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+def test_unstored_apply_and_wgrad_apply(cuda, dt):
+    """1x1 dgrads whose kernel stages the apply prologue (argus_conv_dgrad_stages_prologue == 1) with
+    dy_out = NULL: dx and the BN-backward partials bit-identical to the stored-dy form; the weight
+    gradient staging the same apply from dm (argus_conv_wgrad_apply, non-stem) bit-identical to
+    argus_conv_wgrad of the materialised dy (FAST and ragged pixel indexing, every tile shape).
+    dy_out = NULL where the dgrad cannot stage the apply is an argument error."""
+    from argus_amd._lib import BnBwdEpilogue, BnBwdPrologue
+
+    torch.manual_seed(14)
+    L = lib()
+    staged = 0
+    for cin, cout, k, s, hin, n in [(256, 64, 1, 1, 16, 2), (64, 256, 1, 1, 13, 3), (512, 128, 1, 1, 8, 4),
+                                    (256, 512, 1, 2, 15, 2), (1024, 256, 1, 1, 6, 2), (128, 128, 3, 1, 8, 2)]:
+        d, p = _desc(n, hin, hin, cin, cout, k, s)
+        st = L.dll.argus_conv_dgrad_stages_prologue(C.byref(d), DT[dt])
+        w = torch.randn(cout, k, k, cin) * (2.0 / (k * k * cin)) ** 0.5
+        _, wt = _prep(d, dt, w.to(cuda), cuda)
+        dm = torch.randn(n, d.ho, d.wo, cout, device=cuda).to(TDT[dt])
+        yb = torch.randn(n, d.ho, d.wo, cout, device=cuda).to(TDT[dt])
+        ca, cb, cc = (torch.randn(cout, device=cuda) * 0.3 for _ in range(3))
+        yin = torch.randn(n, hin, hin, cin, device=cuda).to(TDT[dt])
+        mean, invstd = torch.randn(cin, device=cuda) * 0.1, torch.rand(cin, device=cuda) + 0.5
+        sc, sh = torch.randn(cin, device=cuda), torch.randn(cin, device=cuda)
+        rows = L.dll.argus_conv_dgrad_bn_rows(C.byref(d), DT[dt])
+        outs = []
+        for store in (True, False):
+            part = torch.zeros(rows, cin, 2, device=cuda)
+            e = BnBwdEpilogue()
+            e.y, e.mean, e.invstd, e.mask_mode, e.scale, e.shift, e.part = ptr(yin), ptr(mean), ptr(invstd), \
+                2, ptr(sc), ptr(sh), ptr(part)
+            dy = torch.zeros(n, d.ho, d.wo, cout, device=cuda, dtype=TDT[dt])
+            dx = torch.empty(n, hin, hin, cin, device=cuda, dtype=TDT[dt])
+            pro = BnBwdPrologue(ptr(yb), ptr(ca), ptr(cb), ptr(cc), ptr(dy) if store else None)
+            rc = L.dll.argus_conv_dgrad_bn(C.byref(d), DT[dt], ptr(dm), ptr(wt), ptr(dx), None, C.byref(e),
+                                           C.byref(pro), stream())
+            if not store and not st:
+                assert rc != 0  # the library would have to materialise dy: dy_out is required
+                break
+            assert rc == 0, L.dll.argus_last_error()
+            torch.cuda.synchronize()
+            outs.append((dy.cpu(), dx.cpu(), part.cpu()))
+        if not st:
+            continue
+        staged += 1
+        (y0, x0, p0), (y1, x1, p1) = outs
+        assert torch.equal(x0, x1) and torch.equal(p0, p1), (cin, cout, k, s, dt)
+        assert int((y1 != 0).sum()) == 0  # nothing stored
+        # weight gradient: staged apply vs the materialised dy of the first run
+        xw = torch.randn(n, hin, hin, cin, device=cuda).to(TDT[dt])
+        ws = torch.empty(L.dll.argus_conv_wgrad_workspace_bytes(C.byref(d), DT[dt]), dtype=torch.uint8, device=cuda)
+        dw_ref = torch.empty(cout, k, k, cin, device=cuda)
+        L.conv_wgrad(C.byref(d), DT[dt], ptr(xw), None, None, ptr(y0.to(cuda)), ptr(dw_ref), ptr(ws), ws.numel(),
+                     stream())
+        dw = torch.empty_like(dw_ref)
+        ap = BnBwdPrologue(ptr(yb), ptr(ca), ptr(cb), ptr(cc), None)
+        L.conv_wgrad_apply(C.byref(d), DT[dt], ptr(xw), ptr(dm), C.byref(ap), ptr(dw), ptr(ws), ws.numel(), stream())
+        torch.cuda.synchronize()
+        assert torch.equal(dw.cpu(), dw_ref.cpu()), (cin, cout, k, s, dt)
+    assert staged >= 3
 
 
 @pytest.mark.parametrize("dt", ["fp32", "bf16"])
