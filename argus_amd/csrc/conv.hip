@@ -1009,6 +1009,11 @@ static int run_ig(const IgParams& p, hipStream_t st, int bm, int bn) {
 // (0 = heuristic) and the wgrad split target.
 static int g_force_bm[3] = {0, 0, 0}, g_force_bn[3] = {0, 0, 0};
 static int g_wgrad_target_blocks = 512;
+// key 27: split target of the register-staged 3x3 wgrad (Cout > 64). Isolated sweeps favoured 1024;
+// in the full step 512 wins (+0.7 %): fewer fp32 split partials (for layer 4's 3x3, 7 splits wrote
+// 66 MB of partials against 8 MB of operands), which contend with the main stream for HBM
+static int g_wgrad_target_3x3 = 512;
+static int g_wgrad_partial_budget = 0;  // key 28: split-partial bytes <= this x operand bytes (0 = off)
 
 static int* tuning_slot(int key) {
   if (key >= 0 && key < 3) return &g_force_bm[key];
@@ -1033,6 +1038,8 @@ static int* tuning_slot(int key) {
     case 23: return &g_ew_min_ppt;    //   ... min pixels per thread
     case 24: return &g_fin_div;       //   BN finalize group-count divisor
     case 26: return &g_wg_sub;
+    case 27: return &g_wgrad_target_3x3;
+    case 28: return &g_wgrad_partial_budget;
     default: return nullptr;
   }
 }
@@ -1313,13 +1320,20 @@ static WgPlan wgrad_plan(const argus_conv_desc& d, int dtype) {
   // measured (tools/tilesweep.py, MI355X): 1x1 convs peak near 512 workgroups, 3x3 near 1024
   // (2048 when Cout = 64: one row tile, 9 column tiles)
   long target = g_wgrad_target_blocks;
-  if (target == 512 && d.r == 3) target = d.k <= 64 ? 2048 : 1024;
+  if (target == 512 && d.r == 3) target = d.k <= 64 ? 2048 : g_wgrad_target_3x3;
   // two sub-pipelines per workgroup (bf16 register-staged tiles): half the workgroups, each with
   // twice the pixels, same wave count on the chip
   pl.sub = (g_wg_sub == 2 && dtype == ARGUS_BF16 && !d.stem && !(pl.bm == 128 && pl.bn == 128 && g_wg_occ128 != 2))
                ? 2 : 1;
   target /= pl.sub;
   long splits = (target + tiles - 1) / tiles;
+  if (g_wgrad_partial_budget > 0 && !d.stem) {
+    // cap the fp32 split partials (written + read back: 8 B per dW element per split) at a multiple
+    // of the operand bytes: the deep layers' dW is larger than their activations
+    const double ops = (double)(dtype == ARGUS_BF16 ? 2 : 4) * ((double)d.n * d.h * d.w * d.c + (double)P * d.k);
+    const long cap = (long)(g_wgrad_partial_budget * ops / (8.0 * d.k * pl.N));
+    if (splits > cap) splits = cap < 2 ? 2 : cap;
+  }
   const long max_splits = (P + pl.kstep * 4 * pl.sub - 1) / (pl.kstep * 4 * pl.sub);  // >= 4 k-steps per sub
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;

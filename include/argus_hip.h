@@ -190,7 +190,9 @@ int argus_conv_dgrad_bn(const argus_conv_desc* d, int dtype, const void* dy, con
  * blocks per channel group; apply target blocks, min pixels per thread), key 24 the BN finalize
  * group-count divisor, key 18 the stem forward occupancy, key 26 the sub-pipelines per workgroup of
  * the bf16 register-staged weight gradient (1 default; 2 = 512-thread workgroups summing two pixel
- * halves in LDS: half the split partials, but slower).
+ * halves in LDS: half the split partials, but slower), key 27 the split target of the register-staged
+ * 3x3 weight gradient (default 512), key 28 a cap on the weight gradients' split partials as a
+ * multiple of the operand bytes (0 = off, the default; 1-4 measured neutral).
  * Returns 0, or -1 for an unknown key. */
 int argus_conv_tuning(int key, int value);
 /* Current value of a tuning key (-1 for an unknown key). */
