@@ -291,6 +291,8 @@ def main() -> None:
             "concurrency": "weight-gradient kernels run on a side stream, overlapped with the main-stream "
                            "dgrad/BN chain; avg_launch_us is measured while sharing the GPU",
             "isolated_avg_launch_us": round(iso_s["avg_us"], 3) if iso_s else None,
+            "isolated_launches": iso_s["launches"] if iso_s else None,
+            "isolated_flops_per_launch": round(iso_s["flops_per_launch"]) if iso_s else None,
             "isolated_frac": (round((iso_s["flops_per_launch"] / (iso_s["avg_us"] * 1e-6) / 1e12) / peak_flops
                                     if compute_bound else
                                     iso_s["bytes_per_launch"] / (iso_s["avg_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
