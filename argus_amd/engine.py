@@ -22,6 +22,7 @@ Eval mode uses running statistics (bn_eval_coeffs) and skips all statistics / ru
 from __future__ import annotations
 
 import ctypes as C
+import contextlib
 import os
 from dataclasses import dataclass
 
@@ -90,8 +91,8 @@ class ResNetEngine:
         self.debug: dict | None = None  # when a dict: clones of block outputs / block-input grads
         # Weight gradients run on a side stream, overlapped with the dgrad -> BN-backward chain of the
         # main stream (they only feed the gradient buffer). Events order them after their dy and
-        # before any main-stream overwrite of that dy buffer; the trainer joins the side stream before
-        # each bucket all-reduce (on_ready's join) and backward() joins it at its end.
+        # before any main-stream overwrite of that dy buffer; each bucket all-reduce is issued on the
+        # side stream after both streams' work (on_ready's comm) and backward() joins it at its end.
         # ARGUS_WGRAD_STREAM=0 keeps everything on the caller's stream.
         self.wgrad_overlap = os.environ.get("ARGUS_WGRAD_STREAM", "1") != "0"
         # BN finalize (forward statistics and backward coefficients) folded into the producing conv
@@ -402,13 +403,13 @@ class ResNetEngine:
     def backward(self, dpred: torch.Tensor, P: dict, G: dict, on_ready=None) -> None:
         """Write every parameter gradient into G[name] (fp32; conv weights OHWI-contiguous).
 
-        ``on_ready(name, join)`` (optional) is called, in stream order, as soon as the gradients of
+        ``on_ready(name, comm)`` (optional) is called, in stream order, as soon as the gradients of
         parameter ``name`` and of every parameter registered after it have been issued: after the head
         ("resnet.fc.weight"), after each block ("<block>.conv1.weight"), after the stem
         ("resnet.conv1.weight"). Weight gradients may still be running on the side stream then:
-        ``join()`` makes the current stream wait for them, and must be called before anything on the
-        current stream reads those gradients (the trainer calls it right before it issues a bucket's
-        all-reduce, so blocks that do not close a bucket keep their overlap)."""
+        ``with comm():`` is the context to issue a collective over those gradients in - the stream it
+        makes current is ordered after both streams' work so far, and the main stream is not made to
+        wait (the trainer issues each bucket's all-reduce in it, so the backward keeps its overlap)."""
         if not self.saved:
             raise RuntimeError("backward without a saved train-mode forward")
         L, dt, s = self.L, self.dt, stream()
@@ -438,7 +439,7 @@ class ResNetEngine:
         dh = g[0]
         L.avgpool_bwd(dt, N, hf * wf, 2048, ptr(self.dfeat), ptr(dh), s)
         if on_ready is not None:
-            on_ready("resnet.fc.weight", self._join)
+            on_ready("resnet.fc.weight", self._comm)
 
         # BN backward: the reduction over dz = d(BN output) runs in the epilogue of the dgrad that
         # produces dz (argus_conv_dgrad_bn), which stores the ReLU-masked dm and the partial column
@@ -571,7 +572,7 @@ class ResNetEngine:
             dh = dx
             self._flush_side()
             if on_ready is not None:
-                on_ready(pf + ".conv1.weight", self._join)
+                on_ready(pf + ".conv1.weight", self._comm)
             if self.debug is not None:
                 n_in = N * hi * wi * b.cin
                 self.debug["bwd." + pf] = dh[:n_in].view(N, hi, wi, b.cin).clone()
@@ -599,7 +600,7 @@ class ResNetEngine:
             self._wgrad("resnet.conv1", self.x0, None, dy0, G)
         self._join()
         if on_ready is not None:
-            on_ready("resnet.conv1.weight", self._join)
+            on_ready("resnet.conv1.weight", self._comm)
 
     def _dgrad_bn(self, conv, dy, dm, addend, bn, y, mode, bits=None, second=None, P=None, G=None, pro=None):
         """dgrad of ``conv`` whose output feeds BN ``bn`` (input ``y``) backward: stores the masked dm
@@ -767,6 +768,21 @@ class ResNetEngine:
         if ev is not None and ev[0] > self._waited_seq:
             torch.cuda.current_stream().wait_event(ev[1])
             self._waited_seq = ev[0]
+
+    @contextlib.contextmanager
+    def _comm(self):
+        """Stream context for a collective over the gradients issued so far: the side stream waits for
+        the main stream's work so far (one event) and is made current, so the collective (RCCL's
+        stream waits on the current one) follows both streams while the main stream runs on."""
+        self._flush_side()
+        if self._side is None:
+            yield
+            return
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream())
+        self._side.wait_event(ev)
+        with torch.cuda.stream(self._side):
+            yield
 
     def _join(self) -> None:
         """Main stream waits for every weight gradient issued so far."""

@@ -10,7 +10,8 @@ wgrad / BN / head kernels (no autograd), and the step is:
 
     engine.forward (bf16 or fp32 HIP kernels) -> se3_loss kernel (loss + dpred/B)
     -> engine.backward, starting a bucketed RCCL all-reduce (SUM, async, own stream) on each flat
-       suffix of >= bucket_mb as soon as backward has finished it (DDP's overlap, without DDP)
+       suffix of >= bucket_mb as soon as backward has finished it (DDP's overlap, without DDP); the
+       collective is issued behind the weight-gradient side stream, so the main stream never waits
     -> wait -> global-norm kernel -> fused clip + 1/world + Adam kernel (28 B/param, HBM-bound)
 
 Multi-GPU: one process per GPU; torch.distributed "nccl" is RCCL over xGMI on MI355X. BN statistics
@@ -77,14 +78,18 @@ class GradBucketer:
         self.works = []
         self.pending_end = self.grad.numel()
 
-    def ready(self, name: str, join=None) -> None:
-        """Gradients of ``name`` and everything after it are issued; ``join()`` (optional) makes the
-        current stream wait until they are written. Issues a bucket when the suffix is big enough."""
+    def ready(self, name: str, comm=None) -> None:
+        """Gradients of ``name`` and everything after it are issued; ``comm()`` (optional) is the stream
+        context, ordered after the work that writes them, to issue the collective in (the engine's
+        side stream after a wait on the main stream: the main stream itself does not wait). Issues a
+        bucket when the suffix is big enough."""
         start = self.offsets[name]
         if self.pending_end - start >= self.bucket or start == 0:
-            if join is not None:
-                join()
-            self._issue(start)
+            if comm is not None:
+                with comm():
+                    self._issue(start)
+            else:
+                self._issue(start)
 
     def _issue(self, start: int) -> None:
         if self.pending_end > start:
