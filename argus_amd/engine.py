@@ -252,6 +252,7 @@ class ResNetEngine:
                   (128, 128, B), (128, D, B), (B, D, 128), (self.rdim, Fd, N), (N, Fd, self.rdim)]
         hws = max(L.dll.argus_gemm_f32_workspace_bytes(*sh) for sh in shapes)
         self.gemm_ws = torch.empty(max(hws, 16), dtype=torch.uint8, device=self.device)
+        self.gemm_ws_side = torch.empty(max(hws, 16), dtype=torch.uint8, device=self.device)
 
     # ------------------------------------------------------------------ helpers
     def _bn_train(self, P, Bf, name, rows, tile, count, part=None, ws=None):
@@ -418,22 +419,34 @@ class ResNetEngine:
         D = self.n_cams * self.rdim
         dpred = dpred.contiguous().float()
         w0, w2, w4 = P["output_mlp.0.weight"], P["output_mlp.2.weight"], P["output_mlp.4.weight"]
-        # MLP
-        L.gemm_f32(6, 128, B, ptr(dpred), 6, 1, ptr(self.g2), 128, 0, ptr(G["output_mlp.4.weight"]), 128, None, 0, None, ptr(self.gemm_ws), self.gemm_ws.numel(), s)
-        L.colsum_f32(B, 6, ptr(dpred), 6, ptr(G["output_mlp.4.bias"]), s)
-        L.gemm_f32(B, 128, 6, ptr(dpred), 6, 0, ptr(w4), 128, 0, ptr(self.dh2), 128, None, 3, ptr(self.h2), ptr(self.gemm_ws), self.gemm_ws.numel(), s)
-        L.gemm_f32(128, 128, B, ptr(self.dh2), 128, 1, ptr(self.g1), 128, 0, ptr(G["output_mlp.2.weight"]), 128, None, 0, None, ptr(self.gemm_ws), self.gemm_ws.numel(), s)
-        L.colsum_f32(B, 128, ptr(self.dh2), 128, ptr(G["output_mlp.2.bias"]), s)
-        L.gemm_f32(B, 128, 128, ptr(self.dh2), 128, 0, ptr(w2), 128, 0, ptr(self.dh1), 128, None, 3, ptr(self.h1), ptr(self.gemm_ws), self.gemm_ws.numel(), s)
-        L.gemm_f32(128, D, B, ptr(self.dh1), 128, 1, ptr(self.g0), D, 0, ptr(G["output_mlp.0.weight"]), D, None, 0, None, ptr(self.gemm_ws), self.gemm_ws.numel(), s)
-        L.colsum_f32(B, 128, ptr(self.dh1), 128, ptr(G["output_mlp.0.bias"]), s)
-        L.gemm_f32(B, D, 128, ptr(self.dh1), 128, 0, ptr(w0), D, 0, ptr(self.dh0), D, None, 3, ptr(self.h0), ptr(self.gemm_ws), self.gemm_ws.numel(), s)
-        # fc (rows = images)
+        # MLP + fc data path (main stream): dh2 -> dh1 -> dh0 -> dfeat
+        ws, wsn = ptr(self.gemm_ws), self.gemm_ws.numel()
+        L.gemm_f32(B, 128, 6, ptr(dpred), 6, 0, ptr(w4), 128, 0, ptr(self.dh2), 128, None, 3, ptr(self.h2), ws, wsn, s)
+        L.gemm_f32(B, 128, 128, ptr(self.dh2), 128, 0, ptr(w2), 128, 0, ptr(self.dh1), 128, None, 3, ptr(self.h1), ws, wsn, s)
+        L.gemm_f32(B, D, 128, ptr(self.dh1), 128, 0, ptr(w0), D, 0, ptr(self.dh0), D, None, 3, ptr(self.h0), ws, wsn, s)
         fcw = P["resnet.fc.weight"]
         R = self.rdim
-        L.gemm_f32(R, 2048, N, ptr(self.dh0), R, 1, ptr(self.feat), 2048, 0, ptr(G["resnet.fc.weight"]), 2048, None, 0, None, ptr(self.gemm_ws), self.gemm_ws.numel(), s)
-        L.colsum_f32(N, R, ptr(self.dh0), R, ptr(G["resnet.fc.bias"]), s)
-        L.gemm_f32(N, 2048, R, ptr(self.dh0), R, 0, ptr(fcw), 2048, 0, ptr(self.dfeat), 2048, None, 0, None, ptr(self.gemm_ws), self.gemm_ws.numel(), s)
+
+        def head_wgrads():  # weight / bias gradients of the head: nothing downstream reads them
+            ss, w2s, w2n = stream(), ptr(self.gemm_ws_side), self.gemm_ws_side.numel()
+            L.gemm_f32(6, 128, B, ptr(dpred), 6, 1, ptr(self.g2), 128, 0, ptr(G["output_mlp.4.weight"]), 128, None, 0,
+                       None, w2s, w2n, ss)
+            L.colsum_f32(B, 6, ptr(dpred), 6, ptr(G["output_mlp.4.bias"]), ss)
+            L.gemm_f32(128, 128, B, ptr(self.dh2), 128, 1, ptr(self.g1), 128, 0, ptr(G["output_mlp.2.weight"]), 128, None,
+                       0, None, w2s, w2n, ss)
+            L.colsum_f32(B, 128, ptr(self.dh2), 128, ptr(G["output_mlp.2.bias"]), ss)
+            L.gemm_f32(128, D, B, ptr(self.dh1), 128, 1, ptr(self.g0), D, 0, ptr(G["output_mlp.0.weight"]), D, None, 0,
+                       None, w2s, w2n, ss)
+            L.colsum_f32(B, 128, ptr(self.dh1), 128, ptr(G["output_mlp.0.bias"]), ss)
+            L.gemm_f32(R, 2048, N, ptr(self.dh0), R, 1, ptr(self.feat), 2048, 0, ptr(G["resnet.fc.weight"]), 2048, None, 0,
+                       None, w2s, w2n, ss)
+            L.colsum_f32(N, R, ptr(self.dh0), R, ptr(G["resnet.fc.bias"]), ss)
+
+        if self.wgrad_overlap:  # beside the fc data gradient and the last blocks' backward
+            self._last_side = self._on_side(head_wgrads)
+        else:
+            head_wgrads()
+        L.gemm_f32(N, 2048, R, ptr(self.dh0), R, 0, ptr(fcw), 2048, 0, ptr(self.dfeat), 2048, None, 0, None, ws, wsn, s)
         hf, wf = self.final_hw
         g = self.gbuf
         dh = g[0]
