@@ -121,6 +121,9 @@ class ResNetEngine:
         self._deferred: list = []  # (cv, fn, buffer data_ptrs)
         self._side_seq = 0
         self._waited_seq = 0
+        # the stem weight gradient (main stream, its own split workspace) is issued before the final
+        # join, beside the side stream's last weight gradients (+0.2 %); ARGUS_STEM_OVERLAP=0 after it
+        self._stem_overlap = os.environ.get("ARGUS_STEM_OVERLAP", "1") == "1"
 
     # ------------------------------------------------------------------ allocation
     def _t(self, *shape, dtype=None):
@@ -227,6 +230,8 @@ class ResNetEngine:
         ws = max(L.dll.argus_conv_wgrad_workspace_bytes(C.byref(cv.desc), dt) for cv in convs.values())
         self.wg_ws = torch.empty(ws, dtype=torch.uint8, device=self.device)
         self.wg_ws_bytes = ws
+        wss = L.dll.argus_conv_wgrad_workspace_bytes(C.byref(convs["resnet.conv1"].desc), dt)
+        self.wg_ws_stem = torch.empty(wss, dtype=torch.uint8, device=self.device)
         self.stages_pro = {n: bool(L.dll.argus_conv_dgrad_stages_prologue(C.byref(cv.desc), dt))
                            for n, cv in convs.items() if not cv.desc.stem}
         self.gbuf = [self._t(max_elems) for _ in range(4)]  # dh / dx ping-pong, dz ping-pong
@@ -603,9 +608,11 @@ class ResNetEngine:
             cv = self.convs["resnet.conv1"]
             ap = BnBwdPrologue(ptr(self.y0), ptr(cf[0]), ptr(cf[1]), ptr(cf[2]), None)
             fn = lambda: L.conv_wgrad_apply(C.byref(cv.desc), dt, ptr(self.x0), ptr(dz0), C.byref(ap),  # noqa: E731
-                                            ptr(G["resnet.conv1.weight"]), ptr(self.wg_ws), self.wg_ws_bytes, stream())
-            # on the main stream: it is the last work of the backward (the join would wait for it anyway)
-            self._join()
+                                            ptr(G["resnet.conv1.weight"]), ptr(self.wg_ws_stem),
+                                            self.wg_ws_stem.numel(), stream())
+            # on the main stream: it is the last work of the backward
+            if not self._stem_overlap:
+                self._join()
             self._launch(cv, 2, fn)
         else:
             L.maxpool_bwd(dt, N, H1, W1, 64, ptr(dh), ptr(self.amax), ptr(dz0), s)
