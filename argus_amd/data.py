@@ -13,7 +13,9 @@ installed here).
 Augmentation: the "spaghetti" occluder arcs (data.py:212-215, utils.py:252-275) are drawn exactly
 as the reference does (same PIL calls and np.random draws; train and val). The kornia photometric
 augmentations (data.py:41-103: Planckian jitter, ColorJiggle, Gaussian / motion blur, plasma
-shadow) are not applied: a warning says so once whenever an ``AugmentationConfig`` enables them.
+shadow) run on the device instead, on whole uint8 batches after the H2D copy
+(``argus_amd.augment.DeviceAugmentation``; ``argus_amd.train`` applies it to training batches): the
+dataset itself returns them unapplied, and says so once when used outside ``argus_amd.train``.
 ``cfg_aug=None`` works (the reference crashes on it, data.py:213). ``CameraCubePoseDatasetConfig``
 resolves ROOT-relative paths without tripping its own ``frozen=True`` (data.py:126-130).
 ``uint8=True`` keeps images as uint8 (4x less host->device traffic; the engine converts on device).
@@ -43,8 +45,9 @@ _warned = False
 
 @dataclass(frozen=True)
 class AugmentationConfig:
-    """Same fields as argus/data.py:18-39. ``num_spaghetti`` is applied; the photometric flags are
-    accepted but not applied (warned once)."""
+    """Same fields as argus/data.py:18-39. ``num_spaghetti`` is applied by the dataset; the photometric
+    flags by ``argus_amd.augment.DeviceAugmentation`` on the device (random erasing and salt-and-pepper,
+    off in the reference's defaults, are not provided)."""
 
     brightness: Union[float, tuple] = (0.8, 1.0)
     contrast: Union[float, tuple] = (0.5, 1.2)
@@ -95,7 +98,7 @@ class CameraCubePoseDataset(Dataset):
     """The dataset for N cameras and a cube (argus/data.py:145-229)."""
 
     def __init__(self, cfg_dataset: CameraCubePoseDatasetConfig, cfg_aug: Optional[AugmentationConfig] = None,
-                 train: bool = True, uint8: bool = False) -> None:
+                 train: bool = True, uint8: bool = False, device_augmentation: bool = False) -> None:
         dataset_path = cfg_dataset.dataset_path
         with h5lite.File(dataset_path + f"/{Path(dataset_path).stem}.hdf5") as f:
             ds = f["train"] if train else f["test"]
@@ -105,14 +108,14 @@ class CameraCubePoseDataset(Dataset):
             self.q_leap = torch.from_numpy(np.asarray(ds["q_leap"][()]))
             self.img_stems = [s.decode("utf-8") for s in ds["img_stems"][()]]
         self.cfg_aug = cfg_aug
-        self.augmentation = None  # kornia photometric augmentations: not applied (module docstring)
+        self.augmentation = None  # photometric augmentations: on the device (argus_amd.augment)
         enabled = [k for k in PHOTOMETRIC_FLAGS if cfg_aug is not None and getattr(cfg_aug, k)]
         global _warned
-        if enabled and train and not _warned:
+        if enabled and train and not _warned and not device_augmentation:
             _warned = True
-            warnings.warn(f"argus_amd: kornia photometric augmentations {enabled} are not applied (the "
-                          "spaghetti occluders are); pass an AugmentationConfig with them off to silence this",
-                          stacklevel=2)
+            warnings.warn(f"argus_amd: the photometric augmentations {enabled} are applied on the device by "
+                          "argus_amd.augment.DeviceAugmentation (argus_amd.train does); this dataset returns "
+                          "them unapplied (the spaghetti occluders are drawn here)", stacklevel=2)
         self.dataset_path = dataset_path
         self.center_crop = cfg_dataset.center_crop
         self.uint8 = uint8

@@ -147,6 +147,7 @@ def _device_for(cfg: TrainConfig, rank: int) -> torch.device:
 
 def initialize_training(cfg: TrainConfig, rank: int = 0, world: int = 1):
     """Seeds, device, datasets/loaders, model, fused trainer, LR schedule (train.py:122-255)."""
+    from argus_amd.augment import DeviceAugmentation
     from argus_amd.step import FusedTrainer
 
     torch.manual_seed(cfg.random_seed)
@@ -161,7 +162,8 @@ def initialize_training(cfg: TrainConfig, rank: int = 0, world: int = 1):
     torch.cuda.set_device(device)
 
     # uint8 batches: 4x less host->device traffic; the /255 of argus/data.py:214-215 runs on the device
-    train_ds = CameraCubePoseDataset(cfg.dataset_config, cfg_aug=cfg.augmentation_config, train=True, uint8=True)
+    train_ds = CameraCubePoseDataset(cfg.dataset_config, cfg_aug=cfg.augmentation_config, train=True, uint8=True,
+                                     device_augmentation=True)
     val_ds = CameraCubePoseDataset(cfg.dataset_config, cfg_aug=cfg.augmentation_config, train=False, uint8=True)
     distributed = world > 1
     train_sampler = DistributedSampler(train_ds, num_replicas=world, rank=rank, shuffle=True) if distributed else None
@@ -182,6 +184,8 @@ def initialize_training(cfg: TrainConfig, rank: int = 0, world: int = 1):
             dist.broadcast(t.data, src=0)
     trainer = FusedTrainer(model, lr=cfg.learning_rate, max_grad_norm=cfg.max_grad_norm)
     scheduler = PlateauScheduler(trainer, patience=5, factor=0.5)
+    # the reference's kornia augmentations of each training sample (data.py:222-224), on the device
+    trainer.augment = DeviceAugmentation(cfg.augmentation_config, train=True, seed=cfg.random_seed + 1000 * rank)
     return train_loader, val_loader, model, trainer, scheduler, _run_id(), train_sampler, val_sampler, device
 
 
@@ -214,7 +218,7 @@ def train(cfg: TrainConfig, rank: int = 0) -> str:
         model.train()
         epoch_losses = []
         for example in train_loader:
-            images = example["images"].to(device, non_blocking=True)
+            images = trainer.augment(example["images"].to(device, non_blocking=True))
             target = example["cube_pose"].to(device, non_blocking=True)
             losses = trainer.step(images, target)
             epoch_losses.append(losses.clone())

@@ -326,6 +326,16 @@ int argus_se3_loss(int batch, const float* pred, const float* target, float* los
  * [t, qx, qy, qz, qw]; canonical_w != 0 flips q to w >= 0. */
 int argus_se3_exp(int batch, const float* xi, float* out, int canonical_w, argus_stream_t stream);
 
+/* ---- photometric training augmentations (argus/data.py:41-103; csrc/augment.hip) -------------
+ * src: uint8 images (n_img, 3, H, W) planar (a B x 6 x H x W sample batch is 2B such images);
+ * dst: fp32 (same shape) = augmented src / 255; params: n_img AugParams records of
+ * argus_augment_params_bytes() bytes each (device memory; layout in augment.hip / augment.py);
+ * scratch: n_img * 3 * H * W floats. Planckian gains -> ColorJiggle (sampled op order) -> 5x5
+ * Gaussian blur (reflect) -> 3x3 motion blur (zero border) -> plasma shadow, per image. */
+size_t argus_augment_params_bytes(void);
+int argus_augment_photometric(int64_t n_img, int h, int w, const uint8_t* src, float* dst, const void* params,
+                              float* scratch, argus_stream_t stream);
+
 /* ---- optimizer step (clip_grad_norm_ + Adam, argus/train.py:232,317-320) --------------------- */
 size_t argus_sumsq_workspace_bytes(int64_t count);
 /* out[0] = sqrt(sum x^2) (fp32, deterministic two-level reduction). */
