@@ -89,6 +89,44 @@ ARGUS_DEV u32x4 pack(const float (&f)[8]) {
   v.z = pack2_bf16(f[4], f[5]); v.w = pack2_bf16(f[6], f[7]); return v;
 }
 
+typedef int v8i __attribute__((ext_vector_type(8)));
+ARGUS_DEV v8i cat8(u32x4 lo, u32x4 hi) {
+  return v8i{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+}
+
+// OCP MX-fp8 quantization of 16 bf16 (two chunks, this thread's half of a 32-element block): the
+// block amax (bf16 bit patterns: |x| ordered as unsigned, v_pk_max_u16) is shared with the partner
+// lane (lane ^ 1 holds the other half); its E8M0 exponent e is the smallest with amax * 2^-e < 448
+// (the e4m3 maximum, so nothing saturates): amax = 2^(E-127) (1 + f/128) gives e = E - 135, + 1 when
+// f >= 96. v_cvt_scalef32_pk_fp8_bf16 divides by 2^e and rounds to e4m3 (probed:
+// tools/probes/fp8_cvt_probe.hip). Returns e through `e`.
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef short s16x2v __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2v __attribute__((ext_vector_type(2)));
+ARGUS_DEV u32x4 mx_fp8_quant(u32x4 lo, u32x4 hi, int& e) {
+  const unsigned w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  u16x2v m = __builtin_bit_cast(u16x2v, w[0] & 0x7fff7fffu);
+#pragma unroll
+  for (int j = 1; j < 8; ++j) m = __builtin_elementwise_max(m, __builtin_bit_cast(u16x2v, w[j] & 0x7fff7fffu));
+  unsigned mb = m.x > m.y ? m.x : m.y;
+  const unsigned mo = (unsigned)__shfl_xor((int)mb, 1, 64);
+  mb = mb > mo ? mb : mo;
+  const int E = (int)(mb >> 7), f = (int)(mb & 127u);
+  int ex = E == 0 ? 0 : E - 135 + (f >= 96 ? 1 : 0);
+  ex = ex < -126 ? -126 : (ex > 127 ? 127 : ex);
+  e = ex;
+  const float sc = __int_as_float((127 + ex) << 23);
+  unsigned o[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    s16x2v r = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16((s16x2v){0, 0}, __builtin_bit_cast(bf16x2v, w[2 * q]), sc,
+                                                          false);
+    r = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(r, __builtin_bit_cast(bf16x2v, w[2 * q + 1]), sc, true);
+    o[q] = __builtin_bit_cast(unsigned, r);
+  }
+  return u32x4{o[0], o[1], o[2], o[3]};
+}
+
 // ReLU mask of a stored chunk: bit j set <=> element j > 0 (one byte per 16-byte chunk).
 template <typename T>
 ARGUS_DEV uint8_t chunk_positive_bits(u32x4 v) {

@@ -70,11 +70,17 @@ template <typename T, int BM, int BN, bool STEM, bool PRO, int OCC, int BWX>
 __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
   constexpr int BW = BWX & 7;                   // BN-backward epilogue variant
   constexpr bool AP = (BWX & kApplyBit) != 0;   // BN-backward apply prologue
+  constexpr bool F8 = (BWX & kFp8Bit) != 0;     // MX-fp8 operands (bf16 storage)
+  static_assert(!F8 || (sizeof(T) == 2 && !STEM && !PRO && !AP), "fp8: bf16 tensors, no staging transforms");
   constexpr int E = Chunk<T>::E;
-  constexpr int BKE = 8 * E;  // K elements per k-step (8 chunks of 16 B per LDS row)
+  constexpr int EF = F8 ? 2 * E : E;  // elements one thread stages per row per k-step
+  constexpr int BKE = 8 * EF;  // K elements per k-step (8 chunks of 16 B per LDS row)
   constexpr int MI = BM / 32, NI = BN / 32;
   constexpr int AR = BM / 32, BR = BN / 32;
-  constexpr int NBUF = OCC >= 3 ? 1 : 2;
+  // fp8: one LDS buffer, no register ring (the bf16 pair per chunk doubles the staging registers;
+  // an LDS double buffer with one staged copy measured slower: fwd+dgrad 7.37 vs 6.62 ms)
+  constexpr int NBUF = (OCC >= 3 || F8) ? 1 : 2;
+  __shared__ uint8_t lds_sc[1][F8 ? BM + BN : 1][4];  // fp8: E8M0 scale of (row, 32-element block)
   constexpr int HALF_C = (BM / 2) * (BN + 16 / (int)sizeof(T)) * (int)sizeof(T);  // epilogue pass of BM/2 rows
   constexpr int RED_B = (256 / (BN * (int)sizeof(T) / 16)) * BN * 8;            // BN-backward column sums
   constexpr int LDS0 = NBUF * (BM + BN) * 128 > HALF_C ? NBUF * (BM + BN) * 128 : HALF_C;
@@ -125,7 +131,7 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
   const T* b_row[BR];
 #pragma unroll
   for (int i = 0; i < BR; ++i)
-    b_row[i] = B + (size_t)(nt * BN + (tid >> 3) + 32 * i) * p.ldb + cidx * E;
+    b_row[i] = B + (size_t)(nt * BN + (tid >> 3) + 32 * i) * p.ldb + cidx * EF;
 
   f32x4 acc[MI][NI];
 #pragma unroll
@@ -136,6 +142,7 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
   // one k-step of staged operands (two named copies form the 2-deep prefetch ring)
   struct Stage {
     u32x4 a[AR], b[BR];
+    u32x4 a2[F8 ? AR : 1], b2[F8 ? BR : 1];  // fp8: the second bf16 chunk of the thread's 16 elements
     u32x4 y[AP ? AR : 1];  // apply prologue: the BN input rows beside the dm rows
     bool ok[AR];
     int ch, tap0;  // tap0: this k-step is the center tap of phase 0 (the dy store)
@@ -170,19 +177,23 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
       const int t = k0 / p.Cin;
       const int ci0 = k0 - t * p.Cin;
       const int dh = ph.dh[t], dw = ph.dw[t], boff = ph.boff[t];
-      const int ch = ci0 + cidx * E;
+      const int ch = ci0 + cidx * EF;
       const int tap = (dh * p.W + dw) * p.lda + ch;
 #pragma unroll
       for (int i = 0; i < AR; ++i) {
         const int ih = a_ih[i] + dh, iw = a_iw[i] + dw;
         const bool ok = a_ok[i] && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
         S.a[i] = ld16(A + (ok ? a_off[i] + tap : ch));
+        if constexpr (F8) S.a2[i] = sel(ok, ld16(A + (ok ? a_off[i] + tap + E : ch)));
         if constexpr (AP) S.y[i] = ld16(reinterpret_cast<const T*>(p.ap.y) + (ok ? a_off[i] + tap : ch));
         if constexpr (!PRO && !AP) S.a[i] = sel(ok, S.a[i]);
         S.ok[i] = ok;
       }
 #pragma unroll
-      for (int i = 0; i < BR; ++i) S.b[i] = ld16(b_row[i] + boff + ci0);
+      for (int i = 0; i < BR; ++i) {
+        S.b[i] = ld16(b_row[i] + boff + ci0);
+        if constexpr (F8) S.b2[i] = ld16(b_row[i] + boff + ci0 + E);
+      }
       S.ch = ch;
       if constexpr (AP) S.tap0 = dh == 0 && dw == 0 && blockIdx.z == 0 && nt == 0;
     }
@@ -212,6 +223,23 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
         if (p.ap.out && S.tap0 && S.ok[i]) st16(reinterpret_cast<T*>(p.ap.out) + a_off[i] + S.ch, S.a[i]);
       }
     }
+    if constexpr (F8) {  // 16 bf16 -> 16 e4m3 with the 32-element block scale shared with lane ^ 1
+#pragma unroll
+      for (int i = 0; i < AR; ++i) {
+        const int row = (tid >> 3) + 32 * i;
+        int e;
+        L[row * 8 + (cidx ^ swz8(row))] = mx_fp8_quant(S.a[i], S.a2[i], e);
+        if ((cidx & 1) == 0) lds_sc[buf][row][cidx >> 1] = (uint8_t)(127 + e);
+      }
+#pragma unroll
+      for (int i = 0; i < BR; ++i) {
+        const int row = (tid >> 3) + 32 * i;
+        int e;
+        L[BM * 8 + row * 8 + (cidx ^ swz8(row))] = mx_fp8_quant(S.b[i], S.b2[i], e);
+        if ((cidx & 1) == 0) lds_sc[buf][BM + row][cidx >> 1] = (uint8_t)(127 + e);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
       const int row = (tid >> 3) + 32 * i;
@@ -227,6 +255,30 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
   const int g = lane >> 4, i16 = lane & 15;
   auto compute = [&](int buf) {
     const u32x4* L = lds + buf * (BM + BN) * 8;
+    if constexpr (F8) {
+      // v_mfma_scale_f32_16x16x128_f8f6f4 operand layout (probed, tools/probes/): lane (row i16,
+      // group g) holds K bytes [16g, 16g+16) and [64+16g, 64+16g+16) = LDS chunks g and g+4; the
+      // scale operand of lane (i16, g) is the E8M0 scale of (row i16, 32-element block g)
+      v8i fb[NI];
+      int sb[NI];
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) {
+        const int row = wn * (BN / 2) + ni * 16 + i16;
+        fb[ni] = cat8(L[BM * 8 + row * 8 + (g ^ swz8(row))], L[BM * 8 + row * 8 + ((g + 4) ^ swz8(row))]);
+        sb[ni] = lds_sc[buf][BM + row][g];
+      }
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) {
+        const int row = wm * (BM / 2) + mi * 16 + i16;
+        const v8i fa = cat8(L[row * 8 + (g ^ swz8(row))], L[row * 8 + ((g + 4) ^ swz8(row))]);
+        const int sa = lds_sc[buf][row][g];
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fa, fb[ni], acc[mi][ni], 0, 0, 0, sa, 0,
+                                                                          sb[ni]);
+      }
+      return;
+    }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       u32x4 fa[MI], fb[NI];
@@ -975,6 +1027,16 @@ static int g_smallk_max = 1024;
 // argus_conv_tuning key 18: stem forward kernel, 2 (ring) or 4 (single buffer; convbench B=64:
 // 214 -> 179 us)
 static int g_stem_occ = 4;
+static int g_f8_occ = 2;  // argus_conv_tuning key 29: workgroups per CU of the MX-fp8 igemm (2 or 4 -> 3 for 128x128)
+
+// MX-fp8 operands (ARGUS_FP8) need whole 128-element k-steps inside one filter tap and no staging
+// transform of the A operand; other convs of an fp8 network run the bf16 kernels
+static bool f8_ok(const IgParams& p) {
+  if (!p.f8 || p.stem || p.pro_scale || p.ap.y || p.Cin % 128) return false;
+  for (int i = 0; i < p.nphase; ++i)
+    if (p.ph[i].K % 128) return false;
+  return true;
+}
 
 template <typename T>
 static int run_ig(const IgParams& p, hipStream_t st, int bm, int bn) {
@@ -985,6 +1047,25 @@ static int run_ig(const IgParams& p, hipStream_t st, int bm, int bn) {
   }
   const bool smallk = maxK <= g_smallk_max;
   if constexpr (sizeof(T) == 2) {
+    if (f8_ok(p)) {  // single-buffered (the staged bf16 pair per chunk doubles the staging registers)
+      const int v = p.bb.mode ? bwd_variant(p.bb) : 0;
+      if (g_f8_occ == 4) {
+        switch (v) {
+          case 2: dispatch_ig<T, false, 4, 2 | kFp8Bit>(p, maxM, bm, bn, st); break;
+          case 3: dispatch_ig<T, false, 4, 3 | kFp8Bit>(p, maxM, bm, bn, st); break;
+          case 4: dispatch_ig<T, false, 4, 4 | kFp8Bit>(p, maxM, bm, bn, st); break;
+          default: dispatch_ig<T, false, 4, kFp8Bit>(p, maxM, bm, bn, st);
+        }
+      } else {
+        switch (v) {
+          case 2: dispatch_ig<T, false, 2, 2 | kFp8Bit>(p, maxM, bm, bn, st); break;
+          case 3: dispatch_ig<T, false, 2, 3 | kFp8Bit>(p, maxM, bm, bn, st); break;
+          case 4: dispatch_ig<T, false, 2, 4 | kFp8Bit>(p, maxM, bm, bn, st); break;
+          default: dispatch_ig<T, false, 2, kFp8Bit>(p, maxM, bm, bn, st);
+        }
+      }
+      return check_launch("igemm_kernel");
+    }
     if (conv3x3_halo_launch(p, st)) return check_launch("conv3x3_halo_kernel");
     if (igemm_glds_launch(p, maxM, maxK, st)) return check_launch("igemm_glds_kernel");
   }
@@ -1040,6 +1121,7 @@ static int* tuning_slot(int key) {
     case 26: return &g_wg_sub;
     case 27: return &g_wgrad_target_3x3;
     case 28: return &g_wgrad_partial_budget;
+    case 29: return &g_f8_occ;
     default: return nullptr;
   }
 }
@@ -1086,6 +1168,8 @@ static int dgrad_bm(const argus_conv_desc&) {
 int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, void* y,
              const float* sc, const float* sh, float* stats, hipStream_t st) {
   if (int e = check_desc(d)) return e;
+  const bool f8 = dtype == ARGUS_FP8;  // bf16 tensors, MX-fp8 GEMM operands where the shape allows
+  if (f8) dtype = ARGUS_BF16;
   g_launch_work = 2.0 * d.n * d.ho * d.wo * d.k * d.r * d.s * d.c;  // algorithmic flops / bytes (ktimer)
   g_launch_bytes = (double)(dtype == ARGUS_BF16 ? 2 : 4) *
                        ((double)d.n * d.h * d.w * (d.stem ? 4 : d.c) + (double)d.k * d.r * d.s * d.c +
@@ -1113,6 +1197,7 @@ int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, 
   }
   const int bm = fwd_bm(d), bn = d.stem ? 64 : pick_bn(0, d.k);
   p.stat_tile = bm;
+  p.f8 = f8;
   if (g_fwd_fin && stats) {  // argus_conv_fwd_bn: the statistics finalize folded into this launch
     const argus_bn_fwd_fin& f = *g_fwd_fin;
     BnFin& b = p.fin;
@@ -1165,7 +1250,7 @@ static int dgrad_prow(const IgParams& p, int dtype, const argus_conv_desc& d) {
     maxM = p.ph[i].M > maxM ? p.ph[i].M : maxM;
     maxK = p.ph[i].K > maxK ? p.ph[i].K : maxK;
   }
-  if (dtype == ARGUS_BF16) {
+  if (dtype == ARGUS_BF16 && !f8_ok(p)) {
     if (conv3x3_halo_ok(p)) return p.ph[0].M / 256;
     if (igemm_glds_ok(p, maxM, maxK)) return cdiv(maxM, 256);
   }
@@ -1198,10 +1283,13 @@ int conv_fwd_bn(const argus_conv_desc& d, int dtype, const void* x, const void* 
 int conv_dgrad(const argus_conv_desc& d, int dtype, const void* dy, const void* wt, void* dx,
                const void* addend, const uint8_t* addend_mask, hipStream_t st) {
   if (int e = check_desc(d)) return e;
+  const bool f8 = dtype == ARGUS_FP8;
+  if (f8) dtype = ARGUS_BF16;
   dgrad_work(d, dtype, addend != nullptr, addend_mask != nullptr, false, false);
   if (d.stem) { set_error("conv_dgrad: the stem input has no gradient"); return ARGUS_ERR_ARG; }
   IgParams p;
   dgrad_params(d, dy, wt, dx, addend, addend_mask, p);
+  p.f8 = f8;
   const int bm = dgrad_bm(d), bn = pick_bn(1, d.c);
   return dtype == ARGUS_BF16 ? run_ig<bf16>(p, st, bm, bn) : run_ig<float>(p, st, bm, bn);
 }
@@ -1210,7 +1298,8 @@ int conv_dgrad_bn_rows(const argus_conv_desc& d, int dtype) {
   if (check_desc(d) || d.stem) return -1;
   IgParams p;
   dgrad_params(d, nullptr, nullptr, nullptr, nullptr, nullptr, p);
-  return p.nphase * dgrad_prow(p, dtype, d);
+  p.f8 = dtype == ARGUS_FP8;
+  return p.nphase * dgrad_prow(p, p.f8 ? ARGUS_BF16 : dtype, d);
 }
 
 // Whether argus_conv_dgrad_bn stages the apply prologue inside the (register-staged) dgrad kernel:
@@ -1219,6 +1308,10 @@ int conv_dgrad_bn_rows(const argus_conv_desc& d, int dtype) {
 // than the separate pass), so only 1x1 dgrads on the register-staged kernel stage it.
 static bool dgrad_stages_prologue(const argus_conv_desc& d, int dtype, IgParams& p) {
   if (d.r != 1 || d.s != 1) return false;
+  if (p.f8) {  // the fp8 kernels stage no transform: eligible convs get dy materialised
+    p.ap.y = nullptr;
+    if (f8_ok(p)) return false;
+  }
   int maxM = 0, maxK = 0;
   for (int i = 0; i < p.nphase; ++i) {
     maxM = p.ph[i].M > maxM ? p.ph[i].M : maxM;
@@ -1231,13 +1324,16 @@ int conv_dgrad_stages_prologue(const argus_conv_desc& d, int dtype) {
   if (check_desc(d) || d.stem) return 0;
   IgParams p;
   dgrad_params(d, nullptr, nullptr, nullptr, nullptr, nullptr, p);
-  return dgrad_stages_prologue(d, dtype, p) ? 1 : 0;
+  p.f8 = dtype == ARGUS_FP8;
+  return dgrad_stages_prologue(d, p.f8 ? ARGUS_BF16 : dtype, p) ? 1 : 0;
 }
 
 int conv_dgrad_bn(const argus_conv_desc& d, int dtype, const void* dy, const void* wt, void* dm,
                   const void* addend, const argus_bn_bwd_epilogue* bn, const argus_bn_bwd_prologue* pro,
                   hipStream_t st) {
   if (int e = check_desc(d)) return e;
+  const bool f8 = dtype == ARGUS_FP8;
+  if (f8) dtype = ARGUS_BF16;
   if (d.stem) { set_error("conv_dgrad_bn: the stem input has no gradient"); return ARGUS_ERR_ARG; }
   static const argus_bn_bwd_epilogue no_epilogue = {};
   const bool epi = bn != nullptr;
@@ -1254,6 +1350,7 @@ int conv_dgrad_bn(const argus_conv_desc& d, int dtype, const void* dy, const voi
   }
   IgParams p;
   dgrad_params(d, dy, wt, dm, addend, nullptr, p);
+  p.f8 = f8;
   if (pro) {
     // the register-staged kernel stages dy = ca*dm + cb*y + cc itself; the halo / glds kernels (LDS
     // DMA, no staging transform) get it materialised by the apply kernel first
@@ -1491,7 +1588,7 @@ int conv_wgrad_apply(const argus_conv_desc& d, int dtype, const void* x, const v
 int conv_launch_info(const argus_conv_desc& d, int dtype, int pass, int64_t* flops) {
   if (check_desc(d)) return -1;
   if (flops) *flops = 2LL * d.n * d.ho * d.wo * d.k * d.r * d.s * d.c;
-  const int dtag = dtype == ARGUS_BF16 ? 1 : 0;
+  const int dtag = (dtype == ARGUS_BF16 || dtype == ARGUS_FP8) ? 1 : 0;
   if (pass == 0) return 10000000 + dtag * 1000000 + fwd_bm(d) * 1000 + (d.stem ? 64 : pick_bn(0, d.k));
   if (pass == 1) return 10000000 + dtag * 1000000 + dgrad_bm(d) * 1000 + pick_bn(1, d.c);
   const WgPlan pl = wgrad_plan(d, dtype);

@@ -61,11 +61,15 @@ struct IgParams {
   BnBwdEpi bb;    // dgrad only
   BnFin fin;      // BN finalize folded into this launch (fin.mode != 0)
   BnApplyPro ap;  // dgrad only: the A operand is dm (ap.y != nullptr)
+  int f8;         // ARGUS_FP8: MX-fp8 operands where the shape allows (host dispatch only)
 };
 
 // compile-time epilogue/prologue variant of the dgrad kernels: low 3 bits = BN-backward epilogue
 // (BwdMode), bit 4 = BN-backward apply prologue (BnApplyPro)
 constexpr int kApplyBit = 16;
+// bit 5: MX-fp8 operands (OCP e4m3 + one E8M0 scale per 32 K-elements of a row, quantized while
+// staging from the bf16 tensors; v_mfma_scale_f32_16x16x128_f8f6f4)
+constexpr int kFp8Bit = 32;
 
 struct WgParams {
   const void* x;

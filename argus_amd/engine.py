@@ -28,7 +28,7 @@ from dataclasses import dataclass
 
 import torch
 
-from argus_amd._lib import BF16, F32, BnBwdEpilogue, BnBwdPrologue, BnFwdFin, ConvDesc, lib, ptr, stream
+from argus_amd._lib import BF16, F32, FP8, BnBwdEpilogue, BnBwdPrologue, BnFwdFin, ConvDesc, lib, ptr, stream
 
 
 @dataclass(frozen=True)
@@ -70,20 +70,24 @@ class ResNetEngine:
     """Workspace + launch schedule for one (batch, H, W, dtype) configuration on one device."""
 
     def __init__(self, n_cams: int, resnet_output_dim: int, dtype: str, device: torch.device):
-        if dtype not in ("fp32", "bf16"):
-            raise ValueError(f"compute dtype must be 'fp32' or 'bf16', got {dtype!r}")
+        if dtype not in ("fp32", "bf16", "fp8"):
+            raise ValueError(f"compute dtype must be 'fp32', 'bf16' or 'fp8', got {dtype!r}")
         self.L = lib()
         self.n_cams = n_cams
         self.rdim = resnet_output_dim
         self.dtype = dtype
-        self.dt = BF16 if dtype == "bf16" else F32
-        self.tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
-        self.E = 8 if dtype == "bf16" else 4  # elements per 16-byte chunk
+        # "fp8": the bf16 network (tensors, BN, weight gradients) whose conv forward / data-gradient
+        # GEMMs take MX-fp8 operands where the shape allows (ARGUS_FP8, igemm_kernel's kFp8Bit variant)
+        low = dtype in ("bf16", "fp8")
+        self.dt = BF16 if low else F32
+        self.cdt = FP8 if dtype == "fp8" else self.dt  # conv fwd / dgrad entry points
+        self.tdt = torch.bfloat16 if low else torch.float32
+        self.E = 8 if low else 4  # elements per 16-byte chunk
         # materialize a = relu(bn(y)) of bn1/bn2 once per forward (one extra HBM pass each) so that
         # conv2/conv3 forward and weight gradients run without the BN prologue, on the global->LDS
         # kernels; fp32 (parity path) keeps the fused prologue. ARGUS_MATERIALIZE=0/1 overrides.
         env = os.environ.get("ARGUS_MATERIALIZE")
-        self.materialize = (dtype == "bf16") if env is None else env == "1"
+        self.materialize = low if env is None else env == "1"
         self.device = torch.device(device)
         self.blocks = resnet50_blocks()
         self.shape = None
@@ -150,7 +154,7 @@ class ResNetEngine:
             else:
                 wf = self._t(k, ks * ks * c)
                 wd = self._t(c, ks * ks * k)
-            rows = L.dll.argus_conv_fwd_stat_rows(C.byref(d), dt)
+            rows = L.dll.argus_conv_fwd_stat_rows(C.byref(d), self.cdt)
             tile = L.dll.argus_conv_fwd_stat_tile(C.byref(d), dt)
             fl = C.c_int64(0)
             tags = tuple(L.dll.argus_conv_launch_info(C.byref(d), dt, ps, C.byref(fl)) for ps in range(3))
@@ -224,7 +228,7 @@ class ResNetEngine:
                       L.dll.argus_maxpool_bwd_bn_rows(dt, N, H1, W1, 64) * 64)
         for cv in convs.values():  # BN-backward partials written by dgrad epilogues (rows x C_in)
             if not cv.desc.stem:
-                max_bwd = max(max_bwd, L.dll.argus_conv_dgrad_bn_rows(C.byref(cv.desc), dt) * cv.desc.c)
+                max_bwd = max(max_bwd, L.dll.argus_conv_dgrad_bn_rows(C.byref(cv.desc), self.cdt) * cv.desc.c)
         self.bwd_part = self._f(max_bwd * 2)
         self.bwd_part2 = self._f(max_bwd * 2)  # second branch (downsample BN) of a dual reduce
         ws = max(L.dll.argus_conv_wgrad_workspace_bytes(C.byref(cv.desc), dt) for cv in convs.values())
@@ -232,7 +236,7 @@ class ResNetEngine:
         self.wg_ws_bytes = ws
         wss = L.dll.argus_conv_wgrad_workspace_bytes(C.byref(convs["resnet.conv1"].desc), dt)
         self.wg_ws_stem = torch.empty(wss, dtype=torch.uint8, device=self.device)
-        self.stages_pro = {n: bool(L.dll.argus_conv_dgrad_stages_prologue(C.byref(cv.desc), dt))
+        self.stages_pro = {n: bool(L.dll.argus_conv_dgrad_stages_prologue(C.byref(cv.desc), self.cdt))
                            for n, cv in convs.items() if not cv.desc.stem}
         self.gbuf = [self._t(max_elems) for _ in range(4)]  # dh / dx ping-pong, dz ping-pong
         # dy operands of the side-stream weight gradients come from a ring, so the main stream can
@@ -289,10 +293,10 @@ class ResNetEngine:
             f = BnFwdFin(ptr(part), ptr(P[bn + ".weight"]), ptr(P[bn + ".bias"]), Bf.get(bn + ".eps", 1e-5),
                          Bf.get(bn + ".momentum", 0.1), ptr(Bf[bn + ".running_mean"]), ptr(Bf[bn + ".running_var"]),
                          ptr(Bf[bn + ".num_batches_tracked"]), ptr(st[0]), ptr(st[1]), ptr(st[2]), ptr(st[3]), ptr(ws))
-            self._launch(cv, 0, lambda: self.L.conv_fwd_bn(C.byref(cv.desc), self.dt, ptr(x), ptr(cv.wf), ptr(y),
+            self._launch(cv, 0, lambda: self.L.conv_fwd_bn(C.byref(cv.desc), self.cdt, ptr(x), ptr(cv.wf), ptr(y),
                                                             ptr(sc), ptr(sh), C.byref(f), stream()))
             return
-        self._launch(cv, 0, lambda: self.L.conv_fwd(C.byref(cv.desc), self.dt, ptr(x), ptr(cv.wf), ptr(y), ptr(sc),
+        self._launch(cv, 0, lambda: self.L.conv_fwd(C.byref(cv.desc), self.cdt, ptr(x), ptr(cv.wf), ptr(y), ptr(sc),
                                                      ptr(sh), ptr(part) if training else None, stream()))
         if training:
             count = cv.desc.n * cv.desc.ho * cv.desc.wo
@@ -651,9 +655,9 @@ class ResNetEngine:
             e.y2, e.mean2, e.invstd2, e.part2 = ptr(second[1]), ptr(st2[0]), ptr(st2[1]), ptr(self.bwd_part2)
         pp = self._prologue(pro)
         self._guard(dm)
-        self._launch(cv, 1, lambda: self.L.conv_dgrad_bn(C.byref(cv.desc), self.dt, ptr(dy), ptr(cv.wd), ptr(dm),
+        self._launch(cv, 1, lambda: self.L.conv_dgrad_bn(C.byref(cv.desc), self.cdt, ptr(dy), ptr(cv.wd), ptr(dm),
                                                           ptr(addend), C.byref(e), pp, stream()))
-        return 0 if self.fold_fin else self.L.dll.argus_conv_dgrad_bn_rows(C.byref(cv.desc), self.dt)
+        return 0 if self.fold_fin else self.L.dll.argus_conv_dgrad_bn_rows(C.byref(cv.desc), self.cdt)
 
     def _prologue(self, pro):
         """argus_bn_bwd_prologue for ``pro`` = (bn name, y, dy_out): the dgrad stages dy = ca*dm + cb*y + cc
@@ -674,7 +678,7 @@ class ResNetEngine:
         cv = self.convs[conv]
         pp = self._prologue(pro)
         self._guard(dx)
-        self._launch(cv, 1, lambda: self.L.conv_dgrad_bn(C.byref(cv.desc), self.dt, ptr(dy), ptr(cv.wd), ptr(dx),
+        self._launch(cv, 1, lambda: self.L.conv_dgrad_bn(C.byref(cv.desc), self.cdt, ptr(dy), ptr(cv.wd), ptr(dx),
                                                           None, None, pp, stream()))
 
     def _bn_apply_bwd(self, name, px, ch, dm, y, dy_out, second=None):
@@ -816,7 +820,7 @@ class ResNetEngine:
     def _dgrad(self, conv, dy, dx, addend=None, mask=None):
         cv = self.convs[conv]
         self._guard(dx)
-        self._launch(cv, 1, lambda: self.L.conv_dgrad(C.byref(cv.desc), self.dt, ptr(dy), ptr(cv.wd), ptr(dx),
+        self._launch(cv, 1, lambda: self.L.conv_dgrad(C.byref(cv.desc), self.cdt, ptr(dy), ptr(cv.wd), ptr(dx),
                                                        ptr(addend), ptr(mask), stream()))
 
     @staticmethod

@@ -16,8 +16,10 @@ Pretrained ImageNet weights (``weights="DEFAULT"``) are not downloadable offline
 load a local ``.pth``.
 
 Extension: ``compute_dtype`` ("fp32" — parity path, fp32 activations and exact-fp32 MFMA; "bf16" —
-throughput path, bf16 activations/weights with fp32 accumulation, statistics and head). The
-reference's ``--amp`` (fp16 autocast) maps to "bf16".
+throughput path, bf16 activations/weights with fp32 accumulation, statistics and head; "fp8" — the
+bf16 path whose conv forward and data-gradient GEMMs take OCP MX-fp8 operands (e4m3 + E8M0 block
+scales, BASELINE configs[4]) where the channel count allows). The reference's ``--amp`` (fp16
+autocast) maps to "bf16".
 """
 from __future__ import annotations
 

@@ -44,6 +44,7 @@ import torch.distributed as dist
 
 BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 MFMA
 F32_MFMA_PEAK_TFLOPS = 157.3
+FP8_DENSE_PEAK_TFLOPS = 5000.0  # MI355X_MICROARCH.md: ~5 PF dense fp8 MFMA
 HBM_PEAK_GBS = 8000.0
 
 
@@ -61,6 +62,8 @@ def _config_name(B: int, H: int, W: int, world: int) -> str:
     """Which BASELINE.json config this run's shape is (configs[1] is the default bench line)."""
     if (H, W) == (376, 672):
         return "configs[3] cube_unity_data_large-shaped (2-cam 376x672)"
+    if (H, W) == (256, 256) and B == 512:
+        return "configs[4] fp8-shaped (B=512 per rank)"
     if (H, W) == (256, 256) and B == 256:
         return "configs[2] cube_unity_data_medium-shaped"
     if (H, W) == (256, 256) and B == 64:
@@ -141,7 +144,7 @@ def main() -> None:
                     help="samples (camera pairs) per rank (default 64 on one GPU = configs[1], 256 per rank "
                          "for N > 1 = configs[2])")
     ap.add_argument("--hw", type=int, nargs=2, default=(256, 256))
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp8"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--kernels", action="store_true", help="print the probe step's per-kernel table to stderr")
@@ -248,7 +251,11 @@ def main() -> None:
     val_loss = (vsum[0] / vsum[2]).item()
     val_rot = (vsum[1] / vsum[2]).item()
 
-    peak_flops = BF16_DENSE_PEAK_TFLOPS if args.dtype == "bf16" else F32_MFMA_PEAK_TFLOPS
+    # the dominant kernel's own MFMA roof: MX-fp8 igemm variants (template flag 32) run at the dense
+    # fp8 rate; in an "fp8" run the weight gradients and the 64-channel convs stay bf16
+    f8_kernel = dom.startswith("argus::igemm_kernel<") and int(dom.rstrip(">").split(",")[-1]) >= 32
+    peak_flops = (FP8_DENSE_PEAK_TFLOPS if f8_kernel else
+                  BF16_DENSE_PEAK_TFLOPS if args.dtype in ("bf16", "fp8") else F32_MFMA_PEAK_TFLOPS)
     tflops = ks["flops_per_launch"] / (ks["avg_us"] * 1e-6) / 1e12
     gbs = ks["bytes_per_launch"] / (ks["avg_us"] * 1e-6) / 1e9
     # the roof that binds: MFMA if the kernel's algorithmic intensity is above the ridge, else HBM
@@ -269,6 +276,10 @@ def main() -> None:
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": args.dtype,
+        "dtype_detail": ("OCP MX-fp8 (e4m3 + E8M0 scale per 32 K-elements) operands for the conv forward and "
+                         "data-gradient GEMMs with >= 128 reduction channels; bf16 tensors, BN, weight gradients "
+                         "and the 64-channel convs; fp32 accumulation, statistics, head, optimizer"
+                         if args.dtype == "fp8" else None),
         "data": "synthetic (uint8-uniform images, Exp(N(0,0.5^2)) SE(3) targets, seeded random-init weights)",
         "config": {
             "workload": f"{_config_name(B, H, W, world)}: fused train step, {B} samples "

@@ -28,7 +28,11 @@ extern "C" {
 
 typedef void* argus_stream_t; /* hipStream_t */
 
-enum { ARGUS_F32 = 0, ARGUS_BF16 = 1 };
+/* ARGUS_FP8 (conv fwd / dgrad entry points only): bf16 tensors, GEMM operands quantized while
+ * staging to OCP MX-fp8 (e4m3 + one E8M0 scale per 32 K-elements of a row) for the MFMA
+ * v_mfma_scale_f32_16x16x128_f8f6f4, where the conv allows it (reduction channels % 128 == 0,
+ * not the stem); the other convs, and every non-conv entry point (pass ARGUS_BF16), run bf16. */
+enum { ARGUS_F32 = 0, ARGUS_BF16 = 1, ARGUS_FP8 = 2 };
 enum { ARGUS_OK = 0, ARGUS_ERR_ARG = 1, ARGUS_ERR_SHAPE = 2, ARGUS_ERR_HIP = 3 };
 
 typedef struct {

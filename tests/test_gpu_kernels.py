@@ -1183,3 +1183,58 @@ def test_stem_backward_fusions(cuda, dt):
     L.conv_wgrad_apply(C.byref(d), DT[dt], ptr(x0), ptr(dm), C.byref(ap), ptr(dw), ptr(ws), ws.numel(), stream())
     torch.cuda.synchronize()
     assert torch.equal(dw.cpu(), dw_ref.cpu())
+
+
+FP8_CASES = [  # (cin, cout, k, stride, hin, n): reduction channels % 128 == 0 in each pass
+    (256, 128, 1, 1, 12, 2), (128, 128, 3, 1, 12, 2), (256, 256, 3, 2, 13, 2), (512, 1024, 1, 2, 9, 2),
+    (1024, 256, 1, 1, 6, 3), (512, 512, 3, 1, 5, 2),
+]
+
+
+def test_fp8_mx_conv_fwd_dgrad(cuda):
+    """ARGUS_FP8: conv fwd (+ BN statistics) and dgrad (+ BN-backward epilogue) with the A and B
+    operands quantized to OCP MX-fp8 (e4m3, E8M0 scale per 32 K-elements) on the scaled MFMA, vs
+    the fp64 reference on the bf16 inputs. Stated fp8 tolerance: max error <= 6e-2 of the output's
+    max magnitude (e4m3 keeps 3 mantissa bits: 2^-4 relative per operand element)."""
+    from argus_amd._lib import FP8, BnBwdEpilogue
+    from argus_amd.profiling import KernelTimer
+
+    torch.manual_seed(17)
+    L = lib()
+    for cin, cout, k, s, hin, n in FP8_CASES:
+        d, p = _desc(n, hin, hin, cin, cout, k, s)
+        x = _q(torch.randn(n, hin, hin, cin), "bf16")
+        w = torch.randn(cout, k, k, cin) * (2.0 / (k * k * cin)) ** 0.5
+        dy = _q(torch.randn(n, d.ho, d.wo, cout), "bf16")
+        wf, wt = _prep(d, "bf16", w.to(cuda), cuda)
+        y = torch.empty(n, d.ho, d.wo, cout, dtype=torch.bfloat16, device=cuda)
+        rows = L.dll.argus_conv_fwd_stat_rows(C.byref(d), FP8)
+        stats = torch.empty(rows, cout, 2, device=cuda)
+        with KernelTimer("argus::igemm_kernel") as t:
+            L.conv_fwd(C.byref(d), FP8, ptr(x.to(cuda, torch.bfloat16)), ptr(wf), ptr(y), None, None, ptr(stats),
+                       stream())
+        names = list(t.summary())
+        assert any(nm.endswith(", 32>") for nm in names), names  # the fp8 variant ran
+        wr = _q(w, "bf16").permute(0, 3, 1, 2)
+        ref = F.conv2d(x.permute(0, 3, 1, 2), wr, stride=s, padding=p)
+        e = _rel(y.permute(0, 3, 1, 2), ref)
+        assert e < 6e-2, ("fp8 fwd", cin, cout, k, s, e)
+        assert e > 1e-4, ("fp8 fwd: no quantization visible?", e)
+        # dgrad with a BN-backward epilogue (mask recomputed from the BN input)
+        brows = L.dll.argus_conv_dgrad_bn_rows(C.byref(d), FP8)
+        part = torch.zeros(brows, cin, 2, device=cuda)
+        yin = torch.randn(n, hin, hin, cin, device=cuda).to(torch.bfloat16)
+        mean, invstd = torch.zeros(cin, device=cuda), torch.ones(cin, device=cuda)
+        sc, sh = torch.ones(cin, device=cuda), torch.zeros(cin, device=cuda)
+        e_ = BnBwdEpilogue()
+        e_.y, e_.mean, e_.invstd, e_.mask_mode, e_.scale, e_.shift, e_.part = ptr(yin), ptr(mean), ptr(invstd), 2, \
+            ptr(sc), ptr(sh), ptr(part)
+        dm = torch.empty(n, hin, hin, cin, device=cuda, dtype=torch.bfloat16)
+        L.conv_dgrad_bn(C.byref(d), FP8, ptr(dy.to(cuda, torch.bfloat16)), ptr(wt), ptr(dm), None, C.byref(e_), None,
+                        stream())
+        refd = torch.nn.grad.conv2d_input(x.permute(0, 3, 1, 2).shape, wr, dy.permute(0, 3, 1, 2), stride=s, padding=p)
+        refm = refd * (yin.double().cpu().permute(0, 3, 1, 2) > 0)
+        e = _rel(dm.permute(0, 3, 1, 2), refm)
+        assert e < 6e-2, ("fp8 dgrad", cin, cout, k, s, e)
+        colsum = part.double().sum(0)[:, 0].cpu()
+        assert _rel(colsum, dm.double().cpu().reshape(-1, cin).sum(0)) < 1e-3  # partials sum what was stored

@@ -49,11 +49,11 @@ def main():
         wf = cv.wf.normal_() if tdt == torch.float32 else cv.wf.copy_(torch.randn_like(cv.wf, dtype=torch.float32))
         wd = cv.wd if cv.wd is not None else None
         fns = {
-            0: lambda: L.conv_fwd(C.byref(d), dt, ptr(x), ptr(cv.wf), ptr(y), None, None, ptr(st), stream()),
+            0: lambda: L.conv_fwd(C.byref(d), eng.cdt, ptr(x), ptr(cv.wf), ptr(y), None, None, ptr(st), stream()),
             2: lambda: L.conv_wgrad(C.byref(d), dt, ptr(x), None, None, ptr(dy), ptr(dw), ptr(ws), ws.numel(), stream()),
         }
         if not d.stem:
-            fns[1] = lambda: L.conv_dgrad(C.byref(d), dt, ptr(dy), ptr(wd), ptr(dx), None, None, stream())
+            fns[1] = lambda: L.conv_dgrad(C.byref(d), eng.cdt, ptr(dy), ptr(wd), ptr(dx), None, None, stream())
         row = [name]
         for ps, fn in fns.items():
             with KernelTimer() as kt:
