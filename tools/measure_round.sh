@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round measurement set on the GPU box (all outputs under gpurun_out/meas_TAG/):
 #   bench lines for configs[1] (B=64), the configs[2] per-rank point (B=256) and configs[3]
-#   (376x672, B=128); kernel stats + FETCH/WRITE PMC traffic + MFMA/wave-state counters for B=64 and
+#   (376x672, B=128), the configs[4] per-rank batch (B=512) in fp8 and bf16; kernel stats + FETCH/WRITE PMC traffic + MFMA/wave-state counters for B=64 and
 #   376x672; the B=64 step timeline.     bash tools/measure_round.sh TAG
 set -e
 TAG=$1
@@ -14,6 +14,10 @@ timeout -k 10 240 python3 -u bench.py > $O/bench.json 2> $O/bench.err
 timeout -k 10 180 python3 -u bench.py --batch 256 --no-cpu-baseline > $O/bench_b256.json 2> $O/bench_b256.err
 timeout -k 10 240 python3 -u bench.py --hw 376 672 --batch 128 --no-cpu-baseline --kernels \
   > $O/bench_376x672.json 2> $O/bench_376x672_kernels.txt
+timeout -k 10 240 python3 -u bench.py --dtype fp8 --batch 512 --no-cpu-baseline --steps 5 --warmup 2 \
+  > $O/bench_b512_fp8.json 2> $O/bench_b512_fp8.err
+timeout -k 10 240 python3 -u bench.py --batch 512 --no-cpu-baseline --no-isolated --steps 5 --warmup 2 \
+  > $O/bench_b512_bf16.json 2> $O/bench_b512_bf16.err
 bash tools/profile_round.sh $TAG
 python3 tools/pmc_traffic.py gpurun_out/prof_$TAG/pmc_fetch gpurun_out/prof_$TAG/pmc_write $O/pmc_traffic.json 64 256 256 bf16
 python3 tools/profsum.py $(find gpurun_out/prof_$TAG/stats -name "*kernel_stats.csv" | head -1) 28 40 > $O/kernel_summary.txt
