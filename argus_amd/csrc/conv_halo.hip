@@ -46,22 +46,26 @@ ARGUS_DEV void sbar() {
 }  // namespace
 
 constexpr int kHaloPos = 448;  // halo positions per image buffer (max (rows+2)*(W+2) over the shapes served)
+constexpr int kHaloPos1 = 416;  // single-buffer variant: 2 x (416 x 128 B + 3 x 8 KB weight stages) fit one CU
 
-template <int BN, bool PRO, int BW>
-__global__ __launch_bounds__(4 * (BN / 64) * 64, 1) void conv3x3_halo_kernel(const IgParams p) {
+// HB = halo image buffers: 2 (double-buffered over 64-channel chunks) or 1 (Cin = 64: a single chunk,
+// nothing to prefetch; the 64-column tile then fits two workgroups per CU in LDS)
+template <int BN, bool PRO, int BW, int HB>
+__global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_halo_kernel(const IgParams p) {
   constexpr int WN = BN / 64, NW = 4 * WN, NT = NW * 64;
-  constexpr int HALO = kHaloPos * 128;          // bytes per halo image
+  constexpr int HPOS = HB == 1 ? kHaloPos1 : kHaloPos;  // halo positions per image buffer
+  constexpr int HALO = HPOS * 128;              // bytes per halo image
   constexpr int BST = BN * 128;                 // bytes per weight stage
   constexpr int NBS = 3;
   constexpr int LD = BN + 8;
   constexpr int EPI = 256 * LD * 2;
-  constexpr int MAIN = 2 * HALO + NBS * BST;
+  constexpr int MAIN = HB * HALO + NBS * BST;
   constexpr int LDS0 = MAIN > EPI ? MAIN : EPI;
   constexpr int RED_B = (NT / (BN / 8)) * BN * 8;  // BN-backward column sums
   constexpr int LDS_BYTES = LDS0 > RED_B ? LDS0 : RED_B;
-  constexpr int HG = kHaloPos / (8 * NW);       // halo glds per wave per chunk
+  constexpr int HG = HPOS / (8 * NW);           // halo glds per wave per chunk
   constexpr int BG = BN * 8 / NT;               // weight glds per wave per tap
-  static_assert(HG * 8 * NW == kHaloPos && BG * NT == BN * 8, "halo / tile partition");
+  static_assert(HG * 8 * NW == HPOS && BG * NT == BN * 8, "halo / tile partition");
   __shared__ __attribute__((aligned(1024))) u32x4 lds[LDS_BYTES / 16];
 
   const IgPhase& ph = p.ph[0];
@@ -108,7 +112,7 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, 1) void conv3x3_halo_kernel(con
   const int nk = 9 * nch;
 
   auto issue_halo = [&](int cc) {
-    const uint32_t base = lds0 + (cc & 1) * HALO + wave * 1024;
+    const uint32_t base = lds0 + (HB == 2 ? (cc & 1) * HALO : 0) + wave * 1024;
     const int ci0 = cc * 64;
 #pragma unroll
     for (int i = 0; i < HG; ++i) gl16(h_ok[i] ? (const void*)(X + h_off[i] + ci0) : zero, base + i * NW * 1024);
@@ -116,7 +120,7 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, 1) void conv3x3_halo_kernel(con
   auto issue_b = [&](int kt) {
     const int cc = kt / 9, t = kt - cc * 9;
     const int off = ph.boff[t] + cc * 64;
-    const uint32_t base = lds0 + 2 * HALO + (kt % NBS) * BST + wave * 1024;
+    const uint32_t base = lds0 + HB * HALO + (kt % NBS) * BST + wave * 1024;
 #pragma unroll
     for (int i = 0; i < BG; ++i) gl16(b_src[i] + off, base + i * NW * 1024);
   };
@@ -141,8 +145,8 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, 1) void conv3x3_halo_kernel(con
   auto compute = [&](int kt) {
     const int cc = kt / 9, t = kt - cc * 9;
     const int toff = (ph.dh[t] + 1) * HWD + (ph.dw[t] + 1);
-    const char* Hl = reinterpret_cast<const char*>(lds) + (cc & 1) * HALO;
-    const char* Bl = reinterpret_cast<const char*>(lds) + 2 * HALO + (kt % NBS) * BST;
+    const char* Hl = reinterpret_cast<const char*>(lds) + (HB == 2 ? (cc & 1) * HALO : 0);
+    const char* Bl = reinterpret_cast<const char*>(lds) + HB * HALO + (kt % NBS) * BST;
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       u32x4 fa[4], fb[4];
@@ -165,7 +169,7 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, 1) void conv3x3_halo_kernel(con
 
   // BN + ReLU of the producer, applied once per chunk to the landed halo image (in place)
   auto transform_halo = [&](int cc) {
-    char* Hl = reinterpret_cast<char*>(lds) + (cc & 1) * HALO;
+    char* Hl = reinterpret_cast<char*>(lds) + (HB == 2 ? (cc & 1) * HALO : 0);
     for (int idx = tid; idx < npos * 8; idx += NT) {
       const int q = idx >> 3, slot = idx & 7;
       const int ii = q / IMGP, rem = q - ii * IMGP;
@@ -311,19 +315,33 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, 1) void conv3x3_halo_kernel(con
   }
 }
 
-template <int BN, bool PRO, int BW>
+template <int BN, bool PRO, int BW, int HB>
 static const char* halo_name() {
   static const std::string s = std::string("argus::conv3x3_halo_kernel<") + std::to_string(BN) + ", " +
-                               bool_name(PRO) + ", " + std::to_string(BW) + ">";
+                               bool_name(PRO) + ", " + std::to_string(BW) + (HB == 1 ? ", 1>" : ">");
   return s.c_str();
 }
 
-template <int BN, bool PRO, int BW>
-static void launch_halo1(const IgParams& p0, hipStream_t st) {
+template <int BN, bool PRO, int BW, int HB>
+static void launch_halo2(const IgParams& p0, hipStream_t st) {
   IgParams p = p0;
   plan_fin(p, 256);
   dim3 grid((p.ph[0].M / 256) * (p.N / BN));
-  timed_launch(halo_name<BN, PRO, BW>(), conv3x3_halo_kernel<BN, PRO, BW>, grid, dim3(4 * (BN / 64) * 64), st, p);
+  timed_launch(halo_name<BN, PRO, BW, HB>(), conv3x3_halo_kernel<BN, PRO, BW, HB>, grid, dim3(4 * (BN / 64) * 64),
+               st, p);
+}
+
+template <int BN, bool PRO, int BW>
+static void launch_halo1(const IgParams& p, hipStream_t st) {
+  if constexpr (BN == 64) {
+    const int HWi = p.H * p.W;
+    const int npos = HWi >= 256 ? (256 / p.W + 2) * (p.W + 2) : (256 / HWi) * (p.H + 2) * (p.W + 2);
+    if (p.Cin == 64 && npos <= kHaloPos1) {  // one channel chunk: one halo buffer, two workgroups per CU
+      launch_halo2<BN, PRO, BW, 1>(p, st);
+      return;
+    }
+  }
+  launch_halo2<BN, PRO, BW, 2>(p, st);
 }
 
 template <int BN, bool PRO>
@@ -342,6 +360,10 @@ static void launch_halo(const IgParams& p, hipStream_t st) {
 
 int g_halo_enable = 1;      // argus_conv_tuning key 10
 int g_halo_min_grid = 256;  // key 13: fewest workgroups for which the fwd/dgrad halo kernel is chosen
+// key 30: 64-channel 3x3 layers (layer 1: Cin = Cout = 64) on the 4-wave, single-halo-buffer variant
+// (two workgroups per CU). B=64 in the full step: fwd 80 -> 71 us, dgrad + BN epilogue 147 -> 132 us
+// per layer; 8245 -> 8302 img/s (two paired runs on one box)
+int g_halo64 = 1;
 
 // 3x3 / stride 1 / pad 1, same input and output grid, one phase, whole-row / whole-image 256-pixel tiles
 int conv3x3_halo_ok(const IgParams& p) {
@@ -365,6 +387,7 @@ int conv3x3_halo_ok(const IgParams& p) {
   // measured (tools/convbench.py, B=64): wins only with 8-wave workgroups (N % 128) filling every CU;
   // the 4-wave BN=64 tile and sub-CU-count grids lose to the register-staged kernel
   if (p.N % 128 == 0 && (ph.M / 256) * (p.N / 128) >= g_halo_min_grid) return 128;
+  if (g_halo64 && p.N == 64 && p.Cin == 64 && ph.M / 256 >= g_halo_min_grid) return 64;
   if (g_halo_min_grid <= 1 && p.N % 64 == 0) return 64;  // forced (tests): the 4-wave variant
   return 0;
 }

@@ -174,7 +174,12 @@ def initialize_training(cfg: TrainConfig, rank: int = 0, world: int = 1):
         nw = min(nw, max(1, (os.cpu_count() or 2) // max(1, world) - 1))
     kw = dict(batch_size=cfg.batch_size, num_workers=nw, pin_memory=True)
     if nw > 0:
-        kw["multiprocessing_context"] = "fork"
+        # workers are spawned, never forked: this process has initialised the GPU, and a fork()ed child
+        # shares the HSA runtime's host-resident signal / queue pages copy-on-write, so the parent can
+        # miss GPU completions written to a page the fork split off (observed: a hang in the first copy
+        # of a later validation pass). Persistent workers pay the spawn once per loader.
+        kw["multiprocessing_context"] = "spawn"
+        kw["persistent_workers"] = True
     train_loader = DataLoader(train_ds, shuffle=train_sampler is None, sampler=train_sampler, **kw)
     val_loader = DataLoader(val_ds, shuffle=False, sampler=val_sampler, **kw)
 

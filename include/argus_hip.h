@@ -196,7 +196,10 @@ int argus_conv_dgrad_bn(const argus_conv_desc* d, int dtype, const void* dy, con
  * the bf16 register-staged weight gradient (1 default; 2 = 512-thread workgroups summing two pixel
  * halves in LDS: half the split partials, but slower), key 27 the split target of the register-staged
  * 3x3 weight gradient (default 512), key 28 a cap on the weight gradients' split partials as a
- * multiple of the operand bytes (0 = off, the default; 1-4 measured neutral).
+ * multiple of the operand bytes (0 = off, the default; 1-4 measured neutral), key 29 the
+ * workgroups per CU of the MX-fp8 forward/dgrad kernel (2 default, 4), key 30 the 64-channel 3x3
+ * stride-1 layers (Cin = Cout = 64) on the LDS-halo kernel's single-halo-buffer 64-column variant
+ * (1, default) or on the register-staged implicit GEMM (0).
  * Returns 0, or -1 for an unknown key. */
 int argus_conv_tuning(int key, int value);
 /* Current value of a tuning key (-1 for an unknown key). */

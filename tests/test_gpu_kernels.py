@@ -576,6 +576,45 @@ def test_conv3x3_halo_kernel_parity(cuda):
         L.dll.argus_conv_tuning(13, 256)
 
 
+def test_layer1_3x3_on_single_buffer_halo_kernel(cuda):
+    """Default kernel policy (tuning key 30 = 1) for the 64 -> 64 channel 3x3 stride-1 layers of
+    layer 1 at a grid the policy accepts (>= 256 workgroups): forward and dgrad run on the
+    single-halo-buffer 64-column halo kernel and agree with torch (bf16 tolerance) and with the
+    register-staged implicit GEMM the policy replaces (key 30 = 0)."""
+    from argus_amd.profiling import KernelTimer
+
+    torch.manual_seed(31)
+    L = lib()
+    n, hw, c = 16, 64, 64
+    d, p = _desc(n, hw, hw, c, c, 3, 1)
+    x = torch.randn(n, hw, hw, c)
+    w = torch.randn(c, 3, 3, c) * (2.0 / (9 * c)) ** 0.5
+    dy = torch.randn(n, hw, hw, c)
+    wf, wt = _prep(d, "bf16", w.to(cuda), cuda)
+    xd, dyd = x.to(cuda, torch.bfloat16), dy.to(cuda, torch.bfloat16)
+    xr, wr = _q(x, "bf16").permute(0, 3, 1, 2), _q(w, "bf16").permute(0, 3, 1, 2)
+    ref_y = F.conv2d(xr, wr, padding=1).permute(0, 2, 3, 1)
+    ref_dx = torch.nn.grad.conv2d_input(xr.shape, wr, _q(dy, "bf16").permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
+    outs = {}
+    for key30, kname in ((1, "conv3x3_halo_kernel<64, false, 0, 1>"), (0, "igemm_kernel")):
+        with _tuned({30: key30}):
+            rows = L.dll.argus_conv_fwd_stat_rows(C.byref(d), BF16)
+            stats = torch.empty(rows, c, 2, device=cuda)
+            y = torch.empty(n, hw, hw, c, dtype=torch.bfloat16, device=cuda)
+            dx = torch.empty(n, hw, hw, c, dtype=torch.bfloat16, device=cuda)
+            with KernelTimer() as t:
+                L.conv_fwd(C.byref(d), BF16, ptr(xd), ptr(wf), ptr(y), None, None, ptr(stats), stream())
+                L.conv_dgrad(C.byref(d), BF16, ptr(dyd), ptr(wt), ptr(dx), None, None, stream())
+            torch.cuda.synchronize()
+        names = list(t.summary())
+        assert any(kname in nm for nm in names), (key30, names)
+        if key30:
+            assert any("conv3x3_halo_kernel<64, false, 0, 1>" in nm for nm in names) and len(names) == 1, names
+        assert _rel(y, ref_y) < TOL["bf16"] and _rel(dx, ref_dx) < TOL["bf16"], key30
+        outs[key30] = (y.float(), dx.float())
+    assert _rel(outs[1][0], outs[0][0]) < 1e-2 and _rel(outs[1][1], outs[0][1]) < 1e-2
+
+
 def _halo_cases(L, cuda):
     from argus_amd.profiling import KernelTimer
 

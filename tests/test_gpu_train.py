@@ -59,7 +59,7 @@ def test_train_loop_end_to_end_and_reproducible(cuda, dummy_data_path, tmp_path)
                       random_seed=42, val_epochs=1, print_epochs=1, save_epochs=1, save_dir=str(save),
                       model_config=NCameraCNNConfig(n_cams=2),
                       dataset_config=CameraCubePoseDatasetConfig(dataset_path=dummy_data_path),
-                      compile_model=False, wandb_log=False)
+                      compile_model=False, wandb_log=False, num_workers=2)
     train(cfg)
     pths = list(save.glob("*.pth"))
     assert len(pths) == 1
