@@ -18,7 +18,7 @@ import torch  # noqa: F401  (must precede the CDLL, see module docstring)
 LIB_PATH = Path(os.environ.get("ARGUS_HIP_LIB", Path(__file__).resolve().parent / "libargus_hip.so"))
 
 F32, BF16, FP8 = 0, 1, 2
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 
 class ConvDesc(C.Structure):
@@ -80,6 +80,7 @@ SIGNATURES = {
     "argus_conv_launch_info": (_I, [_DESC, _I, _I, C.POINTER(C.c_int64)]),
     "argus_conv_dgrad": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P]),
     "argus_conv_dgrad_bn_rows": (_I, [_DESC, _I]),
+    "argus_conv_fwd_halo": (_I, [_DESC, _I]),
     "argus_conv_dgrad_stages_prologue": (_I, [_DESC, _I]),
     "argus_conv_dgrad_bn": (_I, [_DESC, _I, _P, _P, _P, _P, C.POINTER(BnBwdEpilogue), C.POINTER(BnBwdPrologue), _P]),
     "argus_conv_wgrad_workspace_bytes": (_SZ, [_DESC, _I]),

@@ -27,7 +27,7 @@ using namespace argus;
 
 extern "C" {
 
-int argus_abi_version(void) { return 7; }
+int argus_abi_version(void) { return 8; }
 
 const char* argus_last_error(void) { return g_last_error.c_str(); }
 
@@ -97,6 +97,7 @@ int argus_conv_dgrad(const argus_conv_desc* d, int dtype, const void* dy, const 
 }
 
 int argus_conv_dgrad_bn_rows(const argus_conv_desc* d, int dtype) { return d ? conv_dgrad_bn_rows(*d, dtype) : -1; }
+int argus_conv_fwd_halo(const argus_conv_desc* d, int dtype) { return d ? conv_fwd_halo(*d, dtype) : 0; }
 int argus_conv_dgrad_stages_prologue(const argus_conv_desc* d, int dtype) {
   return d ? conv_dgrad_stages_prologue(*d, dtype) : 0;
 }

@@ -1167,26 +1167,15 @@ static int dgrad_bm(const argus_conv_desc&) {
   return 64;
 }
 
-int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, void* y,
-             const float* sc, const float* sh, float* stats, hipStream_t st) {
-  if (int e = check_desc(d)) return e;
-  const bool f8 = dtype == ARGUS_FP8;  // bf16 tensors, MX-fp8 GEMM operands where the shape allows
-  if (f8) dtype = ARGUS_BF16;
-  g_launch_work = 2.0 * d.n * d.ho * d.wo * d.k * d.r * d.s * d.c;  // algorithmic flops / bytes (ktimer)
-  g_launch_bytes = (double)(dtype == ARGUS_BF16 ? 2 : 4) *
-                       ((double)d.n * d.h * d.w * (d.stem ? 4 : d.c) + (double)d.k * d.r * d.s * d.c +
-                        (double)d.n * d.ho * d.wo * d.k) +
-                   (stats ? 8.0 * conv_fwd_stat_rows(d, dtype) * d.k : 0.0);
-  IgParams p = {};
-  p.a = x; p.b = w; p.c = y; p.pro_scale = sc; p.pro_shift = sh;
-  p.stats = reinterpret_cast<float2*>(stats);
+// implicit-GEMM parameters of a forward conv (operand pointers left null)
+static void fwd_params(const argus_conv_desc& d, IgParams& p) {
+  p = IgParams{};
   p.N = d.k; p.H = d.h; p.W = d.w; p.ish = d.stride; p.isw = d.stride;
   p.Ho = d.ho; p.Wo = d.wo; p.osh = 1; p.osw = 1; p.ldc = d.k;
   p.addend = nullptr; p.addend_mask = nullptr; p.stem = d.stem; p.nphase = 1;
   IgPhase& ph = p.ph[0];
   ph.M = d.n * d.ho * d.wo; ph.Hq = d.ho; ph.Wq = d.wo; ph.oh0 = 0; ph.ow0 = 0;
   if (d.stem) {
-    if (sc) { set_error("conv_fwd: stem has no prologue"); return ARGUS_ERR_ARG; }
     p.Cin = 256; p.lda = 4; p.ldb = 256; ph.K = 256;
     ph.dh[0] = 0; ph.dw[0] = 0; ph.boff[0] = 0;
   } else {
@@ -1197,6 +1186,32 @@ int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, 
         ph.dh[t] = r - d.pad; ph.dw[t] = s - d.pad; ph.boff[t] = t * d.c;
       }
   }
+}
+
+// 1 when the forward of this conv runs on the LDS-halo kernel (bf16 / fp8 networks), which applies a
+// BN+ReLU prologue once per staged halo element: the producer's BN output need not be materialised
+int conv_fwd_halo(const argus_conv_desc& d, int dtype) {
+  if (check_desc(d) || d.stem || dtype == ARGUS_F32) return 0;
+  IgParams p;
+  fwd_params(d, p);
+  return conv3x3_halo_ok(p) ? 1 : 0;
+}
+
+int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, void* y,
+             const float* sc, const float* sh, float* stats, hipStream_t st) {
+  if (int e = check_desc(d)) return e;
+  const bool f8 = dtype == ARGUS_FP8;  // bf16 tensors, MX-fp8 GEMM operands where the shape allows
+  if (f8) dtype = ARGUS_BF16;
+  g_launch_work = 2.0 * d.n * d.ho * d.wo * d.k * d.r * d.s * d.c;  // algorithmic flops / bytes (ktimer)
+  g_launch_bytes = (double)(dtype == ARGUS_BF16 ? 2 : 4) *
+                       ((double)d.n * d.h * d.w * (d.stem ? 4 : d.c) + (double)d.k * d.r * d.s * d.c +
+                        (double)d.n * d.ho * d.wo * d.k) +
+                   (stats ? 8.0 * conv_fwd_stat_rows(d, dtype) * d.k : 0.0);
+  if (d.stem && sc) { set_error("conv_fwd: stem has no prologue"); return ARGUS_ERR_ARG; }
+  IgParams p;
+  fwd_params(d, p);
+  p.a = x; p.b = w; p.c = y; p.pro_scale = sc; p.pro_shift = sh;
+  p.stats = reinterpret_cast<float2*>(stats);
   const int bm = fwd_bm(d), bn = d.stem ? 64 : pick_bn(0, d.k);
   p.stat_tile = bm;
   p.f8 = f8;

@@ -167,24 +167,30 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_h
     }
   };
 
-  // BN + ReLU of the producer, applied once per chunk to the landed halo image (in place)
+  // BN + ReLU of the producer, applied once per chunk to the landed halo image (in place). A thread
+  // transforms the positions it loaded (piece i: position q_i, validity h_ok[i]) for one fixed channel
+  // chunk (lane & 7, at LDS slot (lane & 7) ^ swz8(q)), so its 8 coefficients are loaded once per chunk
   auto transform_halo = [&](int cc) {
     char* Hl = reinterpret_cast<char*>(lds) + (HB == 2 ? (cc & 1) * HALO : 0);
-    for (int idx = tid; idx < npos * 8; idx += NT) {
-      const int q = idx >> 3, slot = idx & 7;
-      const int ii = q / IMGP, rem = q - ii * IMGP;
-      const int hr = rem / HWD, hc = rem - hr * HWD;
-      const int ih = r0 + hr - 1, iw = hc - 1;
-      u32x4* ptr = reinterpret_cast<u32x4*>(Hl + q * 128 + slot * 16);
-      if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) {
-        const int ch = cc * 64 + (slot ^ swz8(q)) * 8;
+    const int c8 = lane & 7, ch = cc * 64 + c8 * 8;
+    float sc[8], sh[8];
+#pragma unroll
+    for (int j = 0; j < 8; j += 4) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(p.pro_scale + ch + j);
+      const f32x4 b = *reinterpret_cast<const f32x4*>(p.pro_shift + ch + j);
+      sc[j] = a.x; sc[j + 1] = a.y; sc[j + 2] = a.z; sc[j + 3] = a.w;
+      sh[j] = b.x; sh[j + 1] = b.y; sh[j + 2] = b.z; sh[j + 3] = b.w;
+    }
+#pragma unroll
+    for (int i = 0; i < HG; ++i) {
+      const int q = 8 * (i * NW + wave) + (lane >> 3);
+      u32x4* ptr = reinterpret_cast<u32x4*>(Hl + q * 128 + ((c8 ^ swz8(q)) << 4));
+      if (h_ok[i]) {  // inside the image (positions past npos / outside it stay 0: zero padding)
         float f[8];
         unpack(*ptr, f);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], p.pro_scale[ch + j], p.pro_shift[ch + j]), 0.f);
+        for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], sc[j], sh[j]), 0.f);
         *ptr = pack(f);
-      } else {
-        *ptr = u32x4{0u, 0u, 0u, 0u};
       }
     }
   };
@@ -459,15 +465,19 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(const WgHaloParam
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
   const uint32_t lds0 = (uint32_t)(uintptr_t)lds;
-  float* coef = reinterpret_cast<float*>(reinterpret_cast<char*>(lds) + 2 * STG);  // [2][64]
 
   const int H = p.H, W = p.W, HWi = H * W;
   int NI, R;
   if (HWi >= 128) { NI = 1; R = 128 / W; } else { NI = 128 / HWi; R = H; }
   const int HWD = W + 2, IMGP = (R + 2) * HWD, npos = NI * IMGP;
 
+  float psc[PRO ? 8 : 1], psh[PRO ? 8 : 1];  // BN+ReLU coefficients of this thread's channel chunk
   if constexpr (PRO) {
-    if (tid < 128) coef[tid] = tid < 64 ? p.pro_scale[ct * 64 + tid] : p.pro_shift[ct * 64 + tid - 64];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      psc[j] = p.pro_scale[ct * 64 + (lane & 7) * 8 + j];
+      psh[j] = p.pro_shift[ct * 64 + (lane & 7) * 8 + j];
+    }
   }
 
   // fragment geometry: pixel 32*s2 + 8g + 4h + q of the tile -> halo row at tap (0,0)
@@ -530,27 +540,25 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(const WgHaloParam
     const char* DYI = reinterpret_cast<const char*>(lds) + stage * STG;
     const char* HXI = DYI + DYB;
     if constexpr (PRO) {
-      int img0, r0;
-      if (HWi >= 128) { img0 = (tile * 128) / HWi; r0 = (tile * 128 - img0 * HWi) / W; }
-      else { img0 = tile * NI; r0 = 0; }
-      (void)img0;
+      // the positions this thread loaded (pieces 2..6), one fixed channel chunk (lane & 7, at slot
+      // (lane & 7) ^ wsw(q)) whose coefficients sit in registers; outside the image stays 0
+      int r0 = 0;
+      if (HWi >= 128) {
+        const int img0 = (tile * 128) / HWi;
+        r0 = (tile * 128 - img0 * HWi) / W;
+      }
       char* Hl = reinterpret_cast<char*>(lds) + stage * STG + DYB;
-      for (int idx = tid; idx < npos * 8; idx += 512) {
-        const int qq = idx >> 3, slot = idx & 7;
-        const int ii = qq / IMGP, rem = qq - ii * IMGP;
-        const int hr = rem / HWD, hc = rem - hr * HWD;
-        const int ih = r0 + hr - 1, iw = hc - 1;
-        (void)ii;
-        u32x4* ptr = reinterpret_cast<u32x4*>(Hl + qq * 128 + slot * 16);
-        if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) {
-          const int ch = (slot ^ wsw(qq)) * 8;
+#pragma unroll
+      for (int i = 2; i < GPW; ++i) {
+        const int qq = 8 * (wave + 8 * (i - 2)) + (lane >> 3);
+        const int ih = r0 + pos_hr[i - 2] - 1, iw = pos_hc[i - 2] - 1;
+        if (pos_in[i - 2] && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) {
+          u32x4* ptr = reinterpret_cast<u32x4*>(Hl + qq * 128 + (((lane & 7) ^ wsw(qq)) << 4));
           float f[8];
           unpack(*ptr, f);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], coef[ch + j], coef[64 + ch + j]), 0.f);
+          for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], psc[j], psh[j]), 0.f);
           *ptr = pack(f);
-        } else {
-          *ptr = u32x4{0u, 0u, 0u, 0u};
         }
       }
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)

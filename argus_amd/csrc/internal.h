@@ -30,6 +30,7 @@ int conv_weight_prep_batch(int dtype, int count, const void* device_table, int n
 int conv_dgrad(const argus_conv_desc& d, int dtype, const void* dy, const void* wt, void* dx,
                const void* addend, const uint8_t* addend_mask, hipStream_t st);
 int conv_dgrad_bn_rows(const argus_conv_desc& d, int dtype);
+int conv_fwd_halo(const argus_conv_desc& d, int dtype);
 int conv_dgrad_stages_prologue(const argus_conv_desc& d, int dtype);
 int conv_dgrad_bn(const argus_conv_desc& d, int dtype, const void* dy, const void* wt, void* dm,
                   const void* addend, const argus_bn_bwd_epilogue* bn, const argus_bn_bwd_prologue* pro,

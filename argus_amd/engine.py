@@ -88,6 +88,12 @@ class ResNetEngine:
         # kernels; fp32 (parity path) keeps the fused prologue. ARGUS_MATERIALIZE=0/1 overrides.
         env = os.environ.get("ARGUS_MATERIALIZE")
         self.materialize = low if env is None else env == "1"
+        # ... except a1 where conv2's forward runs on the LDS-halo kernel (argus_conv_fwd_halo): that kernel
+        # applies bn1+ReLU once per landed halo element, and conv2's weight gradient applies it the same
+        # way (halo wgrad) or while staging (register-staged wgrad). ARGUS_A1_PRO=1 turns this on; measured
+        # slower at B=64 (8200 vs 8290 img/s: the prologue halo forward loses its load/compute overlap at
+        # each chunk start), so every a1 is materialised by default.
+        self.a1_pro = self.materialize and os.environ.get("ARGUS_A1_PRO", "0") == "1"
         self.device = torch.device(device)
         self.blocks = resnet50_blocks()
         self.shape = None
@@ -123,6 +129,11 @@ class ResNetEngine:
         # ARGUS_SIDE_BATCH=0 issues every weight gradient as soon as its dy is ready.
         self.side_batch = os.environ.get("ARGUS_SIDE_BATCH", "1") != "0"
         self._deferred: list = []  # (cv, fn, buffer data_ptrs)
+        # ... except in the last ARGUS_EAGER_BLOCKS blocks of the backward (layer 1's, the largest weight
+        # gradients): their weight gradients are issued as soon as their dy is ready, so they overlap the
+        # block's remaining dgrads instead of forming the step's tail after the last dgrad
+        self.eager_blocks = int(os.environ.get("ARGUS_EAGER_BLOCKS", "0"))
+        self._eager = False
         self._side_seq = 0
         self._waited_seq = 0
         # the stem weight gradient (main stream, its own split workspace) is issued before the final
@@ -175,6 +186,8 @@ class ResNetEngine:
         for b in self.blocks:
             add(b.prefix + ".conv1", N, h, w, b.cin, b.width, 1, 1, 0)
             ho, wo = add(b.prefix + ".conv2", N, h, w, b.width, b.width, 3, b.stride, 1)
+            a1_pro = self.a1_pro and bool(L.dll.argus_conv_fwd_halo(C.byref(convs[b.prefix + ".conv2"].desc),
+                                                                   self.cdt))
             add(b.prefix + ".conv3", N, ho, wo, b.width, b.cout, 1, 1, 0)
             if b.has_ds:
                 add(b.prefix + ".downsample.0", N, h, w, b.cin, b.cout, 1, b.stride, 0)
@@ -183,7 +196,8 @@ class ResNetEngine:
                 "y1": self._t(N, h, w, b.width), "y2": self._t(N, ho, wo, b.width),
                 "y3": self._t(N, ho, wo, b.cout), "out": self._t(N, ho, wo, b.cout),
                 "yd": self._t(N, ho, wo, b.cout) if b.has_ds else None,
-                "a1": self._t(N, h, w, b.width) if self.materialize else None,
+                "a1": self._t(N, h, w, b.width) if self.materialize and not a1_pro else None,
+                "a1_pro": a1_pro,  # conv2 forward / weight gradient apply bn1 + ReLU themselves
                 "a2": self._t(N, ho, wo, b.width) if self.materialize else None,
                 # ReLU mask of `out`, one byte per 16-byte chunk (argus_bn_apply mask_out)
                 "bits": torch.empty(N * ho * wo * b.cout // self.E, dtype=torch.uint8, device=self.device),
@@ -369,8 +383,11 @@ class ResNetEngine:
                                                               self.bn_ws_ds))
             self._conv_bn(P, Bf, pf + ".conv1", pf + ".bn1", h, a["y1"], None, training)
             if self.materialize:
-                self._act(pf + ".bn1", a["y1"], a["a1"], N * a["hw_in"][0] * a["hw_in"][1], b.width)
-                self._conv_bn(P, Bf, pf + ".conv2", pf + ".bn2", a["a1"], a["y2"], None, training)
+                if a["a1_pro"]:
+                    self._conv_bn(P, Bf, pf + ".conv2", pf + ".bn2", a["y1"], a["y2"], pf + ".bn1", training)
+                else:
+                    self._act(pf + ".bn1", a["y1"], a["a1"], N * a["hw_in"][0] * a["hw_in"][1], b.width)
+                    self._conv_bn(P, Bf, pf + ".conv2", pf + ".bn2", a["a1"], a["y2"], None, training)
                 self._act(pf + ".bn2", a["y2"], a["a2"], N * a["hw"][0] * a["hw"][1], b.width)
                 self._conv_bn(P, Bf, pf + ".conv3", pf + ".bn3", a["a2"], a["y3"], None, training)
             else:
@@ -474,6 +491,7 @@ class ResNetEngine:
         for idx in range(nb - 1, -1, -1):
             b, a = self.blocks[idx], self.act[idx]
             pf = b.prefix
+            self._eager = idx < self.eager_blocks
             h_in = self.act[idx - 1]["out"] if idx > 0 else self.p0
             hi, wi = a["hw_in"]
             ho, wo = a["hw"]
@@ -549,7 +567,7 @@ class ResNetEngine:
             cap("b_dy2", dy2, px_o * b.width, (N, ho, wo, b.width))
             cap("b_dz1", dzb, px_i * b.width, (N, hi, wi, b.width))
             s1 = self.bn_state[pf + ".bn1"]
-            if self.materialize:
+            if self.materialize and not a["a1_pro"]:
                 self._wgrad(pf + ".conv2", a["a1"], None, dy2, G)
             else:
                 self._wgrad(pf + ".conv2", a["y1"], s1, dy2, G)
@@ -598,6 +616,7 @@ class ResNetEngine:
             if self.debug is not None:
                 n_in = N * hi * wi * b.cin
                 self.debug["bwd." + pf] = dh[:n_in].view(N, hi, wi, b.cin).clone()
+        self._eager = False
         # stem: maxpool -> relu/bn1 -> conv1 wgrad
         H1, W1 = self.stem_hw
         dz0, dy0 = g[2], self._next_dy()
@@ -741,7 +760,7 @@ class ResNetEngine:
         """Weight gradient ``fn`` (reading ``buf``) on the side stream: now, or deferred to the block's
         _flush_side (side_batch)."""
         self._deferred.append((cv, fn, buf.data_ptr()))
-        if not self.side_batch:
+        if not self.side_batch or self._eager:
             self._flush_side()
 
     def _flush_side(self) -> None:

@@ -208,6 +208,11 @@ int argus_conv_tuning_get(int key);
  * tag (kind*10^7 + dtype*10^6 + tile_m*1000 + tile_n; kind 1 igemm, 2 wgrad) and writes
  * 2*P*K*R*S*C flops (P = n*ho*wo output pixels). */
 int argus_conv_launch_info(const argus_conv_desc* d, int dtype, int pass, int64_t* flops);
+/* 1 when the forward of this conv runs on the LDS-halo kernel (3x3 stride 1, bf16 / fp8 networks),
+ * which applies a BN+ReLU prologue (pro_scale / pro_shift) once per landed halo element: the
+ * producer's BN output need not be materialised for it (argus/models.py:66-90, the bottleneck's
+ * relu(bn1(conv1(x))) -> conv2). 0 otherwise. */
+int argus_conv_fwd_halo(const argus_conv_desc* d, int dtype);
 /* dw (fp32, OHWI 7x7x3 for the stem) = sum over pixels of dy x im2col(x'), x' as in conv_fwd. */
 size_t argus_conv_wgrad_workspace_bytes(const argus_conv_desc* d, int dtype);
 int argus_conv_wgrad(const argus_conv_desc* d, int dtype, const void* x, const float* pro_scale,

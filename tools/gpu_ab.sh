@@ -9,6 +9,8 @@ fi
 i=0
 for cfg in "$@"; do
   i=$((i+1)); tag="ab${i}_$(echo "$cfg" | tr ' =' '__')"
-  timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-isolated --kernels ${cfg:+--tune $cfg} > gpurun_out/$tag.json 2> gpurun_out/$tag.err || { tail -20 gpurun_out/$tag.err; exit 1; }
+  envs=""; tunes=""
+  for kv in $cfg; do case $kv in ARGUS_*) envs="$envs $kv";; *) tunes="$tunes $kv";; esac; done
+  env $envs timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-isolated --kernels ${tunes:+--tune $tunes} > gpurun_out/$tag.json 2> gpurun_out/$tag.err || { tail -20 gpurun_out/$tag.err; exit 1; }
   python3 -c "import json,sys;d=json.load(open('gpurun_out/$tag.json'));print('$tag', d['value'], d['ms_per_step'])"
 done
