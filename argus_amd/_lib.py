@@ -73,6 +73,8 @@ SIGNATURES = {
     "argus_conv_weight_prep_batch": (_I, [_I, _I, _P, _I, _P]),
     "argus_conv_fwd": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P, _P]),
     "argus_conv_fwd_stat_rows": (_I, [_DESC, _I]),
+    "argus_conv_fwd_stores_input": (_I, [_DESC, _I]),
+    "argus_conv_fwd_store_input": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "argus_conv_fwd_bn": (_I, [_DESC, _I, _P, _P, _P, _P, _P, C.POINTER(BnFwdFin), _P]),
     "argus_conv_fwd_stat_tile": (_I, [_DESC, _I]),
     "argus_conv_tuning": (_I, [_I, _I]),

@@ -71,6 +71,17 @@ int argus_conv_fwd(const argus_conv_desc* d, int dtype, const void* x, const voi
 
 int argus_conv_fwd_stat_rows(const argus_conv_desc* d, int dtype) { return d ? conv_fwd_stat_rows(*d, dtype) : 0; }
 
+int argus_conv_fwd_stores_input(const argus_conv_desc* d, int dtype) { return d ? conv_fwd_stores_input(*d, dtype) : 0; }
+
+int argus_conv_fwd_store_input(const argus_conv_desc* d, int dtype, const void* x, const void* w, void* y,
+                               const float* sc, const float* sh, float* stats, void* x_out, argus_stream_t stream) {
+  if (!d || !x || !w || !y) {
+    set_error("conv_fwd_store_input: bad arguments");
+    return ARGUS_ERR_ARG;
+  }
+  return conv_fwd_store_input(*d, dtype, x, w, y, sc, sh, stats, x_out, (hipStream_t)stream);
+}
+
 int argus_conv_fwd_bn(const argus_conv_desc* d, int dtype, const void* x, const void* w, void* y, const float* sc,
                       const float* sh, const argus_bn_fwd_fin* fin, argus_stream_t stream) {
   if (!d || !x || !w || !y || !fin || (sc == nullptr) != (sh == nullptr)) {

@@ -61,6 +61,7 @@ struct IgParams {
   BnBwdEpi bb;    // dgrad only
   BnFin fin;      // BN finalize folded into this launch (fin.mode != 0)
   BnApplyPro ap;  // dgrad only: the A operand is dm (ap.y != nullptr)
+  void* pro_out;  // forward, 1x1 stride 1 with PRO: column tile 0 stores relu(x*scale+shift) (= the staged A)
   int f8;         // ARGUS_FP8: MX-fp8 operands where the shape allows (host dispatch only)
 };
 

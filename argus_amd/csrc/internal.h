@@ -31,6 +31,9 @@ int conv_dgrad(const argus_conv_desc& d, int dtype, const void* dy, const void* 
                const void* addend, const uint8_t* addend_mask, hipStream_t st);
 int conv_dgrad_bn_rows(const argus_conv_desc& d, int dtype);
 int conv_fwd_halo(const argus_conv_desc& d, int dtype);
+int conv_fwd_stores_input(const argus_conv_desc& d, int dtype);
+int conv_fwd_store_input(const argus_conv_desc& d, int dtype, const void* x, const void* w, void* y, const float* sc,
+                         const float* sh, float* stats, void* x_out, hipStream_t st);
 int conv_dgrad_stages_prologue(const argus_conv_desc& d, int dtype);
 int conv_dgrad_bn(const argus_conv_desc& d, int dtype, const void* dy, const void* wt, void* dm,
                   const void* addend, const argus_bn_bwd_epilogue* bn, const argus_bn_bwd_prologue* pro,

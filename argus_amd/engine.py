@@ -94,6 +94,12 @@ class ResNetEngine:
         # slower at B=64 (8200 vs 8290 img/s: the prologue halo forward loses its load/compute overlap at
         # each chunk start), so every a1 is materialised by default.
         self.a1_pro = self.materialize and os.environ.get("ARGUS_A1_PRO", "0") == "1"
+        # a2 = relu(bn2(y2)) is written by conv3's own forward launch (argus_conv_fwd_store_input: the
+        # 1x1 kernel stages bn2 + ReLU in registers and its column-tile-0 workgroups store what they
+        # staged) instead of a separate bn_apply pass. ARGUS_A2_STORE=1 turns it on; measured neutral at
+        # B=64 (8294-8308 vs 8330 img/s: the pass saved, 0.29 ms, is what the slower store inside the
+        # write-heavy 1x1 kernel costs), so the pass is kept by default
+        self.a2_store = self.materialize and os.environ.get("ARGUS_A2_STORE", "0") == "1"
         self.device = torch.device(device)
         self.blocks = resnet50_blocks()
         self.shape = None
@@ -252,6 +258,8 @@ class ResNetEngine:
         self.wg_ws_stem = torch.empty(wss, dtype=torch.uint8, device=self.device)
         self.stages_pro = {n: bool(L.dll.argus_conv_dgrad_stages_prologue(C.byref(cv.desc), self.cdt))
                            for n, cv in convs.items() if not cv.desc.stem}
+        self.stores_input = {n: bool(L.dll.argus_conv_fwd_stores_input(C.byref(cv.desc), self.cdt))
+                             for n, cv in convs.items()}
         self.gbuf = [self._t(max_elems) for _ in range(4)]  # dh / dx ping-pong, dz ping-pong
         # dy operands of the side-stream weight gradients come from a ring, so the main stream can
         # run ahead of the wgrad stream by several layers before it must wait to reuse a buffer
@@ -295,13 +303,23 @@ class ResNetEngine:
                               ptr(Bf[name + ".running_mean"]), ptr(Bf[name + ".running_var"]),
                               C.c_float(Bf.get(name + ".eps", 1e-5)), ptr(st[2]), ptr(st[3]), stream())
 
-    def _conv_bn(self, P, Bf, conv, bn, x, y, pro, training, part=None, ws=None):
+    def _conv_bn(self, P, Bf, conv, bn, x, y, pro, training, part=None, ws=None, x_out=None):
         cv = self.convs[conv]
         sc = sh = None
         if pro is not None:
             sc, sh = self.bn_state[pro][2], self.bn_state[pro][3]
         part = self.stat_part if part is None else part
         ws = self.bn_ws if ws is None else ws
+        if x_out is not None:  # the forward also stores its staged relu(bn(x)) (argus_conv_fwd_store_input)
+            self._launch(cv, 0, lambda: self.L.conv_fwd_store_input(C.byref(cv.desc), self.cdt, ptr(x), ptr(cv.wf),
+                                                                     ptr(y), ptr(sc), ptr(sh),
+                                                                     ptr(part) if training else None, ptr(x_out),
+                                                                     stream()))
+            if training:
+                self._bn_train(P, Bf, bn, cv.stat_rows, cv.stat_tile, cv.desc.n * cv.desc.ho * cv.desc.wo, part, ws)
+            else:
+                self._bn_eval(P, Bf, bn)
+            return
         if training and self.fold_fin_fwd:  # BN statistics finalize folded into the conv launch
             st = self.bn_state[bn]
             f = BnFwdFin(ptr(part), ptr(P[bn + ".weight"]), ptr(P[bn + ".bias"]), Bf.get(bn + ".eps", 1e-5),
@@ -388,8 +406,12 @@ class ResNetEngine:
                 else:
                     self._act(pf + ".bn1", a["y1"], a["a1"], N * a["hw_in"][0] * a["hw_in"][1], b.width)
                     self._conv_bn(P, Bf, pf + ".conv2", pf + ".bn2", a["a1"], a["y2"], None, training)
-                self._act(pf + ".bn2", a["y2"], a["a2"], N * a["hw"][0] * a["hw"][1], b.width)
-                self._conv_bn(P, Bf, pf + ".conv3", pf + ".bn3", a["a2"], a["y3"], None, training)
+                if self.a2_store and self.stores_input[pf + ".conv3"]:
+                    self._conv_bn(P, Bf, pf + ".conv3", pf + ".bn3", a["y2"], a["y3"], pf + ".bn2", training,
+                                  x_out=a["a2"])
+                else:
+                    self._act(pf + ".bn2", a["y2"], a["a2"], N * a["hw"][0] * a["hw"][1], b.width)
+                    self._conv_bn(P, Bf, pf + ".conv3", pf + ".bn3", a["a2"], a["y3"], None, training)
             else:
                 self._conv_bn(P, Bf, pf + ".conv2", pf + ".bn2", a["y1"], a["y2"], pf + ".bn1", training)
                 self._conv_bn(P, Bf, pf + ".conv3", pf + ".bn3", a["y2"], a["y3"], pf + ".bn2", training)

@@ -87,6 +87,14 @@ int argus_conv_fwd(const argus_conv_desc* d, int dtype, const void* x, const voi
                    const float* pro_scale, const float* pro_shift, float* stat_part,
                    argus_stream_t stream);
 int argus_conv_fwd_stat_rows(const argus_conv_desc* d, int dtype);
+/* argus_conv_fwd with a BN+ReLU prologue that also writes the transformed input relu(x*scale+shift)
+ * (the tensor the kernel staged, same layout and dtype as x) to x_out: the bottleneck's
+ * relu(bn2(conv2(.))) -> conv3 (argus/models.py:66-90) materialised by conv3's own launch instead of
+ * a separate pass, for the weight gradient. 1x1 stride-1 convs only: argus_conv_fwd_stores_input. */
+int argus_conv_fwd_stores_input(const argus_conv_desc* d, int dtype);
+int argus_conv_fwd_store_input(const argus_conv_desc* d, int dtype, const void* x, const void* w_fwd, void* y,
+                               const float* pro_scale, const float* pro_shift, float* stat_part, void* x_out,
+                               argus_stream_t stream);
 /* conv_fwd with the train-mode BatchNorm statistics finalize of its output folded into the launch
  * (replaces argus_conv_fwd(..stat_part..) + argus_bn_finalize): `part` is the partial scratch
  * (float2[argus_conv_fwd_stat_rows(d)][k]), the last workgroups merge it (fp64, fixed order) and

@@ -615,6 +615,43 @@ def test_layer1_3x3_on_single_buffer_halo_kernel(cuda):
     assert _rel(outs[1][0], outs[0][0]) < 1e-2 and _rel(outs[1][1], outs[0][1]) < 1e-2
 
 
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+def test_conv_fwd_store_input(cuda, dt):
+    """argus_conv_fwd_store_input (1x1 stride-1 conv with a BN+ReLU prologue that also writes the
+    staged relu(x*scale+shift)): y and the BN partials bit-identical to argus_conv_fwd with the same
+    prologue, x_out bit-identical to argus_bn_apply's relu(bn(x)); 64- to 512-channel outputs (1 to 4
+    column tiles), partial row tiles; a 3x3 conv is refused."""
+    torch.manual_seed(21)
+    L = lib()
+    for cin, cout, hw, n in ((64, 256, 9, 3), (128, 512, 8, 2), (256, 64, 7, 5), (512, 128, 5, 4)):
+        d, _ = _desc(n, hw, hw, cin, cout, 1, 1)
+        assert L.dll.argus_conv_fwd_stores_input(C.byref(d), DT[dt]) == 1
+        w = torch.randn(cout, 1, 1, cin) * (2.0 / cin) ** 0.5
+        wf, _ = _prep(d, dt, w.to(cuda), cuda)
+        x = (torch.randn(n, hw, hw, cin) * 2 + 0.3).to(cuda, TDT[dt])
+        sc, sh = (torch.rand(cin) + 0.5).to(cuda), (torch.randn(cin) * 0.5).to(cuda)
+        rows = L.dll.argus_conv_fwd_stat_rows(C.byref(d), DT[dt])
+        outs = []
+        for store in (False, True):
+            y = torch.empty(n, hw, hw, cout, dtype=TDT[dt], device=cuda)
+            part = torch.empty(rows, cout, 2, device=cuda)
+            xo = torch.full((n, hw, hw, cin), float("nan"), dtype=TDT[dt], device=cuda)
+            if store:
+                assert L.conv_fwd_store_input(C.byref(d), DT[dt], ptr(x), ptr(wf), ptr(y), ptr(sc), ptr(sh), ptr(part),
+                                              ptr(xo), stream()) == 0
+            else:
+                L.conv_fwd(C.byref(d), DT[dt], ptr(x), ptr(wf), ptr(y), ptr(sc), ptr(sh), ptr(part), stream())
+                L.bn_apply(DT[dt], n * hw * hw, cin, ptr(x), ptr(sc), ptr(sh), None, None, None, 1, ptr(xo), None,
+                           stream())
+            torch.cuda.synchronize()
+            outs.append((y.cpu(), part.cpu(), xo.cpu()))
+        (y0, p0, a0), (y1, p1, a1) = outs
+        assert torch.equal(y0, y1) and torch.equal(p0, p1), (cin, cout, dt)
+        assert torch.equal(a0, a1), (cin, cout, dt, "stored input")
+    d3, _ = _desc(2, 8, 8, 64, 64, 3, 1)
+    assert L.dll.argus_conv_fwd_stores_input(C.byref(d3), DT[dt]) == 0
+
+
 def _halo_cases(L, cuda):
     from argus_amd.profiling import KernelTimer
 
