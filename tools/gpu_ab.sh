@@ -11,6 +11,6 @@ for cfg in "$@"; do
   i=$((i+1)); tag="ab${i}_$(echo "$cfg" | tr ' =' '__')"
   envs=""; tunes=""
   for kv in $cfg; do case $kv in ARGUS_*) envs="$envs $kv";; *) tunes="$tunes $kv";; esac; done
-  env $envs timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-isolated --kernels ${tunes:+--tune $tunes} > gpurun_out/$tag.json 2> gpurun_out/$tag.err || { tail -20 gpurun_out/$tag.err; exit 1; }
+  env $envs timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-isolated --kernels $BENCH_ARGS ${tunes:+--tune $tunes} > gpurun_out/$tag.json 2> gpurun_out/$tag.err || { tail -20 gpurun_out/$tag.err; exit 1; }
   python3 -c "import json,sys;d=json.load(open('gpurun_out/$tag.json'));print('$tag', d['value'], d['ms_per_step'])"
 done
