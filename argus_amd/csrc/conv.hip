@@ -524,7 +524,7 @@ __global__ __launch_bounds__(256 * SUB, (OCC == 1 || SUB == 2) ? 1 : 2) void wgr
   const int mtiles = p.M / BM, ntiles = p.N / BN;
   const int nwg = mtiles * ntiles;
   int bid, split;
-  split_tile(nwg, (p.P + p.pps - 1) / p.pps, p.S == 1 && p.N == p.Cin, bid, split);
+  split_tile(nwg, (p.P + p.pps - 1) / p.pps, p.group != 0, bid, split);
   const int mt = bid / ntiles, nt = bid - mt * ntiles;
   // this sub-pipeline's pixels: half (SUB = 2) of the split's k-steps; both halves run the same
   // trip count (the shorter one loads zeros) so the workgroup barriers stay matched
@@ -1128,6 +1128,9 @@ static int g_wgrad_target_blocks = 512;
 // 66 MB of partials against 8 MB of operands), which contend with the main stream for HBM
 static int g_wgrad_target_3x3 = 512;
 static int g_wgrad_partial_budget = 0;  // key 28: split-partial bytes <= this x operand bytes (0 = off)
+// key 31: the register-staged / glds weight gradients of non-1x1 filters run a pixel split's tiles on
+// one XCD too (they then share that XCD's L2 copy of the split's dy / im2col rows)
+static int g_wg_group3x3 = 0;
 
 static int* tuning_slot(int key) {
   if (key >= 0 && key < 3) return &g_force_bm[key];
@@ -1156,6 +1159,7 @@ static int* tuning_slot(int key) {
     case 28: return &g_wgrad_partial_budget;
     case 29: return &g_f8_occ;
     case 30: return &g_halo64;
+    case 31: return &g_wg_group3x3;
     default: return nullptr;
   }
 }
@@ -1616,6 +1620,7 @@ int conv_wgrad(const argus_conv_desc& d, int dtype, const void* x, const float* 
   p.M = d.k; p.N = pl.N; p.Cin = d.stem ? 4 : d.c; p.lda = d.stem ? 4 : d.c;
   p.H = d.h; p.W = d.w; p.Ho = d.ho; p.Wo = d.wo; p.stride = d.stride; p.pad = d.pad; p.S = d.s;
   p.P = d.n * d.ho * d.wo; p.pps = pl.pps; p.stem = d.stem;
+  p.group = (d.s == 1 && pl.N == d.c) || (g_wg_group3x3 && !d.stem) ? 1 : 0;
   p.fd_hw = make_fastdiv(d.ho * d.wo); p.fd_w = make_fastdiv(d.wo);
   if (d.stem && sc) { set_error("conv_wgrad: stem has no prologue"); return ARGUS_ERR_ARG; }
   int splits = pl.splits;

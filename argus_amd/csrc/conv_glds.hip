@@ -376,7 +376,7 @@ __global__ __launch_bounds__((BM / 64) * 2 * 64, 1) void wgrad_glds_kernel(const
   const int mtiles = p.M / BM, ntiles = p.N / 128;
   const int nwg = mtiles * ntiles;
   int bid, split;
-  split_tile(nwg, (p.P + p.pps - 1) / p.pps, p.S == 1 && p.N == p.Cin, bid, split);
+  split_tile(nwg, (p.P + p.pps - 1) / p.pps, p.group != 0, bid, split);
   const int mt = bid / ntiles, nt = bid - mt * ntiles;
   const int pbeg = split * p.pps;
   const int pend = min(p.P, pbeg + p.pps);

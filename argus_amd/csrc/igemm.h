@@ -86,6 +86,7 @@ struct WgParams {
   const void* ap_y;
   const float *ap_ca, *ap_cb, *ap_cc;
   FastDiv fd_hw, fd_w;  // Ho*Wo and Wo (pixel -> (image, row, column) without integer division)
+  int group;            // split_tile: a split's tiles on one XCD (1x1 filters; 3x3 with tuning key 31)
 };
 
 template <typename T> struct Mma;
