@@ -207,7 +207,9 @@ int argus_conv_dgrad_bn(const argus_conv_desc* d, int dtype, const void* dy, con
  * multiple of the operand bytes (0 = off, the default; 1-4 measured neutral), key 29 the
  * workgroups per CU of the MX-fp8 forward/dgrad kernel (2 default, 4), key 30 the 64-channel 3x3
  * stride-1 layers (Cin = Cout = 64) on the LDS-halo kernel's single-halo-buffer 64-column variant
- * (1, default) or on the register-staged implicit GEMM (0).
+ * (1, default) or on the register-staged implicit GEMM (0), key 31 whether the split weight
+ * gradients of non-1x1 filters run a pixel split's output tiles on one XCD as the 1x1 ones do
+ * (0, default; 1 measured neutral).
  * Returns 0, or -1 for an unknown key. */
 int argus_conv_tuning(int key, int value);
 /* Current value of a tuning key (-1 for an unknown key). */
