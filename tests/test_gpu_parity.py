@@ -161,6 +161,36 @@ def test_bf16_block_backward_stages(cuda, golden, shape):
     print("bf16 worst max-relative error per stage:", {k: f"{v:.2e}" for k, v in worst.items()})
 
 
+def test_bf16_optional_schedules_block_backward_stages(cuda, golden, monkeypatch):
+    """The optional bf16 schedules (off by default, DESIGN.md §5 'Measured and rejected in round 2'):
+    no a1 where conv2 runs on the LDS-halo kernel (ARGUS_A1_PRO=1: bn1 + ReLU applied by the halo
+    forward and the conv2 weight gradient) and a2 written by conv3's forward launch
+    (ARGUS_A2_STORE=1) - every backward stage re-derived in fp64 like the default schedule."""
+    from argus_amd.losses import geometric_loss_fn
+
+    from argus_amd._lib import lib
+
+    monkeypatch.setenv("ARGUS_A1_PRO", "1")
+    monkeypatch.setenv("ARGUS_A2_STORE", "1")
+    x = mg.synthetic_images(2, 256, 256, seed=1234)
+    T = torch.tensor(golden["inputs"]["targets"], dtype=torch.float32)
+    L = lib()
+    assert L.dll.argus_conv_tuning(13, 1) == 0  # the halo kernels at this small batch's grids
+    try:
+        m = _product(cuda, "bf16")
+        eng = m._engine(cuda)
+        assert eng.a1_pro and eng.a2_store
+        eng.debug = {}
+        geometric_loss_fn(m(x.to(cuda)), T.to(cuda)).mean().backward()
+        debug, eng.debug = eng.debug, None
+    finally:
+        L.dll.argus_conv_tuning(13, 256)
+    assert all((a["a1"] is None) == (b.stride == 1) for b, a in zip(eng.blocks, eng.act)), \
+        "every stride-1 conv2 (and no strided one) takes the halo prologue path"
+    worst = stage_checks(eng, dict(m.named_parameters()), debug, 1e-2)
+    print("optional bf16 schedules, worst max-relative error per stage:", {k: f"{v:.2e}" for k, v in worst.items()})
+
+
 def test_bf16_b64_forward_and_fused_step(cuda):
     """configs[1] size (B=64, 256x256) on the benched bf16 path against the CPU oracle."""
     from argus_amd.step import FusedTrainer
