@@ -1050,7 +1050,7 @@ extern int g_bwd_min_px, g_bwd_max_rows, g_ew_target, g_ew_min_ppt, g_fin_div;  
 // load, then both compute): 128x128 alone 72 us vs 62 us, step 8000 vs 8100 img/s -> default 1
 static int g_wg_sub = 1;
 static int g_wg_occ128 = 2;  // argus_conv_tuning key 15: workgroups/CU of the 128x128 wgrad tile (1 = with ring)
-extern int g_halo64;  // conv_halo.hip, key 30
+extern int g_halo64, g_halo_epi_prefetch;  // conv_halo.hip, keys 30 and 32
 extern int g_halo_enable, g_wg_halo_enable, g_wg_halo_target_blocks, g_halo_min_grid,
     g_wg_halo_max_tiles;  // conv_halo.hip
 // argus_conv_tuning key 7: largest K (elements) served by the single-buffer OCC=3/4 kernel. Swept with
@@ -1160,6 +1160,7 @@ static int* tuning_slot(int key) {
     case 29: return &g_f8_occ;
     case 30: return &g_halo64;
     case 31: return &g_wg_group3x3;
+    case 32: return &g_halo_epi_prefetch;
     default: return nullptr;
   }
 }

@@ -197,6 +197,16 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_h
 
   // ---- main loop over k-steps kt = chunk*9 + tap ----
   // issue order: H(0) B(0) B(1) | per step j: [H(chunk(j)+1) if tap(j)==0] [B(j+2)]
+  // BN-backward epilogue operands (y, mask bits, y2) of this thread's output rows, loaded at the start
+  // of the last channel chunk (step kpre) so they arrive under its nine taps instead of after the loop
+  // (one workgroup per CU: nothing else would hide that latency). NLD = the loads that certainly
+  // issue (an addend adds more: the wait below then only waits longer).
+  constexpr int CPR_ = BN / 8, NITP = 256 / (NT / CPR_);
+  // (BW 2 only, the 3x3 dgrads of the step: the mask-bit variants would spill the extra registers)
+  constexpr bool PRE = BW == 2;
+  constexpr int NLD = PRE ? NITP : 0;
+  EpiIn pre[PRE ? NITP : 1];
+  const int kpre = p.epi_pre ? nk - 9 : -2;
   issue_halo(0);
   issue_b(0);
   if (nk > 1) issue_b(1);
@@ -209,11 +219,21 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_h
       halo_after = (j % 9 == 0) && (j / 9 + 1 < nch);
     }
     const bool b_after = kt + 1 < nk;
+    const bool after_pre = PRE && kt == kpre + 1;  // the prefetch went out after B(kt)
     if (halo_after && b_after) waitvm<HG + BG>();
     else if (halo_after) waitvm<HG>();
-    else if (b_after) waitvm<BG>();
+    else if (b_after) { if (after_pre) waitvm<BG + NLD>(); else waitvm<BG>(); }
     else waitvm<0>();
     sbar();
+    if constexpr (PRE) {
+      if (kt == kpre) {
+#pragma unroll
+        for (int i = 0; i < NITP; ++i) {
+          const int rr = tid / CPR_ + (NT / CPR_) * i;
+          epi_load<bf16, BW>(p, (size_t)(mt * 256 + rr) * p.ldc + nt * BN + (tid % CPR_) * 8, pre[i]);
+        }
+      }
+    }
     if constexpr (PRO) {
       // before issuing new glds: the coefficient loads' vmcnt wait then drains only B(kt+1)
       if (t == 0) {
@@ -293,7 +313,8 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_h
   BwdEpiAcc<bf16, BW> bwd;
   if constexpr (BW != 0) bwd.init(p.bb, nt * BN + c * 8);
   constexpr int NIT = 256 / RPP, U = 4;
-  static_assert(NIT * RPP == 256 && NIT % U == 0, "epilogue row partition");
+  static_assert(NIT * RPP == 256 && NIT % U == 0 && NIT == NITP, "epilogue row partition");
+#pragma unroll
   for (int i0 = 0; i0 < NIT; i0 += U) {
     size_t off[U];
     EpiIn in[U];
@@ -301,7 +322,8 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_h
     for (int u = 0; u < U; ++u) {
       const int rr = tid / CPR + RPP * (i0 + u);
       off[u] = (size_t)(mt * 256 + rr) * p.ldc + nt * BN + c * 8;
-      epi_load<bf16, BW>(p, off[u], in[u]);
+      if (PRE && p.epi_pre) in[u] = pre[PRE ? i0 + u : 0];
+      else epi_load<bf16, BW>(p, off[u], in[u]);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -328,9 +350,15 @@ static const char* halo_name() {
   return s.c_str();
 }
 
+// key 32: prefetch the BN-backward epilogue operands of the halo dgrad under its last channel chunk:
+// 1 = on the single-buffer 64-column variant (layer 1: 172 -> 163 us), 2 = every variant (the
+// 128-column one measured 83 -> 100 us, the step within noise), 0 = off
+int g_halo_epi_prefetch = 1;
+
 template <int BN, bool PRO, int BW, int HB>
 static void launch_halo2(const IgParams& p0, hipStream_t st) {
   IgParams p = p0;
+  p.epi_pre = g_halo_epi_prefetch == 2 || (g_halo_epi_prefetch == 1 && HB == 1);
   plan_fin(p, 256);
   dim3 grid((p.ph[0].M / 256) * (p.N / BN));
   timed_launch(halo_name<BN, PRO, BW, HB>(), conv3x3_halo_kernel<BN, PRO, BW, HB>, grid, dim3(4 * (BN / 64) * 64),

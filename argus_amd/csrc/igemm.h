@@ -63,6 +63,7 @@ struct IgParams {
   BnApplyPro ap;  // dgrad only: the A operand is dm (ap.y != nullptr)
   void* pro_out;  // forward, 1x1 stride 1 with PRO: column tile 0 stores relu(x*scale+shift) (= the staged A)
   int f8;         // ARGUS_FP8: MX-fp8 operands where the shape allows (host dispatch only)
+  int epi_pre;    // halo dgrad: prefetch the BN-backward epilogue operands under the last chunk (key 32)
 };
 
 // compile-time epilogue/prologue variant of the dgrad kernels: low 3 bits = BN-backward epilogue

@@ -209,7 +209,9 @@ int argus_conv_dgrad_bn(const argus_conv_desc* d, int dtype, const void* dy, con
  * stride-1 layers (Cin = Cout = 64) on the LDS-halo kernel's single-halo-buffer 64-column variant
  * (1, default) or on the register-staged implicit GEMM (0), key 31 whether the split weight
  * gradients of non-1x1 filters run a pixel split's output tiles on one XCD as the 1x1 ones do
- * (0, default; 1 measured neutral).
+ * (0, default; 1 measured neutral), key 32 where the 3x3 LDS-halo dgrad with a BN-backward
+ * epilogue prefetches its epilogue operands under its last channel chunk (1, default: the
+ * single-halo-buffer 64-column variant; 2 every variant; 0 none).
  * Returns 0, or -1 for an unknown key. */
 int argus_conv_tuning(int key, int value);
 /* Current value of a tuning key (-1 for an unknown key). */
