@@ -5,5 +5,4 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout
 tail -1 gpurun_out/gpu_tests.log
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
 cat gpurun_out/smoke.log
-[ $# -gt 0 ] && exec_ab=1
 bash tools/gpu_ab.sh "" "$@"
