@@ -18,7 +18,7 @@ import torch  # noqa: F401  (must precede the CDLL, see module docstring)
 LIB_PATH = Path(os.environ.get("ARGUS_HIP_LIB", Path(__file__).resolve().parent / "libargus_hip.so"))
 
 F32, BF16, FP8 = 0, 1, 2
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 
 class ConvDesc(C.Structure):
@@ -44,15 +44,6 @@ class BnBwdPrologue(C.Structure):
                 ("dy_out", C.c_void_p)]
 
 
-class BnFwdFin(C.Structure):
-    """argus_bn_fwd_fin (include/argus_hip.h)."""
-
-    _fields_ = [("part", C.c_void_p), ("gamma", C.c_void_p), ("beta", C.c_void_p), ("eps", C.c_float),
-                ("momentum", C.c_float), ("running_mean", C.c_void_p), ("running_var", C.c_void_p),
-                ("num_batches_tracked", C.c_void_p), ("mean", C.c_void_p), ("invstd", C.c_void_p),
-                ("scale", C.c_void_p), ("shift", C.c_void_p), ("workspace", C.c_void_p)]
-
-
 _P = C.c_void_p
 _I = C.c_int
 _I64 = C.c_int64
@@ -73,22 +64,19 @@ SIGNATURES = {
     "argus_conv_weight_prep_batch": (_I, [_I, _I, _P, _I, _P]),
     "argus_conv_fwd": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P, _P]),
     "argus_conv_fwd_stat_rows": (_I, [_DESC, _I]),
-    "argus_conv_fwd_stores_input": (_I, [_DESC, _I]),
-    "argus_conv_fwd_store_input": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
-    "argus_conv_fwd_bn": (_I, [_DESC, _I, _P, _P, _P, _P, _P, C.POINTER(BnFwdFin), _P]),
     "argus_conv_fwd_stat_tile": (_I, [_DESC, _I]),
     "argus_conv_tuning": (_I, [_I, _I]),
     "argus_conv_tuning_get": (_I, [_I]),
     "argus_conv_launch_info": (_I, [_DESC, _I, _I, C.POINTER(C.c_int64)]),
     "argus_conv_dgrad": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P]),
     "argus_conv_dgrad_bn_rows": (_I, [_DESC, _I]),
-    "argus_conv_fwd_halo": (_I, [_DESC, _I]),
     "argus_conv_dgrad_stages_prologue": (_I, [_DESC, _I]),
     "argus_conv_dgrad_bn": (_I, [_DESC, _I, _P, _P, _P, _P, C.POINTER(BnBwdEpilogue), C.POINTER(BnBwdPrologue), _P]),
     "argus_conv_wgrad_workspace_bytes": (_SZ, [_DESC, _I]),
     "argus_conv_wgrad": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     "argus_conv_wgrad_apply": (_I, [_DESC, _I, _P, _P, C.POINTER(BnBwdPrologue), _P, _P, _SZ, _P]),
     "argus_ktimer_enable": (_I, [C.c_char_p]),
+    "argus_ktimer_enable_on": (_I, [C.c_char_p, _P]),
     "argus_ktimer_disable": (_I, []),
     "argus_ktimer_count": (_I, []),
     "argus_ktimer_get": (_I, [_I, C.c_char_p, _I, C.POINTER(C.c_int64), C.POINTER(C.c_double),

@@ -49,8 +49,11 @@ def _range(v) -> tuple:
 
 
 def motion_kernel3(angle_deg: float, direction: float) -> np.ndarray:
-    """kornia get_motion_kernel2d(3, angle, direction): a centre-row line with weights
-    linspace(d, 1 - d, 3), d = (direction + 1) / 2, rotated by ``angle`` (bilinear), normalized."""
+    """kornia get_motion_kernel2d(3, angle, direction) with its default nearest-neighbour resampling
+    (RandomMotionBlur's resample="nearest"): a centre-row line with weights linspace(d, 1 - d, 3),
+    d = (direction + 1) / 2, rotated by ``angle`` about the centre (each output tap takes the line tap
+    nearest to its back-rotated position, rounding half to even as torch's grid_sample does), then
+    normalized to sum 1."""
     d = (min(max(direction, -1.0), 1.0) + 1.0) / 2.0
     k = np.zeros((3, 3))
     k[1, :] = np.linspace(d, 1.0 - d, 3)
@@ -60,14 +63,9 @@ def motion_kernel3(angle_deg: float, direction: float) -> np.ndarray:
     for y in range(3):
         for x in range(3):
             dx, dy = x - 1, y - 1  # rotate the sampling point back by the angle
-            sx, sy = ca * dx + sa * dy + 1, -sa * dx + ca * dy + 1
-            x0, y0 = math.floor(sx), math.floor(sy)
-            v = 0.0
-            for yy, wy in ((y0, 1 - (sy - y0)), (y0 + 1, sy - y0)):
-                for xx, wx in ((x0, 1 - (sx - x0)), (x0 + 1, sx - x0)):
-                    if 0 <= yy < 3 and 0 <= xx < 3:
-                        v += wy * wx * k[yy, xx]
-            out[y, x] = v
+            sx, sy = int(np.rint(ca * dx + sa * dy + 1)), int(np.rint(-sa * dx + ca * dy + 1))
+            if 0 <= sy < 3 and 0 <= sx < 3:
+                out[y, x] = k[sy, sx]
     s = out.sum()
     return out / s if s > 0 else k / k.sum()
 
@@ -110,12 +108,15 @@ class DeviceAugmentation:
             br, co, sa = _range(c.brightness), _range(c.contrast), _range(c.saturation)
             hu = c.hue if isinstance(c.hue, (tuple, list)) else (-c.hue, c.hue)
             vals = [self._u(n_samples, *r) for r in (br, co, sa, hu)]
-            order = 0
-            for i, op in enumerate(torch.randperm(4, generator=self.gen).tolist()):
-                order |= op << (2 * i)
+            # kornia ColorJiggle draws a fresh op order on every call: one call per sample (per
+            # __getitem__), shared by that sample's cameras like its factors
+            order = np.zeros(n_samples, dtype=np.int32)
+            for b in range(n_samples):
+                for i, op in enumerate(torch.randperm(4, generator=self.gen).tolist()):
+                    order[b] |= op << (2 * i)
             for key, v in zip(("bright", "contrast", "sat", "hue"), vals):
                 p[key] = np.repeat(v, nc)
-            p["order"] = order
+            p["order"] = np.repeat(order, nc)
             p["jiggle"] = 1
         if c.blur:  # RandomGaussianBlur((5, 5), (3.0, 8.0), p=0.5)
             on = self._u(n, 0, 1) < 0.5

@@ -1,6 +1,7 @@
-// BatchNorm finalize folded into the kernel that produces its partial sums (conv forward epilogue:
-// {sum, M2} per row tile; dgrad BN-backward epilogue: {sum dm, sum dm*xhat}). Replaces the separate
-// stats_finalize / bwd_finalize launches (bn.hip) on the critical path.
+// BatchNorm-backward finalize folded into the dgrad that produces its partial sums (the BN-backward
+// epilogue's {sum dm, sum dm*xhat} per row tile). Replaces the separate bwd_finalize launch (bn.hip)
+// on the critical path. (Folding the forward statistics finalize into the conv measured neutral: the
+// forward keeps stats_finalize_kernel.)
 //
 // Two-level, deterministic, per column tile nt of the producer (COLS channels):
 //  1. every workgroup stores its partial row(s) write-through (8-byte agent-scope atomic stores) and
@@ -8,8 +9,7 @@
 //     merges the group's rows for its COLS channels in fp64, in row order, and publishes the result
 //     write-through to red[g][C];
 //  2. it then takes a ticket on cnt[nt][ng]; the last group merger sums the ng group results in group
-//     order and finalizes those channels (forward: mean / invstd / scale / shift, running statistics,
-//     num_batches_tracked; backward: dgamma / dbeta and the apply coefficients ca / cb / cc).
+//     order and finalizes those channels: dgamma / dbeta and the apply coefficients ca / cb / cc.
 // Hand-off (MI355X_MICROARCH.md §Workgroup dispatch, valid form "sc1 stores + drain + ticket +
 // consumer acquire"): every storing wave drains (s_waitcnt vmcnt(0)) before the workgroup barrier,
 // one lane takes the agent-scope ticket, the last arriver runs an agent-scope acquire before its plain
@@ -54,49 +54,24 @@ ARGUS_DEV bool fin_ticket(unsigned* cnt_, unsigned n, int* flag) {
 }
 
 struct BnFin {
-  int mode;        // 0 off, 1 forward (Chan merge of {sum, M2}), 2 backward (plain sums)
+  int mode;        // 0 off, 2 on (plain column sums)
   int T;           // producer row tiles (all dgrad phases); exactly one arrival per (tile, column tile)
   int rpw;         // partial rows per row tile
-  int rows;        // valid partial rows (forward: cdiv(count, tile_rows))
+  int rows;        // valid partial rows
   int gt, ng;      // tiles per group, groups
   int C;           // channels = partial row length
-  int tile_rows;   // forward: pixels per partial row
   long long count; // pixels per channel
   unsigned* cnt;   // [C / 64 column tiles][ng + 1] (indexed with the producer's column tile width)
   double2* red;    // [ng][C]; the second branch at red + ng * C
   const float2* part;
   const float2* part2;
-  // forward
-  const float *gamma, *beta;
-  float eps, momentum;
-  float *rm, *rv;
-  long long* nbt;
-  float *mean, *invstd, *scale, *shift;
-  // backward: BN statistics of the forward, outputs (+ the second, downsample branch)
+  // BN statistics of the forward, outputs (+ the second, downsample branch)
+  const float* gamma;
   const float *bmean, *binvstd;
   float *dgamma, *dbeta, *ca, *cb, *cc;
   const float *gamma2, *bmean2, *binvstd2;
   float *dgamma2, *dbeta2, *ca2, *cb2, *cc2;
 };
-
-ARGUS_DEV void fin_forward(const BnFin& f, int c, double2 tot) {
-  const double count = (double)f.count;
-  const double mean = tot.x / count;
-  double m2 = tot.y - tot.x * mean;
-  if (m2 < 0.0) m2 = 0.0;
-  const double var = m2 / count;
-  const float invstd = (float)(1.0 / sqrt(var + (double)f.eps));
-  const float sc = f.gamma[c] * invstd;
-  f.mean[c] = (float)mean;
-  f.invstd[c] = invstd;
-  f.scale[c] = sc;
-  f.shift[c] = f.beta[c] - (float)mean * sc;
-  if (f.rm) f.rm[c] = (1.f - f.momentum) * f.rm[c] + f.momentum * (float)mean;
-  if (f.rv) {
-    const double unbiased = count > 1.0 ? m2 / (count - 1.0) : var;
-    f.rv[c] = (1.f - f.momentum) * f.rv[c] + f.momentum * (float)unbiased;
-  }
-}
 
 ARGUS_DEV void fin_backward(int c, double2 tot, double count, const float* gamma, const float* mean,
                             const float* invstd, float* dgamma, float* dbeta, float* ca, float* cb, float* cc) {
@@ -125,7 +100,7 @@ ARGUS_DEV void bn_fin_arrive(const BnFin& f, int t, int nt, double2* scratch, in
   if (!fin_ticket(cnt + g, (unsigned)gsz, flag)) return;
   const int cp = threadIdx.x % CP, lr = threadIdx.x / CP;
   const int c = nt * COLS + 2 * cp;
-  const bool dual = f.mode == 2 && f.part2 != nullptr;
+  const bool dual = f.part2 != nullptr;
   // level 1: the group's rows, fixed order (row lanes, then lanes in order)
   const int r0 = g * f.gt * f.rpw, r1 = min(f.rows, (g * f.gt + gsz) * f.rpw);
 #pragma unroll
@@ -146,15 +121,8 @@ ARGUS_DEV void bn_fin_arrive(const BnFin& f, int t, int nt, double2* scratch, in
         if (r >= r1) break;
         S0 += (double)v[u].x;
         S1 += (double)v[u].z;
-        if (f.mode == 1) {
-          const long long left = f.count - (long long)r * f.tile_rows;
-          const double inv = 1.0 / (left >= f.tile_rows ? (double)f.tile_rows : (double)left);
-          Q0 += (double)v[u].y + (double)v[u].x * (double)v[u].x * inv;
-          Q1 += (double)v[u].w + (double)v[u].z * (double)v[u].z * inv;
-        } else {
-          Q0 += (double)v[u].y;
-          Q1 += (double)v[u].w;
-        }
+        Q0 += (double)v[u].y;
+        Q1 += (double)v[u].w;
       }
     }
     scratch[2 * (lr * CP + cp)] = make_double2(S0, Q0);
@@ -192,16 +160,13 @@ ARGUS_DEV void bn_fin_arrive(const BnFin& f, int t, int nt, double2* scratch, in
       for (int h = 0; h < 2; ++h) {
         double2 a = scratch[2 * cp + h];
         for (int i = 1; i < LR; ++i) { a.x += scratch[2 * (i * CP + cp) + h].x; a.y += scratch[2 * (i * CP + cp) + h].y; }
-        if (f.mode == 1) {
-          fin_forward(f, c + h, a);
-        } else if (br == 0) {
+        if (br == 0) {
           fin_backward(c + h, a, (double)f.count, f.gamma, f.bmean, f.binvstd, f.dgamma, f.dbeta, f.ca, f.cb, f.cc);
         } else {
           fin_backward(c + h, a, (double)f.count, f.gamma2, f.bmean2, f.binvstd2, f.dgamma2, f.dbeta2, f.ca2,
                        f.cb2, f.cc2);
         }
       }
-      if (f.mode == 1 && nt == 0 && cp == 0 && f.nbt) f.nbt[0] += 1;
     }
     __syncthreads();
   }

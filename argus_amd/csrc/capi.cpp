@@ -27,7 +27,7 @@ using namespace argus;
 
 extern "C" {
 
-int argus_abi_version(void) { return 8; }
+int argus_abi_version(void) { return 9; }
 
 const char* argus_last_error(void) { return g_last_error.c_str(); }
 
@@ -71,26 +71,6 @@ int argus_conv_fwd(const argus_conv_desc* d, int dtype, const void* x, const voi
 
 int argus_conv_fwd_stat_rows(const argus_conv_desc* d, int dtype) { return d ? conv_fwd_stat_rows(*d, dtype) : 0; }
 
-int argus_conv_fwd_stores_input(const argus_conv_desc* d, int dtype) { return d ? conv_fwd_stores_input(*d, dtype) : 0; }
-
-int argus_conv_fwd_store_input(const argus_conv_desc* d, int dtype, const void* x, const void* w, void* y,
-                               const float* sc, const float* sh, float* stats, void* x_out, argus_stream_t stream) {
-  if (!d || !x || !w || !y) {
-    set_error("conv_fwd_store_input: bad arguments");
-    return ARGUS_ERR_ARG;
-  }
-  return conv_fwd_store_input(*d, dtype, x, w, y, sc, sh, stats, x_out, (hipStream_t)stream);
-}
-
-int argus_conv_fwd_bn(const argus_conv_desc* d, int dtype, const void* x, const void* w, void* y, const float* sc,
-                      const float* sh, const argus_bn_fwd_fin* fin, argus_stream_t stream) {
-  if (!d || !x || !w || !y || !fin || (sc == nullptr) != (sh == nullptr)) {
-    set_error("conv_fwd_bn: bad arguments");
-    return ARGUS_ERR_ARG;
-  }
-  return conv_fwd_bn(*d, dtype, x, w, y, sc, sh, *fin, (hipStream_t)stream);
-}
-
 int argus_conv_tuning(int key, int value) { return conv_tuning(key, value); }
 int argus_conv_tuning_get(int key) { return conv_tuning_get(key); }
 
@@ -108,7 +88,6 @@ int argus_conv_dgrad(const argus_conv_desc* d, int dtype, const void* dy, const 
 }
 
 int argus_conv_dgrad_bn_rows(const argus_conv_desc* d, int dtype) { return d ? conv_dgrad_bn_rows(*d, dtype) : -1; }
-int argus_conv_fwd_halo(const argus_conv_desc* d, int dtype) { return d ? conv_fwd_halo(*d, dtype) : 0; }
 int argus_conv_dgrad_stages_prologue(const argus_conv_desc* d, int dtype) {
   return d ? conv_dgrad_stages_prologue(*d, dtype) : 0;
 }

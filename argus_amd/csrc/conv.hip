@@ -232,11 +232,6 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
       else pc.load(p.pro_scale, p.pro_shift, S.ch);
 #pragma unroll
       for (int i = 0; i < AR; ++i) S.a[i] = sel(S.ok[i], pc.apply(S.a[i]));
-      if (p.pro_out && nt == 0) {  // 1x1 stride 1: the staged element is x[a_off + ch], each stored once
-#pragma unroll
-        for (int i = 0; i < AR; ++i)
-          if (S.ok[i]) st16_nt(reinterpret_cast<T*>(p.pro_out) + a_off[i] + S.ch, S.a[i]);
-      }
     }
     if constexpr (AP) {  // dy = ca*dm + cb*y + cc; zero outside the image (dgrad's zero padding of dy)
       float ca[E], cb[E], cc[E];
@@ -413,12 +408,6 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
       store_part(p.stats + (size_t)mt * p.N + nt * BN + tid, make_float2(a0.x + a1.x, m2));
     }
     __syncthreads();
-    // forward finalize: ticket taken before the output stores, so its drain waits only for the
-    // partial row just written
-    if (p.fin.mode == 1) {
-      bn_fin_arrive<256, BN>(p.fin, mt, nt, reinterpret_cast<double2*>(lds), &fin_flag);
-      __syncthreads();
-    }
   }
 
   // ---- epilogue: stage the C tile in LDS, then 16-byte coalesced (+accumulating) stores ----
@@ -483,7 +472,7 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
                                  (size_t)blockIdx.z * p.bb.prow + mt, p.N, nt * BN);
   }
   if constexpr (BW != 0) {
-    if (p.fin.mode == 2) {
+    if (p.fin.mode) {
       __syncthreads();
       bn_fin_arrive<256, BN>(p.fin, blockIdx.z * p.bb.prow + mt, nt, reinterpret_cast<double2*>(lds), &fin_flag);
     }
@@ -497,15 +486,11 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
 // ds_read_b64_tr_b16 half-wave touches land on 8 distinct slots.
 ARGUS_DEV int swz32(int row) { return (row & 3) | (((row >> 3) & 1) << 2); }
 
-// OCC: 2 = two workgroups per CU, no register prefetch ring on the 128x128 tile (historical default);
-// 1 = one per CU with the ring; 3 = two per CU with the ring (fits: ~220 VGPRs)
-// SUB: independent 256-thread sub-pipelines per workgroup, each with its own LDS ring, splitting
-// the workgroup's pixel range in two contiguous halves; their accumulators are summed through LDS
-// (sub 0 + sub 1, fixed order) before the one fp32 partial is written. SUB = 2 keeps the
-// occupancy of two 256-thread workgroups per CU and halves the split partials (HBM traffic and
-// the reduce's input).
-template <typename T, int BM, int BN, bool STEM, bool PRO, bool FAST, int OCC = 2, bool AP = false, int SUB = 1>
-__global__ __launch_bounds__(256 * SUB, (OCC == 1 || SUB == 2) ? 1 : 2) void wgrad_kernel(const WgParams p) {
+// Two workgroups per CU; the 128x128 tile keeps a single staged k-step in registers (the 2-deep ring
+// would not fit two waves per SIMD without spilling; with it at one or two waves per SIMD, or as two
+// 256-thread sub-pipelines per workgroup, it measured slower: DESIGN.md §5).
+template <typename T, int BM, int BN, bool STEM, bool PRO, bool FAST, bool AP = false>
+__global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgParams p) {
   constexpr int E = Chunk<T>::E;
   constexpr bool BF = (E == 8);
   constexpr int BKP = BF ? 64 : 32;               // pixels per k-step
@@ -516,25 +501,17 @@ __global__ __launch_bounds__(256 * SUB, (OCC == 1 || SUB == 2) ? 1 : 2) void wgr
   constexpr int RPA = 256 / CA, RPB = 256 / CB;   // rows per staging pass
   constexpr int PA = BKP / RPA, PB = BKP / RPB;   // passes
   constexpr int MI = BM / 32, NI = BN / 32;
-  __shared__ __attribute__((aligned(16))) u32x4 lds_all[SUB][2][BKP * (RSA + RSB)];
-  static_assert(SUB == 1 || (size_t)MI * NI * 256 * 16 <= sizeof(lds_all[0]), "sub-pipeline merge buffer");
-  const int sub = SUB == 1 ? 0 : (int)(threadIdx.x >> 8);
-  auto& lds = lds_all[sub];
+  __shared__ __attribute__((aligned(16))) u32x4 lds[2][BKP * (RSA + RSB)];
 
   const int mtiles = p.M / BM, ntiles = p.N / BN;
   const int nwg = mtiles * ntiles;
   int bid, split;
   split_tile(nwg, (p.P + p.pps - 1) / p.pps, p.group != 0, bid, split);
   const int mt = bid / ntiles, nt = bid - mt * ntiles;
-  // this sub-pipeline's pixels: half (SUB = 2) of the split's k-steps; both halves run the same
-  // trip count (the shorter one loads zeros) so the workgroup barriers stay matched
-  const int sbeg = split * p.pps;
-  const int send = min(p.P, sbeg + p.pps);
-  const int nks = send > sbeg ? (send - sbeg + BKP - 1) / BKP : 0;
-  const int nkh = (nks + SUB - 1) / SUB;
-  const int pbeg = sbeg + sub * nkh * BKP;
-  const int pend = min(send, pbeg + nkh * BKP);
-  const int tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
+  const int pbeg = split * p.pps;
+  const int pend = min(p.P, pbeg + p.pps);
+  const int nkh = pend > pbeg ? (pend - pbeg + BKP - 1) / BKP : 0;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const T* __restrict__ X = reinterpret_cast<const T*>(p.x);
   const T* __restrict__ DY = reinterpret_cast<const T*>(p.dy);
@@ -589,11 +566,11 @@ __global__ __launch_bounds__(256 * SUB, (OCC == 1 || SUB == 2) ? 1 : 2) void wgr
     for (int i = 0; i < PA; ++i) {
       const int pix = p0 + ra0 + RPA * i;
       const bool ok = pix < pend;
-      S.a[i] = ld16(a_col + (size_t)(ok ? pix : sbeg) * p.M);  // sbeg < P: a safe clamp
+      S.a[i] = ld16(a_col + (size_t)(ok ? pix : pbeg) * p.M);  // pbeg < P: a safe clamp
       if constexpr (AP) {  // dy = ca*dm + cb*y + cc (argus_bn_bwd_apply's formula, fp32, rounded to T)
         float d[E], yv[E];
         unpack(S.a[i], d);
-        unpack(ld16(ap_col + (size_t)(ok ? pix : sbeg) * p.M), yv);
+        unpack(ld16(ap_col + (size_t)(ok ? pix : pbeg) * p.M), yv);
 #pragma unroll
         for (int j = 0; j < E; ++j) d[j] = fmaf(apa[j], d[j], fmaf(apb[j], yv[j], apc[j]));
         S.a[i] = pack(d);
@@ -615,7 +592,7 @@ __global__ __launch_bounds__(256 * SUB, (OCC == 1 || SUB == 2) ? 1 : 2) void wgr
       if constexpr (FAST) {
         nimg = n0; oh = oh0 + dr[i]; ow = ow0 + dc[i];
       } else {
-        const int pp = pok ? pix : sbeg;
+        const int pp = pok ? pix : pbeg;
         nimg = fdiv(pp, p.fd_hw);
         const int rem = pp - nimg * HWo;
         oh = fdiv(rem, p.fd_w);
@@ -726,7 +703,7 @@ __global__ __launch_bounds__(256 * SUB, (OCC == 1 || SUB == 2) ? 1 : 2) void wgr
 
   // LDS double buffer + 2-deep register prefetch ring (as igemm_kernel); the 128x128 tile keeps a
   // single staged k-step (the ring would not fit two waves per SIMD without spilling)
-  constexpr bool RING = !(BM == 128 && BN == 128) || OCC != 2;
+  constexpr bool RING = !(BM == 128 && BN == 128);
   const int nk = nkh;
   if (!RING && nk > 0) {
     Stage S0;
@@ -763,22 +740,6 @@ __global__ __launch_bounds__(256 * SUB, (OCC == 1 || SUB == 2) ? 1 : 2) void wgr
     if (kt < nk) compute(0);
   }
 
-  if constexpr (SUB == 2) {  // sub 1 hands its accumulators to sub 0 through (its own) LDS
-    f32x4* red = reinterpret_cast<f32x4*>(&lds_all[1][0][0]);
-    __syncthreads();
-    if (sub == 1) {
-#pragma unroll
-      for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < NI; ++ni) red[(mi * NI + ni) * 256 + tid] = acc[mi][ni];
-    }
-    __syncthreads();
-    if (sub == 1) return;
-#pragma unroll
-    for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < NI; ++ni) acc[mi][ni] += red[(mi * NI + ni) * 256 + tid];
-  }
   float* out = p.part + (size_t)split * p.M * p.N;
 #pragma unroll
   for (int mi = 0; mi < MI; ++mi)
@@ -964,10 +925,8 @@ __global__ __launch_bounds__(256) void weight_prep_batch_kernel(const WpEntry* _
 // host launchers
 // ------------------------------------------------------------------------------------------------
 
-// argus_conv_fwd_bn / argus_conv_wgrad_apply hand their extra arguments to conv_fwd / conv_wgrad
-// through these (host, one thread per process: the library's contract)
-static const argus_bn_fwd_fin* g_fwd_fin = nullptr;
-static void* g_pro_out = nullptr;  // argus_conv_fwd_store_input
+// argus_conv_wgrad_apply hands its extra arguments to conv_wgrad through this (host, one thread per
+// process: the library's contract)
 static const argus_bn_bwd_prologue* g_wg_apply = nullptr;
 
 static int check_desc(const argus_conv_desc& d) {
@@ -1043,13 +1002,8 @@ static void dispatch_ig_bwd(const IgParams& p, int maxM, int bm, int bn, hipStre
   else dispatch_ig_bwd1<T, OCC, 0>(p, maxM, bm, bn, st);
 }
 
-extern int g_glds_min_k, g_glds_min_grid, g_wg_glds_enable, g_wg_glds_target;  // conv_glds.hip
+extern int g_glds_min_k, g_glds_min_grid;  // conv_glds.hip
 extern int g_bwd_min_px, g_bwd_max_rows, g_ew_target, g_ew_min_ppt, g_fin_div;  // bn.hip
-// argus_conv_tuning key 26: wgrad_kernel sub-pipelines per workgroup (1 or 2). Measured on MI355X at
-// B=64: SUB = 2 halves the split partials but the shared barrier couples the two pipelines (both
-// load, then both compute): 128x128 alone 72 us vs 62 us, step 8000 vs 8100 img/s -> default 1
-static int g_wg_sub = 1;
-static int g_wg_occ128 = 2;  // argus_conv_tuning key 15: workgroups/CU of the 128x128 wgrad tile (1 = with ring)
 extern int g_halo64, g_halo_epi_prefetch;  // conv_halo.hip, keys 30 and 32
 extern int g_halo_enable, g_wg_halo_enable, g_wg_halo_target_blocks, g_halo_min_grid,
     g_wg_halo_max_tiles;  // conv_halo.hip
@@ -1060,7 +1014,6 @@ static int g_smallk_max = 1024;
 // argus_conv_tuning key 18: stem forward kernel, 2 (ring) or 4 (single buffer; convbench B=64:
 // 214 -> 179 us)
 static int g_stem_occ = 4;
-static int g_f8_occ = 2;  // argus_conv_tuning key 29: workgroups per CU of the MX-fp8 igemm (2 or 4 -> 3 for 128x128)
 
 // MX-fp8 operands (ARGUS_FP8) need whole 128-element k-steps inside one filter tap and no staging
 // transform of the A operand; other convs of an fp8 network run the bf16 kernels
@@ -1081,21 +1034,11 @@ static int run_ig(const IgParams& p, hipStream_t st, int bm, int bn) {
   const bool smallk = maxK <= g_smallk_max;
   if constexpr (sizeof(T) == 2) {
     if (f8_ok(p)) {  // single-buffered (the staged bf16 pair per chunk doubles the staging registers)
-      const int v = p.bb.mode ? bwd_variant(p.bb) : 0;
-      if (g_f8_occ == 4) {
-        switch (v) {
-          case 2: dispatch_ig<T, false, 4, 2 | kFp8Bit>(p, maxM, bm, bn, st); break;
-          case 3: dispatch_ig<T, false, 4, 3 | kFp8Bit>(p, maxM, bm, bn, st); break;
-          case 4: dispatch_ig<T, false, 4, 4 | kFp8Bit>(p, maxM, bm, bn, st); break;
-          default: dispatch_ig<T, false, 4, kFp8Bit>(p, maxM, bm, bn, st);
-        }
-      } else {
-        switch (v) {
-          case 2: dispatch_ig<T, false, 2, 2 | kFp8Bit>(p, maxM, bm, bn, st); break;
-          case 3: dispatch_ig<T, false, 2, 3 | kFp8Bit>(p, maxM, bm, bn, st); break;
-          case 4: dispatch_ig<T, false, 2, 4 | kFp8Bit>(p, maxM, bm, bn, st); break;
-          default: dispatch_ig<T, false, 2, kFp8Bit>(p, maxM, bm, bn, st);
-        }
+      switch (p.bb.mode ? bwd_variant(p.bb) : 0) {
+        case 2: dispatch_ig<T, false, 2, 2 | kFp8Bit>(p, maxM, bm, bn, st); break;
+        case 3: dispatch_ig<T, false, 2, 3 | kFp8Bit>(p, maxM, bm, bn, st); break;
+        case 4: dispatch_ig<T, false, 2, 4 | kFp8Bit>(p, maxM, bm, bn, st); break;
+        default: dispatch_ig<T, false, 2, kFp8Bit>(p, maxM, bm, bn, st);
       }
       return check_launch("igemm_kernel");
     }
@@ -1127,10 +1070,6 @@ static int g_wgrad_target_blocks = 512;
 // in the full step 512 wins (+0.7 %): fewer fp32 split partials (for layer 4's 3x3, 7 splits wrote
 // 66 MB of partials against 8 MB of operands), which contend with the main stream for HBM
 static int g_wgrad_target_3x3 = 512;
-static int g_wgrad_partial_budget = 0;  // key 28: split-partial bytes <= this x operand bytes (0 = off)
-// key 31: the register-staged / glds weight gradients of non-1x1 filters run a pixel split's tiles on
-// one XCD too (they then share that XCD's L2 copy of the split's dy / im2col rows)
-static int g_wg_group3x3 = 0;
 
 static int* tuning_slot(int key) {
   if (key >= 0 && key < 3) return &g_force_bm[key];
@@ -1145,21 +1084,14 @@ static int* tuning_slot(int key) {
     case 12: return &g_wg_halo_target_blocks;
     case 13: return &g_halo_min_grid;
     case 14: return &g_wg_halo_max_tiles;
-    case 15: return &g_wg_occ128;
-    case 16: return &g_wg_glds_enable;
-    case 17: return &g_wg_glds_target;
     case 18: return &g_stem_occ;
     case 20: return &g_bwd_min_px;    // bn.hip: BN-backward pixels per block (min)
     case 21: return &g_bwd_max_rows;  //   ... and blocks per channel group (max)
     case 22: return &g_ew_target;     //   bn_apply / bwd_apply target blocks
     case 23: return &g_ew_min_ppt;    //   ... min pixels per thread
     case 24: return &g_fin_div;       //   BN finalize group-count divisor
-    case 26: return &g_wg_sub;
     case 27: return &g_wgrad_target_3x3;
-    case 28: return &g_wgrad_partial_budget;
-    case 29: return &g_f8_occ;
     case 30: return &g_halo64;
-    case 31: return &g_wg_group3x3;
     case 32: return &g_halo_epi_prefetch;
     default: return nullptr;
   }
@@ -1225,15 +1157,6 @@ static void fwd_params(const argus_conv_desc& d, IgParams& p) {
   }
 }
 
-// 1 when the forward of this conv runs on the LDS-halo kernel (bf16 / fp8 networks), which applies a
-// BN+ReLU prologue once per staged halo element: the producer's BN output need not be materialised
-int conv_fwd_halo(const argus_conv_desc& d, int dtype) {
-  if (check_desc(d) || d.stem || dtype == ARGUS_F32) return 0;
-  IgParams p;
-  fwd_params(d, p);
-  return conv3x3_halo_ok(p) ? 1 : 0;
-}
-
 int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, void* y,
              const float* sc, const float* sh, float* stats, hipStream_t st) {
   if (int e = check_desc(d)) return e;
@@ -1249,21 +1172,9 @@ int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, 
   fwd_params(d, p);
   p.a = x; p.b = w; p.c = y; p.pro_scale = sc; p.pro_shift = sh;
   p.stats = reinterpret_cast<float2*>(stats);
-  p.pro_out = g_pro_out;
   const int bm = fwd_bm(d), bn = d.stem ? 64 : pick_bn(0, d.k);
   p.stat_tile = bm;
   p.f8 = f8;
-  if (g_fwd_fin && stats) {  // argus_conv_fwd_bn: the statistics finalize folded into this launch
-    const argus_bn_fwd_fin& f = *g_fwd_fin;
-    BnFin& b = p.fin;
-    b.mode = 1; b.C = d.k; b.count = (long long)d.n * d.ho * d.wo; b.tile_rows = bm;
-    b.cnt = reinterpret_cast<unsigned*>(f.workspace);
-    b.red = reinterpret_cast<double2*>(reinterpret_cast<char*>(f.workspace) + kBnCounterBytes);
-    b.part = reinterpret_cast<const float2*>(f.part);
-    b.gamma = f.gamma; b.beta = f.beta; b.eps = f.eps; b.momentum = f.momentum;
-    b.rm = f.running_mean; b.rv = f.running_var; b.nbt = reinterpret_cast<long long*>(f.num_batches_tracked);
-    b.mean = f.mean; b.invstd = f.invstd; b.scale = f.scale; b.shift = f.shift;
-  }
   return dtype == ARGUS_BF16 ? run_ig<bf16>(p, st, bm, bn) : run_ig<float>(p, st, bm, bn);
 }
 
@@ -1320,39 +1231,6 @@ static void dgrad_work(const argus_conv_desc& d, int dtype, bool addend, bool ma
                         (addend ? 2.0 : 1.0) * px_in) +
                    (mask ? px_in / (dtype == ARGUS_BF16 ? 8 : 4) : 0.0) +
                    (bn ? E * px_in * (dual ? 2.0 : 1.0) : 0.0);  // BN input(s) y read by the epilogue
-}
-
-// 1x1 stride-1 convs (the register-staged kernel, which stages a BN+ReLU prologue in registers) can
-// store the transformed input while staging it (argus_conv_fwd_store_input)
-int conv_fwd_stores_input(const argus_conv_desc& d, int) {
-  return !check_desc(d) && !d.stem && d.r == 1 && d.s == 1 && d.stride == 1 && d.pad == 0 ? 1 : 0;
-}
-
-int conv_fwd_store_input(const argus_conv_desc& d, int dtype, const void* x, const void* w, void* y, const float* sc,
-                         const float* sh, float* stats, void* x_out, hipStream_t st) {
-  if (!conv_fwd_stores_input(d, dtype) || !sc || !sh || !x_out || x_out == x || x_out == y) {
-    set_error("conv_fwd_store_input: needs a 1x1 stride-1 conv, a BN+ReLU prologue and a separate x_out");
-    return ARGUS_ERR_ARG;
-  }
-  g_pro_out = x_out;
-  const int rc = conv_fwd(d, dtype, x, w, y, sc, sh, stats, st);
-  g_pro_out = nullptr;
-  if (rc == ARGUS_OK)  // + the stored input (ktimer's algorithmic bytes of this launch)
-    g_launch_bytes += (dtype == ARGUS_F32 ? 4.0 : 2.0) * d.n * d.h * d.w * d.c;
-  return rc;
-}
-
-int conv_fwd_bn(const argus_conv_desc& d, int dtype, const void* x, const void* w, void* y, const float* sc,
-                const float* sh, const argus_bn_fwd_fin& f, hipStream_t st) {
-  if (!f.part || !f.gamma || !f.beta || !f.mean || !f.invstd || !f.scale || !f.shift || !f.workspace) {
-    set_error("conv_fwd_bn: bad finalize arguments");
-    return ARGUS_ERR_ARG;
-  }
-  if (d.k / 64 * 65 * 4 > (int)kBnCounterBytes) { set_error("conv_fwd_bn: too many channels"); return ARGUS_ERR_ARG; }
-  g_fwd_fin = &f;
-  const int rc = conv_fwd(d, dtype, x, w, y, sc, sh, f.part, st);
-  g_fwd_fin = nullptr;
-  return rc;
 }
 
 int conv_dgrad(const argus_conv_desc& d, int dtype, const void* dy, const void* wt, void* dx,
@@ -1475,7 +1353,6 @@ int conv_dgrad_bn(const argus_conv_desc& d, int dtype, const void* dy, const voi
 struct WgPlan {
   int bm, bn, mt, nt, splits, pps, kstep;
   int N;
-  int sub;  // sub-pipelines per workgroup (wgrad_kernel SUB)
 };
 
 static WgPlan wgrad_plan(const argus_conv_desc& d, int dtype) {
@@ -1493,20 +1370,8 @@ static WgPlan wgrad_plan(const argus_conv_desc& d, int dtype) {
   // (2048 when Cout = 64: one row tile, 9 column tiles)
   long target = g_wgrad_target_blocks;
   if (target == 512 && d.r == 3) target = d.k <= 64 ? 2048 : g_wgrad_target_3x3;
-  // two sub-pipelines per workgroup (bf16 register-staged tiles): half the workgroups, each with
-  // twice the pixels, same wave count on the chip
-  pl.sub = (g_wg_sub == 2 && dtype == ARGUS_BF16 && !d.stem && !(pl.bm == 128 && pl.bn == 128 && g_wg_occ128 != 2))
-               ? 2 : 1;
-  target /= pl.sub;
   long splits = (target + tiles - 1) / tiles;
-  if (g_wgrad_partial_budget > 0 && !d.stem) {
-    // cap the fp32 split partials (written + read back: 8 B per dW element per split) at a multiple
-    // of the operand bytes: the deep layers' dW is larger than their activations
-    const double ops = (double)(dtype == ARGUS_BF16 ? 2 : 4) * ((double)d.n * d.h * d.w * d.c + (double)P * d.k);
-    const long cap = (long)(g_wgrad_partial_budget * ops / (8.0 * d.k * pl.N));
-    if (splits > cap) splits = cap < 2 ? 2 : cap;
-  }
-  const long max_splits = (P + pl.kstep * 4 * pl.sub - 1) / (pl.kstep * 4 * pl.sub);  // >= 4 k-steps per sub
+  const long max_splits = (P + pl.kstep * 4 - 1) / (pl.kstep * 4);  // >= 4 k-steps per split
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
   long pps = (P + splits - 1) / splits;
@@ -1526,51 +1391,29 @@ size_t conv_wgrad_ws(const argus_conv_desc& d, int dtype) {
     const size_t hb = (size_t)hs * d.k * 9 * d.c * sizeof(float);
     b = hb > b ? hb : b;
   }
-  int gs, gpps;
-  if (wgrad_glds_plan(d, dtype, false, &gs, &gpps)) {
-    const size_t gb = (size_t)gs * d.k * pl.N * sizeof(float);
-    b = gb > b ? gb : b;
-  }
   return b;
 }
 
-template <typename T, int BM, int BN, bool STEM, bool PRO, bool FAST, int OCC, bool AP, int SUB>
+template <typename T, int BM, int BN, bool STEM, bool PRO, bool FAST, bool AP>
 static const char* wg_name() {
   static const std::string s = std::string("argus::wgrad_kernel<") + type_name<T>() + ", " + std::to_string(BM) +
                                ", " + std::to_string(BN) + ", " + bool_name(STEM) + ", " + bool_name(PRO) + ", " +
-                               bool_name(FAST) + ", " + std::to_string(OCC) + ", " + bool_name(AP) + ", " +
-                               std::to_string(SUB) + ">";
+                               bool_name(FAST) + ", " + bool_name(AP) + ">";
   return s.c_str();
 }
 
-template <typename T, int BM, int BN, bool STEM, bool PRO, bool FAST, int OCC = 2, bool AP = false>
+template <typename T, int BM, int BN, bool STEM, bool PRO, bool FAST, bool AP = false>
 static void launch_wg(const WgParams& p, const WgPlan& pl, hipStream_t st) {
-  dim3 grid(pl.mt * pl.nt * pl.splits);
-  constexpr bool kSub2 = std::is_same<T, bf16>::value && !STEM && OCC == 2;  // wgrad_plan's sub = 2 cases
-  if (pl.sub == 2 && !kSub2) { set_error("wgrad: no two-sub-pipeline variant"); return; }
-  if constexpr (kSub2) {
-    if (pl.sub == 2) {
-      timed_launch(wg_name<T, BM, BN, STEM, PRO, FAST, OCC, AP, 2>(),
-                   wgrad_kernel<T, BM, BN, STEM, PRO, FAST, OCC, AP, 2>, grid, dim3(512), st, p);
-      return;
-    }
-  }
-  {
-    timed_launch(wg_name<T, BM, BN, STEM, PRO, FAST, OCC, AP, 1>(), wgrad_kernel<T, BM, BN, STEM, PRO, FAST, OCC, AP, 1>,
-                 grid, dim3(256), st, p);
-  }
+  timed_launch(wg_name<T, BM, BN, STEM, PRO, FAST, AP>(), wgrad_kernel<T, BM, BN, STEM, PRO, FAST, AP>,
+               dim3(pl.mt * pl.nt * pl.splits), dim3(256), st, p);
 }
 
 template <typename T, bool PRO, bool FAST, bool AP = false>
 static void dispatch_wg_tiles(const WgParams& p, const WgPlan& pl, hipStream_t st) {
-  if (pl.bm == 128 && pl.bn == 128) {
-    if (!AP && g_wg_occ128 == 1) launch_wg<T, 128, 128, false, PRO, FAST, 1>(p, pl, st);
-    else if (!AP && g_wg_occ128 == 3) launch_wg<T, 128, 128, false, PRO, FAST, 3>(p, pl, st);
-    else launch_wg<T, 128, 128, false, PRO, FAST, 2, AP>(p, pl, st);
-  }
-  else if (pl.bm == 128) launch_wg<T, 128, 64, false, PRO, FAST, 2, AP>(p, pl, st);
-  else if (pl.bn == 128) launch_wg<T, 64, 128, false, PRO, FAST, 2, AP>(p, pl, st);
-  else launch_wg<T, 64, 64, false, PRO, FAST, 2, AP>(p, pl, st);
+  if (pl.bm == 128 && pl.bn == 128) launch_wg<T, 128, 128, false, PRO, FAST, AP>(p, pl, st);
+  else if (pl.bm == 128) launch_wg<T, 128, 64, false, PRO, FAST, AP>(p, pl, st);
+  else if (pl.bn == 128) launch_wg<T, 64, 128, false, PRO, FAST, AP>(p, pl, st);
+  else launch_wg<T, 64, 64, false, PRO, FAST, AP>(p, pl, st);
 }
 
 template <typename T>
@@ -1580,8 +1423,8 @@ static void dispatch_wg(const WgParams& p, const WgPlan& pl, hipStream_t st) {
   const bool fast = (p.Ho * p.Wo) % bkp == 0 && (p.Wo % bkp == 0 || bkp % p.Wo == 0);
   if (p.stem) {  // stem: M = 64 channels, N = 256; with the BN-backward apply of dy staged (AP) or not
     if (p.ap_y) {
-      if (fast) launch_wg<T, 64, 128, true, false, true, 2, true>(p, pl, st);
-      else launch_wg<T, 64, 128, true, false, false, 2, true>(p, pl, st);
+      if (fast) launch_wg<T, 64, 128, true, false, true, true>(p, pl, st);
+      else launch_wg<T, 64, 128, true, false, false, true>(p, pl, st);
     } else {
       if (fast) launch_wg<T, 64, 128, true, false, true>(p, pl, st);
       else launch_wg<T, 64, 128, true, false, false>(p, pl, st);
@@ -1621,22 +1464,16 @@ int conv_wgrad(const argus_conv_desc& d, int dtype, const void* x, const float* 
   p.M = d.k; p.N = pl.N; p.Cin = d.stem ? 4 : d.c; p.lda = d.stem ? 4 : d.c;
   p.H = d.h; p.W = d.w; p.Ho = d.ho; p.Wo = d.wo; p.stride = d.stride; p.pad = d.pad; p.S = d.s;
   p.P = d.n * d.ho * d.wo; p.pps = pl.pps; p.stem = d.stem;
-  p.group = (d.s == 1 && pl.N == d.c) || (g_wg_group3x3 && !d.stem) ? 1 : 0;
+  p.group = d.s == 1 && pl.N == d.c ? 1 : 0;  // 1x1: a split's tiles on one XCD (3x3: spread, measured)
   p.fd_hw = make_fastdiv(d.ho * d.wo); p.fd_w = make_fastdiv(d.wo);
   if (d.stem && sc) { set_error("conv_wgrad: stem has no prologue"); return ARGUS_ERR_ARG; }
   int splits = pl.splits;
-  int gs, gpps;
   if (g_wg_apply) {  // the register-staged kernel stages the apply; no halo / glds variant does
     if (dtype == ARGUS_BF16) dispatch_wg<bf16>(p, pl, st);
     else dispatch_wg<float>(p, pl, st);
     if (int e = check_launch("wgrad_kernel")) return e;
   } else if (wgrad3x3_halo_launch(d, dtype, x, sc, sh, dy, ws, ws_bytes, &splits, st)) {
     if (int e = check_launch("wgrad3x3_halo_kernel")) return e;
-  } else if (wgrad_glds_plan(d, dtype, sc != nullptr, &gs, &gpps) &&
-             ws_bytes >= (size_t)gs * d.k * pl.N * sizeof(float)) {
-    wgrad_glds_launch(d, p, gs, gpps, st);
-    splits = gs;
-    if (int e = check_launch("wgrad_glds_kernel")) return e;
   } else {
     if (dtype == ARGUS_BF16) dispatch_wg<bf16>(p, pl, st);
     else dispatch_wg<float>(p, pl, st);

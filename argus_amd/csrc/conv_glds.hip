@@ -218,10 +218,6 @@ __global__ __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) void igemm_glds_kern
       store_part(p.stats + (size_t)(mt * HALVES + h) * p.N + nt * BN + col, make_float2(a0.x + a1.x, m2));
     }
     __syncthreads();
-    if (p.fin.mode == 1) {  // before the output stores (see conv.hip)
-      bn_fin_arrive<NT, BN>(p.fin, mt, nt, reinterpret_cast<double2*>(lds), &fin_flag);
-      __syncthreads();
-    }
   }
 
   // ---- epilogue: stage the C tile in LDS, then 16-byte coalesced (+addend) stores ----
@@ -275,7 +271,7 @@ __global__ __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) void igemm_glds_kern
                                 (size_t)blockIdx.z * p.bb.prow + mt, p.N, nt * BN);
   }
   if constexpr (BW != 0) {
-    if (p.fin.mode == 2) {
+    if (p.fin.mode) {
       __syncthreads();
       bn_fin_arrive<NT, BN>(p.fin, blockIdx.z * p.bb.prow + mt, nt, reinterpret_cast<double2*>(lds), &fin_flag);
     }
@@ -328,189 +324,6 @@ bool igemm_glds_ok(const IgParams& p, int maxM, int maxK) {
 bool igemm_glds_launch(const IgParams& p, int maxM, int maxK, hipStream_t st) {
   if (!igemm_glds_ok(p, maxM, maxK)) return false;
   launch_glds<256, 128>(p, maxM, st);
-  return true;
-}
-
-}  // namespace argus
-
-namespace argus {
-
-// ================================================================================================
-// Weight gradient dW[k][tap*C + c] = sum_p dy[p][k] * x[p + off(tap)][c] (bf16, no prologue) with both
-// operands staged global->LDS by DMA. Tile 256 (k) x 128 (tap, c) over 8 waves (4 x 2, 64 x 64 each);
-// k-step = 64 pixels; per stage three [64 px][256 B] images (dy channels 0-127 / 128-255 of the tile,
-// x at the tile's tap) with 32-byte slot j of row r at j ^ swz32g(r), read as ds_read_b64_tr_b16
-// fragments (both operands are pixel-major). 3-stage ring, counted vmcnt, raw barriers (as
-// igemm_glds_kernel). Pixel ranges are split over workgroups; fp32 partials [split][K][N] are summed by
-// wgrad_reduce_kernel.
-// ================================================================================================
-ARGUS_DEV int swz32g(int row) { return (row & 3) | (((row >> 3) & 1) << 2); }
-
-ARGUS_DEV u32x4 trg(const char* img, int row0, int slot, int pq) {
-  unsigned w[4];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int row = row0 + 4 * h;
-    const char* addr = img + row * 256 + ((slot ^ swz32g(row)) << 5) + pq * 8;
-    const s16x4 t = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (s16x4 __attribute__((address_space(3)))*)(uintptr_t)(uint32_t)(uintptr_t)addr);
-    const uint2 u = __builtin_bit_cast(uint2, t);
-    w[2 * h] = u.x;
-    w[2 * h + 1] = u.y;
-  }
-  return u32x4{w[0], w[1], w[2], w[3]};
-}
-
-template <int BM>
-__global__ __launch_bounds__((BM / 64) * 2 * 64, 1) void wgrad_glds_kernel(const WgParams p) {
-  constexpr int WM = BM / 64, NW = WM * 2, NT = NW * 64;
-  constexpr int AIMG = BM / 128;                 // dy images per stage
-  constexpr int IMG = 64 * 256;                  // one [64 px][128 ch] image
-  constexpr int STAGE = (AIMG + 1) * IMG;
-  constexpr int NSTAGE = 3;
-  constexpr int PIECES = STAGE / 1024;           // 1 KB glds pieces per stage
-  constexpr int GPS = PIECES / NW;               // per wave
-  static_assert(GPS * NW == PIECES, "stage partition");
-  __shared__ __attribute__((aligned(1024))) u32x4 lds[NSTAGE * STAGE / 16];
-
-  const int mtiles = p.M / BM, ntiles = p.N / 128;
-  const int nwg = mtiles * ntiles;
-  int bid, split;
-  split_tile(nwg, (p.P + p.pps - 1) / p.pps, p.group != 0, bid, split);
-  const int mt = bid / ntiles, nt = bid - mt * ntiles;
-  const int pbeg = split * p.pps;
-  const int pend = min(p.P, pbeg + p.pps);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const bf16* __restrict__ X = reinterpret_cast<const bf16*>(p.x);
-  const bf16* __restrict__ DY = reinterpret_cast<const bf16*>(p.dy);
-  const uint32_t lds0 = (uint32_t)(uintptr_t)lds;
-
-  // the tile's tap and channel block (C % 128 == 0: a 128-column tile lies in one tap)
-  const int kcol = nt * 128;
-  const int tap = kcol / p.Cin, c0 = kcol - tap * p.Cin;
-  const int tap_r = tap / p.S, tap_s = tap - tap_r * p.S;
-  const int HWo = p.Ho * p.Wo;
-
-  // per-lane pieces: image = piece / 16 (0..AIMG-1 dy halves, AIMG = x), rows 4*(piece%16) + lane/16
-  int pc_img[GPS], pc_row[GPS], pc_off[GPS], pc_dr[GPS], pc_dc[GPS];
-#pragma unroll
-  for (int i = 0; i < GPS; ++i) {
-    const int piece = wave + NW * i;
-    const int img = piece >> 4, row = 4 * (piece & 15) + (lane >> 4);
-    const int u = lane & 15;
-    pc_img[i] = img;
-    pc_row[i] = row;
-    pc_off[i] = (((u >> 1) ^ swz32g(row)) << 4) + (u & 1) * 8;  // channel offset inside the 128-block
-    if (p.Wo >= 64) { pc_dr[i] = 0; pc_dc[i] = row; } else { pc_dr[i] = row / p.Wo; pc_dc[i] = row - pc_dr[i] * p.Wo; }
-  }
-  const void* zero = (const void*)g_zero_page;
-
-  auto issue = [&](int kt, int stage) {
-    const int p0 = pbeg + kt * 64;
-    const int n0 = fdiv(p0, p.fd_hw), rem0 = p0 - n0 * HWo;
-    const int oh0 = fdiv(rem0, p.fd_w), ow0 = rem0 - oh0 * p.Wo;
-    const uint32_t base = lds0 + stage * STAGE;
-#pragma unroll
-    for (int i = 0; i < GPS; ++i) {
-      const uint32_t dst = base + (wave + NW * i) * 1024;
-      if (pc_img[i] < AIMG) {  // uniform per wave and i
-        glds16(DY + (size_t)(p0 + pc_row[i]) * p.M + mt * BM + pc_img[i] * 128 + pc_off[i], dst);
-      } else {
-        const int ih = (oh0 + pc_dr[i]) * p.stride - p.pad + tap_r;
-        const int iw = (ow0 + pc_dc[i]) * p.stride - p.pad + tap_s;
-        const bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-        glds16(ok ? (const void*)(X + ((size_t)(n0 * p.H + ih) * p.W + iw) * p.lda + c0 + pc_off[i]) : zero, dst);
-      }
-    }
-  };
-
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, pq = i16 & 3;
-  auto compute = [&](int stage) {
-    const char* L = reinterpret_cast<const char*>(lds) + stage * STAGE;
-    const char* Ai = L + (wm >> 1) * IMG;
-    const char* Bi = L + AIMG * IMG;
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      const int row0 = 32 * s2 + 8 * g + q;
-      u32x4 fa[4], fb[4];
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi) fa[mi] = trg(Ai, row0, (wm & 1) * 4 + mi, pq);
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) fb[ni] = trg(Bi, row0, wn * 4 + ni, pq);
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni) Mma<bf16>::run(acc[mi][ni], fa[mi], fb[ni]);
-    }
-  };
-
-  const int nk = pend > pbeg ? (pend - pbeg) / 64 : 0;
-  if (nk > 0) issue(0, 0);
-  if (nk > 1) issue(1, 1);
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) wait_vmcnt<GPS>(); else wait_vmcnt<0>();
-    raw_barrier();
-    if (kt + 2 < nk) issue(kt + 2, (kt + 2) % NSTAGE);
-    compute(kt % NSTAGE);
-  }
-
-  float* out = p.part + (size_t)split * p.M * p.N;
-#pragma unroll
-  for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      const int n = nt * 128 + wn * 64 + ni * 16 + i16;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = mt * BM + wm * 64 + mi * 16 + g * 4 + r;
-        out[(size_t)m * p.N + n] = acc[mi][ni][r];
-      }
-    }
-}
-
-template <int BM>
-static const char* wgg_name() {
-  static const std::string s = std::string("argus::wgrad_glds_kernel<") + std::to_string(BM) + ">";
-  return s.c_str();
-}
-
-// argus_conv_tuning key 16. Off by default since the single-buffer igemm change: swept at B=64 the
-// register-staged wgrad kernel is faster on every layer the glds one served (bench 7030 -> 7115 img/s).
-int g_wg_glds_enable = 0;
-int g_wg_glds_target = 512;   // key 17: split target (workgroups)
-
-bool wgrad_glds_plan(const argus_conv_desc& d, int dtype, bool pro, int* splits, int* pps) {
-  if (!g_wg_glds_enable || dtype != ARGUS_BF16 || pro || d.stem || d.c % 128 || d.k % 128) return false;
-  const int HWo = d.ho * d.wo;
-  const long P = (long)d.n * HWo;
-  if (HWo % 64 || !(d.wo % 64 == 0 || 64 % d.wo == 0) || P % 64) return false;
-  const int bm = d.k % 256 == 0 ? 256 : 128;
-  const long tiles = (long)(d.k / bm) * (d.r * d.s * d.c / 128);
-  long s = (g_wg_glds_target + tiles - 1) / tiles;
-  const long ksteps = P / 64;
-  const long maxs = (ksteps + 3) / 4;  // >= 4 k-steps per split
-  if (s > maxs) s = maxs;
-  if (s < 1) s = 1;
-  const long per = (ksteps + s - 1) / s;
-  *pps = (int)(per * 64);
-  *splits = (int)((ksteps + per - 1) / per);
-  return true;
-}
-
-bool wgrad_glds_launch(const argus_conv_desc& d, const WgParams& base, int splits, int pps, hipStream_t st) {
-  WgParams p = base;
-  p.pps = pps;
-  const int bm = d.k % 256 == 0 ? 256 : 128;
-  dim3 grid((p.M / bm) * (p.N / 128) * splits);
-  if (bm == 256) timed_launch(wgg_name<256>(), wgrad_glds_kernel<256>, grid, dim3(512), st, p);
-  else timed_launch(wgg_name<128>(), wgrad_glds_kernel<128>, grid, dim3(256), st, p);
   return true;
 }
 

@@ -16,9 +16,7 @@
 // LDS: two halo images (double-buffered over chunks, 448 positions x 128 B; slot j of position q holds
 // channel chunk j ^ swz8(q)) + a 3-stage ring of weight tiles, all filled by global_load_lds_dwordx4
 // (lane-linear 1 KB pieces, swizzle on the source address, zero page for halo positions outside the
-// image). With PRO (forward of conv2: the producer's BN + ReLU), the landed halo of each chunk is
-// transformed in place once (positions outside the image set to 0 = PyTorch's zero padding of the
-// post-ReLU tensor) before its nine taps run.
+// image). The input is the materialised BN + ReLU output of the producer (bf16 schedule: engine.py).
 #include "common.h"
 #include "igemm.h"
 #include "internal.h"
@@ -50,7 +48,7 @@ constexpr int kHaloPos1 = 416;  // single-buffer variant: 2 x (416 x 128 B + 3 x
 
 // HB = halo image buffers: 2 (double-buffered over 64-channel chunks) or 1 (Cin = 64: a single chunk,
 // nothing to prefetch; the 64-column tile then fits two workgroups per CU in LDS)
-template <int BN, bool PRO, int BW, int HB>
+template <int BN, int BW, int HB>
 __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_halo_kernel(const IgParams p) {
   constexpr int WN = BN / 64, NW = 4 * WN, NT = NW * 64;
   constexpr int HPOS = HB == 1 ? kHaloPos1 : kHaloPos;  // halo positions per image buffer
@@ -167,34 +165,6 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_h
     }
   };
 
-  // BN + ReLU of the producer, applied once per chunk to the landed halo image (in place). A thread
-  // transforms the positions it loaded (piece i: position q_i, validity h_ok[i]) for one fixed channel
-  // chunk (lane & 7, at LDS slot (lane & 7) ^ swz8(q)), so its 8 coefficients are loaded once per chunk
-  auto transform_halo = [&](int cc) {
-    char* Hl = reinterpret_cast<char*>(lds) + (HB == 2 ? (cc & 1) * HALO : 0);
-    const int c8 = lane & 7, ch = cc * 64 + c8 * 8;
-    float sc[8], sh[8];
-#pragma unroll
-    for (int j = 0; j < 8; j += 4) {
-      const f32x4 a = *reinterpret_cast<const f32x4*>(p.pro_scale + ch + j);
-      const f32x4 b = *reinterpret_cast<const f32x4*>(p.pro_shift + ch + j);
-      sc[j] = a.x; sc[j + 1] = a.y; sc[j + 2] = a.z; sc[j + 3] = a.w;
-      sh[j] = b.x; sh[j + 1] = b.y; sh[j + 2] = b.z; sh[j + 3] = b.w;
-    }
-#pragma unroll
-    for (int i = 0; i < HG; ++i) {
-      const int q = 8 * (i * NW + wave) + (lane >> 3);
-      u32x4* ptr = reinterpret_cast<u32x4*>(Hl + q * 128 + ((c8 ^ swz8(q)) << 4));
-      if (h_ok[i]) {  // inside the image (positions past npos / outside it stay 0: zero padding)
-        float f[8];
-        unpack(*ptr, f);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], sc[j], sh[j]), 0.f);
-        *ptr = pack(f);
-      }
-    }
-  };
-
   // ---- main loop over k-steps kt = chunk*9 + tap ----
   // issue order: H(0) B(0) B(1) | per step j: [H(chunk(j)+1) if tap(j)==0] [B(j+2)]
   // BN-backward epilogue operands (y, mask bits, y2) of this thread's output rows, loaded at the start
@@ -232,14 +202,6 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_h
           const int rr = tid / CPR_ + (NT / CPR_) * i;
           epi_load<bf16, BW>(p, (size_t)(mt * 256 + rr) * p.ldc + nt * BN + (tid % CPR_) * 8, pre[i]);
         }
-      }
-    }
-    if constexpr (PRO) {
-      // before issuing new glds: the coefficient loads' vmcnt wait then drains only B(kt+1)
-      if (t == 0) {
-        transform_halo(cc);
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's rewritten halo is in LDS
-        sbar();
       }
     }
     if (t == 0 && cc + 1 < nch) issue_halo(cc + 1);
@@ -290,11 +252,6 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_h
       }
     }
     __syncthreads();
-    if (p.fin.mode == 1) {  // before the output stores (see conv.hip)
-      bn_fin_arrive<NT, BN>(p.fin, mt, nt, reinterpret_cast<double2*>(lds),
-                            reinterpret_cast<int*>(reinterpret_cast<char*>(lds) + NT * 32));
-      __syncthreads();
-    }
   }
 
   // ---- epilogue: LDS-staged C tile, 16-byte coalesced (+addend) stores; output pixels are contiguous ----
@@ -336,17 +293,17 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_h
     __syncthreads();
     bwd.template reduce<BN, NT>(p.bb, reinterpret_cast<float2*>(lds), tid / CPR, RPP, c, (size_t)mt, p.N, nt * BN);
   }
-  if (p.fin.mode == 2) {  // LDS is free now: scratch [2 NT] double2, then the ticket flag
+  if (p.fin.mode) {  // LDS is free now: scratch [2 NT] double2, then the ticket flag
     __syncthreads();
     bn_fin_arrive<NT, BN>(p.fin, mt, nt, reinterpret_cast<double2*>(lds),
                           reinterpret_cast<int*>(reinterpret_cast<char*>(lds) + NT * 32));
   }
 }
 
-template <int BN, bool PRO, int BW, int HB>
+template <int BN, int BW, int HB>
 static const char* halo_name() {
   static const std::string s = std::string("argus::conv3x3_halo_kernel<") + std::to_string(BN) + ", " +
-                               bool_name(PRO) + ", " + std::to_string(BW) + (HB == 1 ? ", 1>" : ">");
+                               std::to_string(BW) + ", " + std::to_string(HB) + ">";
   return s.c_str();
 }
 
@@ -355,40 +312,36 @@ static const char* halo_name() {
 // 128-column one measured 83 -> 100 us, the step within noise), 0 = off
 int g_halo_epi_prefetch = 1;
 
-template <int BN, bool PRO, int BW, int HB>
+template <int BN, int BW, int HB>
 static void launch_halo2(const IgParams& p0, hipStream_t st) {
   IgParams p = p0;
   p.epi_pre = g_halo_epi_prefetch == 2 || (g_halo_epi_prefetch == 1 && HB == 1);
   plan_fin(p, 256);
   dim3 grid((p.ph[0].M / 256) * (p.N / BN));
-  timed_launch(halo_name<BN, PRO, BW, HB>(), conv3x3_halo_kernel<BN, PRO, BW, HB>, grid, dim3(4 * (BN / 64) * 64),
+  timed_launch(halo_name<BN, BW, HB>(), conv3x3_halo_kernel<BN, BW, HB>, grid, dim3(4 * (BN / 64) * 64),
                st, p);
 }
 
-template <int BN, bool PRO, int BW>
+template <int BN, int BW>
 static void launch_halo1(const IgParams& p, hipStream_t st) {
   if constexpr (BN == 64) {
     const int HWi = p.H * p.W;
     const int npos = HWi >= 256 ? (256 / p.W + 2) * (p.W + 2) : (256 / HWi) * (p.H + 2) * (p.W + 2);
     if (p.Cin == 64 && npos <= kHaloPos1) {  // one channel chunk: one halo buffer, two workgroups per CU
-      launch_halo2<BN, PRO, BW, 1>(p, st);
+      launch_halo2<BN, BW, 1>(p, st);
       return;
     }
   }
-  launch_halo2<BN, PRO, BW, 2>(p, st);
+  launch_halo2<BN, BW, 2>(p, st);
 }
 
-template <int BN, bool PRO>
+template <int BN>
 static void launch_halo(const IgParams& p, hipStream_t st) {
-  if constexpr (PRO) {
-    launch_halo1<BN, true, 0>(p, st);  // forward (prologue) never carries the backward epilogue
-  } else {
-    switch (bwd_variant(p.bb)) {
-      case 2: launch_halo1<BN, false, 2>(p, st); break;
-      case 3: launch_halo1<BN, false, 3>(p, st); break;
-      case 4: launch_halo1<BN, false, 4>(p, st); break;
-      default: launch_halo1<BN, false, 0>(p, st);
-    }
+  switch (bwd_variant(p.bb)) {
+    case 2: launch_halo1<BN, 2>(p, st); break;
+    case 3: launch_halo1<BN, 3>(p, st); break;
+    case 4: launch_halo1<BN, 4>(p, st); break;
+    default: launch_halo1<BN, 0>(p, st);
   }
 }
 
@@ -401,7 +354,9 @@ int g_halo64 = 1;
 
 // 3x3 / stride 1 / pad 1, same input and output grid, one phase, whole-row / whole-image 256-pixel tiles
 int conv3x3_halo_ok(const IgParams& p) {
-  if (!g_halo_enable || p.stem || p.nphase != 1 || p.ish != 1 || p.isw != 1 || p.osh != 1 || p.osw != 1) return 0;
+  if (!g_halo_enable || p.stem || p.pro_scale || p.nphase != 1 || p.ish != 1 || p.isw != 1 || p.osh != 1 ||
+      p.osw != 1)
+    return 0;
   const IgPhase& ph = p.ph[0];
   if (ph.K != 9 * p.Cin || p.Cin % 64 || p.lda % 8 || p.ldb % 8 || p.H != p.Ho || p.W != p.Wo) return 0;
   for (int t = 0; t < 9; ++t)
@@ -428,18 +383,15 @@ int conv3x3_halo_ok(const IgParams& p) {
 
 bool conv3x3_halo_launch(const IgParams& p, hipStream_t st) {
   const int bn = conv3x3_halo_ok(p);
-  if (bn == 128) {
-    if (p.pro_scale) launch_halo<128, true>(p, st); else launch_halo<128, false>(p, st);
-  } else if (bn == 64) {
-    if (p.pro_scale) launch_halo<64, true>(p, st); else launch_halo<64, false>(p, st);
-  }
+  if (bn == 128) launch_halo<128>(p, st);
+  else if (bn == 64) launch_halo<64>(p, st);
   return bn != 0;
 }
 
 
 // ================================================================================================
 // 3x3 stride-1 weight gradient with the input halo tile in LDS (dW[k][tap][c] = sum_p dy[p][k] *
-// x'[p + off(tap)][c], x' = relu(x*scale+shift) with PRO). A workgroup (8 waves, 2 x 4) owns 64
+// x[p + off(tap)][c]). A workgroup (8 waves, 2 x 4) owns 64
 // output channels x 9 taps x 64 input channels (a 64 x 576 tile; wave (wm, wn) holds rows 32wm..+31
 // and the 9 column blocks of 16 at 9wn..9wn+8) and reduces over a range of 128-pixel tiles (whole
 // rows of one image, or whole images when H*W < 128). Per tile it glds-loads dy [128 px][64 k] and
@@ -452,8 +404,6 @@ bool conv3x3_halo_launch(const IgParams& p, hipStream_t st) {
 struct WgHaloParams {
   const bf16* x;
   const bf16* dy;
-  const float* pro_scale;
-  const float* pro_shift;
   float* part;
   int n, H, W, C, K;
   int ptiles, tps;  // 128-pixel tiles in total, tiles per split
@@ -475,7 +425,6 @@ ARGUS_DEV u32x4 tr_frag(const char* img, int r_lo, int r_hi, int slot, int half8
   return u32x4{u0.x, u0.y, u1.x, u1.y};
 }
 
-template <bool PRO>
 __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(const WgHaloParams p) {
   constexpr int DYB = 128 * 128;                // dy image bytes
   constexpr int HXB = kWgHaloPos * 128;         // halo image bytes
@@ -499,14 +448,6 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(const WgHaloParam
   if (HWi >= 128) { NI = 1; R = 128 / W; } else { NI = 128 / HWi; R = H; }
   const int HWD = W + 2, IMGP = (R + 2) * HWD, npos = NI * IMGP;
 
-  float psc[PRO ? 8 : 1], psh[PRO ? 8 : 1];  // BN+ReLU coefficients of this thread's channel chunk
-  if constexpr (PRO) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      psc[j] = p.pro_scale[ct * 64 + (lane & 7) * 8 + j];
-      psh[j] = p.pro_shift[ct * 64 + (lane & 7) * 8 + j];
-    }
-  }
 
   // fragment geometry: pixel 32*s2 + 8g + 4h + q of the tile -> halo row at tap (0,0)
   const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, pp = i16 & 3;
@@ -567,31 +508,6 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(const WgHaloParam
     sbar();
     const char* DYI = reinterpret_cast<const char*>(lds) + stage * STG;
     const char* HXI = DYI + DYB;
-    if constexpr (PRO) {
-      // the positions this thread loaded (pieces 2..6), one fixed channel chunk (lane & 7, at slot
-      // (lane & 7) ^ wsw(q)) whose coefficients sit in registers; outside the image stays 0
-      int r0 = 0;
-      if (HWi >= 128) {
-        const int img0 = (tile * 128) / HWi;
-        r0 = (tile * 128 - img0 * HWi) / W;
-      }
-      char* Hl = reinterpret_cast<char*>(lds) + stage * STG + DYB;
-#pragma unroll
-      for (int i = 2; i < GPW; ++i) {
-        const int qq = 8 * (wave + 8 * (i - 2)) + (lane >> 3);
-        const int ih = r0 + pos_hr[i - 2] - 1, iw = pos_hc[i - 2] - 1;
-        if (pos_in[i - 2] && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) {
-          u32x4* ptr = reinterpret_cast<u32x4*>(Hl + qq * 128 + (((lane & 7) ^ wsw(qq)) << 4));
-          float f[8];
-          unpack(*ptr, f);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], psc[j], psh[j]), 0.f);
-          *ptr = pack(f);
-        }
-      }
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-      sbar();
-    }
 #pragma unroll 1
     for (int s2 = 0; s2 < 4; ++s2) {
       const int rlo = 32 * s2 + 8 * g + q;
@@ -627,11 +543,6 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(const WgHaloParam
   }
 }
 
-template <bool PRO>
-static const char* wg_halo_name() {
-  static const std::string s = std::string("argus::wgrad3x3_halo_kernel<") + bool_name(PRO) + ">";
-  return s.c_str();
-}
 
 int g_wg_halo_enable = 1;          // argus_conv_tuning key 11
 // key 12: split target of the 3x3 halo wgrad. 512 -> 256 once it runs on the side stream beside the
@@ -672,20 +583,17 @@ bool wgrad3x3_halo_plan(const argus_conv_desc& d, int dtype, int* splits, int* t
 bool wgrad3x3_halo_launch(const argus_conv_desc& d, int dtype, const void* x, const float* sc, const float* sh,
                           const void* dy, void* ws, size_t ws_bytes, int* splits_out, hipStream_t st) {
   int splits, tps;
-  if (!wgrad3x3_halo_plan(d, dtype, &splits, &tps)) return false;
+  if (sc || sh || !wgrad3x3_halo_plan(d, dtype, &splits, &tps)) return false;  // inputs are materialised
   if (ws_bytes < (size_t)splits * d.k * 9 * d.c * sizeof(float)) return false;
   WgHaloParams p;
   p.x = reinterpret_cast<const bf16*>(x);
   p.dy = reinterpret_cast<const bf16*>(dy);
-  p.pro_scale = sc;
-  p.pro_shift = sh;
   p.part = reinterpret_cast<float*>(ws);
   p.n = d.n; p.H = d.h; p.W = d.w; p.C = d.c; p.K = d.k;
   p.ptiles = d.n * d.h * d.w / 128;
   p.tps = tps;
   dim3 grid((d.k / 64) * (d.c / 64) * splits);
-  if (sc) timed_launch(wg_halo_name<true>(), wgrad3x3_halo_kernel<true>, grid, dim3(512), st, p);
-  else timed_launch(wg_halo_name<false>(), wgrad3x3_halo_kernel<false>, grid, dim3(512), st, p);
+  timed_launch("argus::wgrad3x3_halo_kernel", wgrad3x3_halo_kernel, grid, dim3(512), st, p);
   *splits_out = splits;
   return true;
 }

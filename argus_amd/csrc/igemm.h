@@ -61,7 +61,6 @@ struct IgParams {
   BnBwdEpi bb;    // dgrad only
   BnFin fin;      // BN finalize folded into this launch (fin.mode != 0)
   BnApplyPro ap;  // dgrad only: the A operand is dm (ap.y != nullptr)
-  void* pro_out;  // forward, 1x1 stride 1 with PRO: column tile 0 stores relu(x*scale+shift) (= the staged A)
   int f8;         // ARGUS_FP8: MX-fp8 operands where the shape allows (host dispatch only)
   int epi_pre;    // halo dgrad: prefetch the BN-backward epilogue operands under the last chunk (key 32)
 };
@@ -236,17 +235,11 @@ ARGUS_DEV u32x4 epi_apply(const IgParams& p, u32x4 v, const EpiIn& in, BwdEpiAcc
   return v;
 }
 
-// host: group plan of a folded BN finalize for a launch whose row tile is tile_m pixels
-inline void plan_fin(IgParams& p, int tile_m) {
+// host: group plan of a folded BN-backward finalize (one partial row per (phase, row tile))
+inline void plan_fin(IgParams& p, int) {
   if (!p.fin.mode) return;
-  if (p.fin.mode == 1) {  // forward: one phase; partial rows of stat_tile pixels
-    const int M = p.ph[0].M;
-    bn_fin_plan(p.fin, (M + tile_m - 1) / tile_m, tile_m / p.stat_tile);
-    p.fin.rows = (M + p.stat_tile - 1) / p.stat_tile;
-  } else {  // backward: one partial row per (phase, row tile)
-    bn_fin_plan(p.fin, p.nphase * p.bb.prow, 1);
-    p.fin.rows = p.fin.T;
-  }
+  bn_fin_plan(p.fin, p.nphase * p.bb.prow, 1);
+  p.fin.rows = p.fin.T;
 }
 
 // host: the epilogue variant of a BnBwdEpi (0 when off)
@@ -281,9 +274,6 @@ int conv3x3_halo_ok(const IgParams& p);
 bool conv3x3_halo_launch(const IgParams& p, hipStream_t st);
 // 3x3 stride-1 weight gradient with an LDS-resident halo tile (conv_halo.hip): plan / launch of the
 // split partials (fp32 [splits][K][9C]); false = not served
-// bf16 weight gradient on global->LDS staged operands (conv_glds.hip): plan / launch; false = not served
-bool wgrad_glds_plan(const argus_conv_desc& d, int dtype, bool pro, int* splits, int* pps);
-bool wgrad_glds_launch(const argus_conv_desc& d, const WgParams& base, int splits, int pps, hipStream_t st);
 bool wgrad3x3_halo_plan(const argus_conv_desc& d, int dtype, int* splits, int* tiles_per_split);
 bool wgrad3x3_halo_launch(const argus_conv_desc& d, int dtype, const void* x, const float* sc, const float* sh,
                           const void* dy, void* ws, size_t ws_bytes, int* splits, hipStream_t st);

@@ -15,8 +15,6 @@ int check_launch(const char* what);
 int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, void* y,
              const float* sc, const float* sh, float* stats, hipStream_t st);
 int conv_fwd_stat_rows(const argus_conv_desc& d, int dtype);
-int conv_fwd_bn(const argus_conv_desc& d, int dtype, const void* x, const void* w, void* y, const float* sc,
-                const float* sh, const argus_bn_fwd_fin& fin, hipStream_t st);
 // BN workspace layout (bn.hip): [0, kBnCounterBytes) ticket counters, then double2 group results
 constexpr size_t kBnCounterBytes = 16384;
 int conv_fwd_stat_tile(const argus_conv_desc& d, int dtype);
@@ -30,10 +28,6 @@ int conv_weight_prep_batch(int dtype, int count, const void* device_table, int n
 int conv_dgrad(const argus_conv_desc& d, int dtype, const void* dy, const void* wt, void* dx,
                const void* addend, const uint8_t* addend_mask, hipStream_t st);
 int conv_dgrad_bn_rows(const argus_conv_desc& d, int dtype);
-int conv_fwd_halo(const argus_conv_desc& d, int dtype);
-int conv_fwd_stores_input(const argus_conv_desc& d, int dtype);
-int conv_fwd_store_input(const argus_conv_desc& d, int dtype, const void* x, const void* w, void* y, const float* sc,
-                         const float* sh, float* stats, void* x_out, hipStream_t st);
 int conv_dgrad_stages_prologue(const argus_conv_desc& d, int dtype);
 int conv_dgrad_bn(const argus_conv_desc& d, int dtype, const void* dy, const void* wt, void* dm,
                   const void* addend, const argus_bn_bwd_epilogue* bn, const argus_bn_bwd_prologue* pro,

@@ -26,6 +26,8 @@ struct Agg {
 std::mutex g_mu;
 std::atomic<bool> g_on{false};
 std::string g_filter;
+hipStream_t g_stream = nullptr;  // only launches on this stream (nullptr: any)
+bool g_any_stream = true;
 std::vector<Rec> g_recs;
 std::vector<hipEvent_t> g_pool;  // free events
 std::vector<std::pair<std::string, Agg>> g_aggs;
@@ -49,9 +51,10 @@ void recycle_all() {
 }
 }  // namespace
 
-bool ktimer_wants(const char* name) {
+bool ktimer_wants(const char* name, hipStream_t st) {
   if (!g_on.load(std::memory_order_relaxed)) return false;
   std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_any_stream && st != g_stream) return false;
   return g_filter.empty() || std::strncmp(name, g_filter.c_str(), g_filter.size()) == 0;
 }
 
@@ -74,8 +77,17 @@ int argus_ktimer_enable(const char* filter) {
   recycle_all();
   g_aggs.clear();
   g_filter = filter ? filter : "";
+  g_any_stream = true;
   g_on = true;
   return ARGUS_OK;
+}
+
+int argus_ktimer_enable_on(const char* filter, argus_stream_t stream) {
+  const int rc = argus_ktimer_enable(filter);
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_stream = (hipStream_t)stream;
+  g_any_stream = false;
+  return rc;
 }
 
 int argus_ktimer_disable(void) {

@@ -13,7 +13,7 @@
 
 namespace argus {
 
-bool ktimer_wants(const char* name);
+bool ktimer_wants(const char* name, hipStream_t st);
 // Returns the (start, stop) events for one timed launch of `name` doing `work` flops and moving
 // `bytes` algorithmic HBM bytes.
 void ktimer_slot(const char* name, double work, double bytes, hipEvent_t* start, hipEvent_t* stop);
@@ -22,7 +22,7 @@ extern thread_local double g_launch_work, g_launch_bytes;
 
 template <typename K, typename... Args>
 inline void timed_launch(const char* name, K kernel, dim3 grid, dim3 block, hipStream_t st, Args... args) {
-  if (ktimer_wants(name)) {
+  if (ktimer_wants(name, st)) {
     hipEvent_t a, b;
     ktimer_slot(name, g_launch_work, g_launch_bytes, &a, &b);
     hipExtLaunchKernelGGL(kernel, grid, block, 0, st, a, b, 0, args...);

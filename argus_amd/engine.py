@@ -28,7 +28,7 @@ from dataclasses import dataclass
 
 import torch
 
-from argus_amd._lib import BF16, F32, FP8, BnBwdEpilogue, BnBwdPrologue, BnFwdFin, ConvDesc, lib, ptr, stream
+from argus_amd._lib import BF16, F32, FP8, BnBwdEpilogue, BnBwdPrologue, ConvDesc, lib, ptr, stream
 
 
 @dataclass(frozen=True)
@@ -88,18 +88,6 @@ class ResNetEngine:
         # kernels; fp32 (parity path) keeps the fused prologue. ARGUS_MATERIALIZE=0/1 overrides.
         env = os.environ.get("ARGUS_MATERIALIZE")
         self.materialize = low if env is None else env == "1"
-        # ... except a1 where conv2's forward runs on the LDS-halo kernel (argus_conv_fwd_halo): that kernel
-        # applies bn1+ReLU once per landed halo element, and conv2's weight gradient applies it the same
-        # way (halo wgrad) or while staging (register-staged wgrad). ARGUS_A1_PRO=1 turns this on; measured
-        # slower at B=64 (8200 vs 8290 img/s: the prologue halo forward loses its load/compute overlap at
-        # each chunk start), so every a1 is materialised by default.
-        self.a1_pro = self.materialize and os.environ.get("ARGUS_A1_PRO", "0") == "1"
-        # a2 = relu(bn2(y2)) is written by conv3's own forward launch (argus_conv_fwd_store_input: the
-        # 1x1 kernel stages bn2 + ReLU in registers and its column-tile-0 workgroups store what they
-        # staged) instead of a separate bn_apply pass. ARGUS_A2_STORE=1 turns it on; measured neutral at
-        # B=64 (8294-8308 vs 8330 img/s: the pass saved, 0.29 ms, is what the slower store inside the
-        # write-heavy 1x1 kernel costs), so the pass is kept by default
-        self.a2_store = self.materialize and os.environ.get("ARGUS_A2_STORE", "0") == "1"
         self.device = torch.device(device)
         self.blocks = resnet50_blocks()
         self.shape = None
@@ -111,9 +99,6 @@ class ResNetEngine:
         # side stream after both streams' work (on_ready's comm) and backward() joins it at its end.
         # ARGUS_WGRAD_STREAM=0 keeps everything on the caller's stream.
         self.wgrad_overlap = os.environ.get("ARGUS_WGRAD_STREAM", "1") != "0"
-        # BN finalize (forward statistics and backward coefficients) folded into the producing conv
-        # launch (argus_conv_fwd_bn / argus_conv_dgrad_bn with a workspace); ARGUS_FOLD_FIN=0 keeps the
-        # separate finalize kernels (A/B measurements, tests)
         # BN-backward apply (dy = ca*dm + cb*y + cc) staged by the consuming dgrad, which also stores dy for
         # the weight gradient (argus_conv_dgrad_bn with a prologue); ARGUS_FUSE_APPLY=0 runs the apply pass
         self.fuse_apply = os.environ.get("ARGUS_FUSE_APPLY", "1") != "0"
@@ -122,9 +107,11 @@ class ResNetEngine:
         # stages the same apply from dm and y (argus_conv_wgrad_apply). Moves the dy write off the main
         # stream (one more read on the side stream). ARGUS_WGRAD_APPLY=0 stores dy as before.
         self.wgrad_apply = os.environ.get("ARGUS_WGRAD_APPLY", "1") != "0"
-        fold = os.environ.get("ARGUS_FOLD_FIN", "bwd")  # A/B at B=64: fwd fold neutral, bwd +0.3 %
-        self.fold_fin_fwd = fold in ("1", "fwd")
-        self.fold_fin = fold in ("1", "bwd")  # backward
+        # BN-backward finalize (dgamma, dbeta, ca / cb / cc) folded into the dgrad launch that produces
+        # its partial sums (argus_conv_dgrad_bn with a workspace; +0.3 % at B=64); ARGUS_FOLD_FIN=0 runs
+        # the separate bwd_finalize kernels (A/B measurements). The forward statistics keep their own
+        # finalize launch (folding it into the conv measured neutral).
+        self.fold_fin = os.environ.get("ARGUS_FOLD_FIN", "1") != "0"
         self._side: torch.cuda.Stream | None = None
         self._pending: dict = {}  # buffer data_ptr -> (seq, event) of the last side-stream wgrad reading it
         self._last_side = None
@@ -135,11 +122,6 @@ class ResNetEngine:
         # ARGUS_SIDE_BATCH=0 issues every weight gradient as soon as its dy is ready.
         self.side_batch = os.environ.get("ARGUS_SIDE_BATCH", "1") != "0"
         self._deferred: list = []  # (cv, fn, buffer data_ptrs)
-        # ... except in the last ARGUS_EAGER_BLOCKS blocks of the backward (layer 1's, the largest weight
-        # gradients): their weight gradients are issued as soon as their dy is ready, so they overlap the
-        # block's remaining dgrads instead of forming the step's tail after the last dgrad
-        self.eager_blocks = int(os.environ.get("ARGUS_EAGER_BLOCKS", "0"))
-        self._eager = False
         self._side_seq = 0
         self._waited_seq = 0
         # the stem weight gradient (main stream, its own split workspace) is issued before the final
@@ -192,8 +174,6 @@ class ResNetEngine:
         for b in self.blocks:
             add(b.prefix + ".conv1", N, h, w, b.cin, b.width, 1, 1, 0)
             ho, wo = add(b.prefix + ".conv2", N, h, w, b.width, b.width, 3, b.stride, 1)
-            a1_pro = self.a1_pro and bool(L.dll.argus_conv_fwd_halo(C.byref(convs[b.prefix + ".conv2"].desc),
-                                                                   self.cdt))
             add(b.prefix + ".conv3", N, ho, wo, b.width, b.cout, 1, 1, 0)
             if b.has_ds:
                 add(b.prefix + ".downsample.0", N, h, w, b.cin, b.cout, 1, b.stride, 0)
@@ -202,8 +182,7 @@ class ResNetEngine:
                 "y1": self._t(N, h, w, b.width), "y2": self._t(N, ho, wo, b.width),
                 "y3": self._t(N, ho, wo, b.cout), "out": self._t(N, ho, wo, b.cout),
                 "yd": self._t(N, ho, wo, b.cout) if b.has_ds else None,
-                "a1": self._t(N, h, w, b.width) if self.materialize and not a1_pro else None,
-                "a1_pro": a1_pro,  # conv2 forward / weight gradient apply bn1 + ReLU themselves
+                "a1": self._t(N, h, w, b.width) if self.materialize else None,
                 "a2": self._t(N, ho, wo, b.width) if self.materialize else None,
                 # ReLU mask of `out`, one byte per 16-byte chunk (argus_bn_apply mask_out)
                 "bits": torch.empty(N * ho * wo * b.cout // self.E, dtype=torch.uint8, device=self.device),
@@ -258,9 +237,7 @@ class ResNetEngine:
         self.wg_ws_stem = torch.empty(wss, dtype=torch.uint8, device=self.device)
         self.stages_pro = {n: bool(L.dll.argus_conv_dgrad_stages_prologue(C.byref(cv.desc), self.cdt))
                            for n, cv in convs.items() if not cv.desc.stem}
-        self.stores_input = {n: bool(L.dll.argus_conv_fwd_stores_input(C.byref(cv.desc), self.cdt))
-                             for n, cv in convs.items()}
-        self.gbuf = [self._t(max_elems) for _ in range(4)]  # dh / dx ping-pong, dz ping-pong
+        self.gbuf = [self._t(max_elems) for _ in range(3)]  # avgpool dh; dza / dzb (the dz of bn2 / bn1)
         # dy operands of the side-stream weight gradients come from a ring, so the main stream can
         # run ahead of the wgrad stream by several layers before it must wait to reuse a buffer
         # (ARGUS_DY_RING buffers; a reuse waits on the event of the wgrad that last read it)
@@ -303,31 +280,13 @@ class ResNetEngine:
                               ptr(Bf[name + ".running_mean"]), ptr(Bf[name + ".running_var"]),
                               C.c_float(Bf.get(name + ".eps", 1e-5)), ptr(st[2]), ptr(st[3]), stream())
 
-    def _conv_bn(self, P, Bf, conv, bn, x, y, pro, training, part=None, ws=None, x_out=None):
+    def _conv_bn(self, P, Bf, conv, bn, x, y, pro, training, part=None, ws=None):
         cv = self.convs[conv]
         sc = sh = None
         if pro is not None:
             sc, sh = self.bn_state[pro][2], self.bn_state[pro][3]
         part = self.stat_part if part is None else part
         ws = self.bn_ws if ws is None else ws
-        if x_out is not None:  # the forward also stores its staged relu(bn(x)) (argus_conv_fwd_store_input)
-            self._launch(cv, 0, lambda: self.L.conv_fwd_store_input(C.byref(cv.desc), self.cdt, ptr(x), ptr(cv.wf),
-                                                                     ptr(y), ptr(sc), ptr(sh),
-                                                                     ptr(part) if training else None, ptr(x_out),
-                                                                     stream()))
-            if training:
-                self._bn_train(P, Bf, bn, cv.stat_rows, cv.stat_tile, cv.desc.n * cv.desc.ho * cv.desc.wo, part, ws)
-            else:
-                self._bn_eval(P, Bf, bn)
-            return
-        if training and self.fold_fin_fwd:  # BN statistics finalize folded into the conv launch
-            st = self.bn_state[bn]
-            f = BnFwdFin(ptr(part), ptr(P[bn + ".weight"]), ptr(P[bn + ".bias"]), Bf.get(bn + ".eps", 1e-5),
-                         Bf.get(bn + ".momentum", 0.1), ptr(Bf[bn + ".running_mean"]), ptr(Bf[bn + ".running_var"]),
-                         ptr(Bf[bn + ".num_batches_tracked"]), ptr(st[0]), ptr(st[1]), ptr(st[2]), ptr(st[3]), ptr(ws))
-            self._launch(cv, 0, lambda: self.L.conv_fwd_bn(C.byref(cv.desc), self.cdt, ptr(x), ptr(cv.wf), ptr(y),
-                                                            ptr(sc), ptr(sh), C.byref(f), stream()))
-            return
         self._launch(cv, 0, lambda: self.L.conv_fwd(C.byref(cv.desc), self.cdt, ptr(x), ptr(cv.wf), ptr(y), ptr(sc),
                                                      ptr(sh), ptr(part) if training else None, stream()))
         if training:
@@ -401,17 +360,10 @@ class ResNetEngine:
                                                               self.bn_ws_ds))
             self._conv_bn(P, Bf, pf + ".conv1", pf + ".bn1", h, a["y1"], None, training)
             if self.materialize:
-                if a["a1_pro"]:
-                    self._conv_bn(P, Bf, pf + ".conv2", pf + ".bn2", a["y1"], a["y2"], pf + ".bn1", training)
-                else:
-                    self._act(pf + ".bn1", a["y1"], a["a1"], N * a["hw_in"][0] * a["hw_in"][1], b.width)
-                    self._conv_bn(P, Bf, pf + ".conv2", pf + ".bn2", a["a1"], a["y2"], None, training)
-                if self.a2_store and self.stores_input[pf + ".conv3"]:
-                    self._conv_bn(P, Bf, pf + ".conv3", pf + ".bn3", a["y2"], a["y3"], pf + ".bn2", training,
-                                  x_out=a["a2"])
-                else:
-                    self._act(pf + ".bn2", a["y2"], a["a2"], N * a["hw"][0] * a["hw"][1], b.width)
-                    self._conv_bn(P, Bf, pf + ".conv3", pf + ".bn3", a["a2"], a["y3"], None, training)
+                self._act(pf + ".bn1", a["y1"], a["a1"], N * a["hw_in"][0] * a["hw_in"][1], b.width)
+                self._conv_bn(P, Bf, pf + ".conv2", pf + ".bn2", a["a1"], a["y2"], None, training)
+                self._act(pf + ".bn2", a["y2"], a["a2"], N * a["hw"][0] * a["hw"][1], b.width)
+                self._conv_bn(P, Bf, pf + ".conv3", pf + ".bn3", a["a2"], a["y3"], None, training)
             else:
                 self._conv_bn(P, Bf, pf + ".conv2", pf + ".bn2", a["y1"], a["y2"], pf + ".bn1", training)
                 self._conv_bn(P, Bf, pf + ".conv3", pf + ".bn3", a["y2"], a["y3"], pf + ".bn2", training)
@@ -513,7 +465,6 @@ class ResNetEngine:
         for idx in range(nb - 1, -1, -1):
             b, a = self.blocks[idx], self.act[idx]
             pf = b.prefix
-            self._eager = idx < self.eager_blocks
             h_in = self.act[idx - 1]["out"] if idx > 0 else self.p0
             hi, wi = a["hw_in"]
             ho, wo = a["hw"]
@@ -534,7 +485,7 @@ class ResNetEngine:
 
             cap("b_dout", dh, px_o * b.cout, (N, ho, wo, b.cout))
             fuse = self.fuse_apply
-            dza, dzb = g[2], g[3]
+            dza, dzb = g[1], g[2]
             # bn3 (+ downsample BN) backward
             if rows3 is None:  # last block: mask + reduce pass over the pooled gradient
                 L.bn_bwd_reduce(dt, px_o, b.cout, ptr(dh), 3, ptr(a["bits"]), ptr(a["y3"]), None, None,
@@ -589,7 +540,7 @@ class ResNetEngine:
             cap("b_dy2", dy2, px_o * b.width, (N, ho, wo, b.width))
             cap("b_dz1", dzb, px_i * b.width, (N, hi, wi, b.width))
             s1 = self.bn_state[pf + ".bn1"]
-            if self.materialize and not a["a1_pro"]:
+            if self.materialize:
                 self._wgrad(pf + ".conv2", a["a1"], None, dy2, G)
             else:
                 self._wgrad(pf + ".conv2", a["y1"], s1, dy2, G)
@@ -638,10 +589,9 @@ class ResNetEngine:
             if self.debug is not None:
                 n_in = N * hi * wi * b.cin
                 self.debug["bwd." + pf] = dh[:n_in].view(N, hi, wi, b.cin).clone()
-        self._eager = False
         # stem: maxpool -> relu/bn1 -> conv1 wgrad
         H1, W1 = self.stem_hw
-        dz0, dy0 = g[2], self._next_dy()
+        dz0, dy0 = g[1], self._next_dy()
         if self.fuse_apply:
             # maxpool backward + the stem BN's backward reduction in one pass (stores dm0), finalize, then
             # the stem weight gradient stages dy0 = ca*dm0 + cb*y0 + cc itself (dy0 is never written)
@@ -782,7 +732,7 @@ class ResNetEngine:
         """Weight gradient ``fn`` (reading ``buf``) on the side stream: now, or deferred to the block's
         _flush_side (side_batch)."""
         self._deferred.append((cv, fn, buf.data_ptr()))
-        if not self.side_batch or self._eager:
+        if not self.side_batch:
             self._flush_side()
 
     def _flush_side(self) -> None:

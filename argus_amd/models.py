@@ -92,7 +92,7 @@ class _NetFn(torch.autograd.Function):
         if engine.fwd_id != ctx.fwd_id:
             raise RuntimeError("argus_amd: another forward ran before this backward; the engine keeps one "
                                "set of saved activations per model")
-        P, _ = model._maps()
+        P, _ = model._maps(forward=False)
         G = {}
         for name, p in model.named_parameters():
             if name.endswith(".weight") and p.dim() == 4:
@@ -159,16 +159,32 @@ class NCameraCNN(nn.Module):
             self._engines[key] = eng
         return eng
 
-    def _maps(self):
+    def _maps(self, forward: bool = True):
+        """name -> parameter, name -> buffer (+ per-BN ".eps" / ".momentum"). ``forward``: the maps of a
+        forward about to run (a train-mode one advances the momentum=None shadow counts below)."""
         P = dict(self.named_parameters())
         Bf = dict(self.named_buffers())
         cma = [(name, m) for name, m in self.named_modules() if isinstance(m, nn.BatchNorm2d) and m.momentum is None]
         # momentum=None is torch's cumulative moving average: factor 1 / num_batches_tracked after the
-        # increment. The counters live on the device: one host read per forward, only in that mode.
+        # increment. The counters live on the device and the finalize kernels increment them; the host
+        # keeps a shadow count per layer (one read when a counter was last written by torch, e.g. by
+        # load_state_dict, detected through the tensor's version counter), so a training step does not
+        # synchronise with the device to know it.
         counts = {}
         if cma and self.training:
-            nbt = torch.stack([m.num_batches_tracked for _, m in cma]).cpu().tolist()
-            counts = {name: n for (name, _), n in zip(cma, nbt)}
+            shadow = self.__dict__.setdefault("_nbt_shadow", {})
+            stale = [(name, m) for name, m in cma
+                     if shadow.get(name, (None,))[0] != (m.num_batches_tracked.data_ptr(),
+                                                         m.num_batches_tracked._version)]
+            if stale:
+                vals = torch.stack([m.num_batches_tracked for _, m in stale]).cpu().tolist()
+                for (name, m), v in zip(stale, vals):
+                    shadow[name] = ((m.num_batches_tracked.data_ptr(), m.num_batches_tracked._version), int(v))
+            for name, m in cma:
+                key, n = shadow[name]
+                counts[name] = n
+                if forward:
+                    shadow[name] = (key, n + 1)  # the forward's finalize increments the device counter
         for name, m in self.named_modules():
             if isinstance(m, nn.BatchNorm2d):
                 Bf[name + ".eps"] = m.eps

@@ -11,11 +11,18 @@ from argus_amd._lib import lib
 class KernelTimer:
     """``with KernelTimer(prefix) as t: ...; t.summary()`` -> per-instantiation timing of conv and BN kernels."""
 
-    def __init__(self, prefix: str | None = None):
+    def __init__(self, prefix: str | None = None, stream: int | None = None):
+        """``stream``: only launches on that HIP stream handle (e.g. the main stream's
+        ``torch.cuda.current_stream().cuda_stream``); None = every stream."""
         self.prefix = prefix
+        self.stream = stream
 
     def start(self) -> None:
-        lib().ktimer_enable(self.prefix.encode() if self.prefix else None)
+        f = self.prefix.encode() if self.prefix else None
+        if self.stream is None:
+            lib().ktimer_enable(f)
+        else:
+            lib().ktimer_enable_on(f, self.stream)
 
     def stop(self) -> None:
         lib().ktimer_disable()

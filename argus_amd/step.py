@@ -66,10 +66,13 @@ class FlatParams:
 class GradBucketer:
     """Bucketed async SUM all-reduce of a flat gradient buffer, driven by suffix-ready callbacks."""
 
-    def __init__(self, grad: torch.Tensor, offsets: dict, group=None, bucket_mb: float = 25.0):
+    def __init__(self, grad: torch.Tensor, offsets: dict, group=None, bucket_mb: float = 25.0, op=None):
         self.grad = grad
         self.offsets = offsets
         self.group = group
+        # SUM (DDP's all-reduce; the 1/world of its average is folded into the Adam kernel). Tests pass
+        # a PREMUL_SUM to make a one-rank RCCL all-reduce change the values it reduces.
+        self.op = dist.ReduceOp.SUM if op is None else op
         self.bucket = int(bucket_mb * 1024 * 1024 / grad.element_size())
         self.works = []
         self.pending_end = grad.numel()
@@ -93,7 +96,7 @@ class GradBucketer:
 
     def _issue(self, start: int) -> None:
         if self.pending_end > start:
-            w = dist.all_reduce(self.grad[start:self.pending_end], op=dist.ReduceOp.SUM, group=self.group,
+            w = dist.all_reduce(self.grad[start:self.pending_end], op=self.op, group=self.group,
                                 async_op=True)
             self.works.append(w)
             self.pending_end = start

@@ -145,6 +145,29 @@ def _device_for(cfg: TrainConfig, rank: int) -> torch.device:
     return torch.device("cuda", local)
 
 
+def make_loaders(cfg: TrainConfig, train_ds, val_ds, rank: int = 0, world: int = 1):
+    """DataLoaders and DistributedSamplers of argus/train.py:150-191 (per-rank batch, shuffled
+    DistributedSampler for training, ordered for validation). Workers are spawned, never forked: the
+    caller has initialised the GPU by then, and a fork()ed child shares the HSA runtime's host-resident
+    signal / queue pages copy-on-write, so the parent can miss GPU completions written to a page the
+    fork split off (observed: a hang in the first copy of a later validation pass). Persistent workers
+    pay the spawn once per loader. Returns (train_loader, val_loader, train_sampler, val_sampler)."""
+    distributed = world > 1
+    train_sampler = DistributedSampler(train_ds, num_replicas=world, rank=rank, shuffle=True) if distributed else None
+    val_sampler = DistributedSampler(val_ds, num_replicas=world, rank=rank, shuffle=False) if distributed else None
+    nw = cfg.num_workers
+    if nw < 0:
+        nw = (8 if distributed else 16) * (2 if cfg.amp else 1)
+        nw = min(nw, max(1, (os.cpu_count() or 2) // max(1, world) - 1))
+    kw = dict(batch_size=cfg.batch_size, num_workers=nw, pin_memory=True)
+    if nw > 0:  # spawn, never fork (docstring)
+        kw["multiprocessing_context"] = "spawn"
+        kw["persistent_workers"] = True
+    train_loader = DataLoader(train_ds, shuffle=train_sampler is None, sampler=train_sampler, **kw)
+    val_loader = DataLoader(val_ds, shuffle=False, sampler=val_sampler, **kw)
+    return train_loader, val_loader, train_sampler, val_sampler
+
+
 def initialize_training(cfg: TrainConfig, rank: int = 0, world: int = 1):
     """Seeds, device, datasets/loaders, model, fused trainer, LR schedule (train.py:122-255)."""
     from argus_amd.augment import DeviceAugmentation
@@ -165,23 +188,8 @@ def initialize_training(cfg: TrainConfig, rank: int = 0, world: int = 1):
     train_ds = CameraCubePoseDataset(cfg.dataset_config, cfg_aug=cfg.augmentation_config, train=True, uint8=True,
                                      device_augmentation=True)
     val_ds = CameraCubePoseDataset(cfg.dataset_config, cfg_aug=cfg.augmentation_config, train=False, uint8=True)
+    train_loader, val_loader, train_sampler, val_sampler = make_loaders(cfg, train_ds, val_ds, rank, world)
     distributed = world > 1
-    train_sampler = DistributedSampler(train_ds, num_replicas=world, rank=rank, shuffle=True) if distributed else None
-    val_sampler = DistributedSampler(val_ds, num_replicas=world, rank=rank, shuffle=False) if distributed else None
-    nw = cfg.num_workers
-    if nw < 0:
-        nw = (8 if distributed else 16) * (2 if cfg.amp else 1)
-        nw = min(nw, max(1, (os.cpu_count() or 2) // max(1, world) - 1))
-    kw = dict(batch_size=cfg.batch_size, num_workers=nw, pin_memory=True)
-    if nw > 0:
-        # workers are spawned, never forked: this process has initialised the GPU, and a fork()ed child
-        # shares the HSA runtime's host-resident signal / queue pages copy-on-write, so the parent can
-        # miss GPU completions written to a page the fork split off (observed: a hang in the first copy
-        # of a later validation pass). Persistent workers pay the spawn once per loader.
-        kw["multiprocessing_context"] = "spawn"
-        kw["persistent_workers"] = True
-    train_loader = DataLoader(train_ds, shuffle=train_sampler is None, sampler=train_sampler, **kw)
-    val_loader = DataLoader(val_ds, shuffle=False, sampler=val_sampler, **kw)
 
     model = NCameraCNN(cfg.model_config, compute_dtype="bf16" if cfg.amp else "fp32").to(device)
     if distributed:  # DDP's constructor broadcast (train.py:199): every rank starts from rank 0's weights

@@ -199,6 +199,16 @@ def main() -> None:
     summ = probe.summary()
     probe.stop()
     dom = max(summ, key=lambda k: summ[k]["total_ms"])
+    # the critical path: the main stream (the dgrad / BN chain; weight gradients run beside it on a
+    # side stream) - its kernel instantiation with the largest total time
+    main_stream = torch.cuda.current_stream().cuda_stream
+    mprobe = KernelTimer(stream=main_stream)
+    mprobe.start()
+    for _ in range(nprobe):
+        trainer.step(images, targets)
+    msumm = mprobe.summary()
+    mprobe.stop()
+    crit = max(msumm, key=lambda k: msumm[k]["total_ms"])
     if args.kernels and rank == 0:
         for k, v in sorted(summ.items(), key=lambda kv: -kv[1]["total_ms"]):
             us = v["avg_us"]
@@ -240,6 +250,16 @@ def main() -> None:
         iso.stop()
         eng.wgrad_overlap = True
 
+    # the critical-path kernel, timed live (overlap on) over a few more steps after the timed region
+    ncrit = 5
+    ctimer = KernelTimer(crit, stream=main_stream)
+    ctimer.start()
+    for _ in range(ncrit):
+        trainer.step(images, targets)
+    cs = ctimer.summary()[crit]
+    ctimer.stop()
+    main_busy_ms = sum(v["total_ms"] for v in msumm.values()) / nprobe
+
     # validation SE(3) error (eval mode, running BN statistics), synthetic held-out batch
     model.eval()
     vimg, vtgt = synthetic_batch(B, H, W, 5000 + rank, dev)
@@ -265,6 +285,15 @@ def main() -> None:
     # the roof that binds: MFMA if the kernel's algorithmic intensity is above the ridge, else HBM
     compute_bound = ks["flops_per_launch"] / ks["bytes_per_launch"] > peak_flops * 1e12 / (HBM_PEAK_GBS * 1e9)
     ms = 1e3 * elapsed / args.steps
+
+    def roof_of(k):  # {bound, achieved, peak, unit, frac} of one kernel timer record
+        tf = k["flops_per_launch"] / (k["avg_us"] * 1e-6) / 1e12
+        gb = k["bytes_per_launch"] / (k["avg_us"] * 1e-6) / 1e9
+        mf = k["flops_per_launch"] / max(k["bytes_per_launch"], 1.0) > peak_flops * 1e12 / (HBM_PEAK_GBS * 1e9)
+        return {"bound": "mfma" if mf else "hbm", "achieved": round(tf, 2) if mf else round(gb, 1),
+                "peak": peak_flops if mf else HBM_PEAK_GBS, "unit": "TFLOP/s" if mf else "GB/s",
+                "frac": round(tf / peak_flops if mf else gb / HBM_PEAK_GBS, 4),
+                "achieved_tflops": round(tf, 2), "achieved_gbs": round(gb, 1)}
     images_per_s = world * B * 2 * args.steps / elapsed
     # algorithmic conv FLOPs per step: fwd + dgrad + wgrad (the stem has no dgrad)
     step_flops = sum((2 if n == "resnet.conv1" else 3) * c.flops for n, c in eng.convs.items())
@@ -312,6 +341,15 @@ def main() -> None:
                                     if compute_bound else
                                     iso_s["bytes_per_launch"] / (iso_s["avg_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
                               if iso_s else None),
+        },
+        "critical_path": {
+            "kernel": crit, "stream": "main (dgrad / BN chain)", "launches_per_step": msumm[crit]["launches"] // nprobe,
+            "ms_per_step": round(msumm[crit]["total_ms"] / nprobe, 3),
+            "flops_per_launch": round(cs["flops_per_launch"]), "algorithmic_bytes_per_launch": round(cs["bytes_per_launch"]),
+            "avg_launch_us": round(cs["avg_us"], 3), "timed_steps": ncrit, **roof_of(cs),
+            "traffic": pmc_traffic(crit, B, H, W, args.dtype),
+            "mfma_counters": pmc_mfma(crit, B, H, W, args.dtype),
+            "main_stream_busy_ms_per_step": round(main_busy_ms, 3),
         },
         "samples_per_s": round(images_per_s / 2, 2),
         "step_conv_tflops_per_gpu": round(step_flops / (ms * 1e-3) / 1e12, 2),

@@ -87,38 +87,6 @@ int argus_conv_fwd(const argus_conv_desc* d, int dtype, const void* x, const voi
                    const float* pro_scale, const float* pro_shift, float* stat_part,
                    argus_stream_t stream);
 int argus_conv_fwd_stat_rows(const argus_conv_desc* d, int dtype);
-/* argus_conv_fwd with a BN+ReLU prologue that also writes the transformed input relu(x*scale+shift)
- * (the tensor the kernel staged, same layout and dtype as x) to x_out: the bottleneck's
- * relu(bn2(conv2(.))) -> conv3 (argus/models.py:66-90) materialised by conv3's own launch instead of
- * a separate pass, for the weight gradient. 1x1 stride-1 convs only: argus_conv_fwd_stores_input. */
-int argus_conv_fwd_stores_input(const argus_conv_desc* d, int dtype);
-int argus_conv_fwd_store_input(const argus_conv_desc* d, int dtype, const void* x, const void* w_fwd, void* y,
-                               const float* pro_scale, const float* pro_shift, float* stat_part, void* x_out,
-                               argus_stream_t stream);
-/* conv_fwd with the train-mode BatchNorm statistics finalize of its output folded into the launch
- * (replaces argus_conv_fwd(..stat_part..) + argus_bn_finalize): `part` is the partial scratch
- * (float2[argus_conv_fwd_stat_rows(d)][k]), the last workgroups merge it (fp64, fixed order) and
- * write mean / invstd / scale / shift, update running_mean / running_var (momentum, unbiased
- * variance; NULL = skip) and num_batches_tracked (+1; NULL = skip). workspace: argus_bn_workspace_bytes(k),
- * zero-filled once, not shared by concurrent launches. */
-typedef struct {
-  float* part;
-  const float* gamma;
-  const float* beta;
-  float eps;
-  float momentum;
-  float* running_mean;
-  float* running_var;
-  int64_t* num_batches_tracked;
-  float* mean;
-  float* invstd;
-  float* scale;
-  float* shift;
-  void* workspace;
-} argus_bn_fwd_fin;
-int argus_conv_fwd_bn(const argus_conv_desc* d, int dtype, const void* x, const void* w_fwd, void* y,
-                      const float* pro_scale, const float* pro_shift, const argus_bn_fwd_fin* fin,
-                      argus_stream_t stream);
 int argus_conv_fwd_stat_tile(const argus_conv_desc* d, int dtype);
 /* dx = dgrad(dy, w_dgrad) [+ addend]: when addend != NULL (same NHWC layout as dx; may be dx itself
  * for in-place accumulation) it is added, element-wise masked by addend_mask when that is non-NULL
@@ -186,32 +154,22 @@ int argus_conv_dgrad_stages_prologue(const argus_conv_desc* d, int dtype);
 int argus_conv_dgrad_bn(const argus_conv_desc* d, int dtype, const void* dy, const void* w_dgrad,
                         void* dm, const void* addend, const argus_bn_bwd_epilogue* bn,
                         const argus_bn_bwd_prologue* pro, argus_stream_t stream);
-/* Tuning knobs (process-wide; for autotuning / experiments): key 0..2 force the row tile (64|128,
- * 0 = heuristic) of pass fwd/dgrad/wgrad, key 3..5 force the column tile, key 6 sets the wgrad
- * split target (workgroups), key 7 the largest K (= taps*C) served by the 4-workgroups-per-CU
- * single-buffer forward/dgrad kernel (default 128), key 8 the smallest K served by the bf16
- * global->LDS (glds) forward/dgrad kernel (default 512; 0 disables it), key 9 the fewest
- * workgroups for which that kernel is chosen (default 256), key 10 enables (1, default) or
- * disables (0) the LDS-halo kernel for 3x3 stride-1 forward/dgrad, key 11 the same for the 3x3
- * stride-1 weight gradient and key 12 its split target (workgroups, default 512), key 13 the fewest
- * workgroups for the fwd/dgrad halo kernel (default 256; 1 also allows its 64-channel variant),
- * key 14 the most (64 x 64) channel tiles for the wgrad halo kernel (default 4), key 15 the
- * 128x128 register-staged wgrad variant (2 default, 1 / 3 with the prefetch ring), key 16 enables
- * (1, default) or disables the bf16 glds wgrad kernel, key 17 its split target (default 512).
- * Keys 20-23 set the BatchNorm elementwise-kernel geometry (backward min pixels per block, max
- * blocks per channel group; apply target blocks, min pixels per thread), key 24 the BN finalize
- * group-count divisor, key 18 the stem forward occupancy, key 26 the sub-pipelines per workgroup of
- * the bf16 register-staged weight gradient (1 default; 2 = 512-thread workgroups summing two pixel
- * halves in LDS: half the split partials, but slower), key 27 the split target of the register-staged
- * 3x3 weight gradient (default 512), key 28 a cap on the weight gradients' split partials as a
- * multiple of the operand bytes (0 = off, the default; 1-4 measured neutral), key 29 the
- * workgroups per CU of the MX-fp8 forward/dgrad kernel (2 default, 4), key 30 the 64-channel 3x3
- * stride-1 layers (Cin = Cout = 64) on the LDS-halo kernel's single-halo-buffer 64-column variant
- * (1, default) or on the register-staged implicit GEMM (0), key 31 whether the split weight
- * gradients of non-1x1 filters run a pixel split's output tiles on one XCD as the 1x1 ones do
- * (0, default; 1 measured neutral), key 32 where the 3x3 LDS-halo dgrad with a BN-backward
- * epilogue prefetches its epilogue operands under its last channel chunk (1, default: the
- * single-halo-buffer 64-column variant; 2 every variant; 0 none).
+/* Tuning knobs (process-wide; for autotuning / experiments; every default is the measured best):
+ * key 0..2 force the row tile (64|128, 0 = heuristic) of pass fwd/dgrad/wgrad, key 3..5 the column
+ * tile, key 6 the wgrad split target (workgroups), key 7 the largest K (= taps*C) served by the
+ * 4-workgroups-per-CU single-buffer forward/dgrad kernel, key 8 the smallest K served by the bf16
+ * global->LDS (glds) forward/dgrad kernel (0 disables it), key 9 the fewest workgroups for which
+ * that kernel is chosen, key 10 enables (1) or disables (0) the LDS-halo kernel for 3x3 stride-1
+ * forward/dgrad, key 11 the same for the 3x3 stride-1 weight gradient and key 12 its split target,
+ * key 13 the fewest workgroups for the fwd/dgrad halo kernel (1 also allows its 64-channel variant
+ * at any size), key 14 the most (64 x 64) channel tiles for the wgrad halo kernel, key 18 the stem
+ * forward occupancy (2 | 4), keys 20-23 the BatchNorm elementwise-kernel geometry (backward min
+ * pixels per block, max blocks per channel group; apply target blocks, min pixels per thread), key
+ * 24 the BN finalize group-count divisor, key 27 the split target of the register-staged 3x3 weight
+ * gradient, key 30 the 64-channel 3x3 stride-1 layers on the LDS-halo kernel's single-halo-buffer
+ * variant (1) or on the implicit GEMM (0), key 32 where the 3x3 LDS-halo dgrad with a BN-backward
+ * epilogue prefetches its epilogue operands under its last channel chunk (1: the single-halo-buffer
+ * variant; 2 every variant; 0 none).
  * Returns 0, or -1 for an unknown key. */
 int argus_conv_tuning(int key, int value);
 /* Current value of a tuning key (-1 for an unknown key). */
@@ -220,11 +178,6 @@ int argus_conv_tuning_get(int key);
  * tag (kind*10^7 + dtype*10^6 + tile_m*1000 + tile_n; kind 1 igemm, 2 wgrad) and writes
  * 2*P*K*R*S*C flops (P = n*ho*wo output pixels). */
 int argus_conv_launch_info(const argus_conv_desc* d, int dtype, int pass, int64_t* flops);
-/* 1 when the forward of this conv runs on the LDS-halo kernel (3x3 stride 1, bf16 / fp8 networks),
- * which applies a BN+ReLU prologue (pro_scale / pro_shift) once per landed halo element: the
- * producer's BN output need not be materialised for it (argus/models.py:66-90, the bottleneck's
- * relu(bn1(conv1(x))) -> conv2). 0 otherwise. */
-int argus_conv_fwd_halo(const argus_conv_desc* d, int dtype);
 /* dw (fp32, OHWI 7x7x3 for the stem) = sum over pixels of dy x im2col(x'), x' as in conv_fwd. */
 size_t argus_conv_wgrad_workspace_bytes(const argus_conv_desc* d, int dtype);
 int argus_conv_wgrad(const argus_conv_desc* d, int dtype, const void* x, const float* pro_scale,
@@ -249,14 +202,17 @@ int argus_conv_wgrad_apply(const argus_conv_desc* d, int dtype, const void* x, c
  * total algorithmic HBM bytes (each operand read once and each result written once; for wgrad the
  * fp32 split partials it writes count too). */
 int argus_ktimer_enable(const char* filter);
+/* argus_ktimer_enable restricted to launches on `stream` (e.g. the caller's main stream: the
+ * critical path of a step whose weight gradients run on a side stream). */
+int argus_ktimer_enable_on(const char* filter, argus_stream_t stream);
 int argus_ktimer_disable(void);
 int argus_ktimer_count(void);
 int argus_ktimer_get(int index, char* name, int name_len, int64_t* launches, double* total_ms,
                      double* work, double* bytes);
 
 /* ---- BatchNorm2d (train: batch stats, eps, momentum; eval: running stats) --------------------- */
-/* Workspace of argus_bn_finalize / argus_bn_bwd_finalize / the folded finalize of argus_conv_fwd_bn and
- * argus_conv_dgrad_bn for up to `channels` channels. Its first 16 KiB hold inter-workgroup ticket counters: zero-fill the workspace ONCE when it is allocated;
+/* Workspace of argus_bn_finalize / argus_bn_bwd_finalize / the folded finalize of argus_conv_dgrad_bn
+ * for up to `channels` channels. Its first 16 KiB hold inter-workgroup ticket counters: zero-fill the workspace ONCE when it is allocated;
  * the kernels leave the counters zero (do not share one workspace between concurrent streams). */
 size_t argus_bn_workspace_bytes(int channels);
 /* From tile partials float2[rows][C] = {sum, M2 (sum of squared deviations from the tile mean)},

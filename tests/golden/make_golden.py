@@ -275,5 +275,187 @@ def damped_golden(ref_models) -> None:
     print("wrote", OUT / "golden_b8_damped.json", "fp32 vs fp64", e32, "bf16 autocast vs fp64", e16)
 
 
+def _fresh_damped(ref_models, dt=torch.float32):
+    torch.manual_seed(42)
+    m = ref_models.NCameraCNN(ref_models.NCameraCNNConfig(n_cams=2))
+    return damp_residual(m, DAMPED["damp"]).to(dt).train()
+
+
+def _sums(sd, suffixes):
+    return {k: [float(v.double().sum()), float(v.double().abs().sum())] for k, v in sd.items() if k.endswith(suffixes)}
+
+
+# DDP with DistributedSampler(shuffle=False) (argus/train.py:155-168,199): rank r takes samples r::world of
+# the global batch; BN statistics are per rank (no SyncBatchNorm); DDP averages the per-rank mean-loss
+# gradients (all-reduce SUM / world) before clip_grad_norm_ and Adam, which every rank then runs alike.
+TWO_RANK = {"world": 2, "shard": "rank r takes samples r::world (DistributedSampler, shuffle=False)"}
+
+
+def shards(x, T, world=2):
+    return [(x[r::world], T[r::world]) for r in range(world)]
+
+
+def two_rank_golden(ref_models) -> None:
+    """golden_b8_damped_2rank.json: the reference's DDP train step with two ranks at the damped point
+    (global batch 8 = 4 + 4 at 128x128): per-shard BN, averaged gradient, clip 1.0, Adam 1e-4; with the
+    reference's own fp32 error of the averaged gradient against fp64."""
+    cfg = DAMPED
+    B, (H, W) = cfg["batch"], cfg["hw"]
+    x = synthetic_images(B, H, W, seed=cfg["image_seed"])
+    T = synthetic_targets(B, seed=cfg["target_seed"])
+    sh = shards(x, T, TWO_RANK["world"])
+    avg = {}
+    for mode, dt in (("fp64", torch.float64), ("fp32", torch.float32)):
+        gs = []
+        for xs, ts in sh:
+            m = _fresh_damped(ref_models, dt)
+            oracle_se3.geometric_loss(m(xs.to(dt)), ts.to(dt)).mean().backward()
+            gs.append(flat_grads(m))
+        avg[mode] = {n: (gs[0][n] + gs[1][n]) / 2 for n in gs[0]}
+    e32, per32 = grad_errors(avg["fp32"], avg["fp64"])
+    norm = lambda d: torch.cat([v.flatten() for v in d.values()]).norm().item()  # noqa: E731
+
+    # the DDP step itself, fp32: one replica per rank
+    reps = [_fresh_damped(ref_models) for _ in sh]
+    opts = [torch.optim.Adam(m.parameters(), lr=1e-4) for m in reps]
+    losses = []
+    for m, o, (xs, ts) in zip(reps, opts, sh):
+        o.zero_grad()
+        lr_ = oracle_se3.geometric_loss(m(xs).to(torch.float32), ts)
+        lr_.mean().backward()
+        losses.append(lr_.detach())
+    with torch.no_grad():  # DDP: all-reduce SUM, then / world, in fp32
+        for ps in zip(*(m.parameters() for m in reps)):
+            g = (ps[0].grad + ps[1].grad) / len(ps)
+            for p in ps:
+                p.grad.copy_(g)
+    gnorms = [float(torch.nn.utils.clip_grad_norm_(m.parameters(), 1.0)) for m in reps]
+    for o in opts:
+        o.step()
+    for a, b in zip(reps[0].parameters(), reps[1].parameters()):
+        assert torch.equal(a, b), "DDP replicas diverged"
+    sds = [{k: v.clone() for k, v in m.state_dict().items()} for m in reps]
+    with torch.no_grad():
+        after = [m(xs) for m, (xs, _) in zip(reps, sh)]
+    out = {
+        "generator": "tests/golden/make_golden.py::two_rank_golden",
+        "pinned_against": "reference argus/models.py executed with oracle.resnet as torchvision.models",
+        "config": cfg,
+        "ddp": TWO_RANK,
+        "images_sum": float(x.double().sum()),
+        "targets": T.tolist(),
+        "grad_norm_fp64": norm(avg["fp64"]),
+        "ref_fp32_vs_fp64": {"global": e32, "per_tensor": per32},
+        "tensor_grad_norms_fp64": {n: v.norm().item() for n, v in avg["fp64"].items()},
+        "step": {
+            "loss": [v.tolist() for v in losses],
+            "grad_norm": gnorms[0],
+            "pred_after_step_train": [v.tolist() for v in after],
+            "param_sums": _sums(sds[0], ("weight", "bias")),
+            "bn_running_sums": [_sums(sd, ("running_mean", "running_var")) for sd in sds],
+        },
+    }
+    with open(OUT / "golden_b8_damped_2rank.json", "w") as f:
+        json.dump(out, f, indent=1)
+    print("wrote", OUT / "golden_b8_damped_2rank.json", "fp32 vs fp64", e32, "losses", out["step"]["loss"])
+
+
+# Ten reference train steps at the damped point (argus/train.py:295-348 with one batch per "epoch"):
+# fresh batch per step, clip 1.0 + Adam 1e-4, then an eval-mode validation batch whose mean loss drives
+# ReduceLROnPlateau('min', patience=5, factor=0.5) (train.py:232).
+TRAJ = {"batch": 8, "hw": [128, 128], "damp": 0.1, "steps": 10, "lr": 1e-3, "max_grad_norm": 1.0,
+        "image_seed0": 7000, "target_seed0": 7100, "val_batch": 8, "val_image_seed": 7200, "val_target_seed": 7201,
+        "scheduler": {"patience": 1, "factor": 0.5}}
+
+
+def trajectory_batches(cfg=TRAJ):
+    B, (H, W) = cfg["batch"], cfg["hw"]
+    train = [(synthetic_images(B, H, W, seed=cfg["image_seed0"] + t), synthetic_targets(B, seed=cfg["target_seed0"] + t))
+             for t in range(cfg["steps"])]
+    val = (synthetic_images(cfg["val_batch"], H, W, seed=cfg["val_image_seed"]),
+           synthetic_targets(cfg["val_batch"], seed=cfg["val_target_seed"]))
+    return train, val
+
+
+def run_trajectory(ref_models, dt):
+    cfg = TRAJ
+    train, (xv, Tv) = trajectory_batches(cfg)
+    m = _fresh_damped(ref_models, dt)
+    opt = torch.optim.Adam(m.parameters(), lr=cfg["lr"])
+    sched = torch.optim.lr_scheduler.ReduceLROnPlateau(opt, "min", **cfg["scheduler"])
+    steps = []
+    for x, T in train:
+        m.train()
+        losses = oracle_se3.geometric_loss(m(x.to(dt)).to(dt), T.to(dt))
+        opt.zero_grad()
+        losses.mean().backward()
+        gn = float(torch.nn.utils.clip_grad_norm_(m.parameters(), cfg["max_grad_norm"]))
+        opt.step()
+        m.eval()
+        with torch.no_grad():
+            vl = oracle_se3.geometric_loss(m(xv.to(dt)).to(dt), Tv.to(dt)).mean().item()
+        sched.step(vl)
+        steps.append({"loss": losses.detach().tolist(), "grad_norm": gn, "val_loss": vl,
+                      "lr": opt.param_groups[0]["lr"]})
+    sd = m.state_dict()
+    return steps, {"param_sums": _sums(sd, ("weight", "bias")),
+                   "bn_running_sums": _sums(sd, ("running_mean", "running_var")),
+                   "num_batches_tracked": int(sd["resnet.bn1.num_batches_tracked"]),
+                   "param_sample": param_sample(m)}
+
+
+def param_sample(model, per_tensor: int = 64) -> dict:
+    """Up to ``per_tensor`` evenly spaced elements of every parameter (flattened in its state_dict layout):
+    a fixed subsample to compare whole trajectories element by element without storing 100 MB."""
+    out = {}
+    for n, p in model.named_parameters():
+        flat = p.detach().double().flatten()
+        idx = torch.linspace(0, flat.numel() - 1, min(flat.numel(), per_tensor)).round().long()
+        out[n] = flat[idx].tolist()
+    return out
+
+
+def trajectory_golden(ref_models) -> None:
+    """golden_b8_damped_traj.json: the reference's 10-step trajectory in fp32 and fp64 (the fp32-vs-fp64
+    spread per step is what the GPU test's tolerances are stated against)."""
+    s32, end32 = run_trajectory(ref_models, torch.float32)
+    s64, end64 = run_trajectory(ref_models, torch.float64)
+    init = param_sample(_fresh_damped(ref_models))
+    flat = lambda d: torch.tensor([v for k in init for v in d[k]], dtype=torch.float64)  # noqa: E731
+    upd = (flat(end64["param_sample"]) - flat(init)).norm()
+    e_ref = ((flat(end32["param_sample"]) - flat(end64["param_sample"])).norm() / upd).item()
+    out = {
+        "generator": "tests/golden/make_golden.py::trajectory_golden",
+        "pinned_against": "reference argus/models.py executed with oracle.resnet as torchvision.models",
+        "config": TRAJ,
+        "fp32": {"steps": s32, "end": end32},
+        "fp64": {"steps": s64, "end": end64},
+        "param_sample_init": init,
+        # || p32 - p64 || / || p64 - p_init || over the sample: the reference fp32's own update error
+        "ref_fp32_update_error": e_ref,
+    }
+    with open(OUT / "golden_b8_damped_traj.json", "w") as f:
+        json.dump(out, f, indent=1)
+    spread = [max(abs(a - b) for a, b in zip(p["loss"], q["loss"])) for p, q in zip(s32, s64)]
+    print("wrote", OUT / "golden_b8_damped_traj.json", "lr", [s["lr"] for s in s32], "val", [s["val_loss"] for s in s32],
+          "fp32-fp64 loss spread", spread, "update error", e_ref)
+
+
 if __name__ == "__main__":
-    main()
+    # no argument: every fixture; otherwise only the named ones (two_rank, traj)
+    parts = set(sys.argv[1:])
+    if not parts:
+        main()
+    if parts:
+        if not (REF / "argus" / "models.py").exists():
+            raise SystemExit("reference not present: fixtures can only be regenerated in the build container")
+        torch.set_num_threads(8)
+        _ref = load_reference_models()
+        if "two_rank" in parts:
+            two_rank_golden(_ref)
+        if "traj" in parts:
+            trajectory_golden(_ref)
+    else:
+        _ref = load_reference_models()
+        two_rank_golden(_ref)
+        trajectory_golden(_ref)

@@ -16,6 +16,11 @@ def test_record_layout_and_kernels():
         for d in (-0.5, 0.3):
             k = motion_kernel3(ang, d)
             assert abs(k.sum() - 1) < 1e-12 and (k >= 0).all()
+    # nearest-neighbour rotation: small angles keep the line, 35 degrees moves its end taps diagonally;
+    # every nonzero weight is one of the line's own weights (renormalized), no bilinear blending
+    assert np.allclose(motion_kernel3(10.0, 0.0), motion_kernel3(0.0, 0.0))
+    k35 = motion_kernel3(35.0, 0.0)
+    assert np.count_nonzero(k35) == 3 and np.allclose(k35[k35 > 0], 1 / 3) and k35[1, 1] > 0
     r3000, _, b3000 = BLACKBODY[0]
     r15k, _, b15k = BLACKBODY[-1]
     assert r3000 > 1 > b3000 and r15k < 1 < b15k  # warm -> red gain, cold -> blue gain
@@ -31,7 +36,10 @@ def test_sampling_ranges_and_sharing():
         v = p[key]
         assert v.min() >= lo and v.max() <= hi
         assert np.array_equal(v[0::2], v[1::2])  # ColorJiggle same_on_batch: the two cameras share it
-    assert sorted((p["order"][0] >> (2 * i)) & 3 for i in range(4)) == [0, 1, 2, 3]
+    for o in p["order"][:64]:
+        assert sorted((int(o) >> (2 * i)) & 3 for i in range(4)) == [0, 1, 2, 3]
+    assert np.array_equal(p["order"][0::2], p["order"][1::2])  # one order per sample, shared by its cameras
+    assert len(set(p["order"][0::2].tolist())) > 12  # drawn per sample (24 permutations)
     blur_on = (p["blur_w"][:, 2] > 0).mean()
     motion_on = (np.abs(p["motion"]).sum(1) > 0).mean()
     planck_on = (np.abs(p["gain"] - 1).sum(1) > 1e-6).mean()

@@ -1,19 +1,26 @@
-"""Data-parallel parity of FusedTrainer with two ranks on the GPU box.
+"""Data-parallel parity of FusedTrainer on the GPU box, against the oracle.
 
-Reference semantics (argus/train.py:137-168, 298-321 under DDP): every rank draws its own shard of
-the global batch, BatchNorm statistics stay per rank (no SyncBN), the per-rank mean-loss gradients
-are averaged, and every rank applies the same clip + Adam step.
+Reference semantics (argus/train.py:137-168,199,288-321 under DDP): every rank draws its own shard of
+the global batch (DistributedSampler), BatchNorm statistics stay per rank (no SyncBN), the per-rank
+mean-loss gradients are averaged (all-reduce SUM / world), and every rank applies the same clip + Adam.
+Pinned by tests/golden/golden_b8_damped_2rank.json, which make_golden.py writes from the reference's own
+models.py run as two DDP replicas at the damped point (global batch 8 = 4 + 4 at 128x128).
 
-The box has one GPU and RCCL refuses two ranks on one device. Both ranks therefore share cuda:0,
-and the flat-gradient buckets go over gloo (CUDA tensors, staged through the host). FusedTrainer
-issues the same bucketed all-reduce calls it issues over RCCL; only the transport differs.
+The box has one GPU and RCCL refuses two ranks on one device ("Duplicate GPU detected"), so the
+two-rank test shares cuda:0 and its buckets go over gloo (CUDA tensors staged through the host);
+FusedTrainer issues the same bucketed all-reduce calls it issues over RCCL. The RCCL transport and
+its stream ordering are exercised by the one-rank "nccl" test below.
 
-Checks, fp32 parity path, global batch of 4 samples split 2 + 2:
-- each rank's all-reduced flat gradient equals g(shard 0) + g(shard 1), both computed locally
-  without the collective. The SUM of two addends is order-free, so this holds bit for bit;
-- after the step the parameters are bitwise identical on both ranks;
-- the per-rank BN running statistics are those of the rank's own shard (no SyncBN).
+Stated tolerances (fp32 path; the bars of test_gpu_parity.py::test_damped_fp32_*):
+- averaged gradient vs the fp64 oracle (per-shard BN emulated by running the oracle per shard):
+  global relative L2 <= 2x the reference fp32's own error, each tensor <= 4x its error + 2e-4;
+- per-rank losses within 1e-5 and grad norm within 1e-4 relative of the reference's DDP step;
+  post-step per-rank prediction within 2e-5; parameter sums as the single-rank step test;
+  per-rank BN running sums within 1e-4 relative;
+- the all-reduced flat gradient equals g(shard 0) + g(shard 1) computed locally, bit for bit (the
+  SUM of two addends is order-free), and both ranks hold bitwise-identical parameters after the step.
 """
+import json
 import os
 import socket
 
@@ -21,7 +28,11 @@ import pytest
 import torch
 import torch.multiprocessing as mp
 
+import tests.golden.make_golden as mg
+
 pytestmark = pytest.mark.gpu
+
+LR, MAX_NORM = 1e-4, 1.0
 
 
 def _free_port():
@@ -32,26 +43,46 @@ def _free_port():
     return p
 
 
-def _local_grads(x, T, dev):
+def _golden():
+    with open(mg.OUT / "golden_b8_damped_2rank.json") as f:
+        return json.load(f)
+
+
+def _inputs(g):
+    c = g["config"]
+    x = mg.synthetic_images(c["batch"], *c["hw"], seed=c["image_seed"])
+    T = mg.synthetic_targets(c["batch"], seed=c["target_seed"])
+    assert abs(float(x.double().sum()) - g["images_sum"]) < 1e-3
+    assert torch.allclose(T, torch.tensor(g["targets"]))
+    return x, T
+
+
+def _model(dev, damp):
+    from argus_amd.models import NCameraCNN
+
+    torch.manual_seed(42)
+    return mg.damp_residual(NCameraCNN(), damp).to(dev).train()
+
+
+def _local_grads(shards, dev, damp):
     """g(shard) for each shard, with no collective: the engine schedule FusedTrainer.step runs."""
     import ctypes as C
 
     from argus_amd._lib import lib, ptr, stream
-    from argus_amd.models import NCameraCNN
     from argus_amd.step import FlatParams
 
-    torch.manual_seed(42)
-    model = NCameraCNN().to(dev).train()
+    model = _model(dev, damp)
     flat = FlatParams(model)
     eng = model._engine(dev)
     P, Bf = model._maps()
     out = []
-    for r in range(2):
-        xs, ts = x[2 * r:2 * r + 2].to(dev), T[2 * r:2 * r + 2].to(dev).contiguous()
+    for xs, ts in shards:
+        n = xs.shape[0]
+        xs, ts = xs.to(dev), ts.to(dev).contiguous()
         pred = eng.forward(xs, P, Bf, True)
-        loss = torch.empty(2, device=dev)
-        dpred = torch.empty(2, 6, device=dev)
-        lib().se3_loss(2, ptr(pred), ptr(ts), ptr(loss), ptr(dpred), C.c_float(0.5), stream())
+        loss = torch.empty(n, device=dev)
+        dpred = torch.empty(n, 6, device=dev)
+        lib().se3_loss(n, ptr(pred), ptr(ts), ptr(loss), ptr(dpred), C.c_float(1.0 / n), stream())
         flat.grad.zero_()
         eng.backward(dpred, P, flat.G)
         torch.cuda.synchronize()
@@ -59,7 +90,7 @@ def _local_grads(x, T, dev):
     return out
 
 
-def _worker(rank, port, x, T, outdir, q):
+def _worker(rank, port, x, T, damp, outdir, q):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
         import torch.distributed as dist
@@ -67,40 +98,56 @@ def _worker(rank, port, x, T, outdir, q):
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
         dist.init_process_group("gloo", rank=rank, world_size=2)
-        from argus_amd.models import NCameraCNN
         from argus_amd.step import FusedTrainer
 
-        g0, g1 = _local_grads(x, T, dev)
-        torch.manual_seed(42)
-        model = NCameraCNN().to(dev).train()
-        tr = FusedTrainer(model, lr=1e-3, max_grad_norm=1.0, bucket_mb=8.0)
+        sh = mg.shards(x, T, 2)
+        g0, g1 = _local_grads(sh, dev, damp)
+        model = _model(dev, damp)
+        tr = FusedTrainer(model, lr=LR, max_grad_norm=MAX_NORM, bucket_mb=8.0)
         assert tr.distributed and tr.world == 2
-        tr.step(x[2 * rank:2 * rank + 2].to(dev), T[2 * rank:2 * rank + 2].to(dev))
+        xs, ts = sh[rank]
+        losses = tr.step(xs.to(dev), ts.to(dev)).cpu()
         torch.cuda.synchronize()
         grad_ok = bool(torch.equal(tr.flat.grad, g0 + g1))
         gmax = (tr.flat.grad - (g0 + g1)).abs().max().item()
-        torch.save({"param": tr.flat.param.cpu(), "rm": model.resnet.bn1.running_mean.cpu()},
-                   os.path.join(outdir, f"rank{rank}.pt"))
+        grads = {n: p.grad.detach().double().cpu() for n, p in model.named_parameters()}  # OIHW views
+        sd = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+        with torch.no_grad():
+            after = model(xs.to(dev)).cpu()
+        torch.save({"param": tr.flat.param.cpu(), "grads": grads, "sd": sd, "losses": losses, "after": after,
+                    "grad_norm": float(tr.grad_norm())}, os.path.join(outdir, f"rank{rank}.pt"))
         dist.destroy_process_group()
         q.put((rank, grad_ok, gmax, None))
     except Exception as e:  # report, don't hang the parent
-        q.put((rank, False, float("nan"), repr(e)))
+        import traceback
+
+        q.put((rank, False, float("nan"), repr(e) + traceback.format_exc()))
 
 
-def test_two_rank_step_matches_shard_gradient_sum(cuda, tmp_path):
+def test_two_rank_step_matches_reference_ddp_step(cuda, tmp_path):
     from oracle import se3
+    from oracle.ncamera import build_reference_model
 
-    g = torch.Generator().manual_seed(77)
-    x = torch.randint(0, 256, (4, 6, 64, 64), generator=g, dtype=torch.uint8).float() / 255.0
-    T = se3.random_targets(4, generator=g).float()
+    g = _golden()
+    damp = g["config"]["damp"]
+    x, T = _inputs(g)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, port, x, T, str(tmp_path), q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, port, x, T, damp, str(tmp_path), q)) for r in range(2)]
     for p in procs:
         p.start()
+    # the fp64 oracle of the averaged gradient (per-shard BN), on the host while the ranks run
+    gs = []
+    for xs, ts in mg.shards(x, T, 2):
+        m = mg.damp_residual(build_reference_model(42), damp).double().train()
+        se3.geometric_loss(m(xs.double()), ts.double()).mean().backward()
+        gs.append(mg.flat_grads(m))
+    g64 = {n: (gs[0][n] + gs[1][n]) / 2 for n in gs[0]}
+    n64 = torch.cat([v.flatten() for v in g64.values()]).norm().item()
+    assert abs(n64 / g["grad_norm_fp64"] - 1) < 1e-9, "the live oracle is the pinned one"
     try:
-        res = sorted(q.get(timeout=240) for _ in procs)
+        res = sorted(q.get(timeout=300) for _ in procs)
     finally:
         for p in procs:
             p.join(timeout=60)
@@ -109,8 +156,98 @@ def test_two_rank_step_matches_shard_gradient_sum(cuda, tmp_path):
     for rank, ok, gmax, err in res:
         assert err is None, f"rank {rank}: {err}"
         assert ok, f"rank {rank}: all-reduced gradient != g0 + g1 (max |diff| {gmax:.3e})"
-    s0 = torch.load(tmp_path / "rank0.pt", weights_only=True)
-    s1 = torch.load(tmp_path / "rank1.pt", weights_only=True)
-    assert torch.equal(s0["param"], s1["param"]), "ranks diverged after the step"
-    # per-rank BN (no SyncBN): the stem's running mean differs between the two shards
-    assert not torch.equal(s0["rm"], s1["rm"])
+    s = [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(2)]
+    assert torch.equal(s[0]["param"], s[1]["param"]), "ranks diverged after the step"
+    gst = g["step"]
+    for r in range(2):
+        dl = (s[r]["losses"] - torch.tensor(gst["loss"][r])).abs().max().item()
+        assert dl < 1e-5, (r, dl)
+        assert abs(s[r]["grad_norm"] / gst["grad_norm"] - 1) < 1e-4, (r, s[r]["grad_norm"], gst["grad_norm"])
+        d = (s[r]["after"] - torch.tensor(gst["pred_after_step_train"][r])).abs().max().item()
+        print(f"rank {r}: loss {dl:.2e}, post-step prediction {d:.2e}")
+        assert d < 2e-5, (r, d)
+        for k, (sm, ab) in gst["bn_running_sums"][r].items():  # per-rank BN, no SyncBN
+            v = s[r]["sd"][k].double()
+            assert abs(v.sum().item() - sm) <= 1e-4 * ab + 1e-6, (r, k)
+    # the all-reduced SUM / world against the oracle's averaged gradient
+    ours = {n: v / 2 for n, v in s[0]["grads"].items()}
+    e, per = mg.grad_errors(ours, g64)
+    e_ref, per_ref = g["ref_fp32_vs_fp64"]["global"], g["ref_fp32_vs_fp64"]["per_tensor"]
+    print(f"averaged gradient vs fp64 oracle: ours {e:.3e}, reference fp32 DDP {e_ref:.3e}")
+    assert e <= 2 * e_ref, (e, e_ref)
+    bad = {n: (per[n], per_ref[n]) for n in per if per[n] > 4 * per_ref[n] + 2e-4}
+    assert not bad, bad
+    for k, (sm, ab) in gst["param_sums"].items():  # as test_damped_fp32_fused_step_tight
+        v = s[0]["sd"][k].double()
+        tol = 2e-4 * max(0.0025 * v.numel(), 2.0) + 1e-6
+        assert abs(v.sum().item() - sm) <= tol and abs(v.abs().sum().item() - ab) <= tol, k
+    assert not torch.equal(s[0]["sd"]["resnet.bn1.running_mean"], s[1]["sd"]["resnet.bn1.running_mean"])
+
+
+def _rccl_worker(port, x, T, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+        import torch.distributed as dist
+
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+        from argus_amd.models import NCameraCNN
+        from argus_amd.step import FusedTrainer, GradBucketer
+
+        class Counting(GradBucketer):
+            issued = 0
+
+            def _issue(self, start):
+                if self.pending_end > start:
+                    Counting.issued += 1
+                super()._issue(start)
+
+        def run(bucketed):
+            torch.manual_seed(42)
+            model = NCameraCNN(compute_dtype="bf16").to(dev).train()
+            tr = FusedTrainer(model, lr=LR, max_grad_norm=MAX_NORM)
+            if bucketed:
+                # a one-rank RCCL PREMUL_SUM(2) scales each bucket it reduces: any bucket reduced before
+                # its last weight gradient was written (wrong stream order) leaves unscaled elements
+                tr.bucketer = Counting(tr.flat.grad, tr.flat.offset, None, bucket_mb=4.0,
+                                           op=dist._make_nccl_premul_sum(2.0))
+            tr.step(x.to(dev), T.to(dev))
+            torch.cuda.synchronize()
+            return tr.flat.grad.clone()
+
+        g1 = run(False)
+        g2 = run(True)
+        ok = bool(torch.equal(g2, 2 * g1))
+        bad = int((g2 != 2 * g1).sum())
+        dist.destroy_process_group()
+        q.put((ok, bad, Counting.issued, None))
+    except Exception as e:
+        import traceback
+
+        q.put((False, -1, 0, repr(e) + traceback.format_exc()))
+
+
+def test_rccl_bucketed_allreduce_stream_order(cuda):
+    """The bucketed all-reduce over RCCL (backend "nccl", one rank: the only RCCL world one GPU allows),
+    issued from the weight-gradient side stream during the bf16 backward (engine.py _comm). Every
+    bucket must be reduced after all the kernels that write it: with PREMUL_SUM(2) the reduced
+    gradient is exactly 2x the gradient of an identical step without collectives."""
+    g = torch.Generator().manual_seed(5)
+    x = torch.randint(0, 256, (8, 6, 128, 128), generator=g, dtype=torch.uint8).float() / 255.0
+    from oracle import se3
+
+    T = se3.random_targets(8, generator=g).float()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), x, T, q))
+    p.start()
+    try:
+        ok, bad, nbuckets, err = q.get(timeout=240)
+    finally:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    assert err is None, err
+    assert ok, f"{bad} gradient elements not scaled by the RCCL all-reduce (bucket issued too early)"
+    assert nbuckets >= 10, nbuckets  # 103.5 MB of gradients in 4 MB buckets, issued during the backward

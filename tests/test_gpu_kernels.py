@@ -562,9 +562,10 @@ HALO_SHAPES = [  # (cin, cout, hw, n): 256-pixel tiles = 4 rows / 8 rows / 1 ima
 
 
 def test_conv3x3_halo_kernel_parity(cuda):
-    """3x3 stride-1 LDS-halo kernel vs torch (bf16): forward with and without the fused BN+ReLU
-    prologue (zero padding of the post-ReLU tensor), BN partials at 64- and 128-row tiles, dgrad with
-    in-place and masked addends; the kernel timer confirms the halo kernel served every call."""
+    """3x3 stride-1 LDS-halo kernel vs torch (bf16): forward with BN partials at 64- and 128-row tiles,
+    dgrad with in-place and masked addends; the kernel timer confirms the halo kernel served every
+    call, and a forward with a BN+ReLU prologue (bf16 inputs are materialised by the benched schedule)
+    is served by the register-staged kernel instead."""
     from argus_amd.profiling import KernelTimer
 
     torch.manual_seed(13)
@@ -596,7 +597,7 @@ def test_layer1_3x3_on_single_buffer_halo_kernel(cuda):
     ref_y = F.conv2d(xr, wr, padding=1).permute(0, 2, 3, 1)
     ref_dx = torch.nn.grad.conv2d_input(xr.shape, wr, _q(dy, "bf16").permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
     outs = {}
-    for key30, kname in ((1, "conv3x3_halo_kernel<64, false, 0, 1>"), (0, "igemm_kernel")):
+    for key30, kname in ((1, "conv3x3_halo_kernel<64, 0, 1>"), (0, "igemm_kernel")):
         with _tuned({30: key30}):
             rows = L.dll.argus_conv_fwd_stat_rows(C.byref(d), BF16)
             stats = torch.empty(rows, c, 2, device=cuda)
@@ -609,47 +610,10 @@ def test_layer1_3x3_on_single_buffer_halo_kernel(cuda):
         names = list(t.summary())
         assert any(kname in nm for nm in names), (key30, names)
         if key30:
-            assert any("conv3x3_halo_kernel<64, false, 0, 1>" in nm for nm in names) and len(names) == 1, names
+            assert any("conv3x3_halo_kernel<64, 0, 1>" in nm for nm in names) and len(names) == 1, names
         assert _rel(y, ref_y) < TOL["bf16"] and _rel(dx, ref_dx) < TOL["bf16"], key30
         outs[key30] = (y.float(), dx.float())
     assert _rel(outs[1][0], outs[0][0]) < 1e-2 and _rel(outs[1][1], outs[0][1]) < 1e-2
-
-
-@pytest.mark.parametrize("dt", ["fp32", "bf16"])
-def test_conv_fwd_store_input(cuda, dt):
-    """argus_conv_fwd_store_input (1x1 stride-1 conv with a BN+ReLU prologue that also writes the
-    staged relu(x*scale+shift)): y and the BN partials bit-identical to argus_conv_fwd with the same
-    prologue, x_out bit-identical to argus_bn_apply's relu(bn(x)); 64- to 512-channel outputs (1 to 4
-    column tiles), partial row tiles; a 3x3 conv is refused."""
-    torch.manual_seed(21)
-    L = lib()
-    for cin, cout, hw, n in ((64, 256, 9, 3), (128, 512, 8, 2), (256, 64, 7, 5), (512, 128, 5, 4)):
-        d, _ = _desc(n, hw, hw, cin, cout, 1, 1)
-        assert L.dll.argus_conv_fwd_stores_input(C.byref(d), DT[dt]) == 1
-        w = torch.randn(cout, 1, 1, cin) * (2.0 / cin) ** 0.5
-        wf, _ = _prep(d, dt, w.to(cuda), cuda)
-        x = (torch.randn(n, hw, hw, cin) * 2 + 0.3).to(cuda, TDT[dt])
-        sc, sh = (torch.rand(cin) + 0.5).to(cuda), (torch.randn(cin) * 0.5).to(cuda)
-        rows = L.dll.argus_conv_fwd_stat_rows(C.byref(d), DT[dt])
-        outs = []
-        for store in (False, True):
-            y = torch.empty(n, hw, hw, cout, dtype=TDT[dt], device=cuda)
-            part = torch.empty(rows, cout, 2, device=cuda)
-            xo = torch.full((n, hw, hw, cin), float("nan"), dtype=TDT[dt], device=cuda)
-            if store:
-                assert L.conv_fwd_store_input(C.byref(d), DT[dt], ptr(x), ptr(wf), ptr(y), ptr(sc), ptr(sh), ptr(part),
-                                              ptr(xo), stream()) == 0
-            else:
-                L.conv_fwd(C.byref(d), DT[dt], ptr(x), ptr(wf), ptr(y), ptr(sc), ptr(sh), ptr(part), stream())
-                L.bn_apply(DT[dt], n * hw * hw, cin, ptr(x), ptr(sc), ptr(sh), None, None, None, 1, ptr(xo), None,
-                           stream())
-            torch.cuda.synchronize()
-            outs.append((y.cpu(), part.cpu(), xo.cpu()))
-        (y0, p0, a0), (y1, p1, a1) = outs
-        assert torch.equal(y0, y1) and torch.equal(p0, p1), (cin, cout, dt)
-        assert torch.equal(a0, a1), (cin, cout, dt, "stored input")
-    d3, _ = _desc(2, 8, 8, 64, 64, 3, 1)
-    assert L.dll.argus_conv_fwd_stores_input(C.byref(d3), DT[dt]) == 0
 
 
 def _halo_cases(L, cuda):
@@ -672,7 +636,7 @@ def _halo_cases(L, cuda):
             with KernelTimer("argus::conv3x3_halo_kernel") as t:
                 L.conv_fwd(C.byref(d), BF16, ptr(xd), ptr(wf), ptr(y), ptr(scd) if pro else None,
                            ptr(shd) if pro else None, ptr(stats), stream())
-            assert len(t.summary()) == 1, ("halo kernel not used", cin, cout, hw, n, pro)
+            assert len(t.summary()) == (0 if pro else 1), ("halo kernel use", cin, cout, hw, n, pro)
             xin = torch.relu(xr * sc[None, :, None, None] + sh[None, :, None, None]) if pro else xr
             xin = _q(xin.permute(0, 2, 3, 1), "bf16").permute(0, 3, 1, 2) if pro else xin
             ref = F.conv2d(xin, wr, padding=1)
@@ -739,8 +703,9 @@ def test_weight_prep_batch_matches_single(cuda, dt):
 
 @pytest.mark.parametrize("pro", [False, True])
 def test_wgrad3x3_halo_kernel_parity(cuda, pro):
-    """3x3 stride-1 weight gradient through the LDS-halo kernel vs torch (bf16 inputs, fp32 dW), with
-    and without the fused BN+ReLU of the input; the kernel timer confirms the halo kernel ran."""
+    """3x3 stride-1 weight gradient through the LDS-halo kernel vs torch (bf16 inputs, fp32 dW); with
+    a BN+ReLU prologue on the input (not a benched schedule: bf16 inputs are materialised) the
+    register-staged kernel serves it. The kernel timer confirms which kernel ran."""
     from argus_amd.profiling import KernelTimer
 
     torch.manual_seed(19)
@@ -767,7 +732,7 @@ def _wgrad_halo_cases(L, cuda, pro):
         with KernelTimer("argus::wgrad3x3_halo_kernel") as t:
             L.conv_wgrad(C.byref(d), BF16, ptr(xg), ptr(scg) if pro else None, ptr(shg) if pro else None, ptr(dyg),
                          ptr(dw), ptr(ws), wsb, stream())
-        assert len(t.summary()) == 1, ("halo wgrad not used", cin, cout, hw, n)
+        assert len(t.summary()) == (0 if pro else 1), ("halo wgrad use", cin, cout, hw, n, pro)
         xin = x.permute(0, 3, 1, 2)
         if pro:
             xin = _q(torch.relu(xin * sc[None, :, None, None] + sh[None, :, None, None]).permute(0, 2, 3, 1),
@@ -799,79 +764,6 @@ def test_conv_large_tile_small_k(cuda, dt):
         mean, var = _merge_stats(stats.double().cpu(), tile, n * hw * hw)
         yr = ref.permute(0, 2, 3, 1).reshape(-1, cout)
         assert _rel(var, yr.var(0, unbiased=False)) < (1e-4 if dt == "fp32" else 2e-2), (dt, cin, cout)
-
-
-def test_wgrad_glds_kernel_parity(cuda):
-    """bf16 weight gradient through the global->LDS wgrad kernel (both 256- and 128-row tiles, 1x1 and
-    3x3, stride 1 and 2, zero-padded taps) vs torch; the kernel timer confirms it ran."""
-    from argus_amd.profiling import KernelTimer
-
-    torch.manual_seed(29)
-    L = lib()
-    halo, glds = L.dll.argus_conv_tuning_get(11), L.dll.argus_conv_tuning_get(16)
-    assert L.dll.argus_conv_tuning(11, 0) == 0  # the 3x3 halo wgrad would take the 128-channel 3x3 case
-    assert L.dll.argus_conv_tuning(16, 1) == 0  # the glds wgrad is off by default (tuning key 16)
-    try:
-        _wgrad_glds_cases(cuda, L, KernelTimer)
-    finally:
-        L.dll.argus_conv_tuning(11, halo)
-        L.dll.argus_conv_tuning(16, glds)
-
-
-def _wgrad_glds_cases(cuda, L, KernelTimer):
-    for cin, cout, k, s, hw, n in [(128, 128, 3, 1, 16, 2), (256, 512, 1, 1, 16, 4), (256, 256, 3, 2, 16, 2),
-                                   (512, 256, 1, 1, 8, 2), (128, 256, 3, 1, 32, 1), (256, 128, 1, 2, 16, 2)]:
-        d, p = _desc(n, hw, hw, cin, cout, k, s)
-        x = _q(torch.randn(n, hw, hw, cin), "bf16")
-        dy = _q(torch.randn(n, d.ho, d.wo, cout), "bf16")
-        xg, dyg = x.to(cuda, torch.bfloat16), dy.to(cuda, torch.bfloat16)
-        dw = torch.empty(cout, k, k, cin, device=cuda)
-        wsb = L.dll.argus_conv_wgrad_workspace_bytes(C.byref(d), BF16)
-        ws = torch.empty(wsb, dtype=torch.uint8, device=cuda)
-        with KernelTimer("argus::wgrad_glds_kernel") as t:
-            L.conv_wgrad(C.byref(d), BF16, ptr(xg), None, None, ptr(dyg), ptr(dw), ptr(ws), wsb, stream())
-        assert len(t.summary()) == 1, ("glds wgrad not used", cin, cout, k, s, hw, n)
-        ref = torch.nn.grad.conv2d_weight(x.permute(0, 3, 1, 2).double(), (cout, cin, k, k),
-                                          dy.permute(0, 3, 1, 2).double(), stride=s, padding=p)
-        assert _rel(dw.permute(0, 3, 1, 2), ref) < 2e-3, ("wgrad glds", cin, cout, k, s, hw, n)
-
-
-def test_wgrad_sub_pipelines(cuda):
-    """bf16 register-staged weight gradient with two sub-pipelines per workgroup (tuning key 26 = 2:
-    512 threads, the split's pixel range halved, the halves summed in LDS) and with one (key 26 = 1,
-    the default), vs torch fp64: FAST and ragged pixel indexing, odd k-step counts per split (the
-    second half runs a zero-filled tail step), a last split shorter than one half, every row/column
-    tile shape, stride 2. The kernel timer confirms which variant ran."""
-    from argus_amd.profiling import KernelTimer
-
-    torch.manual_seed(31)
-    L = lib()
-    cases = [  # (cin, cout, k, s, hw, n, split target)
-        (256, 256, 1, 1, 16, 4, 512), (64, 256, 1, 1, 13, 3, 512), (256, 64, 1, 1, 13, 3, 64),
-        (128, 128, 3, 2, 17, 2, 512), (256, 512, 1, 2, 16, 2, 512), (512, 128, 1, 1, 9, 5, 8),
-        (128, 128, 3, 1, 16, 2, 96), (64, 64, 1, 1, 64, 2, 2048),
-    ]
-    for cin, cout, k, s, hw, n, target in cases:
-        d, p = _desc(n, hw, hw, cin, cout, k, s)
-        x = _q(torch.randn(n, hw, hw, cin), "bf16")
-        dy = _q(torch.randn(n, d.ho, d.wo, cout), "bf16")
-        xg, dyg = x.to(cuda, torch.bfloat16), dy.to(cuda, torch.bfloat16)
-        ref = torch.nn.grad.conv2d_weight(x.permute(0, 3, 1, 2).double(), (cout, cin, k, k),
-                                          dy.permute(0, 3, 1, 2).double(), stride=s, padding=p)
-        out = {}
-        for sub in (1, 2):
-            with _tuned({26: sub, 6: target, 11: 0, 16: 0}):
-                wsb = L.dll.argus_conv_wgrad_workspace_bytes(C.byref(d), BF16)
-                ws = torch.full((wsb,), 255, dtype=torch.uint8, device=cuda)  # NaN-filled partials
-                dw = torch.empty(cout, k, k, cin, device=cuda)
-                with KernelTimer("argus::wgrad_kernel") as t:
-                    L.conv_wgrad(C.byref(d), BF16, ptr(xg), None, None, ptr(dyg), ptr(dw), ptr(ws), wsb, stream())
-                names = list(t.summary())
-            assert len(names) == 1 and names[0].endswith(f", {sub}>"), (names, sub)
-            e = _rel(dw.permute(0, 3, 1, 2), ref)
-            assert e < 2e-3, ("wgrad sub", sub, cin, cout, k, s, hw, n, target, e)
-            out[sub] = dw.cpu()
-        assert _rel(out[2], out[1]) < 1e-5, (cin, cout, k, s, hw, n)
 
 
 @pytest.mark.parametrize("dt", ["fp32", "bf16"])
@@ -1005,7 +897,7 @@ def test_conv_dgrad_bn_epilogue(cuda, dt):
                 assert (pc2[:, 0] - S).abs().max() <= tol * scale
 
 
-FOLD_CASES = [  # (cin, cout, k, stride, hin, n, tuning): forward kernels igemm / halo / glds / stem
+FOLD_CASES = [  # (cin, cout, k, stride, hin, n, tuning): dgrad kernels igemm / halo / glds / strided phases
     (64, 256, 1, 1, 40, 4, {}),
     (128, 128, 3, 1, 16, 4, {13: 1}),
     (256, 256, 1, 1, 32, 2, {8: 64, 9: 1}),
@@ -1015,10 +907,11 @@ FOLD_CASES = [  # (cin, cout, k, stride, hin, n, tuning): forward kernels igemm 
 
 @pytest.mark.parametrize("dt", ["fp32", "bf16"])
 def test_folded_bn_finalize_matches_separate_kernels(cuda, dt):
-    """argus_conv_fwd_bn / argus_conv_dgrad_bn(workspace): the BN finalize folded into the producing
-    conv launch (two-level ticket merge) gives what argus_bn_finalize / argus_bn_bwd_finalize give from
-    the same partials, up to fp64 summation order (1e-6 relative), and leaves its counters at zero."""
-    from argus_amd._lib import BnBwdEpilogue, BnFwdFin
+    """argus_conv_dgrad_bn(workspace): the BN-backward finalize folded into the producing dgrad launch
+    (two-level ticket merge) gives what argus_bn_bwd_finalize gives from the same partials, up to fp64
+    summation order (1e-6 relative), and leaves its counters at zero; dgrad kernels igemm / halo /
+    glds, strided phases."""
+    from argus_amd._lib import BnBwdEpilogue
 
     torch.manual_seed(9)
     L = lib()
@@ -1029,35 +922,6 @@ def test_folded_bn_finalize_matches_separate_kernels(cuda, dt):
         d, p = _desc(n, hin, hin, cin, cout, k, s)
         w = torch.randn(cout, k, k, cin) * (2.0 / (k * k * cin)) ** 0.5
         wf, wt = _prep(d, dt, w.to(cuda), cuda)
-        x = torch.randn(n, hin, hin, cin, device=cuda).to(TDT[dt])
-        gamma, beta = torch.rand(cout, device=cuda) + 0.5, torch.randn(cout, device=cuda)
-        outs = []
-        with _tuned(tune):
-            rows = L.dll.argus_conv_fwd_stat_rows(C.byref(d), DT[dt])
-            tile = L.dll.argus_conv_fwd_stat_tile(C.byref(d), DT[dt])
-            for folded in (False, True):
-                ws = torch.zeros(ws_bytes, dtype=torch.uint8, device=cuda)
-                part = torch.empty(rows, cout, 2, device=cuda)
-                y = torch.empty(n, d.ho, d.wo, cout, dtype=TDT[dt], device=cuda)
-                st = torch.zeros(4, cout, device=cuda)
-                rm, rv = torch.zeros(cout, device=cuda), torch.ones(cout, device=cuda)
-                nbt = torch.zeros((), dtype=torch.int64, device=cuda)
-                if folded:
-                    f = BnFwdFin(ptr(part), ptr(gamma), ptr(beta), 1e-5, 0.1, ptr(rm), ptr(rv), ptr(nbt),
-                                 ptr(st[0]), ptr(st[1]), ptr(st[2]), ptr(st[3]), ptr(ws))
-                    L.conv_fwd_bn(C.byref(d), DT[dt], ptr(x), ptr(wf), ptr(y), None, None, C.byref(f), stream())
-                else:
-                    L.conv_fwd(C.byref(d), DT[dt], ptr(x), ptr(wf), ptr(y), None, None, ptr(part), stream())
-                    L.bn_finalize(cout, rows, tile, ptr(part), n * d.ho * d.wo, ptr(gamma), ptr(beta),
-                                  C.c_float(1e-5), C.c_float(0.1), ptr(rm), ptr(rv), ptr(nbt), ptr(st[0]),
-                                  ptr(st[1]), ptr(st[2]), ptr(st[3]), ptr(ws), stream())
-                torch.cuda.synchronize()
-                assert int(ws[:16384].view(torch.int32).abs().sum()) == 0  # counters back at zero
-                outs.append((y.cpu(), st.cpu(), rm.cpu(), rv.cpu(), int(nbt)))
-        (y0, s0, m0, v0, n0), (y1, s1, m1, v1, n1) = outs
-        assert torch.equal(y0, y1) and n0 == n1 == 1
-        for a_, b_ in ((s0, s1), (m0, m1), (v0, v1)):
-            assert _rel(a_, b_) < 1e-6, (cin, cout, k, s, dt)
         # backward: dgrad_bn with the finalize folded vs bn_bwd_finalize on its partials
         dy = torch.randn(n, d.ho, d.wo, cout, device=cuda).to(TDT[dt])
         yb = torch.randn(n, hin, hin, cin, device=cuda).to(TDT[dt])

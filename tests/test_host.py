@@ -94,6 +94,14 @@ def test_bn_momentum_none_is_cumulative_average():
     _, Bf = m._maps()
     assert Bf["resnet.bn1.momentum"] == 0.25
     assert Bf["resnet.layer1.0.bn1.momentum"] == 0.1
+    # later train-mode forwards use the host shadow count (the finalize kernels increment the device
+    # counter; nothing reads it back), a maps call for a backward does not advance it, and a write by
+    # torch (load_state_dict, fill_) is picked up through the tensor's version counter
+    assert m._maps(forward=False)[1]["resnet.bn1.momentum"] == 0.2
+    assert m._maps()[1]["resnet.bn1.momentum"] == 0.2
+    assert m._maps()[1]["resnet.bn1.momentum"] == 1 / 6
+    m.resnet.bn1.num_batches_tracked.fill_(10)
+    assert m._maps()[1]["resnet.bn1.momentum"] == 1 / 11
 
 
 def test_spaghetti_draws_reference_arcs():
@@ -134,3 +142,31 @@ def test_validate_config_checks(tmp_path):
         ValConfig(model_path=str(tmp_path / "x.pt"), dataset_config=CameraCubePoseDatasetConfig(d))
     with pytest.raises(FileNotFoundError):
         ValConfig(model_path=str(tmp_path / "missing.pth"), dataset_config=CameraCubePoseDatasetConfig(d))
+
+
+def test_train_loaders_never_fork(tmp_path):
+    """argus_amd.train builds its DataLoaders spawned and persistent, never forked (the process has
+    initialised the GPU by then: a fork()ed loader hung the GPU suite twice in round 2),
+    for the default worker count, an explicit one and the distributed samplers; initialize_training
+    builds its loaders only through make_loaders."""
+    import inspect
+
+    from argus_amd import train as T
+    from argus_amd.data import CameraCubePoseDataset, CameraCubePoseDatasetConfig
+    from tests.conftest import make_dummy_dataset
+
+    path = make_dummy_dataset(tmp_path, hw=(32, 32))
+    dcfg = CameraCubePoseDatasetConfig(dataset_path=path, center_crop=(32, 32))
+    tr = CameraCubePoseDataset(dcfg, train=True, uint8=True)
+    va = CameraCubePoseDataset(dcfg, train=False, uint8=True)
+    for workers, world in ((-1, 1), (3, 1), (2, 2)):
+        cfg = T.TrainConfig(dataset_config=dcfg, batch_size=4, num_workers=workers, wandb_log=False,
+                            save_dir=str(tmp_path / "out"))
+        loaders = T.make_loaders(cfg, tr, va, rank=world - 1, world=world)[:2]
+        for ld in loaders:
+            assert ld.num_workers > 0 and ld.persistent_workers
+            ctx = ld.multiprocessing_context
+            assert ctx is not None and ctx.get_start_method() == "spawn", (workers, world, ctx)
+    src = inspect.getsource(T)
+    assert '"fork"' not in src and "'fork'" not in src  # no fork start method named anywhere
+    assert inspect.getsource(T.initialize_training).count("DataLoader(") == 0

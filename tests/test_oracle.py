@@ -98,3 +98,49 @@ def test_damped_golden_pins_oracle():
     e, _ = mg.grad_errors(grads[torch.float32], grads[torch.float64])
     assert abs(e - g["ref_fp32_vs_fp64"]["global"]) < 0.2 * g["ref_fp32_vs_fp64"]["global"]
     assert e < 2e-3  # the point is well conditioned (vs 2.2e-2 at seeded init)
+
+
+def _load(name):
+    import json
+
+    import tests.golden.make_golden as mg
+
+    with open(mg.OUT / name) as f:
+        return json.load(f)
+
+
+def test_two_rank_golden_pins_oracle():
+    """golden_b8_damped_2rank.json (the reference's DDP step, two ranks of 4 samples at the damped point):
+    the oracle reproduces each rank's per-sample losses (per-shard train-mode BN)."""
+    import tests.golden.make_golden as mg
+
+    g = _load("golden_b8_damped_2rank.json")
+    c = g["config"]
+    x = mg.synthetic_images(c["batch"], *c["hw"], seed=c["image_seed"])
+    T = mg.synthetic_targets(c["batch"], seed=c["target_seed"])
+    assert abs(float(x.double().sum()) - g["images_sum"]) < 1e-3
+    m = mg.damp_residual(build_reference_model(42), c["damp"]).train()
+    with torch.no_grad():
+        for r, (xs, ts) in enumerate(mg.shards(x, T, g["ddp"]["world"])):
+            l = se3.geometric_loss(m(xs), ts)
+            assert (l - torch.tensor(g["step"]["loss"][r])).abs().max().item() < 1e-5, r
+    assert g["ref_fp32_vs_fp64"]["global"] < 2e-3  # well conditioned, as the single-rank point
+
+
+def test_trajectory_golden_pins_oracle():
+    """golden_b8_damped_traj.json: the oracle reproduces the first step's losses, the schedule really
+    reduces the learning rate inside the 10 steps, and fp32 stays close to fp64 over the trajectory."""
+    import tests.golden.make_golden as mg
+
+    g = _load("golden_b8_damped_traj.json")
+    c = g["config"]
+    assert c == mg.TRAJ
+    (x, T), = mg.trajectory_batches(c)[0][:1]
+    m = mg.damp_residual(build_reference_model(42), c["damp"]).train()
+    with torch.no_grad():
+        l = se3.geometric_loss(m(x), T)
+    assert (l - torch.tensor(g["fp32"]["steps"][0]["loss"])).abs().max().item() < 1e-5
+    lrs = [s["lr"] for s in g["fp32"]["steps"]]
+    assert lrs == [s["lr"] for s in g["fp64"]["steps"]] and min(lrs) < c["lr"]
+    for s32, s64 in zip(g["fp32"]["steps"], g["fp64"]["steps"]):
+        assert max(abs(a - b) for a, b in zip(s32["loss"], s64["loss"])) < 1e-2
