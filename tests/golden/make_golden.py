@@ -401,7 +401,9 @@ def run_trajectory(ref_models, dt):
     return steps, {"param_sums": _sums(sd, ("weight", "bias")),
                    "bn_running_sums": _sums(sd, ("running_mean", "running_var")),
                    "num_batches_tracked": int(sd["resnet.bn1.num_batches_tracked"]),
-                   "param_sample": param_sample(m)}
+                   "param_sample": param_sample(m),
+                   "bn_running": {k: [float(f"{x:.8g}") for x in v.double().tolist()] for k, v in sd.items()
+                                  if k.endswith(("running_mean", "running_var"))}}
 
 
 def param_sample(model, per_tensor: int = 64) -> dict:
@@ -411,7 +413,7 @@ def param_sample(model, per_tensor: int = 64) -> dict:
     for n, p in model.named_parameters():
         flat = p.detach().double().flatten()
         idx = torch.linspace(0, flat.numel() - 1, min(flat.numel(), per_tensor)).round().long()
-        out[n] = flat[idx].tolist()
+        out[n] = [float(f"{x:.10g}") for x in flat[idx].tolist()]
     return out
 
 
@@ -424,6 +426,10 @@ def trajectory_golden(ref_models) -> None:
     flat = lambda d: torch.tensor([v for k in init for v in d[k]], dtype=torch.float64)  # noqa: E731
     upd = (flat(end64["param_sample"]) - flat(init)).norm()
     e_ref = ((flat(end32["param_sample"]) - flat(end64["param_sample"])).norm() / upd).item()
+    rs = lambda d: torch.cat([torch.tensor(d[k], dtype=torch.float64) for k in sorted(d)])  # noqa: E731
+    rs0 = torch.cat([torch.zeros(len(v)) if k.endswith("mean") else torch.ones(len(v))
+                     for k, v in sorted(end64["bn_running"].items())]).double()
+    e_rs = ((rs(end32["bn_running"]) - rs(end64["bn_running"])).norm() / (rs(end64["bn_running"]) - rs0).norm()).item()
     out = {
         "generator": "tests/golden/make_golden.py::trajectory_golden",
         "pinned_against": "reference argus/models.py executed with oracle.resnet as torchvision.models",
@@ -433,12 +439,14 @@ def trajectory_golden(ref_models) -> None:
         "param_sample_init": init,
         # || p32 - p64 || / || p64 - p_init || over the sample: the reference fp32's own update error
         "ref_fp32_update_error": e_ref,
+        # the same for the BN running statistics (update from their initial 0 / 1)
+        "ref_fp32_running_stats_error": e_rs,
     }
     with open(OUT / "golden_b8_damped_traj.json", "w") as f:
-        json.dump(out, f, indent=1)
+        json.dump(out, f, separators=(",", ":"))
     spread = [max(abs(a - b) for a, b in zip(p["loss"], q["loss"])) for p, q in zip(s32, s64)]
     print("wrote", OUT / "golden_b8_damped_traj.json", "lr", [s["lr"] for s in s32], "val", [s["val_loss"] for s in s32],
-          "fp32-fp64 loss spread", spread, "update error", e_ref)
+          "fp32-fp64 loss spread", spread, "update error", e_ref, "running stats error", e_rs)
 
 
 if __name__ == "__main__":

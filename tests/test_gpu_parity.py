@@ -354,10 +354,9 @@ def test_fp32_ten_step_trajectory_matches_reference(cuda):
 
     Stated tolerances, against the fp64 trajectory with the reference fp32's own spread from it
     (s_t = max |l32 - l64| at step t): per-step losses within 4 s_t + 2e-5 (1 + |l|); validation loss
-    within 4 |v32 - v64| + 2e-5; the learning rate identical at every step; end-of-trajectory BN
-    running-statistic sums within 4x the reference fp32's distance from fp64 + 1e-4 (1 + |.|); the
-    parameters' 10-step update, on a fixed subsample of every tensor, no further from fp64 than 2x the
-    reference fp32's update is (relative L2 of the update)."""
+    within 4 |v32 - v64| + 2e-5; the learning rate identical at every step; at the end, the BN running
+    statistics' update and the parameters' update (a fixed subsample of every tensor) no further from
+    fp64 than 2x the reference fp32's are (relative L2 of the update)."""
     from argus_amd.losses import geometric_loss_fn
     from argus_amd.step import FusedTrainer
     from argus_amd.train import PlateauScheduler
@@ -388,14 +387,18 @@ def test_fp32_ten_step_trajectory_matches_reference(cuda):
         vbar = 4 * abs(s32["val_loss"] - s64["val_loss"]) + 2e-5
         assert abs(vl - s64["val_loss"]) <= vbar, (t, vl, s64["val_loss"])
         assert tr.lr == s64["lr"] == s32["lr"], (t, tr.lr, s64["lr"])
+    # BN running statistics (EMA of the batch statistics of a drifting network): their update from the
+    # initial 0 / 1, relative L2 against fp64, within 2x the reference fp32's own error
     sd = m.state_dict()
-    e32, e64 = g["fp32"]["end"]["bn_running_sums"], g["fp64"]["end"]["bn_running_sums"]
-    for k, (s64_, a64) in e64.items():  # BN running statistics: EMA of batch statistics, smooth in the weights
-        v = sd[k].double().cpu()
-        s32_, a32 = e32[k]
-        tol_s = 4 * abs(s32_ - s64_) + 1e-4 * (1 + abs(a64))
-        tol_a = 4 * abs(a32 - a64) + 1e-4 * (1 + abs(a64))
-        assert abs(v.sum().item() - s64_) <= tol_s and abs(v.abs().sum().item() - a64) <= tol_a, (k, v.sum().item(), s64_)
+    e64 = g["fp64"]["end"]["bn_running"]
+    keys = sorted(e64)
+    rs64 = torch.cat([torch.tensor(e64[k], dtype=torch.float64) for k in keys])
+    rs0 = torch.cat([(torch.zeros if k.endswith("mean") else torch.ones)(len(e64[k]), dtype=torch.float64)
+                     for k in keys])
+    ours_rs = torch.cat([sd[k].double().cpu().flatten() for k in keys])
+    e_rs = ((ours_rs - rs64).norm() / (rs64 - rs0).norm()).item()
+    print(f"BN running statistics vs fp64: ours {e_rs:.3e}, reference fp32 {g['ref_fp32_running_stats_error']:.3e}")
+    assert e_rs <= 2 * g["ref_fp32_running_stats_error"], e_rs
     # parameters: Adam moves every element by ~lr per step whatever its gradient's size, so elements with
     # near-zero gradients wander (the reference's own fp32 trajectory is 11 % of the update away from
     # fp64); compare the update itself on a fixed subsample of every tensor (golden param_sample)
