@@ -1014,6 +1014,9 @@ static int g_smallk_max = 1024;
 // argus_conv_tuning key 18: stem forward kernel, 2 (ring) or 4 (single buffer; convbench B=64:
 // 214 -> 179 us)
 static int g_stem_occ = 4;
+// argus_conv_tuning key 19: the bf16 stem forward on the LDS-patch kernel (stem.hip, 1) or on the
+// implicit GEMM (0)
+static int g_stem_halo = 1;
 
 // MX-fp8 operands (ARGUS_FP8) need whole 128-element k-steps inside one filter tap and no staging
 // transform of the A operand; other convs of an fp8 network run the bf16 kernels
@@ -1070,6 +1073,7 @@ static int g_wgrad_target_blocks = 512;
 // in the full step 512 wins (+0.7 %): fewer fp32 split partials (for layer 4's 3x3, 7 splits wrote
 // 66 MB of partials against 8 MB of operands), which contend with the main stream for HBM
 static int g_wgrad_target_3x3 = 512;
+static int g_wgrad_split_floor = 1;  // key 33 (A/B): splits = floor(target / tiles) (1) or ceil (0)
 
 static int* tuning_slot(int key) {
   if (key >= 0 && key < 3) return &g_force_bm[key];
@@ -1085,12 +1089,14 @@ static int* tuning_slot(int key) {
     case 13: return &g_halo_min_grid;
     case 14: return &g_wg_halo_max_tiles;
     case 18: return &g_stem_occ;
+    case 19: return &g_stem_halo;
     case 20: return &g_bwd_min_px;    // bn.hip: BN-backward pixels per block (min)
     case 21: return &g_bwd_max_rows;  //   ... and blocks per channel group (max)
     case 22: return &g_ew_target;     //   bn_apply / bwd_apply target blocks
     case 23: return &g_ew_min_ppt;    //   ... min pixels per thread
     case 24: return &g_fin_div;       //   BN finalize group-count divisor
     case 27: return &g_wgrad_target_3x3;
+    case 33: return &g_wgrad_split_floor;
     case 30: return &g_halo64;
     case 32: return &g_halo_epi_prefetch;
     default: return nullptr;
@@ -1168,6 +1174,8 @@ int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, 
                         (double)d.n * d.ho * d.wo * d.k) +
                    (stats ? 8.0 * conv_fwd_stat_rows(d, dtype) * d.k : 0.0);
   if (d.stem && sc) { set_error("conv_fwd: stem has no prologue"); return ARGUS_ERR_ARG; }
+  if (d.stem && g_stem_halo && stem_fwd_launch(d, dtype, x, w, y, stats, st))  // stem.hip (bf16)
+    return check_launch("stem_fwd_kernel");
   IgParams p;
   fwd_params(d, p);
   p.a = x; p.b = w; p.c = y; p.pro_scale = sc; p.pro_shift = sh;
@@ -1370,7 +1378,9 @@ static WgPlan wgrad_plan(const argus_conv_desc& d, int dtype) {
   // (2048 when Cout = 64: one row tile, 9 column tiles)
   long target = g_wgrad_target_blocks;
   if (target == 512 && d.r == 3) target = d.k <= 64 ? 2048 : g_wgrad_target_3x3;
-  long splits = (target + tiles - 1) / tiles;
+  // the grid (tiles x splits) stays within the target: a grid just past it (e.g. 36 tiles x 15 splits
+  // = 540 for 512 two-per-CU slots) runs a second, nearly empty round of workgroups
+  long splits = g_wgrad_split_floor ? target / tiles : (target + tiles - 1) / tiles;
   const long max_splits = (P + pl.kstep * 4 - 1) / (pl.kstep * 4);  // >= 4 k-steps per split
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
@@ -1464,7 +1474,9 @@ int conv_wgrad(const argus_conv_desc& d, int dtype, const void* x, const float* 
   p.M = d.k; p.N = pl.N; p.Cin = d.stem ? 4 : d.c; p.lda = d.stem ? 4 : d.c;
   p.H = d.h; p.W = d.w; p.Ho = d.ho; p.Wo = d.wo; p.stride = d.stride; p.pad = d.pad; p.S = d.s;
   p.P = d.n * d.ho * d.wo; p.pps = pl.pps; p.stem = d.stem;
-  p.group = d.s == 1 && pl.N == d.c ? 1 : 0;  // 1x1: a split's tiles on one XCD (3x3: spread, measured)
+  // a split's tiles on one XCD for the 1x1 convs and the stem (its two 128-column tiles then share the
+  // XCD's L2 copy of the split's dy: read once from HBM, not twice); 3x3: spread (measured faster)
+  p.group = (d.s == 1 && pl.N == d.c) || d.stem ? 1 : 0;
   p.fd_hw = make_fastdiv(d.ho * d.wo); p.fd_w = make_fastdiv(d.wo);
   if (d.stem && sc) { set_error("conv_wgrad: stem has no prologue"); return ARGUS_ERR_ARG; }
   int splits = pl.splits;

@@ -174,23 +174,30 @@ struct BwdEpiAcc {
   }
 
   // Fixed-order reduction over the RG row groups of the workgroup (thread = (row group rg, chunk c))
-  // through LDS red[RG][COLS] (float2), written as partial row `row` of columns col0..col0+COLS.
+  // through LDS red[E][RG][CPR] (float2; CPR = COLS / E chunks), written as partial row `row` of
+  // columns col0..col0+COLS. Element j of every thread's chunk goes to its own [RG][CPR] plane, so the
+  // 16 lanes of a ds_write_b64 group (consecutive chunks, one row group) fill 128 contiguous bytes and
+  // the summing lanes (consecutive chunks of one element plane) read contiguous slots: no bank
+  // conflicts (a [RG][COLS] layout put a wave's lanes 64 bytes apart: 8-way on the writes).
   template <int COLS, int NT>
   ARGUS_DEV void reduce(const BnBwdEpi& b, float2* red, int rg, int RG, int c, size_t row, int N, int col0) {
+    constexpr int CPR = COLS / E;
 #pragma unroll
     for (int br = 0; br < (BwdMode<BW>::DUAL ? 2 : 1); ++br) {
 #pragma unroll
       for (int j = 0; j < E; ++j) {
         float tv = t[j];
         if constexpr (BwdMode<BW>::DUAL) tv = br == 0 ? t[j] : t2[j];
-        red[rg * COLS + c * E + j] = make_float2(s[j], tv);
+        red[(j * RG + rg) * CPR + c] = make_float2(s[j], tv);
       }
       __syncthreads();
       float2* out = (br == 0 ? b.part : b.part2) + row * N + col0;
       for (int idx = threadIdx.x; idx < COLS; idx += NT) {
-        float2 a = red[idx];
-        for (int g = 1; g < RG; ++g) { a.x += red[g * COLS + idx].x; a.y += red[g * COLS + idx].y; }
-        store_part(out + idx, a);  // write-through: the folded finalize (bnfin.h) reads it cross-CU
+        const int cc = idx % CPR, j = idx / CPR;  // column cc * E + j
+        const float2* plane = red + j * RG * CPR + cc;
+        float2 a = plane[0];
+        for (int g = 1; g < RG; ++g) { a.x += plane[g * CPR].x; a.y += plane[g * CPR].y; }
+        store_part(out + cc * E + j, a);  // write-through: the folded finalize (bnfin.h) reads it cross-CU
       }
       __syncthreads();
     }
@@ -275,6 +282,10 @@ bool conv3x3_halo_launch(const IgParams& p, hipStream_t st);
 // 3x3 stride-1 weight gradient with an LDS-resident halo tile (conv_halo.hip): plan / launch of the
 // split partials (fp32 [splits][K][9C]); false = not served
 bool wgrad3x3_halo_plan(const argus_conv_desc& d, int dtype, int* splits, int* tiles_per_split);
+// stem forward on an LDS input patch (stem.hip): false = shape / dtype not served
+bool stem_fwd_ok(const argus_conv_desc& d, int dtype);
+bool stem_fwd_launch(const argus_conv_desc& d, int dtype, const void* x, const void* w, void* y, float* stats,
+                     hipStream_t st);
 bool wgrad3x3_halo_launch(const argus_conv_desc& d, int dtype, const void* x, const float* sc, const float* sh,
                           const void* dy, void* ws, size_t ws_bytes, int* splits, hipStream_t st);
 

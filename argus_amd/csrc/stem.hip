@@ -1,0 +1,189 @@
+// ResNet-50 stem convolution (torchvision conv1: 7x7, stride 2, pad 3, 3 -> 64 channels, bias=False;
+// argus/models.py:43) forward, bf16, with the input patch of each output tile staged in LDS once.
+//
+// Why: the implicit GEMM (conv.hip, STEM variant) gathers its im2col operand from global memory per
+// k-step: every input pixel is fetched by ~12 output pixels (49 taps at stride 2), and its K of 256
+// = (8 rows x 8 cols x 4 channels) carries a zero filter row. Here a workgroup owns an 8 x 32 output
+// tile (256 pixels x 64 channels): it loads the (2*8+5) x (2*32+6) input patch (NHWC4, 8 bytes a
+// pixel) and the 64 x 224 filter once, then runs K = 7 filter rows x 32 (8 columns x 4 channels, the
+// 8th column's weights are zero) straight from LDS: the A fragment of lane (pixel j, group g) for
+// filter row r is the two adjacent input pixels (2j + 2g, 2j + 2g + 1) of patch row 2i + r, one
+// 16-byte read.
+//
+// Epilogue as igemm_kernel's forward: BN statistics {sum, M2} per 128 output pixels (the tile's two
+// halves: rows 0-3 and 4-7), the C tile staged through LDS and written as 16-byte non-temporal stores.
+// Served: bf16, output H and W multiples of 8 and 32 (256 x 256 inputs); other shapes keep conv.hip.
+#include "common.h"
+#include "bnfin.h"
+#include "internal.h"
+#include "ktimer.h"
+
+namespace argus {
+
+namespace {
+constexpr int kTH = 8, kTW = 32;           // output tile
+constexpr int kPR = 2 * kTH + 5;           // patch rows (21)
+constexpr int kPC = 2 * kTW + 6;           // patch columns (70): column pc = input column 2*ow0 - 3 + pc
+constexpr int kWS = 7 * 32 + 8;            // LDS weight row stride, elements (224 + 8: 464 B, conflict-free)
+constexpr int kPatchB = kPR * kPC * 8;     // 11760
+constexpr int kWB = 64 * kWS * 2;          // 29696
+constexpr int kLD = 64 + 8;                // C staging row stride, elements
+constexpr int kLdsB = (kPatchB + kWB) > 256 * kLD * 2 ? (kPatchB + kWB) : 256 * kLD * 2;
+}  // namespace
+
+struct StemParams {
+  const bf16* x;   // (n, H, W, 4) bf16, channel 3 zero
+  const bf16* w;   // w_fwd of the stem: [64][8][8][4] (r, s, c), padding zero
+  bf16* y;         // (n, Ho, Wo, 64)
+  float2* stats;   // {sum, M2} per 128 output pixels x 64 channels, or null
+  int n, H, W, Ho, Wo;
+};
+
+__global__ __launch_bounds__(256, 3) void stem_fwd_kernel(const StemParams p) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsB];
+  uint2* patch = reinterpret_cast<uint2*>(lds);
+  bf16* wl = reinterpret_cast<bf16*>(lds + kPatchB);
+
+  const int tpr = p.Wo / kTW, tpi = (p.Ho / kTH) * tpr;  // tiles per tile-row, per image
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int img = tile / tpi, rem = tile - img * tpi;
+  const int oh0 = (rem / tpr) * kTH, ow0 = (rem % tpr) * kTW;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+
+  // ---- stage the input patch (zero outside the image) and the 64 x 224 filter ----
+  const uint2* X = reinterpret_cast<const uint2*>(p.x) + (size_t)img * p.H * p.W;
+  const int ih0 = 2 * oh0 - 3, iw0 = 2 * ow0 - 3;
+  uint2 pv[(kPR * kPC + 255) / 256];
+#pragma unroll
+  for (int i = 0; i < (kPR * kPC + 255) / 256; ++i) {
+    const int q = tid + 256 * i;
+    const int pr = q / kPC, pc = q - pr * kPC;
+    const int ih = ih0 + pr, iw = iw0 + pc;
+    const bool ok = q < kPR * kPC && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+    const uint2 v = X[ok ? ih * p.W + iw : 0];
+    pv[i] = ok ? v : make_uint2(0u, 0u);
+  }
+  u32x4 wv[7];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {  // 64 rows x 28 chunks of 16 B (filter rows 0..6)
+    const int q = tid + 256 * i;
+    const int n = q / 28, ch = q - n * 28;
+    wv[i] = ld16(p.w + n * 256 + ch * 8);
+  }
+#pragma unroll
+  for (int i = 0; i < (kPR * kPC + 255) / 256; ++i) {
+    const int q = tid + 256 * i;
+    if (q < kPR * kPC) patch[q] = pv[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    const int q = tid + 256 * i;
+    const int n = q / 28, ch = q - n * 28;
+    *reinterpret_cast<u32x4*>(wl + n * kWS + ch * 8) = wv[i];
+  }
+  __syncthreads();
+
+  // ---- MFMA: wave w owns tile rows 2w, 2w+1 (64 pixels) x 64 channels ----
+  const int g = lane >> 4, i16 = lane & 15;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const uint8_t* pb = lds;
+#pragma unroll
+  for (int r = 0; r < 7; ++r) {
+    u32x4 fa[4], fb[4];
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      const int tr = 2 * wave + (mi >> 1), j = (mi & 1) * 16 + i16;
+      fa[mi] = *reinterpret_cast<const u32x4*>(pb + ((2 * tr + r) * kPC + 2 * j + 2 * g) * 8);
+    }
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+      fb[ni] = *reinterpret_cast<const u32x4*>(wl + (ni * 16 + i16) * kWS + r * 32 + g * 8);
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[mi]),
+                                                              __builtin_bit_cast(bf16x8, fb[ni]), acc[mi][ni], 0, 0, 0);
+  }
+  __syncthreads();  // LDS is reused below
+
+  // ---- BN statistics: {sum, M2} per 64-pixel wave, merged per 128-pixel half (waves 2h, 2h+1) ----
+  const size_t tile_lin = (size_t)img * tpi + rem;
+  if (p.stats) {
+    float2* red = reinterpret_cast<float2*>(lds);  // [4 waves][64]
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      float s = 0.f;
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s += acc[mi][ni][r];
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      const float mean_w = s * (1.f / 64.f);
+      float q = 0.f;
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float d = acc[mi][ni][r] - mean_w;
+          q = fmaf(d, d, q);
+        }
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      if (lane < 16) red[wave * 64 + ni * 16 + lane] = make_float2(s, q);
+    }
+    __syncthreads();
+    if (tid < 128) {
+      const int h = tid >> 6, col = tid & 63;
+      const float2 a0 = red[(2 * h) * 64 + col], a1 = red[(2 * h + 1) * 64 + col];
+      const float d = (a0.x - a1.x) * (1.f / 64.f);
+      store_part(p.stats + (tile_lin * 2 + h) * 64 + col, make_float2(a0.x + a1.x, a0.y + a1.y + d * d * 32.f));
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: C tile through LDS, 16-byte coalesced non-temporal stores ----
+  bf16* Cs = reinterpret_cast<bf16*>(lds);
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        Cs[(wave * 64 + mi * 16 + g * 4 + r) * kLD + ni * 16 + i16] = (bf16)acc[mi][ni][r];
+  __syncthreads();
+  const int c = tid & 7;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = (tid >> 3) + 32 * i;  // C row: tile row m / 32, column m % 32
+    const int oh = oh0 + (m >> 5), ow = ow0 + (m & 31);
+    const u32x4 v = *reinterpret_cast<const u32x4*>(Cs + m * kLD + c * 8);
+    st16_nt(p.y + (((size_t)img * p.Ho + oh) * p.Wo + ow) * 64 + c * 8, v);
+  }
+}
+
+bool stem_fwd_ok(const argus_conv_desc& d, int dtype) {
+  return dtype == ARGUS_BF16 && d.stem && d.k == 64 && d.ho % kTH == 0 && d.wo % kTW == 0;
+}
+
+// The partial-row layout this kernel writes equals argus_conv_fwd_stat_rows / _stat_tile (128)
+bool stem_fwd_launch(const argus_conv_desc& d, int dtype, const void* x, const void* w, void* y, float* stats,
+                     hipStream_t st) {
+  if (!stem_fwd_ok(d, dtype)) return false;
+  StemParams p;
+  p.x = reinterpret_cast<const bf16*>(x);
+  p.w = reinterpret_cast<const bf16*>(w);
+  p.y = reinterpret_cast<bf16*>(y);
+  p.stats = reinterpret_cast<float2*>(stats);
+  p.n = d.n; p.H = d.h; p.W = d.w; p.Ho = d.ho; p.Wo = d.wo;
+  const int grid = d.n * (d.ho / kTH) * (d.wo / kTW);
+  timed_launch("argus::stem_fwd_kernel", stem_fwd_kernel, dim3(grid), dim3(256), st, p);
+  return true;
+}
+
+}  // namespace argus

@@ -163,13 +163,15 @@ int argus_conv_dgrad_bn(const argus_conv_desc* d, int dtype, const void* dy, con
  * forward/dgrad, key 11 the same for the 3x3 stride-1 weight gradient and key 12 its split target,
  * key 13 the fewest workgroups for the fwd/dgrad halo kernel (1 also allows its 64-channel variant
  * at any size), key 14 the most (64 x 64) channel tiles for the wgrad halo kernel, key 18 the stem
- * forward occupancy (2 | 4), keys 20-23 the BatchNorm elementwise-kernel geometry (backward min
+ * forward occupancy (2 | 4) of the implicit GEMM, key 19 the bf16 stem forward on the LDS-patch
+ * kernel (1) or the implicit GEMM (0), keys 20-23 the BatchNorm elementwise-kernel geometry (backward min
  * pixels per block, max blocks per channel group; apply target blocks, min pixels per thread), key
  * 24 the BN finalize group-count divisor, key 27 the split target of the register-staged 3x3 weight
  * gradient, key 30 the 64-channel 3x3 stride-1 layers on the LDS-halo kernel's single-halo-buffer
  * variant (1) or on the implicit GEMM (0), key 32 where the 3x3 LDS-halo dgrad with a BN-backward
  * epilogue prefetches its epilogue operands under its last channel chunk (1: the single-halo-buffer
- * variant; 2 every variant; 0 none).
+ * variant; 2 every variant; 0 none), key 33 the weight-gradient split count floor(target / tiles)
+ * (1) or ceil (0).
  * Returns 0, or -1 for an unknown key. */
 int argus_conv_tuning(int key, int value);
 /* Current value of a tuning key (-1 for an unknown key). */

@@ -177,6 +177,50 @@ def test_stem_fwd_wgrad(cuda, dt):
         assert e < (TOL[dt] if dt == "fp32" else 2e-3), f"stem wgrad {hw} {dt}: {e}"
 
 
+def test_stem_lds_patch_kernel(cuda):
+    """bf16 stem forward on the LDS-patch kernel (stem.hip: 8 x 32 output tiles, K = 7 filter rows x 32)
+    vs torch (bf16 tolerance) and vs the implicit GEMM it replaces (tuning key 19 = 0): outputs within
+    the bf16 tolerance of each other, BN statistics partials (one per 128 pixels) merging to the same
+    mean / variance; shapes whose output does not tile (19 x 15) keep the implicit GEMM."""
+    from argus_amd.profiling import KernelTimer
+
+    torch.manual_seed(33)
+    L = lib()
+    for n, H, W, served in ((2, 64, 128, True), (1, 256, 256, True), (3, 38, 30, False)):
+        d, p = _desc(n, H, W, 3, 64, 7, 2, stem=True)
+        img = torch.rand(n, 3, H, W)
+        x4 = torch.empty(n, H, W, 4, dtype=torch.bfloat16, device=cuda)
+        imgg = img.to(cuda)
+        L.images_to_nhwc4(BF16, n, H, W, ptr(imgg), ptr(x4), stream())
+        w = torch.randn(64, 7, 7, 3) * 0.1
+        wmaster = w.permute(0, 3, 1, 2).contiguous().to(cuda)
+        wf = torch.empty(64, 256, dtype=torch.bfloat16, device=cuda)
+        strides = (C.c_int64 * 4)(*wmaster.stride())
+        L.conv_weight_prep(C.byref(d), BF16, ptr(wmaster), strides, ptr(wf), None, stream())
+        ref = F.conv2d(_q(img, "bf16"), _q(w, "bf16").permute(0, 3, 1, 2), stride=2, padding=3)
+        rows = L.dll.argus_conv_fwd_stat_rows(C.byref(d), BF16)
+        tile = L.dll.argus_conv_fwd_stat_tile(C.byref(d), BF16)
+        M = n * d.ho * d.wo
+        outs = []
+        for key19 in (1, 0):
+            y = torch.empty(n, d.ho, d.wo, 64, dtype=torch.bfloat16, device=cuda)
+            stats = torch.full((rows, 64, 2), float("nan"), device=cuda)
+            with _tuned({19: key19}):
+                with KernelTimer() as t:
+                    L.conv_fwd(C.byref(d), BF16, ptr(x4), ptr(wf), ptr(y), None, None, ptr(stats), stream())
+                names = list(t.summary())
+            assert ("argus::stem_fwd_kernel" in names) == (served and key19 == 1), (n, H, W, key19, names)
+            assert _rel(y.permute(0, 3, 1, 2), ref) < TOL["bf16"], ("stem fwd", n, H, W, key19)
+            assert torch.isfinite(stats).all()
+            mean, var = _merge_stats(stats.double().cpu(), tile, M)
+            yr = ref.permute(0, 2, 3, 1).reshape(-1, 64)
+            assert (mean - yr.mean(0)).abs().max() < 2e-2 * yr.std(0).max(), ("stats mean", n, H, W, key19)
+            assert _rel(var, yr.var(0, unbiased=False)) < 2e-2, ("stats var", n, H, W, key19)
+            outs.append((y.float(), mean, var))
+        assert _rel(outs[0][0], outs[1][0]) < 1e-2
+        assert _rel(outs[0][2], outs[1][2]) < 1e-4 and (outs[0][1] - outs[1][1]).abs().max() < 1e-4
+
+
 @pytest.mark.parametrize("dt", ["fp32", "bf16"])
 def test_bn_train_forward_backward(cuda, dt):
     """finalize + apply(+residual, relu) + backward reduce/finalize/apply vs autograd BatchNorm2d."""
