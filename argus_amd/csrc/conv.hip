@@ -1017,6 +1017,9 @@ static int g_stem_occ = 4;
 // argus_conv_tuning key 19: the bf16 stem forward on the LDS-patch kernel (stem.hip, 1) or on the
 // implicit GEMM (0)
 static int g_stem_halo = 1;
+// argus_conv_tuning key 34: the bf16 stem weight gradient on the LDS-patch kernel (stem.hip, 1) or on
+// wgrad_kernel's STEM variant (0)
+static int g_stem_wg = 1;
 
 // MX-fp8 operands (ARGUS_FP8) need whole 128-element k-steps inside one filter tap and no staging
 // transform of the A operand; other convs of an fp8 network run the bf16 kernels
@@ -1097,6 +1100,7 @@ static int* tuning_slot(int key) {
     case 24: return &g_fin_div;       //   BN finalize group-count divisor
     case 27: return &g_wgrad_target_3x3;
     case 33: return &g_wgrad_split_floor;
+    case 34: return &g_stem_wg;
     case 30: return &g_halo64;
     case 32: return &g_halo_epi_prefetch;
     default: return nullptr;
@@ -1397,6 +1401,10 @@ size_t conv_wgrad_ws(const argus_conv_desc& d, int dtype) {
   const WgPlan pl = wgrad_plan(d, dtype);
   size_t b = (size_t)pl.splits * d.k * pl.N * sizeof(float);
   int hs, htps;
+  if (stem_wgrad_plan(d, dtype, &hs, &htps)) {
+    const size_t sb = (size_t)hs * 64 * 256 * sizeof(float);
+    b = sb > b ? sb : b;
+  }
   if (wgrad3x3_halo_plan(d, dtype, &hs, &htps)) {
     const size_t hb = (size_t)hs * d.k * 9 * d.c * sizeof(float);
     b = hb > b ? hb : b;
@@ -1480,7 +1488,9 @@ int conv_wgrad(const argus_conv_desc& d, int dtype, const void* x, const float* 
   p.fd_hw = make_fastdiv(d.ho * d.wo); p.fd_w = make_fastdiv(d.wo);
   if (d.stem && sc) { set_error("conv_wgrad: stem has no prologue"); return ARGUS_ERR_ARG; }
   int splits = pl.splits;
-  if (g_wg_apply) {  // the register-staged kernel stages the apply; no halo / glds variant does
+  if (d.stem && g_stem_wg && stem_wgrad_launch(d, dtype, x, dy, g_wg_apply, ws, ws_bytes, &splits, st)) {
+    if (int e = check_launch("stem_wgrad_kernel")) return e;
+  } else if (g_wg_apply) {  // the register-staged kernel stages the apply; no halo / glds variant does
     if (dtype == ARGUS_BF16) dispatch_wg<bf16>(p, pl, st);
     else dispatch_wg<float>(p, pl, st);
     if (int e = check_launch("wgrad_kernel")) return e;

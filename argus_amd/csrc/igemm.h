@@ -286,6 +286,11 @@ bool wgrad3x3_halo_plan(const argus_conv_desc& d, int dtype, int* splits, int* t
 bool stem_fwd_ok(const argus_conv_desc& d, int dtype);
 bool stem_fwd_launch(const argus_conv_desc& d, int dtype, const void* x, const void* w, void* y, float* stats,
                      hipStream_t st);
+// stem weight gradient on the LDS patch + dy tile (stem.hip): split plan and launch of the fp32
+// partials [splits][64][256]; ap = the fused BN-backward apply (dy = ca*dm + cb*y + cc) or null
+bool stem_wgrad_plan(const argus_conv_desc& d, int dtype, int* splits, int* tiles_per_split);
+bool stem_wgrad_launch(const argus_conv_desc& d, int dtype, const void* x, const void* dm,
+                       const argus_bn_bwd_prologue* ap, void* ws, size_t ws_bytes, int* splits, hipStream_t st);
 bool wgrad3x3_halo_launch(const argus_conv_desc& d, int dtype, const void* x, const float* sc, const float* sh,
                           const void* dy, void* ws, size_t ws_bytes, int* splits, hipStream_t st);
 

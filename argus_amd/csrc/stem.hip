@@ -13,6 +13,15 @@
 // Epilogue as igemm_kernel's forward: BN statistics {sum, M2} per 128 output pixels (the tile's two
 // halves: rows 0-3 and 4-7), the C tile staged through LDS and written as 16-byte non-temporal stores.
 // Served: bf16, output H and W multiples of 8 and 32 (256 x 256 inputs); other shapes keep conv.hip.
+//
+// The weight gradient (stem_wgrad_kernel) uses the same tile: dW[oc][(r, s, c)] = sum over pixels of
+// dy[px][oc] * patch(2i + r, 2j + s)[c]. Both MFMA operands need 8 consecutive PIXELS per lane, which
+// ds_read_b64_tr_b16 provides from pixel-major LDS rows: for dy (rows of 64 channels) and for the
+// patch, where the 16 k-columns (s0..s0+3) x 4 channels of filter row r at output pixel (i, j) are
+// the 32 contiguous bytes at patch(2i + r, 2j + s0). So the im2col operand is never materialised:
+// a workgroup stages dy (staged through the BN-backward apply when fused) and the patch once per
+// 256-pixel tile, loops over its run of tiles with the next tile's loads in flight, and writes one
+// fp32 64 x 256 partial per split for wgrad_reduce_kernel.
 #include "common.h"
 #include "bnfin.h"
 #include "internal.h"
@@ -165,6 +174,189 @@ __global__ __launch_bounds__(256, 3) void stem_fwd_kernel(const StemParams p) {
     const u32x4 v = *reinterpret_cast<const u32x4*>(Cs + m * kLD + c * 8);
     st16_nt(p.y + (((size_t)img * p.Ho + oh) * p.Wo + ow) * 64 + c * 8, v);
   }
+}
+
+// ------------------------------------------------------------------------------------------------
+// weight gradient
+// ------------------------------------------------------------------------------------------------
+namespace {
+constexpr int kDyB = 256 * 128;  // dy tile: 256 pixel rows x 64 channels bf16
+constexpr int kWgLdsB = kDyB + kPatchB;
+constexpr int kPatchPT = (kPR * kPC + 255) / 256;  // patch pixels per thread (6)
+// dy row slot swizzle (4 slots of 32 B per 128-B row): the 8 rows one ds_read_b64_tr_b16 half-wave
+// touches (q = 0..3 of two 8-row groups) land on 8 distinct (row parity, slot) bank spans
+ARGUS_DEV int dswz(int row) { return ((row >> 1) & 1) | (((row >> 3) & 1) << 1); }
+}  // namespace
+
+struct StemWgParams {
+  const bf16* x;    // (n, H, W, 4)
+  const bf16* dm;   // dy, or dm of the fused BN-backward apply: (n, Ho, Wo, 64)
+  const bf16* y;    // apply: y (same layout), else null
+  const float *ca, *cb, *cc;  // apply: dy = ca*dm + cb*y + cc per channel
+  float* part;      // [splits][64][256] fp32 (columns (r, s, c) = r*32 + s*4 + c; s = 7 and r = 7 unused)
+  int n, H, W, Ho, Wo, tiles, tps;
+};
+
+template <bool AP>
+__global__ __launch_bounds__(256, 2) void stem_wgrad_kernel(const StemWgParams p) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kWgLdsB];
+  uint8_t* dyl = lds;
+  uint2* patch = reinterpret_cast<uint2*>(lds + kDyB);
+
+  const int split = blockIdx.x;
+  const int t0 = split * p.tps, t1 = min(p.tiles, t0 + p.tps);
+  const int tpr = p.Wo / kTW, tpi = (p.Ho / kTH) * tpr;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c8 = tid & 7;  // this thread's 8-channel chunk of every dy row it stages
+
+  float ca[8], cb[8], cc[8];
+  if constexpr (AP) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { ca[j] = p.ca[c8 * 8 + j]; cb[j] = p.cb[c8 * 8 + j]; cc[j] = p.cc[c8 * 8 + j]; }
+  }
+
+  struct Stage {
+    u32x4 d[8], y[AP ? 8 : 1];
+    uint2 x[kPatchPT];
+  } S;
+  auto load = [&](int tile) {
+    const int img = tile / tpi, rem = tile - img * tpi;
+    const int oh0 = (rem / tpr) * kTH, ow0 = (rem % tpr) * kTW;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = (tid >> 3) + 32 * i;  // tile pixel: row i of the tile, column tid >> 3
+      const size_t off = (((size_t)img * p.Ho + oh0 + (row >> 5)) * p.Wo + ow0 + (row & 31)) * 64 + c8 * 8;
+      S.d[i] = ld16(p.dm + off);
+      if constexpr (AP) S.y[i] = ld16(p.y + off);
+    }
+    const uint2* X = reinterpret_cast<const uint2*>(p.x) + (size_t)img * p.H * p.W;
+    const int ih0 = 2 * oh0 - 3, iw0 = 2 * ow0 - 3;
+#pragma unroll
+    for (int i = 0; i < kPatchPT; ++i) {
+      const int q = tid + 256 * i;
+      const int pr = q / kPC, pc = q - pr * kPC;
+      const int ih = ih0 + pr, iw = iw0 + pc;
+      const bool ok = q < kPR * kPC && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+      const uint2 v = X[ok ? ih * p.W + iw : 0];
+      S.x[i] = ok ? v : make_uint2(0u, 0u);
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = (tid >> 3) + 32 * i;
+      u32x4 v = S.d[i];
+      if constexpr (AP) {  // argus_bn_bwd_apply's formula, fp32, rounded to bf16 (as wgrad_kernel's AP)
+        float d[8], yv[8];
+        unpack(v, d);
+        unpack(S.y[i], yv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d[j] = fmaf(ca[j], d[j], fmaf(cb[j], yv[j], cc[j]));
+        v = pack(d);
+      }
+      *reinterpret_cast<u32x4*>(dyl + row * 128 + (((c8 >> 1) ^ dswz(row)) << 5) + (c8 & 1) * 16) = v;
+    }
+#pragma unroll
+    for (int i = 0; i < kPatchPT; ++i) {
+      const int q = tid + 256 * i;
+      if (q < kPR * kPC) patch[q] = S.x[i];
+    }
+  };
+
+  // wave w: output channels 32*(w & 1) .. +31 (two 16-blocks) x k-column blocks 7*(w >> 1) .. +6
+  // (block nb: filter row nb >> 1, columns s0 = 4*(nb & 1) .. s0+3, 4 channels each)
+  const int wm = wave & 1, wn = wave >> 1;
+  const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, pq = i16 & 3;
+  f32x4 acc[2][7];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 7; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto tr_read = [](const uint8_t* a0, const uint8_t* a1) {
+    const s16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (s16x4 __attribute__((address_space(3)))*)(uintptr_t)(uint32_t)(uintptr_t)a0);
+    const s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (s16x4 __attribute__((address_space(3)))*)(uintptr_t)(uint32_t)(uintptr_t)a1);
+    const uint2 u0 = __builtin_bit_cast(uint2, t0), u1 = __builtin_bit_cast(uint2, t1);
+    return __builtin_bit_cast(bf16x8, u32x4{u0.x, u0.y, u1.x, u1.y});
+  };
+
+  if (t0 < t1) load(t0);
+  for (int t = t0; t < t1; ++t) {
+    store();
+    __syncthreads();
+    if (t + 1 < t1) load(t + 1);  // in flight while this tile's MFMAs run
+#pragma unroll 1
+    for (int ks = 0; ks < kTH; ++ks) {  // k-step = one tile row (32 pixels)
+      // lane (g, i16) reads pixels j = 8g + 4h + q, h = 0, 1: its operand's 8 k-values (pixels 8g .. 8g+7)
+      bf16x8 fa[2], fb[7];
+#pragma unroll
+      for (int m2 = 0; m2 < 2; ++m2) {
+        const int mi = 2 * wm + m2;
+        const int r0 = 32 * ks + 8 * g + q, r1 = r0 + 4;
+        fa[m2] = tr_read(dyl + r0 * 128 + ((mi ^ dswz(r0)) << 5) + pq * 8,
+                         dyl + r1 * 128 + ((mi ^ dswz(r1)) << 5) + pq * 8);
+      }
+      const uint8_t* pb = lds + kDyB;
+#pragma unroll
+      for (int t7 = 0; t7 < 7; ++t7) {
+        const int nb = 7 * wn + t7, r = nb >> 1, s0 = (nb & 1) * 4;
+        const int j0 = 8 * g + q;
+        const uint8_t* a0 = pb + ((2 * ks + r) * kPC + 2 * j0 + s0 + pq) * 8;
+        fb[t7] = tr_read(a0, a0 + 8 * 8);  // pixel j0 + 4: 8 patch columns further
+      }
+#pragma unroll
+      for (int m2 = 0; m2 < 2; ++m2)
+#pragma unroll
+        for (int t7 = 0; t7 < 7; ++t7)
+          acc[m2][t7] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[m2], fb[t7], acc[m2][t7], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+
+  // C[oc = 16*mi + 4g + e][col = 16*nb + i16]
+  float* out = p.part + (size_t)split * 64 * 256;
+#pragma unroll
+  for (int m2 = 0; m2 < 2; ++m2)
+#pragma unroll
+    for (int t7 = 0; t7 < 7; ++t7)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        out[(16 * (2 * wm + m2) + 4 * g + e) * 256 + 16 * (7 * wn + t7) + i16] = acc[m2][t7][e];
+}
+
+static bool stem_wg_shape_ok(const argus_conv_desc& d, int dtype) {
+  return dtype == ARGUS_BF16 && d.stem && d.k == 64 && d.ho % kTH == 0 && d.wo % kTW == 0;
+}
+
+// splits: ~2 workgroups per CU (the LDS of two 43.5 KB tiles), each a run of whole tiles
+bool stem_wgrad_plan(const argus_conv_desc& d, int dtype, int* splits, int* tps) {
+  if (!stem_wg_shape_ok(d, dtype)) return false;
+  const int tiles = d.n * (d.ho / kTH) * (d.wo / kTW);
+  int t = (tiles + 511) / 512;
+  *tps = t;
+  *splits = (tiles + t - 1) / t;
+  return true;
+}
+
+bool stem_wgrad_launch(const argus_conv_desc& d, int dtype, const void* x, const void* dm,
+                       const argus_bn_bwd_prologue* ap, void* ws, size_t ws_bytes, int* splits, hipStream_t st) {
+  int s, tps;
+  if (!stem_wgrad_plan(d, dtype, &s, &tps)) return false;
+  if (ws_bytes < (size_t)s * 64 * 256 * sizeof(float)) return false;
+  StemWgParams p;
+  p.x = reinterpret_cast<const bf16*>(x);
+  p.dm = reinterpret_cast<const bf16*>(dm);
+  p.y = ap ? reinterpret_cast<const bf16*>(ap->y) : nullptr;
+  p.ca = ap ? ap->ca : nullptr; p.cb = ap ? ap->cb : nullptr; p.cc = ap ? ap->cc : nullptr;
+  p.part = reinterpret_cast<float*>(ws);
+  p.n = d.n; p.H = d.h; p.W = d.w; p.Ho = d.ho; p.Wo = d.wo;
+  p.tiles = d.n * (d.ho / kTH) * (d.wo / kTW); p.tps = tps;
+  if (ap) timed_launch("argus::stem_wgrad_kernel<true>", stem_wgrad_kernel<true>, dim3(s), dim3(256), st, p);
+  else timed_launch("argus::stem_wgrad_kernel<false>", stem_wgrad_kernel<false>, dim3(s), dim3(256), st, p);
+  *splits = s;
+  return true;
 }
 
 bool stem_fwd_ok(const argus_conv_desc& d, int dtype) {

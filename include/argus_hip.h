@@ -171,7 +171,8 @@ int argus_conv_dgrad_bn(const argus_conv_desc* d, int dtype, const void* dy, con
  * variant (1) or on the implicit GEMM (0), key 32 where the 3x3 LDS-halo dgrad with a BN-backward
  * epilogue prefetches its epilogue operands under its last channel chunk (1: the single-halo-buffer
  * variant; 2 every variant; 0 none), key 33 the weight-gradient split count floor(target / tiles)
- * (1) or ceil (0).
+ * (1) or ceil (0), key 34 the bf16 stem weight gradient on the LDS-patch kernel (1) or on the
+ * register-staged weight-gradient kernel (0).
  * Returns 0, or -1 for an unknown key. */
 int argus_conv_tuning(int key, int value);
 /* Current value of a tuning key (-1 for an unknown key). */

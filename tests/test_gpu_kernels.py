@@ -221,6 +221,53 @@ def test_stem_lds_patch_kernel(cuda):
         assert _rel(outs[0][2], outs[1][2]) < 1e-4 and (outs[0][1] - outs[1][1]).abs().max() < 1e-4
 
 
+def test_stem_wgrad_lds_patch_kernel(cuda):
+    """bf16 stem weight gradient on the LDS-patch kernel (stem.hip: dy tile + input patch, both MFMA
+    operands read pixel-major with ds_read_b64_tr_b16) vs torch's conv2d_weight and vs wgrad_kernel's
+    STEM variant it replaces (tuning key 34 = 0), with dy given and with dy staged through the fused
+    BN-backward apply (argus_conv_wgrad_apply). 304 x 1856: 551 tiles -> 2 per split, the last split
+    ragged; 38 x 30 does not tile and keeps wgrad_kernel."""
+    from argus_amd._lib import BnBwdPrologue
+    from argus_amd.profiling import KernelTimer
+
+    torch.manual_seed(34)
+    L = lib()
+    for n, H, W, served in ((2, 64, 128, True), (1, 304, 1856, True), (3, 38, 30, False)):
+        d, _ = _desc(n, H, W, 3, 64, 7, 2, stem=True)
+        img = torch.rand(n, 3, H, W)
+        x4 = torch.empty(n, H, W, 4, dtype=torch.bfloat16, device=cuda)
+        imgg = img.to(cuda)
+        L.images_to_nhwc4(BF16, n, H, W, ptr(imgg), ptr(x4), stream())
+        dm = torch.randn(n, d.ho, d.wo, 64, device=cuda).to(torch.bfloat16)
+        y0 = torch.randn(n, d.ho, d.wo, 64, device=cuda).to(torch.bfloat16)
+        ca, cb, cc = (torch.randn(64, device=cuda) * 0.3 for _ in range(3))
+        dy_ap = (ca * dm.float() + (cb * y0.float() + cc)).to(torch.bfloat16)  # fmaf rounding aside
+        ws = torch.empty(L.dll.argus_conv_wgrad_workspace_bytes(C.byref(d), BF16), dtype=torch.uint8, device=cuda)
+        for apply in (False, True):
+            dyq = dy_ap if apply else dm
+            ref = torch.nn.grad.conv2d_weight(_q(img, "bf16"), (64, 3, 7, 7), dyq.double().cpu().permute(0, 3, 1, 2),
+                                              stride=2, padding=3)
+            outs = []
+            for key34 in (1, 0):
+                dw = torch.full((64, 7, 7, 3), float("nan"), device=cuda)
+                with _tuned({34: key34}):
+                    with KernelTimer() as t:
+                        if apply:
+                            ap = BnBwdPrologue(ptr(y0), ptr(ca), ptr(cb), ptr(cc), None)
+                            L.conv_wgrad_apply(C.byref(d), BF16, ptr(x4), ptr(dm), C.byref(ap), ptr(dw), ptr(ws),
+                                               ws.numel(), stream())
+                        else:
+                            L.conv_wgrad(C.byref(d), BF16, ptr(x4), None, None, ptr(dm), ptr(dw), ptr(ws),
+                                         ws.numel(), stream())
+                    names = list(t.summary())
+                want = f"argus::stem_wgrad_kernel<{'true' if apply else 'false'}>"
+                assert (want in names) == (served and key34 == 1), (n, H, W, apply, key34, names)
+                e = _rel(dw.permute(0, 3, 1, 2), ref)
+                assert e < 2e-3, ("stem wgrad", n, H, W, apply, key34, e)
+                outs.append(dw.clone())
+            assert _rel(outs[0], outs[1]) < 2e-3
+
+
 @pytest.mark.parametrize("dt", ["fp32", "bf16"])
 def test_bn_train_forward_backward(cuda, dt):
     """finalize + apply(+residual, relu) + backward reduce/finalize/apply vs autograd BatchNorm2d."""
