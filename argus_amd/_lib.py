@@ -18,7 +18,7 @@ import torch  # noqa: F401  (must precede the CDLL, see module docstring)
 LIB_PATH = Path(os.environ.get("ARGUS_HIP_LIB", Path(__file__).resolve().parent / "libargus_hip.so"))
 
 F32, BF16, FP8 = 0, 1, 2
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 
 class ConvDesc(C.Structure):
@@ -97,6 +97,7 @@ SIGNATURES = {
     "argus_avgpool_bwd": (_I, [_I, _I, _I, _I, _P, _P, _P]),
     "argus_gemm_f32_workspace_bytes": (_SZ, [_I, _I, _I]),
     "argus_augment_params_bytes": (_SZ, []),
+    "argus_augment_scratch_bytes": (_SZ, [_I64, _I, _I]),
     "argus_augment_photometric": (_I, [_I64, _I, _I, _P, _P, _P, _P, _P]),
     "argus_gemm_f32": (_I, [_I, _I, _I, _P, _I, _I, _P, _I, _I, _P, _I, _P, _I, _P, _P, _SZ, _P]),
     "argus_colsum_f32": (_I, [_I, _I, _P, _I, _P, _P]),

@@ -1,20 +1,30 @@
 // Photometric training augmentations on the device: the sequence of argus/data.py:41-103
-// (Planckian jitter -> ColorJiggle -> Gaussian blur -> motion blur -> plasma shadow) applied to a
-// uint8 batch after the host->device copy, replacing kornia on the CPU data-loader workers.
+// (random erasing x2 -> Planckian jitter -> ColorJiggle -> Gaussian blur -> motion blur -> plasma
+// shadow -> salt-and-pepper) applied to a uint8 batch after the host->device copy, replacing kornia
+// on the CPU data-loader workers.
 //
 // Per-image parameters are sampled on the host (argus_amd/augment.py, seeded torch generator, the
 // reference's ranges) and passed as AugParams. The arithmetic restates kornia's published
 // definitions (kornia is not installed here, so parity with kornia itself is unpinned; the tests pin
-// these kernels to a torch restatement of the same formulas):
+// these kernels to a float64 restatement of the same formulas, tests/aug_reference.py):
+//   erasing     pixels of a (y0, x0, h, w) rectangle set to `value` in all channels (RandomErasing;
+//               rectangle drawn on the host as kornia's random_rectangles_params_generator)
+//   Planckian   per-channel gains of a blackbody white point (mode "blackbody"), clamp [0, 1]
 //   brightness  x + (b - 1)                       (kornia adjust_brightness, additive), clamp [0, 1]
 //   contrast    x * c                             (adjust_contrast, multiplicative), clamp [0, 1]
 //   saturation  HSV s * f, clamp [0, 1]           (adjust_saturation)
 //   hue         HSV h + 2*pi*f mod 2*pi           (adjust_hue)
-//   Planckian   per-channel gains of a blackbody white point (mode "blackbody")
 //   blur        5x5 Gaussian, separable, reflect borders
 //   motion      3x3 line kernel (host-built from angle / direction), zero borders
-//   plasma      x * (1 + intensity * [noise < quantity]), fractal value noise with amplitude decay
-//               `roughness` per octave
+//   plasma      x + intensity * [map < quantity], clamp [0, 1]; map = diamond-square plasma fractal
+//               (kornia diamond_square): a (2^k + 1)^2 grid, 2^k >= max(H, W) - 1, corners U[0, 1),
+//               then per level (step halving) the diamond step (square centres = mean of the 4
+//               corners) and the square step (edge midpoints = mean of the in-grid neighbours at
+//               +-step/2), each plus (U - 0.5) * roughness^(level + 1); cropped to H x W and min-max
+//               normalized to [0, 1]
+//   salt/pepper per pixel (all channels): U < amount -> (U' < salt_vs_pepper ? 1 : 0)
+// The random numbers of the plasma map and the salt-and-pepper mask are a hash of (image seed,
+// stream, index) - reproducible and identical in the restatement.
 // Layout: images planar NCHW (n_img, 3, H, W); the 6-channel sample is two such images.
 #include "common.h"
 #include "internal.h"
@@ -29,7 +39,11 @@ struct AugParams {
   float blur_w[5];     // normalized 5-tap Gaussian (blur_w[2] == 0 => no blur)
   float motion[9];     // 3x3 motion kernel (all 0 => no motion blur)
   float plasma_int, plasma_q, plasma_rough;  // plasma shadow (intensity 0 => off)
-  unsigned seed;
+  unsigned seed;       // plasma map seed
+  int erase[2][4];     // random erasing rectangles: y0, x0, h, w (h == 0 => off), applied in order
+  float erase_val[2];
+  float sp_amount, sp_salt;  // salt-and-pepper (amount 0 => off)
+  unsigned sp_seed;
 };
 
 ARGUS_DEV float clamp01(float x) { return fminf(fmaxf(x, 0.f), 1.f); }
@@ -66,7 +80,7 @@ ARGUS_DEV void hsv2rgb(float h, float s, float v, float& r, float& g, float& b) 
 }
 
 // one thread per pixel: /255, Planckian gains, ColorJiggle ops in the sampled order -> fp32
-__global__ __launch_bounds__(256) void aug_color_kernel(int64_t nimg, int hw, const uint8_t* __restrict__ src,
+__global__ __launch_bounds__(256) void aug_color_kernel(int64_t nimg, int hw, int w, const uint8_t* __restrict__ src,
                                                         float* __restrict__ dst, const AugParams* __restrict__ prm) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= nimg * hw) return;
@@ -76,7 +90,16 @@ __global__ __launch_bounds__(256) void aug_color_kernel(int64_t nimg, int hw, co
   const uint8_t* s = src + img * 3 * hw + px;
   float c[3];
 #pragma unroll
-  for (int k = 0; k < 3; ++k) c[k] = clamp01((float)s[(int64_t)k * hw] / 255.0f * P.gain[k]);
+  for (int k = 0; k < 3; ++k) c[k] = (float)s[(int64_t)k * hw] / 255.0f;
+  const int py = (int)(px / w), pxx = (int)(px - (int64_t)py * w);
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int* r = P.erase[e];
+    if (r[2] > 0 && py >= r[0] && py < r[0] + r[2] && pxx >= r[1] && pxx < r[1] + r[3])
+      c[0] = c[1] = c[2] = P.erase_val[e];
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) c[k] = clamp01(c[k] * P.gain[k]);
   if (P.jiggle) {
 #pragma unroll
     for (int o = 0; o < 4; ++o) {
@@ -136,36 +159,108 @@ __global__ __launch_bounds__(256) void aug_blur_kernel(int64_t nimg, int h, int 
   (pass == 0 ? tmp : x)[plane * hw + p] = acc;
 }
 
-// hashed lattice value noise in [0, 1)
-ARGUS_DEV float lattice(unsigned seed, int o, int gx, int gy) {
-  unsigned hsh = seed * 0x9E3779B1u ^ (unsigned)o * 0x85EBCA77u ^ (unsigned)gx * 0xC2B2AE3Du ^ (unsigned)gy * 0x27D4EB2Fu;
-  hsh ^= hsh >> 15; hsh *= 0x2C1B3C6Du; hsh ^= hsh >> 12; hsh *= 0x297A2D39u; hsh ^= hsh >> 15;
-  return (float)(hsh >> 8) * (1.0f / 16777216.0f);
+// counter-based uniform in [0, 1): hash of (seed, stream, index)
+ARGUS_DEV float hash_u01(unsigned seed, unsigned stream, unsigned idx) {
+  unsigned h = seed * 0x9E3779B1u ^ stream * 0x85EBCA77u ^ idx * 0xC2B2AE3Du;
+  h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12; h *= 0x297A2D39u; h ^= h >> 15;
+  return (float)(h >> 8) * (1.0f / 16777216.0f);
 }
 
-// plasma-like fractal noise at (y, x): octaves of bilinear value noise, cell size halving, amplitude
-// x roughness per octave, normalized to [0, 1)
-ARGUS_DEV float plasma(unsigned seed, float rough, int h, int w, int y, int x) {
-  float cell = (float)(h > w ? h : w) * 0.5f, amp = 1.f, sum = 0.f, norm = 0.f;
-  for (int o = 0; o < 6 && cell >= 1.f; ++o) {
-    const float fy = y / cell, fx = x / cell;
-    const int gy = (int)floorf(fy), gx = (int)floorf(fx);
-    const float ty = fy - gy, tx = fx - gx;
-    const float v00 = lattice(seed, o, gx, gy), v01 = lattice(seed, o, gx + 1, gy);
-    const float v10 = lattice(seed, o, gx, gy + 1), v11 = lattice(seed, o, gx + 1, gy + 1);
-    const float v = (v00 * (1.f - tx) + v01 * tx) * (1.f - ty) + (v10 * (1.f - tx) + v11 * tx) * ty;
-    sum = fmaf(amp, v, sum);
-    norm += amp;
-    amp *= rough;
-    cell *= 0.5f;
+// diamond-square grid side: 2^k + 1 with 2^k >= max(h, w) - 1 (k >= 1)
+static int ds_side(int h, int w) {
+  int k = 1;
+  while ((1 << k) < (h > w ? h : w) - 1) ++k;
+  return (1 << k) + 1;
+}
+
+// corners of every plasma image's grid (stream 0)
+__global__ __launch_bounds__(256) void aug_ds_seed_kernel(int64_t nimg, int S, float* __restrict__ map,
+                                                          const AugParams* __restrict__ prm) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nimg * 4) return;
+  const int64_t img = i >> 2;
+  const AugParams& P = prm[img];
+  if (P.plasma_int == 0.f) return;
+  const int c = (int)(i & 3);
+  const int y = (c >> 1) * (S - 1), x = (c & 1) * (S - 1);
+  map[img * S * S + (int64_t)y * S + x] = hash_u01(P.seed, 0u, (unsigned)(y * S + x));
+}
+
+// one level's diamond (phase 0: square centres) or square (phase 1: edge midpoints) step; step =
+// distance between the points already set, m = (S - 1) / step squares per side; stream 1 + 2*level + phase
+__global__ __launch_bounds__(256) void aug_ds_step_kernel(int64_t nimg, int S, int level, int step, int phase,
+                                                          float* __restrict__ map, const AugParams* __restrict__ prm) {
+  const int m = (S - 1) / step, half = step >> 1;
+  const int64_t count = phase == 0 ? (int64_t)m * m : 2LL * m * (m + 1);
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nimg * count) return;
+  const int64_t img = i / count;
+  const AugParams& P = prm[img];
+  if (P.plasma_int == 0.f) return;
+  const int t = (int)(i - img * count);
+  float amp = 1.f;
+  for (int l = 0; l <= level; ++l) amp *= P.plasma_rough;
+  float* g = map + img * S * S;
+  int y, x;
+  float mean;
+  if (phase == 0) {
+    y = (t / m) * step + half;
+    x = (t % m) * step + half;
+    mean = 0.25f * ((g[(y - half) * S + x - half] + g[(y - half) * S + x + half]) +
+                    (g[(y + half) * S + x - half] + g[(y + half) * S + x + half]));
+  } else {
+    const int mm = m * (m + 1);
+    if (t < mm) {  // rows on the coarse grid, midpoints between its columns
+      y = (t / m) * step;
+      x = (t % m) * step + half;
+    } else {       // rows between, on the coarse columns
+      y = ((t - mm) / (m + 1)) * step + half;
+      x = ((t - mm) % (m + 1)) * step;
+    }
+    float sum = 0.f;
+    int cnt = 0;
+    if (y - half >= 0) { sum += g[(y - half) * S + x]; ++cnt; }
+    if (y + half < S) { sum += g[(y + half) * S + x]; ++cnt; }
+    if (x - half >= 0) { sum += g[y * S + x - half]; ++cnt; }
+    if (x + half < S) { sum += g[y * S + x + half]; ++cnt; }
+    mean = sum / (float)cnt;
   }
-  return sum / norm;
+  const float u = hash_u01(P.seed, 1u + 2u * level + phase, (unsigned)(y * S + x));
+  g[y * S + x] = fmaf(u - 0.5f, amp, mean);
+}
+
+// min and max of each plasma map over its H x W crop (one workgroup per image)
+__global__ __launch_bounds__(256) void aug_ds_minmax_kernel(int h, int w, int S, const float* __restrict__ map,
+                                                            float2* __restrict__ mm, const AugParams* __restrict__ prm) {
+  const int64_t img = blockIdx.x;
+  if (prm[img].plasma_int == 0.f) return;
+  const float* g = map + img * S * S;
+  float lo = 3.4e38f, hi = -3.4e38f;
+  for (int i = threadIdx.x; i < h * w; i += 256) {
+    const int y = i / w, x = i - y * w;
+    const float v = g[y * S + x];
+    lo = fminf(lo, v);
+    hi = fmaxf(hi, v);
+  }
+  __shared__ float sl[256], sh[256];
+  sl[threadIdx.x] = lo;
+  sh[threadIdx.x] = hi;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      sl[threadIdx.x] = fminf(sl[threadIdx.x], sl[threadIdx.x + o]);
+      sh[threadIdx.x] = fmaxf(sh[threadIdx.x], sh[threadIdx.x + o]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) mm[img] = make_float2(sl[0], sh[0]);
 }
 
 // motion blur (3x3, zero borders) from x into tmp for the images that have it, then plasma shadow
 // and the final write: pass 0 = motion into tmp, pass 1 = x <- (motion ? tmp : x) * shade
 __global__ __launch_bounds__(256) void aug_motion_plasma_kernel(int64_t nimg, int h, int w, float* __restrict__ x,
-                                                                float* __restrict__ tmp,
+                                                                float* __restrict__ tmp, const float* __restrict__ map,
+                                                                const float2* __restrict__ mm, int S,
                                                                 const AugParams* __restrict__ prm, int pass) {
   const int64_t hw = (int64_t)h * w;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -193,11 +288,19 @@ __global__ __launch_bounds__(256) void aug_motion_plasma_kernel(int64_t nimg, in
     return;
   }
   float v = motion ? tmp[plane * hw + p] : x[plane * hw + p];
+  const int64_t img = plane / 3;
   if (P.plasma_int != 0.f) {
-    const float n = plasma(P.seed, P.plasma_rough, h, w, y, xx);
-    if (n < P.plasma_q) v *= 1.f + P.plasma_int;
+    const float2 r = mm[img];
+    const float d = r.y - r.x;
+    const float n = d > 0.f ? (map[img * S * S + (int64_t)y * S + xx] - r.x) / d : 0.f;
+    if (n < P.plasma_q) v += P.plasma_int;
   }
-  x[plane * hw + p] = clamp01(v);
+  v = clamp01(v);
+  if (P.sp_amount > 0.f) {
+    const unsigned idx = (unsigned)p;
+    if (hash_u01(P.sp_seed, 0u, idx) < P.sp_amount) v = hash_u01(P.sp_seed, 1u, idx) < P.sp_salt ? 1.f : 0.f;
+  }
+  x[plane * hw + p] = v;
 }
 
 }  // namespace argus
@@ -207,6 +310,12 @@ using namespace argus;
 extern "C" {
 
 size_t argus_augment_params_bytes(void) { return sizeof(AugParams); }
+
+size_t argus_augment_scratch_bytes(int64_t nimg, int h, int w) {
+  if (nimg <= 0 || h <= 0 || w <= 0) return 0;
+  const int64_t S = ds_side(h, w);
+  return sizeof(float) * (size_t)(nimg * 3 * (int64_t)h * w + nimg * S * S + 2 * nimg);
+}
 
 int argus_augment_photometric(int64_t nimg, int h, int w, const uint8_t* src, float* dst, const void* params,
                               float* scratch, argus_stream_t stream) {
@@ -218,11 +327,25 @@ int argus_augment_photometric(int64_t nimg, int h, int w, const uint8_t* src, fl
   const AugParams* prm = reinterpret_cast<const AugParams*>(params);
   const int64_t hw = (int64_t)h * w;
   const unsigned g1 = (unsigned)((nimg * hw + 255) / 256), g3 = (unsigned)((nimg * 3 * hw + 255) / 256);
-  hipLaunchKernelGGL(aug_color_kernel, dim3(g1), dim3(256), 0, st, nimg, (int)hw, src, dst, prm);
+  const int S = ds_side(h, w);
+  float* map = scratch + nimg * 3 * hw;
+  float2* mm = reinterpret_cast<float2*>(map + nimg * S * S);
+  hipLaunchKernelGGL(aug_color_kernel, dim3(g1), dim3(256), 0, st, nimg, (int)hw, w, src, dst, prm);
   for (int pass = 0; pass < 2; ++pass)
     hipLaunchKernelGGL(aug_blur_kernel, dim3(g3), dim3(256), 0, st, nimg, h, w, dst, scratch, prm, pass);
+  // plasma maps: seed the corners, then one launch per level and phase (each reads the previous)
+  hipLaunchKernelGGL(aug_ds_seed_kernel, dim3((unsigned)((nimg * 4 + 255) / 256)), dim3(256), 0, st, nimg, S, map, prm);
+  for (int step = S - 1, level = 0; step >= 2; step >>= 1, ++level)
+    for (int phase = 0; phase < 2; ++phase) {
+      const int64_t m = (S - 1) / step;
+      const int64_t count = phase == 0 ? m * m : 2 * m * (m + 1);
+      hipLaunchKernelGGL(aug_ds_step_kernel, dim3((unsigned)((nimg * count + 255) / 256)), dim3(256), 0, st, nimg,
+                         S, level, step, phase, map, prm);
+    }
+  hipLaunchKernelGGL(aug_ds_minmax_kernel, dim3((unsigned)nimg), dim3(256), 0, st, h, w, S, map, mm, prm);
   for (int pass = 0; pass < 2; ++pass)
-    hipLaunchKernelGGL(aug_motion_plasma_kernel, dim3(g3), dim3(256), 0, st, nimg, h, w, dst, scratch, prm, pass);
+    hipLaunchKernelGGL(aug_motion_plasma_kernel, dim3(g3), dim3(256), 0, st, nimg, h, w, dst, scratch, map, mm, S,
+                       prm, pass);
   return check_launch("augment_photometric");
 }
 

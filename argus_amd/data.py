@@ -46,8 +46,8 @@ _warned = False
 @dataclass(frozen=True)
 class AugmentationConfig:
     """Same fields as argus/data.py:18-39. ``num_spaghetti`` is applied by the dataset; the photometric
-    flags by ``argus_amd.augment.DeviceAugmentation`` on the device (random erasing and salt-and-pepper,
-    off in the reference's defaults, are not provided)."""
+    flags (random erasing and salt-and-pepper included, off in the reference's defaults) by
+    ``argus_amd.augment.DeviceAugmentation`` on the device."""
 
     brightness: Union[float, tuple] = (0.8, 1.0)
     contrast: Union[float, tuple] = (0.5, 1.2)

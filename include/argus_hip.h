@@ -313,9 +313,11 @@ int argus_se3_exp(int batch, const float* xi, float* out, int canonical_w, argus
  * src: uint8 images (n_img, 3, H, W) planar (a B x 6 x H x W sample batch is 2B such images);
  * dst: fp32 (same shape) = augmented src / 255; params: n_img AugParams records of
  * argus_augment_params_bytes() bytes each (device memory; layout in augment.hip / augment.py);
- * scratch: n_img * 3 * H * W floats. Planckian gains -> ColorJiggle (sampled op order) -> 5x5
- * Gaussian blur (reflect) -> 3x3 motion blur (zero border) -> plasma shadow, per image. */
+ * scratch: argus_augment_scratch_bytes() bytes. Random erasing (two rectangles) -> Planckian gains
+ * -> ColorJiggle (sampled op order) -> 5x5 Gaussian blur (reflect) -> 3x3 motion blur (zero border)
+ * -> plasma shadow (diamond-square map) -> salt-and-pepper, per image. */
 size_t argus_augment_params_bytes(void);
+size_t argus_augment_scratch_bytes(int64_t n_img, int h, int w);
 int argus_augment_photometric(int64_t n_img, int h, int w, const uint8_t* src, float* dst, const void* params,
                               float* scratch, argus_stream_t stream);
 

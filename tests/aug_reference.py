@@ -42,8 +42,9 @@ def hsv2rgb(h, s, v):
 
 
 def color(img_u8, P):
-    """(3, H, W) uint8 -> float64 after Planckian gains and the ColorJiggle ops."""
-    c = (img_u8.double() / 255.0 * torch.tensor(P["gain"], dtype=torch.float64)[:, None, None]).clamp(0, 1)
+    """(3, H, W) uint8 -> float64 after random erasing, Planckian gains and the ColorJiggle ops."""
+    c = erase(img_u8.double() / 255.0, P)
+    c = (c * torch.tensor(P["gain"], dtype=torch.float64)[:, None, None]).clamp(0, 1)
     if P["jiggle"]:
         for o in range(4):
             op = (int(P["order"]) >> (2 * o)) & 3
@@ -89,8 +90,11 @@ def motion(c, k9):
 M32 = 0xFFFFFFFF
 
 
-def lattice(seed, o, gx, gy):
-    h = ((seed * 0x9E3779B1) ^ (o * 0x85EBCA77) ^ (gx.astype(np.int64) * 0xC2B2AE3D) ^ (gy.astype(np.int64) * 0x27D4EB2F)) & M32
+def hash_u01(seed, stream, idx):
+    """augment.hip hash_u01: uniform in [0, 1) from (seed, stream, index), uint32 arithmetic."""
+    idx = np.asarray(idx, dtype=np.uint64)
+    h = ((int(seed) * 0x9E3779B1) & M32) ^ ((int(stream) * 0x85EBCA77) & M32) ^ ((idx * 0xC2B2AE3D) & M32)
+    h = np.asarray(h, dtype=np.uint64)
     h ^= h >> 15
     h = (h * 0x2C1B3C6D) & M32
     h ^= h >> 12
@@ -99,23 +103,64 @@ def lattice(seed, o, gx, gy):
     return (h >> 8).astype(np.float64) / 16777216.0
 
 
-def plasma(seed, rough, H, W):
-    y, x = np.meshgrid(np.arange(H), np.arange(W), indexing="ij")
-    cell, amp, tot, norm = max(H, W) * 0.5, 1.0, 0.0, 0.0
-    o = 0
-    while o < 6 and cell >= 1.0:
-        fy, fx = y / cell, x / cell
-        gy, gx = np.floor(fy).astype(np.int64), np.floor(fx).astype(np.int64)
-        ty, tx = fy - gy, fx - gx
-        v00, v01 = lattice(seed, o, gx, gy), lattice(seed, o, gx + 1, gy)
-        v10, v11 = lattice(seed, o, gx, gy + 1), lattice(seed, o, gx + 1, gy + 1)
-        v = (v00 * (1 - tx) + v01 * tx) * (1 - ty) + (v10 * (1 - tx) + v11 * tx) * ty
-        tot = tot + amp * v
-        norm += amp
-        amp *= float(np.float32(rough))
-        cell *= 0.5
-        o += 1
-    return torch.tensor(tot / norm)
+def diamond_square(seed, rough, H, W):
+    """The plasma map of augment.hip's header: (2^k + 1)^2 grid, corners U[0, 1), per level the
+    diamond then the square step with (U - 0.5) * rough^(level + 1) noise; H x W crop, min-max to [0, 1]."""
+    k = 1
+    while (1 << k) < max(H, W) - 1:
+        k += 1
+    S = (1 << k) + 1
+    g = np.zeros((S, S))
+    for y in (0, S - 1):
+        for x in (0, S - 1):
+            g[y, x] = hash_u01(seed, 0, y * S + x)
+    rough = float(np.float32(rough))
+    step, level, amp = S - 1, 0, 1.0
+    while step >= 2:
+        half = step // 2
+        amp = amp * rough
+        m = (S - 1) // step
+        # diamond
+        c = np.arange(m) * step + half
+        yy, xx = np.meshgrid(c, c, indexing="ij")
+        mean = 0.25 * ((g[yy - half, xx - half] + g[yy - half, xx + half]) + (g[yy + half, xx - half] + g[yy + half, xx + half]))
+        g[yy, xx] = mean + (hash_u01(seed, 1 + 2 * level, yy * S + xx) - 0.5) * amp
+        # square
+        ys1, xs1 = np.meshgrid(np.arange(m + 1) * step, np.arange(m) * step + half, indexing="ij")
+        ys2, xs2 = np.meshgrid(np.arange(m) * step + half, np.arange(m + 1) * step, indexing="ij")
+        ys, xs = np.concatenate([ys1.ravel(), ys2.ravel()]), np.concatenate([xs1.ravel(), xs2.ravel()])
+        tot, cnt = np.zeros(len(ys)), np.zeros(len(ys))
+        for dy, dx in ((-half, 0), (half, 0), (0, -half), (0, half)):
+            ny, nx = ys + dy, xs + dx
+            ok = (ny >= 0) & (ny < S) & (nx >= 0) & (nx < S)
+            tot[ok] += g[ny[ok], nx[ok]]
+            cnt[ok] += 1
+        g[ys, xs] = tot / cnt + (hash_u01(seed, 2 + 2 * level, ys * S + xs) - 0.5) * amp
+        step, level = half, level + 1
+    crop = g[:H, :W]
+    lo, hi = crop.min(), crop.max()
+    return torch.tensor((crop - lo) / (hi - lo) if hi > lo else np.zeros_like(crop))
+
+
+def erase(c, P):
+    for e in range(2):
+        y0, x0, h, w = (int(v) for v in P["erase"][e])
+        if h > 0:
+            c = c.clone()
+            c[:, y0:y0 + h, x0:x0 + w] = float(P["erase_val"][e])
+    return c
+
+
+def salt_pepper(c, P):
+    amount = float(np.float32(P["sp_amount"]))
+    if amount <= 0:
+        return c
+    H, W = c.shape[-2:]
+    idx = np.arange(H * W)
+    noisy = hash_u01(int(P["sp_seed"]), 0, idx) < amount
+    salt = hash_u01(int(P["sp_seed"]), 1, idx) < float(np.float32(P["sp_salt"]))
+    val = torch.tensor(salt.astype(np.float64)).reshape(H, W)
+    return torch.where(torch.tensor(noisy).reshape(H, W)[None], val[None], c)
 
 
 def augment_image(img_u8, P):
@@ -123,6 +168,6 @@ def augment_image(img_u8, P):
     c = blur(color(img_u8, P), P["blur_w"])
     c = motion(c, P["motion"])
     if float(P["plasma_int"]) != 0:
-        n = plasma(int(P["seed"]), P["plasma_rough"], *c.shape[-2:])
-        c = torch.where((n < float(P["plasma_q"]))[None], c * (1 + float(P["plasma_int"])), c)
-    return c.clamp(0, 1)
+        n = diamond_square(int(P["seed"]), P["plasma_rough"], *c.shape[-2:])
+        c = torch.where((n < float(np.float32(P["plasma_q"])))[None], c + float(np.float32(P["plasma_int"])), c)
+    return salt_pepper(c.clamp(0, 1), P)

@@ -56,17 +56,54 @@ def test_ops_match_restatement(cuda, ops):
     assert err < 2e-5, (ops, err)
 
 
-def test_plasma_shadow_matches_restatement(cuda):
+@pytest.mark.parametrize("hw", [(64, 64), (37, 70)])
+def test_plasma_shadow_matches_restatement(cuda, hw):
+    """Diamond-square plasma map (65 x 65 grid for 64 x 64; 129 x 129 cropped to 37 x 70) and the
+    additive shade, against the float64 restatement."""
     g = torch.Generator().manual_seed(2)
-    B, H, W = 1, 64, 64
+    B, (H, W) = 1, hw
     x = torch.randint(0, 256, (B, 6, H, W), generator=g, dtype=torch.uint8)
     p = _params(2, plasma_int=[-0.5, -0.3], plasma_q=[0.4, 0.2], plasma_rough=[0.3, 0.15], seed=[12345, 777])
     out = DeviceAugmentation(AugmentationConfig()).apply(x.to(cuda), p).cpu().double()
     want = torch.stack([ref.augment_image(x.reshape(2, 3, H, W)[i], p[i]) for i in range(2)]).reshape(B, 6, H, W)
     bad = ((out - want).abs() > 2e-5).double().mean().item()
     assert bad < 1e-3, bad  # fp32 vs fp64 noise can flip the threshold only at exact ties
-    shaded = (out < x.double() / 255.0 - 1e-6).double().mean().item()
-    assert 0.05 < shaded < 0.6, shaded  # a real shadow: some, not all, pixels darkened
+    for i, q in ((0, 0.4), (1, 0.2)):
+        m = ref.diamond_square(int(p["seed"][i]), p["plasma_rough"][i], H, W)
+        assert m.min() == 0 and m.max() == 1
+        shaded = (m < q).double().mean().item()
+        assert 0.005 < shaded < 0.9, shaded  # a real shadow: some, not all, pixels
+        cam = out[0, 3 * i:3 * i + 3]
+        src = x[0, 3 * i:3 * i + 3].double() / 255.0
+        dark = (cam < src - 1e-6).any(0)
+        assert (dark <= (m < q)).all()  # only shaded pixels get darker
+
+
+def test_erasing_and_salt_pepper_match_restatement(cuda):
+    """Two erasing rectangles (values 0 and 1, the second over the first) ahead of the colour ops,
+    salt-and-pepper last (after the clamp): against the restatement, bit-exact positions."""
+    g = torch.Generator().manual_seed(4)
+    B, H, W = 2, 40, 52
+    x = torch.randint(0, 256, (B, 6, H, W), generator=g, dtype=torch.uint8)
+    n = 2 * B
+    p = _params(n)
+    p["erase"][0, 0] = (3, 5, 10, 20)
+    p["erase"][0, 1] = (8, 15, 12, 9)
+    p["erase"][2, 1] = (0, 0, 40, 1)
+    p["erase_val"][:, 1] = 1.0
+    p["gain"][0] = (1.2, 1.0, 0.7)
+    p["sp_amount"] = [0.05, 0.0, 0.2, 0.01]
+    p["sp_salt"] = [0.5, 0.5, 0.4, 0.6]
+    p["sp_seed"] = [11, 12, 13, 14]
+    out = DeviceAugmentation(AugmentationConfig()).apply(x.to(cuda), p).cpu().double()
+    imgs = x.reshape(n, 3, H, W)
+    want = torch.stack([ref.augment_image(imgs[i], p[i]) for i in range(n)]).reshape(B, 6, H, W)
+    err = (out - want).abs().max().item()
+    assert err < 2e-5, err
+    o = out.reshape(n, 3, H, W)
+    assert (o[0, :, 3:8, 5:15] == 0).sum() > 0.8 * 3 * 5 * 10  # erased to 0 (salt may flip a few)
+    noisy = ((o[2] == 0) | (o[2] == 1)).all(0).double().mean().item()
+    assert 0.15 < noisy < 0.3, noisy
 
 
 def test_sampled_batch_runs_and_stays_in_range(cuda):
