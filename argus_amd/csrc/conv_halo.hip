@@ -393,9 +393,11 @@ bool conv3x3_halo_launch(const IgParams& p, hipStream_t st) {
 // 3x3 stride-1 weight gradient with the input halo tile in LDS (dW[k][tap][c] = sum_p dy[p][k] *
 // x[p + off(tap)][c]). A workgroup (8 waves, 2 x 4) owns 64
 // output channels x 9 taps x 64 input channels (a 64 x 576 tile; wave (wm, wn) holds rows 32wm..+31
-// and the 9 column blocks of 16 at 9wn..9wn+8) and reduces over a range of 128-pixel tiles (whole
-// rows of one image, or whole images when H*W < 128). Per tile it glds-loads dy [128 px][64 k] and
-// the x halo [(rows+2)*(W+2) positions][64 c] once (7 uniform 1 KB pieces per wave, double-buffered
+// and the 9 column blocks of 16 at 9wn..9wn+8) and reduces over a range of 128-pixel-slot tiles: a
+// TH x TW block of one image (TW divides W; 256 x 256 frames: whole rows, 376 x 672 frames: 3 x 42
+// blocks of the 168- and 84-wide layers, slots past TH*TW or below the image carry zero dy), or NI
+// whole images when H*W < 128. Per tile it glds-loads dy [128 slots][64 k] and the x halo
+// [(TH+2)*(TW+2) positions][64 c] once (7 uniform 1 KB pieces per wave, double-buffered
 // over tiles with a counted vmcnt); both MFMA operands are k(=pixel)-major, read with
 // ds_read_b64_tr_b16. Images are [row][128 B], 16-byte slot j of row r at slot j ^ wsw(r): the eight
 // rows a 32-lane half touches in one transposed read (r0..r0+3, r0+8..r0+11) hit distinct banks.
@@ -406,7 +408,9 @@ struct WgHaloParams {
   const bf16* dy;
   float* part;
   int n, H, W, C, K;
-  int ptiles, tps;  // 128-pixel tiles in total, tiles per split
+  int ptiles, tps;  // 128-slot tiles in total, tiles per split
+  int TH, TW, NI;   // tile block (TH x TW pixels of one image), images per tile (NI > 1: TH = H, TW = W)
+  int RT, CT;       // row / column blocks per image (NI == 1)
 };
 
 constexpr int kWgHaloPos = 320;
@@ -443,19 +447,17 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(const WgHaloParam
   const int wm = wave >> 2, wn = wave & 3;
   const uint32_t lds0 = (uint32_t)(uintptr_t)lds;
 
-  const int H = p.H, W = p.W, HWi = H * W;
-  int NI, R;
-  if (HWi >= 128) { NI = 1; R = 128 / W; } else { NI = 128 / HWi; R = H; }
-  const int HWD = W + 2, IMGP = (R + 2) * HWD, npos = NI * IMGP;
+  const int H = p.H, W = p.W, TH = p.TH, TW = p.TW, NI = p.NI, THW = TH * TW;
+  const int HWD = TW + 2, IMGP = (TH + 2) * HWD, npos = NI * IMGP;
 
-
-  // fragment geometry: pixel 32*s2 + 8g + 4h + q of the tile -> halo row at tap (0,0)
+  // fragment geometry: slot 32*s2 + 8g + 4h + q of the tile -> halo row at tap (0,0); slots past the
+  // tile's pixels read position 0 (loaded, finite) against their zero dy
   const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, pp = i16 & 3;
   const int half8 = (pp & 1) * 8;
   auto halo_row = [&](int m) {
-    const int ii = m / (R * W), rem = m - ii * (R * W);
-    const int lr = rem / W, lc = rem - lr * W;
-    return ii * IMGP + lr * HWD + lc;
+    const int ii = m / THW, rem = m - ii * THW;
+    const int lr = rem / TW, lc = rem - lr * TW;
+    return ii < NI ? ii * IMGP + lr * HWD + lc : 0;
   };
   // glds pieces of this wave: i = 0, 1 -> dy rows; i = 2..6 -> halo positions
   int pos_ii[GPW - 2], pos_hr[GPW - 2], pos_hc[GPW - 2];
@@ -472,20 +474,30 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(const WgHaloParam
   const void* zero = (const void*)halo_zero_page;
 
   auto issue = [&](int tile, int stage) {
-    int img0, r0;
-    if (HWi >= 128) { img0 = (tile * 128) / HWi; r0 = (tile * 128 - img0 * HWi) / W; }
-    else { img0 = tile * NI; r0 = 0; }
+    int img0, r0 = 0, c0 = 0;
+    if (NI > 1) {
+      img0 = tile * NI;
+    } else {
+      const int tpi = p.RT * p.CT;
+      img0 = tile / tpi;
+      const int rem = tile - img0 * tpi, rt = rem / p.CT;
+      r0 = rt * TH;
+      c0 = (rem - rt * p.CT) * TW;
+    }
     const uint32_t base = lds0 + stage * STG;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int row = 8 * (wave + 8 * i) + (lane >> 3);
-      gl16(p.dy + (size_t)(tile * 128 + row) * p.K + kt * 64 + ((lane & 7) ^ wsw(row)) * 8,
-           base + (wave + 8 * i) * 1024);
+      const int ii = row / THW, rem = row - ii * THW, lr = rem / TW, lc = rem - lr * TW;
+      const bool ok = ii < NI && r0 + lr < H;
+      const bf16* src = p.dy + ((size_t)((img0 + ii) * H + r0 + lr) * W + c0 + lc) * p.K + kt * 64 +
+                        ((lane & 7) ^ wsw(row)) * 8;
+      gl16(ok ? (const void*)src : zero, base + (wave + 8 * i) * 1024);
     }
 #pragma unroll
     for (int i = 2; i < GPW; ++i) {
       const int qq = 8 * (wave + 8 * (i - 2)) + (lane >> 3);
-      const int ih = r0 + pos_hr[i - 2] - 1, iw = pos_hc[i - 2] - 1;
+      const int ih = r0 + pos_hr[i - 2] - 1, iw = c0 + pos_hc[i - 2] - 1;
       const bool ok = pos_in[i - 2] && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
       const bf16* src = p.x + ((size_t)((img0 + pos_ii[i - 2]) * H + ih) * W + iw) * p.C + ct * 64 +
                         ((lane & 7) ^ wsw(qq)) * 8;
@@ -550,23 +562,52 @@ int g_wg_halo_enable = 1;          // argus_conv_tuning key 11
 int g_wg_halo_target_blocks = 256;
 int g_wg_halo_max_tiles = 4;        // key 14
 
+// Tile geometry of the halo weight gradient. H*W < 128: NI = 128 / (H*W) whole images per tile
+// (128 % HW == 0). Otherwise a TH x TW block of one image: over the divisors TW of W (<= 128) with
+// TH = min(128 / TW, H) rows and a (TH+2) x (TW+2) halo within kWgHaloPos, the most useful pixels per
+// 128 slots (ragged last row block included), ties to the wider block. 256 x 256 frames: TW = W
+// (whole rows, as before); 168- and 84-wide frames: 3 x 42.
+struct WgHaloGeom {
+  int TH, TW, NI, RT, CT;
+  long ptiles;
+};
+static bool wg_halo_geom(const argus_conv_desc& d, WgHaloGeom& gm) {
+  const int H = d.h, W = d.w, HW = H * W;
+  if (HW < 128) {
+    if (128 % HW || (d.n * 128 / HW) == 0 || d.n % (128 / HW)) return false;
+    gm.NI = 128 / HW; gm.TH = H; gm.TW = W; gm.RT = gm.CT = 1;
+    if (gm.NI * (H + 2) * (W + 2) > kWgHaloPos) return false;
+    gm.ptiles = (long)d.n / gm.NI;
+    return true;
+  }
+  double best = 0.0;
+  for (int tw = W < 128 ? W : 128; tw >= 1; --tw) {
+    if (W % tw) continue;
+    int th = 128 / tw;
+    if (th > H) th = H;
+    if ((th + 2) * (tw + 2) > kWgHaloPos) continue;
+    const int rt = (H + th - 1) / th;
+    const double eff = (double)H * tw / ((double)rt * 128.0);  // image pixels per slot
+    if (eff > best + 1e-9) {
+      best = eff;
+      gm.TH = th; gm.TW = tw; gm.RT = rt; gm.CT = W / tw;
+    }
+  }
+  if (best < 0.75) return false;  // mostly padding: the register-staged kernel
+  gm.NI = 1;
+  gm.ptiles = (long)d.n * gm.RT * gm.CT;
+  return true;
+}
+
 // Plan for a 3x3 / stride 1 / pad 1 bf16 weight gradient: false when not served. splits * K * 9C
 // fp32 partials.
 bool wgrad3x3_halo_plan(const argus_conv_desc& d, int dtype, int* splits, int* tps) {
   if (!g_wg_halo_enable || dtype != ARGUS_BF16 || d.stem || d.r != 3 || d.s != 3 || d.stride != 1 || d.pad != 1 ||
       d.c % 64 || d.k % 64 || d.ho != d.h || d.wo != d.w)
     return false;
-  const int HWi = d.h * d.w;
-  int npos;
-  if (HWi >= 128) {
-    if (128 % d.w || HWi % 128) return false;
-    npos = (128 / d.w + 2) * (d.w + 2);
-  } else {
-    if (128 % HWi) return false;
-    npos = (128 / HWi) * (d.h + 2) * (d.w + 2);
-  }
-  if (npos > kWgHaloPos || ((long)d.n * HWi) % 128) return false;  // whole 128-pixel tiles only
-  const long ptiles = (long)d.n * HWi / 128;
+  WgHaloGeom gm;
+  if (!wg_halo_geom(d, gm)) return false;
+  const long ptiles = gm.ptiles;
   const long tiles = (long)(d.k / 64) * (d.c / 64);
   // measured: a win for <= 4 (k, c) tiles (the 64- and 128-channel layers); beyond, its two tr16
   // operand streams make it LDS-read-bound and the register-staged wgrad_kernel is faster
@@ -590,7 +631,10 @@ bool wgrad3x3_halo_launch(const argus_conv_desc& d, int dtype, const void* x, co
   p.dy = reinterpret_cast<const bf16*>(dy);
   p.part = reinterpret_cast<float*>(ws);
   p.n = d.n; p.H = d.h; p.W = d.w; p.C = d.c; p.K = d.k;
-  p.ptiles = d.n * d.h * d.w / 128;
+  WgHaloGeom gm;
+  wg_halo_geom(d, gm);
+  p.ptiles = (int)gm.ptiles;
+  p.TH = gm.TH; p.TW = gm.TW; p.NI = gm.NI; p.RT = gm.RT; p.CT = gm.CT;
   p.tps = tps;
   dim3 grid((d.k / 64) * (d.c / 64) * splits);
   timed_launch("argus::wgrad3x3_halo_kernel", wgrad3x3_halo_kernel, grid, dim3(512), st, p);

@@ -811,10 +811,15 @@ def test_wgrad3x3_halo_kernel_parity(cuda, pro):
 def _wgrad_halo_cases(L, cuda, pro):
     from argus_amd.profiling import KernelTimer
 
-    for cin, cout, hw, n in [(64, 64, 64, 1), (128, 128, 32, 1), (64, 128, 16, 2), (128, 64, 8, 4), (256, 128, 16, 1)]:
-        d, p = _desc(n, hw, hw, cin, cout, 3, 1)
-        x = _q(torch.randn(n, hw, hw, cin) * 1.3 + 0.1, "bf16")
-        dy = _q(torch.randn(n, hw, hw, cout), "bf16")
+    # square frames: whole-row tiles / whole images; 84-, 168- and 21-wide frames (the 376 x 672
+    # layers' widths): 3 x 42, 2 x 56 and 6 x 21 blocks, ragged last row blocks
+    for cin, cout, hw, n in [(64, 64, 64, 1), (128, 128, 32, 1), (64, 128, 16, 2), (128, 64, 8, 4), (256, 128, 16, 1),
+                             (64, 64, (10, 84), 1), (128, 128, (7, 168), 1), (64, 64, (12, 21), 2),
+                             (128, 128, (47, 84), 1)]:
+        hh, ww = hw if isinstance(hw, tuple) else (hw, hw)
+        d, p = _desc(n, hh, ww, cin, cout, 3, 1)
+        x = _q(torch.randn(n, hh, ww, cin) * 1.3 + 0.1, "bf16")
+        dy = _q(torch.randn(n, hh, ww, cout), "bf16")
         sc, sh = torch.rand(cin) + 0.5, torch.randn(cin) * 0.5
         xg, dyg, scg, shg = x.to(cuda, torch.bfloat16), dy.to(cuda, torch.bfloat16), sc.to(cuda), sh.to(cuda)
         dw = torch.empty(cout, 3, 3, cin, device=cuda)
