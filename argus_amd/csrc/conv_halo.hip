@@ -413,30 +413,38 @@ struct WgHaloParams {
   int RT, CT;       // row / column blocks per image (NI == 1)
 };
 
-constexpr int kWgHaloPos = 320;
+constexpr int kWgHaloPos = 256;  // halo positions per stage ((TH+2) x (TW+2) <= 256)
+constexpr int kWgStages = 3;     // tiles in flight: LDS 3 x 48 KB (two tiles' loads overlap each tile's MFMAs)
 
-ARGUS_DEV int wsw(int r) { return (((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2); }
+ARGUS_DEV int wsw(int r) { return (r & 2) | ((r >> 1) & 4); }  // bit 1 -> bit 1, bit 3 -> bit 2
 
-ARGUS_DEV u32x4 tr_frag(const char* img, int r_lo, int r_hi, int slot, int half8) {
-  // two ds_read_b64_tr_b16: rows r_lo (elements 0..3) and r_hi (elements 4..7) of this lane's group
-  const char* a0 = img + r_lo * 128 + ((slot ^ wsw(r_lo)) << 4) + half8;
-  const char* a1 = img + r_hi * 128 + ((slot ^ wsw(r_hi)) << 4) + half8;
-  const s16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (s16x4 __attribute__((address_space(3)))*)(uintptr_t)(uint32_t)(uintptr_t)a0);
-  const s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (s16x4 __attribute__((address_space(3)))*)(uintptr_t)(uint32_t)(uintptr_t)a1);
-  const uint2 u0 = __builtin_bit_cast(uint2, t0), u1 = __builtin_bit_cast(uint2, t1);
-  return u32x4{u0.x, u0.y, u1.x, u1.y};
+// Transposed LDS reads (ds_read_b64_tr_b16) issued as inline asm. The compiler treats a ds_read_tr16_b64 builtin
+// as possibly aliasing the global_load_lds stages in flight and put an `s_waitcnt vmcnt(0)` in front
+// of the first one of every k-step, which drained the next tiles' loads each time (the ring overlapped
+// nothing). As asm the reads are invisible to that analysis: the ring's own counted vmcnt waits and
+// barriers order them, and lgkm_tie() waits for their data before the MFMAs use it.
+ARGUS_DEV uint2 ds_tr_asm(uint32_t addr) {
+  uint2 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(addr) : "memory");
+  return r;
+}
+// every LDS read issued so far has landed; the operands pass through the asm so no use moves above it
+ARGUS_DEV void lgkm_tie(u32x4 (&a)[2], u32x4 (&b)[9]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(a[0]), "+v"(a[1]), "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]), "+v"(b[4]), "+v"(b[5]),
+                 "+v"(b[6]), "+v"(b[7]), "+v"(b[8])
+               :
+               : "memory");
 }
 
 __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(const WgHaloParams p) {
   constexpr int DYB = 128 * 128;                // dy image bytes
   constexpr int HXB = kWgHaloPos * 128;         // halo image bytes
   constexpr int STG = DYB + HXB;                // one stage
-  constexpr int PIECES = STG / 1024;            // 1 KB glds pieces per stage (56)
-  constexpr int GPW = PIECES / 8;               // per wave (7)
+  constexpr int PIECES = STG / 1024;            // 1 KB glds pieces per stage (48)
+  constexpr int GPW = PIECES / 8;               // per wave (6)
   static_assert(GPW * 8 == PIECES && DYB / 1024 == 16, "stage partition");
-  __shared__ __attribute__((aligned(1024))) u32x4 lds[(2 * STG + 512) / 16];
+  __shared__ __attribute__((aligned(1024))) u32x4 lds[(kWgStages * STG + 512) / 16];
 
   const int ctiles = p.C / 64;
   int tile, split;
@@ -459,17 +467,28 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(const WgHaloParam
     const int lr = rem / TW, lc = rem - lr * TW;
     return ii < NI ? ii * IMGP + lr * HWD + lc : 0;
   };
-  // glds pieces of this wave: i = 0, 1 -> dy rows; i = 2..6 -> halo positions
-  int pos_ii[GPW - 2], pos_hr[GPW - 2], pos_hc[GPW - 2];
-  bool pos_in[GPW - 2];
+  // glds pieces of this wave: i = 0, 1 -> dy rows; i = 2.. -> halo positions. Their element offsets from
+  // the tile's corner (image img0, row r0, column c0) and the coordinates the bounds checks need are the
+  // same in every tile: computed once (per tile only a scalar base and two compares per piece remain).
+  constexpr int HP = GPW - 2;
+  int dy_off[2], dy_lr[2];
+  int hx_off[HP], hx_rc[HP];  // hx_rc: halo row - 1 (high 16 bits, signed) | halo column - 1 (low, signed)
+  bool hx_in[HP];
 #pragma unroll
-  for (int i = 2; i < GPW; ++i) {
-    const int qq = 8 * (wave + 8 * (i - 2)) + (lane >> 3);
+  for (int i = 0; i < 2; ++i) {
+    const int row = 8 * (wave + 8 * i) + (lane >> 3);
+    const int ii = row / THW, rem = row - ii * THW, lr = rem / TW, lc = rem - lr * TW;
+    dy_lr[i] = ii < NI ? lr : (1 << 30);  // slots past the tile's pixels: never in the image (zero dy)
+    dy_off[i] = ((ii * H + lr) * W + lc) * p.K + kt * 64 + ((lane & 7) ^ wsw(row)) * 8;
+  }
+#pragma unroll
+  for (int i = 0; i < HP; ++i) {
+    const int qq = 8 * (wave + 8 * i) + (lane >> 3);
     const int ii = qq / IMGP, rem = qq - ii * IMGP;
-    pos_ii[i - 2] = ii;
-    pos_hr[i - 2] = rem / HWD;
-    pos_hc[i - 2] = rem - pos_hr[i - 2] * HWD;
-    pos_in[i - 2] = qq < npos;
+    const int hr = rem / HWD, hc = rem - hr * HWD;
+    hx_in[i] = qq < npos;
+    hx_rc[i] = ((hr - 1) << 16) | ((hc - 1) & 0xffff);
+    hx_off[i] = ((ii * H + hr - 1) * W + hc - 1) * p.C + ct * 64 + ((lane & 7) ^ wsw(qq)) * 8;
   }
   const void* zero = (const void*)halo_zero_page;
 
@@ -484,24 +503,20 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(const WgHaloParam
       r0 = rt * TH;
       c0 = (rem - rt * p.CT) * TW;
     }
+    const size_t corner = ((size_t)img0 * H + r0) * W + c0;
+    const bf16* dyb = p.dy + corner * p.K;
+    const bf16* xb = p.x + corner * p.C;
     const uint32_t base = lds0 + stage * STG;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int row = 8 * (wave + 8 * i) + (lane >> 3);
-      const int ii = row / THW, rem = row - ii * THW, lr = rem / TW, lc = rem - lr * TW;
-      const bool ok = ii < NI && r0 + lr < H;
-      const bf16* src = p.dy + ((size_t)((img0 + ii) * H + r0 + lr) * W + c0 + lc) * p.K + kt * 64 +
-                        ((lane & 7) ^ wsw(row)) * 8;
-      gl16(ok ? (const void*)src : zero, base + (wave + 8 * i) * 1024);
+      const bool ok = r0 + dy_lr[i] < H;
+      gl16(ok ? (const void*)(dyb + dy_off[i]) : zero, base + (wave + 8 * i) * 1024);
     }
 #pragma unroll
-    for (int i = 2; i < GPW; ++i) {
-      const int qq = 8 * (wave + 8 * (i - 2)) + (lane >> 3);
-      const int ih = r0 + pos_hr[i - 2] - 1, iw = c0 + pos_hc[i - 2] - 1;
-      const bool ok = pos_in[i - 2] && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
-      const bf16* src = p.x + ((size_t)((img0 + pos_ii[i - 2]) * H + ih) * W + iw) * p.C + ct * 64 +
-                        ((lane & 7) ^ wsw(qq)) * 8;
-      gl16(ok ? (const void*)src : zero, base + DYB + (wave + 8 * (i - 2)) * 1024);
+    for (int i = 0; i < HP; ++i) {
+      const int ih = r0 + (hx_rc[i] >> 16), iw = c0 + (int)(short)(hx_rc[i] & 0xffff);
+      const bool ok = hx_in[i] && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+      gl16(ok ? (const void*)(xb + hx_off[i]) : zero, base + DYB + (wave + 8 * i) * 1024);
     }
   };
 
@@ -511,33 +526,69 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(const WgHaloParam
 #pragma unroll
     for (int j = 0; j < 9; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // LDS byte offsets of this lane's transposed reads, relative to its stage's dy / halo image. They are
+  // the same in every tile (fixed geometry), so they are computed once and kept packed as two 16-bit
+  // halves per VGPR (images < 64 KB): per read one unpack + one add instead of the row / swizzle math
+  // that made the k-step VALU-bound (SQ_INSTS_VALU 16x SQ_INSTS_MFMA).
+  auto tr_off = [&](int r, int slot) { return r * 128 + ((slot ^ wsw(r)) << 4) + half8; };
+  unsigned offa[4][2], offb[4][9];
+#pragma unroll
+  for (int s2 = 0; s2 < 4; ++s2) {
+    const int rlo = 32 * s2 + 8 * g + q;
+    const int h0 = halo_row(rlo), h1 = halo_row(rlo + 4);
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+      const int slot = 2 * (2 * wm + mi) + (pp >> 1);
+      offa[s2][mi] = (unsigned)tr_off(rlo, slot) | ((unsigned)tr_off(rlo + 4, slot) << 16);
+    }
+#pragma unroll
+    for (int ni = 0; ni < 9; ++ni) {
+      const int nb = 9 * wn + ni;  // 16-column block of the 576 columns: tap nb/4, channels 16*(nb%4)
+      const int t = nb >> 2, cb = nb & 3;
+      const int toff = (t / 3) * HWD + (t % 3);
+      const int slot = 2 * cb + (pp >> 1);
+      offb[s2][ni] = (unsigned)tr_off(h0 + toff, slot) | ((unsigned)tr_off(h1 + toff, slot) << 16);
+    }
+  }
+  auto frag = [&](uint32_t img, unsigned packed) {
+    const uint2 u0 = ds_tr_asm(img + (packed & 0xffffu));
+    const uint2 u1 = ds_tr_asm(img + (packed >> 16));
+    return u32x4{u0.x, u0.y, u1.x, u1.y};
+  };
+
+  // 3-stage ring: tile i lands in stage i % 3; tiles i+1 and i+2 stay in flight over tile i's MFMAs
   if (t0 < t1) issue(t0, 0);
+  if (t0 + 1 < t1) issue(t0 + 1, 1);
+  int stage = 0;
   for (int tile = t0; tile < t1; ++tile) {
-    const int stage = (tile - t0) & 1;
-    const bool more = tile + 1 < t1;
-    if (more) issue(tile + 1, stage ^ 1);  // its buffer was last read before the previous barrier
-    if (more) waitvm<GPW>(); else waitvm<0>();
+    const int ahead = min(t1 - 1 - tile, kWgStages - 1);  // tiles issued after this one
+    if (ahead == kWgStages - 1) {
+      // stage (stage + 2) % 3 was last read in the previous iteration, before its closing barrier
+      issue(tile + 2, stage == 0 ? 2 : stage - 1);
+      waitvm<2 * GPW>();
+    } else if (ahead == 1) {
+      waitvm<GPW>();
+    } else {
+      waitvm<0>();
+    }
     sbar();
-    const char* DYI = reinterpret_cast<const char*>(lds) + stage * STG;
-    const char* HXI = DYI + DYB;
-#pragma unroll 1
+    const uint32_t DYI = lds0 + stage * STG;
+    const uint32_t HXI = DYI + DYB;
+#pragma unroll
     for (int s2 = 0; s2 < 4; ++s2) {
-      const int rlo = 32 * s2 + 8 * g + q;
-      const int h0 = halo_row(rlo), h1 = halo_row(rlo + 4);
-      u32x4 fa[2];
+      u32x4 fa[2], fb[9];
 #pragma unroll
-      for (int mi = 0; mi < 2; ++mi) fa[mi] = tr_frag(DYI, rlo, rlo + 4, 2 * (2 * wm + mi) + (pp >> 1), half8);
+      for (int mi = 0; mi < 2; ++mi) fa[mi] = frag(DYI, offa[s2][mi]);
 #pragma unroll
-      for (int ni = 0; ni < 9; ++ni) {
-        const int nb = 9 * wn + ni;  // 16-column block of the 576 columns: tap nb/4, channels 16*(nb%4)
-        const int t = nb >> 2, cb = nb & 3;
-        const int toff = (t / 3) * HWD + (t % 3);
-        const u32x4 fb = tr_frag(HXI, h0 + toff, h1 + toff, 2 * cb + (pp >> 1), half8);
+      for (int ni = 0; ni < 9; ++ni) fb[ni] = frag(HXI, offb[s2][ni]);
+      lgkm_tie(fa, fb);
 #pragma unroll
-        for (int mi = 0; mi < 2; ++mi) Mma<bf16>::run(acc[mi][ni], fa[mi], fb);
-      }
+      for (int ni = 0; ni < 9; ++ni)
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi) Mma<bf16>::run(acc[mi][ni], fa[mi], fb[ni]);
     }
     sbar();  // every wave is done with this stage before it is refilled
+    stage = stage == kWgStages - 1 ? 0 : stage + 1;
   }
 
   // ---- fp32 partial tile: part[split][k][tap*C + c] ----

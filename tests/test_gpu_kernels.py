@@ -802,10 +802,16 @@ def test_wgrad3x3_halo_kernel_parity(cuda, pro):
     torch.manual_seed(19)
     L = lib()
     assert L.dll.argus_conv_tuning(14, 1 << 20) == 0  # every channel-tile count
+    target = L.dll.argus_conv_tuning_get(12)
     try:
-        _wgrad_halo_cases(L, cuda, pro)
+        # default split target (mostly one tile per split) and a target of 3 workgroups per (k, c) tile
+        # (long tile runs: the 3-stage ring's steady state, its drain and ragged run lengths)
+        for tg in (target, 3):
+            assert L.dll.argus_conv_tuning(12, tg) == 0
+            _wgrad_halo_cases(L, cuda, pro)
     finally:
         L.dll.argus_conv_tuning(14, 4)
+        L.dll.argus_conv_tuning(12, target)
 
 
 def _wgrad_halo_cases(L, cuda, pro):
