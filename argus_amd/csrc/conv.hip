@@ -142,16 +142,27 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
   int a_off[AR], a_ih[AR], a_iw[AR];
   bool a_ok[AR];
   const int HWq = ph.Hq * ph.Wq;
+  // 1x1 / stride-1 GEMM (one tap at offset 0, input grid = GEMM row grid): input pixel = GEMM row, so
+  // no (image, row, column) split is needed (its integer divisions made the small-K 1x1 convs
+  // VALU-bound: SQ_INSTS_VALU 9-20x SQ_INSTS_MFMA)
+  const bool a_ident = !STEM && ph.K == p.Cin && ph.dh[0] == 0 && ph.dw[0] == 0 && p.ish == 1 && p.isw == 1 &&
+                       ph.Hq == p.H && ph.Wq == p.W;
 #pragma unroll
   for (int i = 0; i < AR; ++i) {
     const int m = mt * BM + (tid >> 3) + 32 * i;
     a_ok[i] = m < ph.M;
     const int mm = a_ok[i] ? m : 0;
-    const int nimg = mm / HWq, rem = mm - nimg * HWq;
-    const int qh = rem / ph.Wq, qw = rem - qh * ph.Wq;
-    a_ih[i] = qh * p.ish;
-    a_iw[i] = qw * p.isw;
-    a_off[i] = ((nimg * p.H + a_ih[i]) * p.W + a_iw[i]) * p.lda;
+    if (a_ident) {
+      a_ih[i] = 0;
+      a_iw[i] = 0;
+      a_off[i] = mm * p.lda;
+    } else {
+      const int nimg = mm / HWq, rem = mm - nimg * HWq;
+      const int qh = rem / ph.Wq, qw = rem - qh * ph.Wq;
+      a_ih[i] = qh * p.ish;
+      a_iw[i] = qw * p.isw;
+      a_off[i] = ((nimg * p.H + a_ih[i]) * p.W + a_iw[i]) * p.lda;
+    }
   }
   const T* b_row[BR];
 #pragma unroll
@@ -419,6 +430,8 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
   constexpr int RPP = 256 / CPR;                  // rows per store pass
   T* Cs = reinterpret_cast<T*>(lds);
   T* __restrict__ Cg = reinterpret_cast<T*>(p.c);
+  // output pixel = GEMM row (forward, stride-1 dgrad): no division per stored row
+  const bool c_ident = p.osh == 1 && p.osw == 1 && ph.oh0 == 0 && ph.ow0 == 0 && ph.Hq == p.Ho && ph.Wq == p.Wo;
   BwdEpiAcc<T, BW> bwd;
   if constexpr (BW != 0) bwd.init(p.bb, nt * BN + (tid % CPR) * E);
 #pragma unroll
@@ -450,10 +463,14 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
         const int m = mt * BM + q * ROWS + rr;
         ok[u] = m < ph.M;
         const int mm = ok[u] ? m : 0;
-        const int nimg = mm / HWq, rem = mm - nimg * HWq;
-        const int qh = rem / ph.Wq, qw = rem - qh * ph.Wq;
-        const int oh = qh * p.osh + ph.oh0, ow = qw * p.osw + ph.ow0;
-        off[u] = (((size_t)nimg * p.Ho + oh) * p.Wo + ow) * p.ldc + nt * BN + c * E;
+        if (c_ident) {
+          off[u] = (size_t)mm * p.ldc + nt * BN + c * E;
+        } else {
+          const int nimg = mm / HWq, rem = mm - nimg * HWq;
+          const int qh = rem / ph.Wq, qw = rem - qh * ph.Wq;
+          const int oh = qh * p.osh + ph.oh0, ow = qw * p.osw + ph.ow0;
+          off[u] = (((size_t)nimg * p.Ho + oh) * p.Wo + ow) * p.ldc + nt * BN + c * E;
+        }
         if (ok[u]) epi_load<T, BW>(p, off[u], in[u]);
       }
 #pragma unroll

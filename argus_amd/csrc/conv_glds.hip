@@ -86,17 +86,26 @@ __global__ __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) void igemm_glds_kern
   const int HWq = ph.Hq * ph.Wq;
   int a_off[AI], a_ih[AI], a_iw[AI], a_ch[AI];
   bool a_ok[AI];
+  // 1x1 / stride-1 GEMM: input pixel = GEMM row (no per-row integer divisions; igemm_kernel, conv.hip)
+  const bool a_ident = ph.K == p.Cin && ph.dh[0] == 0 && ph.dw[0] == 0 && p.ish == 1 && p.isw == 1 &&
+                       ph.Hq == p.H && ph.Wq == p.W;
 #pragma unroll
   for (int i = 0; i < AI; ++i) {
     const int row = 8 * (i * NW + wave) + (lane >> 3);
     const int m = mt * BM + row;
     a_ok[i] = m < ph.M;
     const int mm = a_ok[i] ? m : 0;
-    const int nimg = mm / HWq, rem = mm - nimg * HWq;
-    const int qh = rem / ph.Wq, qw = rem - qh * ph.Wq;
-    a_ih[i] = qh * p.ish;
-    a_iw[i] = qw * p.isw;
-    a_off[i] = ((nimg * p.H + a_ih[i]) * p.W + a_iw[i]) * p.lda;
+    if (a_ident) {
+      a_ih[i] = 0;
+      a_iw[i] = 0;
+      a_off[i] = mm * p.lda;
+    } else {
+      const int nimg = mm / HWq, rem = mm - nimg * HWq;
+      const int qh = rem / ph.Wq, qw = rem - qh * ph.Wq;
+      a_ih[i] = qh * p.ish;
+      a_iw[i] = qw * p.isw;
+      a_off[i] = ((nimg * p.H + a_ih[i]) * p.W + a_iw[i]) * p.lda;
+    }
     a_ch[i] = ((lane & 7) ^ swz8(row)) * 8;
   }
   const bf16* b_src[BI];
@@ -239,6 +248,8 @@ __global__ __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) void igemm_glds_kern
   const int c = tid % CPR;
   BwdEpiAcc<bf16, BW> bwd;
   if constexpr (BW != 0) bwd.init(p.bb, nt * BN + c * 8);
+  // output pixel = GEMM row (forward, stride-1 dgrad): no division per stored row
+  const bool c_ident = p.osh == 1 && p.osw == 1 && ph.oh0 == 0 && ph.ow0 == 0 && ph.Hq == p.Ho && ph.Wq == p.Wo;
   constexpr int NIT = BM / RPP, U = 4;
   static_assert(NIT * RPP == BM && NIT % U == 0, "epilogue row partition");
   for (int i0 = 0; i0 < NIT; i0 += U) {
@@ -251,10 +262,14 @@ __global__ __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) void igemm_glds_kern
       const int m = mt * BM + rr;
       ok[u] = m < ph.M;
       const int mm = ok[u] ? m : 0;
-      const int nimg = mm / HWq, rem = mm - nimg * HWq;
-      const int qh = rem / ph.Wq, qw = rem - qh * ph.Wq;
-      const int oh = qh * p.osh + ph.oh0, ow = qw * p.osw + ph.ow0;
-      off[u] = (((size_t)nimg * p.Ho + oh) * p.Wo + ow) * p.ldc + nt * BN + c * 8;
+      if (c_ident) {
+        off[u] = (size_t)mm * p.ldc + nt * BN + c * 8;
+      } else {
+        const int nimg = mm / HWq, rem = mm - nimg * HWq;
+        const int qh = rem / ph.Wq, qw = rem - qh * ph.Wq;
+        const int oh = qh * p.osh + ph.oh0, ow = qw * p.osw + ph.ow0;
+        off[u] = (((size_t)nimg * p.Ho + oh) * p.Wo + ow) * p.ldc + nt * BN + c * 8;
+      }
       if (ok[u]) epi_load<bf16, BW>(p, off[u], in[u]);
     }
 #pragma unroll
