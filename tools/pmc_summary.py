@@ -11,6 +11,8 @@ demangled kernel instantiation, then derived:
                 FLOP each) - cross-check against the algorithmic flops
   wait / issue-stall / active = SQ_WAIT_ANY / SQ_WAIT_INST_ANY / SQ_ACTIVE_INST_ANY over SQ_WAVE_CYCLES
   lds_conflict = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE (extra LDS cycles per LDS-array cycle)
+  valu_per_mfma = SQ_INSTS_VALU / SQ_INSTS_MFMA (vector-ALU instructions issued per MFMA: index math,
+                staging transforms and epilogue work competing with the MFMAs for issue)
   clock_ghz   = GRBM_GUI_ACTIVE / 8 / kernel time (when a duration is present in the CSV)
 """
 import argparse
@@ -57,6 +59,8 @@ def main():
                            ("active_frac", "SQ_ACTIVE_INST_ANY"), ("lds_stall_frac", "SQ_WAIT_INST_LDS")):
                 if c in m:
                     d[key] = m[c] / wc
+        if m.get("SQ_INSTS_MFMA"):
+            d["valu_per_mfma"] = m.get("SQ_INSTS_VALU", 0.0) / m["SQ_INSTS_MFMA"]
         if m.get("SQ_LDS_IDX_ACTIVE"):
             d["lds_conflict"] = m.get("SQ_LDS_BANK_CONFLICT", 0.0) / m["SQ_LDS_IDX_ACTIVE"]
         if g:
@@ -66,11 +70,12 @@ def main():
             "derived_from": a.dirs}
     Path(a.out).write_text(json.dumps({"meta": meta, "kernels": res}, indent=1))
     order = sorted(res.items(), key=lambda kv: -kv[1].get("gpu_cycles", 0) * kv[1]["dispatches"])
-    print(f"{'cyc/disp':>9} {'n':>4} {'mfma':>5} {'wait':>5} {'stall':>5} {'act':>5} {'ldsc':>5}  kernel")
+    print(f"{'cyc/disp':>9} {'n':>4} {'mfma':>5} {'wait':>5} {'stall':>5} {'act':>5} {'ldsc':>5} {'v/mf':>6}  kernel")
     for k, d in order[:a.top]:
         f = lambda x: f"{d[x]:5.2f}" if x in d else "    -"  # noqa: E731
         print(f"{d.get('gpu_cycles', 0):9.0f} {d['dispatches']:4d} {f('mfma_busy')} {f('wait_frac')} "
-              f"{f('issue_stall_frac')} {f('active_frac')} {f('lds_conflict')}  {k[:100]}")
+              f"{f('issue_stall_frac')} {f('active_frac')} {f('lds_conflict')} "
+              f"{d['valu_per_mfma'] if 'valu_per_mfma' in d else float('nan'):6.1f}  {k[:100]}")
 
 
 if __name__ == "__main__":

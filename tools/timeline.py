@@ -57,6 +57,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--first", type=int, default=None,
+                    help="index (0-based, in Adam launches) of the first step to report; default: the last --steps "
+                         "steps. bench.py runs warmup + 2 x 3 probe steps before its timed region and 5 critical-path "
+                         "timer steps after it, whose per-launch events perturb the main stream")
     ap.add_argument("--list", action="store_true", help="also list the last step's main-stream kernels in order "
                                                         "(start offset, gap before, duration)")
     a = ap.parse_args()
@@ -67,7 +71,11 @@ def main():
     ks.sort()
     adam = [k for k in ks if "adam_kernel" in k[3]]
     main_stream = adam[-1][2]
-    bounds = [k[1] for k in adam][-(a.steps + 1):]
+    ends = [k[1] for k in adam]
+    if a.first is None:
+        bounds = ends[-(a.steps + 1):]
+    else:
+        bounds = ends[a.first - 1:a.first + a.steps]
     per_stream = defaultdict(list)
     fam_main = defaultdict(float)
     fam_side = defaultdict(float)
