@@ -127,6 +127,12 @@ class ResNetEngine:
         # the stem weight gradient (main stream, its own split workspace) is issued before the final
         # join, beside the side stream's last weight gradients (+0.2 %); ARGUS_STEM_OVERLAP=0 after it
         self._stem_overlap = os.environ.get("ARGUS_STEM_OVERLAP", "1") == "1"
+        # the first block's downsample weight gradient runs on the main stream after the stem weight
+        # gradient instead of on the side stream: the side stream's last weight gradients otherwise
+        # outlast the main stream's stem work (an exposed ~150 us tail before the join; +0.4 % at B=64,
+        # two paired runs)
+        self.tail_main = True
+        self._tail: list = []
 
     # ------------------------------------------------------------------ allocation
     def _t(self, *shape, dtype=None):
@@ -234,6 +240,11 @@ class ResNetEngine:
         self.wg_ws = torch.empty(ws, dtype=torch.uint8, device=self.device)
         self.wg_ws_bytes = ws
         wss = L.dll.argus_conv_wgrad_workspace_bytes(C.byref(convs["resnet.conv1"].desc), dt)
+        # the stem weight gradient's workspace; also the first block's downsample weight gradient's, which
+        # runs after it on the main stream (tail_main)
+        ds0 = self.blocks[0].prefix + ".downsample.0"
+        if ds0 in convs:
+            wss = max(wss, L.dll.argus_conv_wgrad_workspace_bytes(C.byref(convs[ds0].desc), dt))
         self.wg_ws_stem = torch.empty(wss, dtype=torch.uint8, device=self.device)
         self.stages_pro = {n: bool(L.dll.argus_conv_dgrad_stages_prologue(C.byref(cv.desc), self.cdt))
                            for n, cv in convs.items() if not cv.desc.stem}
@@ -581,7 +592,15 @@ class ResNetEngine:
             else:
                 self._wgrad(pf + ".conv1", h_in, None, dy1, G)
             if b.has_ds:
-                self._wgrad(pf + ".downsample.0", h_in, None, dyd, G)
+                # (single process only: with on_ready a bucket holding this gradient could be reduced first)
+                if (idx == 0 and on_ready is None and self.tail_main and self.wgrad_overlap and self._stem_overlap
+                        and self.fuse_apply):
+                    cvd = self.convs[pf + ".downsample.0"]
+                    self._tail.append((cvd, lambda cvd=cvd, x=h_in, dy=dyd: self.L.conv_wgrad(
+                        C.byref(cvd.desc), self.dt, ptr(x), None, None, ptr(dy), ptr(G[pf + ".downsample.0.weight"]),
+                        ptr(self.wg_ws_stem), self.wg_ws_stem.numel(), stream())))
+                else:
+                    self._wgrad(pf + ".downsample.0", h_in, None, dyd, G)
             dh = dx
             self._flush_side()
             if on_ready is not None:
@@ -609,6 +628,9 @@ class ResNetEngine:
             if not self._stem_overlap:
                 self._join()
             self._launch(cv, 2, fn)
+            for cvt, fnt in self._tail:  # after the stem's: they share its workspace (stream order)
+                self._launch(cvt, 2, fnt)
+            self._tail.clear()
         else:
             L.maxpool_bwd(dt, N, H1, W1, 64, ptr(dh), ptr(self.amax), ptr(dz0), s)
             self._bn_bwd(P, G, "resnet.bn1", N * H1 * W1, 64, dz0, 2, None, self.y0, dy0, None)
