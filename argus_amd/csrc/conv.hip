@@ -1021,7 +1021,7 @@ static void dispatch_ig_bwd(const IgParams& p, int maxM, int bm, int bn, hipStre
 
 extern int g_glds_min_k, g_glds_min_grid;  // conv_glds.hip
 extern int g_bwd_min_px, g_bwd_max_rows, g_ew_target, g_ew_min_ppt, g_fin_div;  // bn.hip
-extern int g_halo64, g_halo_epi_prefetch;  // conv_halo.hip, keys 30 and 32
+extern int g_halo64, g_halo_epi_prefetch, g_halo_blocks;  // conv_halo.hip, keys 30, 32 and 37
 extern int g_halo_enable, g_wg_halo_enable, g_wg_halo_target_blocks, g_halo_min_grid,
     g_wg_halo_max_tiles;  // conv_halo.hip
 // argus_conv_tuning key 7: largest K (elements) served by the single-buffer OCC=3/4 kernel. Swept with
@@ -1118,6 +1118,7 @@ static int* tuning_slot(int key) {
     case 27: return &g_wgrad_target_3x3;
     case 33: return &g_wgrad_split_floor;
     case 34: return &g_stem_wg;
+    case 37: return &g_halo_blocks;
     case 30: return &g_halo64;
     case 32: return &g_halo_epi_prefetch;
     default: return nullptr;
@@ -1246,7 +1247,7 @@ static int dgrad_prow(const IgParams& p, int dtype, const argus_conv_desc& d) {
     maxK = p.ph[i].K > maxK ? p.ph[i].K : maxK;
   }
   if (dtype == ARGUS_BF16 && !f8_ok(p)) {
-    if (conv3x3_halo_ok(p)) return p.ph[0].M / 256;
+    if (conv3x3_halo_ok(p)) return conv3x3_halo_tiles(p);
     if (igemm_glds_ok(p, maxM, maxK)) return cdiv(maxM, 256);
   }
   return cdiv(maxM, dgrad_bm(d));

@@ -63,6 +63,9 @@ struct IgParams {
   BnApplyPro ap;  // dgrad only: the A operand is dm (ap.y != nullptr)
   int f8;         // ARGUS_FP8: MX-fp8 operands where the shape allows (host dispatch only)
   int epi_pre;    // halo dgrad: prefetch the BN-backward epilogue operands under the last chunk (key 32)
+  // halo fwd/dgrad tile geometry (conv_halo.hip, host-planned): hTW == 0 -> 256 consecutive pixels
+  // (whole rows / whole images); else a hTH x hTW block of one image, hRT x hCT blocks per image
+  int hTH, hTW, hRT, hCT;
 };
 
 // compile-time epilogue/prologue variant of the dgrad kernels: low 3 bits = BN-backward epilogue
@@ -278,6 +281,8 @@ bool igemm_glds_launch(const IgParams& p, int maxM, int maxK, hipStream_t st);
 // 3x3 stride-1 forward / dgrad with an LDS-resident halo tile (conv_halo.hip); false = not served.
 // _ok returns the column tile it would launch (128 / 64) or 0.
 int conv3x3_halo_ok(const IgParams& p);
+// workgroup row tiles of the halo fwd/dgrad for these params (BN-backward partial rows of its dgrad)
+int conv3x3_halo_tiles(const IgParams& p);
 bool conv3x3_halo_launch(const IgParams& p, hipStream_t st);
 // 3x3 stride-1 weight gradient with an LDS-resident halo tile (conv_halo.hip): plan / launch of the
 // split partials (fp32 [splits][K][9C]); false = not served

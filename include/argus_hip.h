@@ -172,7 +172,8 @@ int argus_conv_dgrad_bn(const argus_conv_desc* d, int dtype, const void* dy, con
  * epilogue prefetches its epilogue operands under its last channel chunk (1: the single-halo-buffer
  * variant; 2 every variant; 0 none), key 33 the weight-gradient split count floor(target / tiles)
  * (1) or ceil (0), key 34 the bf16 stem weight gradient on the LDS-patch kernel (1) or on the
- * register-staged weight-gradient kernel (0).
+ * register-staged weight-gradient kernel (0), key 37 the 3x3 dgrad of frames whose width does not
+ * divide 256 on the LDS-halo kernel's TH x TW block tiles (1) or on the implicit GEMM (0, default).
  * Returns 0, or -1 for an unknown key. */
 int argus_conv_tuning(int key, int value);
 /* Current value of a tuning key (-1 for an unknown key). */

@@ -752,6 +752,62 @@ def _halo_cases(L, cuda):
         assert _rel(dx.permute(0, 3, 1, 2), refd + (dx0 * keep).permute(0, 3, 1, 2)) < TOL["bf16"], ("dgrad m", cin)
 
 
+def test_conv3x3_halo_dgrad_block_tiles(cuda):
+    """3x3 dgrads of frames whose width does not divide 256 (the 376 x 672 layers' 168-, 84-, 42- and
+    21-wide frames) on the halo kernel's TH x TW block tiles (tuning key 37): ragged last row blocks and
+    padded slots; vs torch (plain dgrad into a non-zero addend) and vs the kernel the shape used before
+    (key 37 = 0) with the BN-backward epilogue (masked dm and the per-channel sums of its partials)."""
+    from argus_amd._lib import BnBwdEpilogue
+    from argus_amd.profiling import KernelTimer
+
+    torch.manual_seed(31)
+    L = lib()
+    keep13, keep37 = L.dll.argus_conv_tuning_get(13), L.dll.argus_conv_tuning_get(37)
+    assert L.dll.argus_conv_tuning(13, 1) == 0  # any grid size (small test shapes)
+    try:
+        for cin, cout, (h, w), n in [(64, 64, (10, 84), 2), (128, 128, (7, 168), 1), (128, 128, (12, 21), 3),
+                                     (256, 256, (12, 42), 2), (64, 64, (13, 168), 1)]:
+            assert L.dll.argus_conv_tuning(37, 1) == 0
+            d, p = _desc(n, h, w, cin, cout, 3, 1)
+            wt_ = torch.randn(cout, 3, 3, cin) * (2.0 / (9 * cin)) ** 0.5
+            _, wt = _prep(d, "bf16", wt_.to(cuda), cuda)
+            wr = _q(wt_, "bf16").permute(0, 3, 1, 2)
+            dy = _q(torch.randn(n, h, w, cout), "bf16")
+            dyd = dy.to(cuda, torch.bfloat16)
+            refd = torch.nn.grad.conv2d_input((n, cin, h, w), wr, dy.permute(0, 3, 1, 2), padding=1)
+            dx0 = _q(torch.randn(n, h, w, cin), "bf16")
+            dx = dx0.to(cuda, torch.bfloat16)
+            with KernelTimer("argus::conv3x3_halo_kernel") as t:
+                L.conv_dgrad(C.byref(d), BF16, ptr(dyd), ptr(wt), ptr(dx), ptr(dx), None, stream())
+            assert len(t.summary()) == 1, ("halo block dgrad not used", cin, cout, h, w, n)
+            assert _rel(dx.permute(0, 3, 1, 2), refd + dx0.permute(0, 3, 1, 2)) < TOL["bf16"], (cin, cout, h, w)
+            # BN-backward epilogue (mask recomputed from y, partials): blocks vs the previous kernel
+            yin = torch.randn(n, h, w, cin, device=cuda).to(torch.bfloat16)
+            mean, invstd = torch.randn(cin, device=cuda) * 0.1, torch.rand(cin, device=cuda) + 0.5
+            sc, sh = torch.randn(cin, device=cuda), torch.randn(cin, device=cuda)
+            outs = []
+            for key37 in (1, 0):
+                assert L.dll.argus_conv_tuning(37, key37) == 0
+                rows = L.dll.argus_conv_dgrad_bn_rows(C.byref(d), BF16)
+                part = torch.zeros(rows, cin, 2, device=cuda)
+                e = BnBwdEpilogue()
+                e.y, e.mean, e.invstd, e.mask_mode, e.scale, e.shift, e.part = ptr(yin), ptr(mean), ptr(invstd), \
+                    2, ptr(sc), ptr(sh), ptr(part)
+                dm = torch.empty(n, h, w, cin, device=cuda, dtype=torch.bfloat16)
+                with KernelTimer("argus::conv3x3_halo_kernel") as t:
+                    rc = L.dll.argus_conv_dgrad_bn(C.byref(d), BF16, ptr(dyd), ptr(wt), ptr(dm), None, C.byref(e),
+                                                   None, stream())
+                assert rc == 0, L.dll.argus_last_error()
+                assert (len(t.summary()) == 1) == (key37 == 1 or (w <= 256 and 256 % w == 0)), (key37, h, w)
+                torch.cuda.synchronize()
+                outs.append((dm.double().cpu(), part.double().sum(0).cpu()))
+            assert _rel(outs[0][0], outs[1][0]) < 1e-2, ("dm", cin, cout, h, w)
+            assert _rel(outs[0][1], outs[1][1]) < 1e-3, ("partial sums", cin, cout, h, w)
+    finally:
+        L.dll.argus_conv_tuning(13, keep13)
+        L.dll.argus_conv_tuning(37, keep37)
+
+
 @pytest.mark.parametrize("dt", ["fp32", "bf16"])
 def test_weight_prep_batch_matches_single(cuda, dt):
     L = lib()
