@@ -64,23 +64,14 @@ ARGUS_DEV bool ticket_last(unsigned* cnt_, int G, int* flag) {
 }
 
 // fixed-order sum over the G group results of this block's 64 channels: 4 row lanes, then lanes 0..3
-// (loads of a batch are issued before any of their adds: one dependent round trip per batch, not per
-// group; the summation order is unchanged)
-constexpr int kFinU = 16;  // G <= 64: one batch of <= 16 loads per row lane
 ARGUS_DEV double2 merge_groups(const double2* red, int G, int C, int c, double2 (*lds)[64]) {
   const int lane_r = threadIdx.x >> 6, cl = threadIdx.x & 63;
   double S = 0.0, Q = 0.0;
   if (c < C)
-    for (int g0 = lane_r; g0 < G; g0 += 4 * kFinU) {
-      double2 v[kFinU];
-#pragma unroll
-      for (int u = 0; u < kFinU; ++u) {
-        const int g = g0 + 4 * u;
-        v[u] = red[(size_t)(g < G ? g : lane_r) * C + c];  // clamped address: unconditional, batched loads
-      }
-#pragma unroll
-      for (int u = 0; u < kFinU; ++u)
-        if (g0 + 4 * u < G) { S += v[u].x; Q += v[u].y; }
+    for (int g = lane_r; g < G; g += 4) {
+      const double2 v = red[(size_t)g * C + c];
+      S += v.x;
+      Q += v.y;
     }
   lds[lane_r][cl] = make_double2(S, Q);
   __syncthreads();
@@ -110,23 +101,13 @@ __global__ __launch_bounds__(256) void stats_finalize_kernel(const BnFinArgs a) 
   const double inv_full = 1.0 / (double)a.tile_rows;
   double S = 0.0, Q = 0.0;
   if (c < a.C)
-    for (int rb = r0 + lane_r; rb < r1; rb += 4 * kFinU) {
-      float2 v[kFinU];
-#pragma unroll
-      for (int u = 0; u < kFinU; ++u) {
-        const int r = rb + 4 * u;
-        v[u] = a.part[(size_t)(r < r1 ? r : r0) * a.C + c];  // clamped address: unconditional, batched loads
-      }
-#pragma unroll
-      for (int u = 0; u < kFinU; ++u) {
-        const int r = rb + 4 * u;
-        if (r >= r1) break;
-        const int64_t left = a.count - (int64_t)r * a.tile_rows;
-        double inv = inv_full;
-        if (left < a.tile_rows) inv = 1.0 / (double)left;  // the last, partial tile only
-        S += (double)v[u].x;
-        Q += (double)v[u].y + (double)v[u].x * (double)v[u].x * inv;
-      }
+#pragma unroll 8
+    for (int r = r0 + lane_r; r < r1; r += 4) {
+      const float2 v = a.part[(size_t)r * a.C + c];
+      const int64_t left = a.count - (int64_t)r * a.tile_rows;
+      const double inv = left >= a.tile_rows ? inv_full : 1.0 / (double)left;
+      S += (double)v.x;
+      Q += (double)v.y + (double)v.x * (double)v.x * inv;
     }
   __shared__ double2 red[4][64];
   __shared__ int flag;
@@ -385,16 +366,11 @@ __global__ __launch_bounds__(256) void bwd_finalize_kernel(const BnBwdFinArgs a)
   const int r0 = g * a.rpg, r1 = min(a.rows, r0 + a.rpg);
   double s = 0.0, q = 0.0;
   if (c < a.C)
-    for (int rb = r0 + lane_r; rb < r1; rb += 4 * kFinU) {
-      float2 v[kFinU];
-#pragma unroll
-      for (int u = 0; u < kFinU; ++u) {
-        const int r = rb + 4 * u;
-        v[u] = a.part[(size_t)(r < r1 ? r : r0) * a.C + c];  // clamped address: unconditional, batched loads
-      }
-#pragma unroll
-      for (int u = 0; u < kFinU; ++u)
-        if (rb + 4 * u < r1) { s += v[u].x; q += v[u].y; }
+#pragma unroll 8
+    for (int r = r0 + lane_r; r < r1; r += 4) {
+      const float2 v = a.part[(size_t)r * a.C + c];
+      s += v.x;
+      q += v.y;
     }
   __shared__ double2 red[4][64];
   __shared__ int flag;

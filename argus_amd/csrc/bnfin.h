@@ -88,10 +88,7 @@ ARGUS_DEV void fin_backward(int c, double2 tot, double count, const float* gamma
 // Called by every thread of a producer workgroup after its partial rows are stored (store_part):
 // tile t, column tile nt of width COLS. `scratch` = LDS of >= NT * 32 bytes (reused; callers are done
 // with it) and an int flag. A thread merges a pair of adjacent columns (16-byte loads of two float2
-// partials), kArriveU rows in flight per batch (the merge is the producer's tail: one dependent round
-// trip per batch).
-constexpr int kArriveU = 8;
-
+// partials), 4 rows in flight per batch.
 template <int NT, int COLS>
 ARGUS_DEV void bn_fin_arrive(const BnFin& f, int t, int nt, double2* scratch, int* flag) {
   constexpr int CP = COLS / 2;   // column pairs
@@ -111,15 +108,15 @@ ARGUS_DEV void bn_fin_arrive(const BnFin& f, int t, int nt, double2* scratch, in
     if (br == 1 && !dual) break;
     const float2* part = br == 0 ? f.part : f.part2;
     double S0 = 0.0, Q0 = 0.0, S1 = 0.0, Q1 = 0.0;
-    for (int rb = r0 + lr; rb < r1; rb += kArriveU * LR) {
-      f32x4 v[kArriveU];
+    for (int rb = r0 + lr; rb < r1; rb += 4 * LR) {
+      f32x4 v[4];
 #pragma unroll
-      for (int u = 0; u < kArriveU; ++u) {
+      for (int u = 0; u < 4; ++u) {
         const int r = rb + u * LR;
-        v[u] = *reinterpret_cast<const f32x4*>(part + (size_t)(r < r1 ? r : rb) * f.C + c);  // clamped: batched
+        v[u] = r < r1 ? *reinterpret_cast<const f32x4*>(part + (size_t)r * f.C + c) : f32x4{0.f, 0.f, 0.f, 0.f};
       }
 #pragma unroll
-      for (int u = 0; u < kArriveU; ++u) {
+      for (int u = 0; u < 4; ++u) {
         const int r = rb + u * LR;
         if (r >= r1) break;
         S0 += (double)v[u].x;

@@ -8,7 +8,7 @@ if [ -n "$KTESTS" ]; then
 fi
 i=0
 for cfg in "$@"; do
-  i=$((i+1)); tag="ab${i}_$(echo "$cfg" | tr ' =' '__')"
+  i=$((i+1)); tag="ab${i}_$(echo "$cfg" | tr ' =/' '___')"
   envs=""; tunes=""
   for kv in $cfg; do case $kv in ARGUS_*) envs="$envs $kv";; *) tunes="$tunes $kv";; esac; done
   env $envs timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-isolated --kernels $BENCH_ARGS ${tunes:+--tune $tunes} > gpurun_out/$tag.json 2> gpurun_out/$tag.err || { tail -20 gpurun_out/$tag.err; exit 1; }
