@@ -18,11 +18,33 @@ import torch  # noqa: F401  (must precede the CDLL, see module docstring)
 LIB_PATH = Path(os.environ.get("ARGUS_HIP_LIB", Path(__file__).resolve().parent / "libargus_hip.so"))
 
 F32, BF16, FP8 = 0, 1, 2
-ABI_VERSION = 10
+ABI_VERSION = 11
+
+
+class Tuning(C.Structure):
+    """argus_tuning: one {key, value} override of the kernel-selection policy."""
+
+    _fields_ = [("key", C.c_int32), ("value", C.c_int32)]
 
 
 class ConvDesc(C.Structure):
-    _fields_ = [(n, C.c_int32) for n in ("n", "h", "w", "c", "k", "r", "s", "stride", "pad", "ho", "wo", "stem")]
+    """argus_conv_desc. ``ConvDesc(n, h, w, c, k, r, s, stride, pad, ho, wo, stem)`` uses the library's
+    kernel-selection defaults; ``with_tuning`` attaches per-call overrides."""
+
+    _fields_ = [(n, C.c_int32) for n in ("n", "h", "w", "c", "k", "r", "s", "stride", "pad", "ho", "wo", "stem")] + [
+        ("n_tuning", C.c_int32), ("tuning", C.POINTER(Tuning))]
+
+    def with_tuning(self, tuning: dict | None) -> "ConvDesc":
+        """A copy of this descriptor carrying ``tuning`` ({key: value}, argus_conv_policy_default keys) as
+        its per-call overrides (None / {} = the defaults). The override array lives on the copy."""
+        d = ConvDesc(*(getattr(self, f) for f, _ in self._fields_[:12]))
+        items = sorted((tuning or {}).items())
+        if items:
+            arr = (Tuning * len(items))(*[Tuning(int(k), int(v)) for k, v in items])
+            d._tuning_keep = arr
+            d.n_tuning = len(items)
+            d.tuning = C.cast(arr, C.POINTER(Tuning))
+        return d
 
 
 class BnBwdEpilogue(C.Structure):
@@ -65,8 +87,7 @@ SIGNATURES = {
     "argus_conv_fwd": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P, _P]),
     "argus_conv_fwd_stat_rows": (_I, [_DESC, _I]),
     "argus_conv_fwd_stat_tile": (_I, [_DESC, _I]),
-    "argus_conv_tuning": (_I, [_I, _I]),
-    "argus_conv_tuning_get": (_I, [_I]),
+    "argus_conv_policy_default": (_I, [_I]),
     "argus_conv_launch_info": (_I, [_DESC, _I, _I, C.POINTER(C.c_int64)]),
     "argus_conv_dgrad": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P]),
     "argus_conv_dgrad_bn_rows": (_I, [_DESC, _I]),
@@ -133,7 +154,7 @@ class _Lib:
 
     def __getattr__(self, name: str):
         fn = getattr(self.dll, "argus_" + name)
-        if fn.restype is _I and not name.endswith(("rows", "tile", "version", "info", "tuning", "count")):
+        if fn.restype is _I and not name.endswith(("rows", "tile", "version", "info", "default", "count")):
             def call(*args, _fn=fn, _name=name):
                 rc = _fn(*args)
                 if rc != 0:

@@ -311,10 +311,17 @@ extern "C" {
 
 size_t argus_augment_params_bytes(void) { return sizeof(AugParams); }
 
+// scratch layout (floats): blur planes [nimg*3*h*w] | plasma maps [nimg*S*S] | per-image {min, max}
+// (float2). The float2 region starts at a 16-byte boundary: the map region is odd-sized (S*S odd), so
+// an unrounded offset misaligns the 8-byte accesses whenever nimg*(3hw + S*S) is odd.
+static int64_t aug_minmax_offset(int64_t nimg, int64_t hw, int64_t S) {
+  return (nimg * 3 * hw + nimg * S * S + 3) & ~(int64_t)3;
+}
+
 size_t argus_augment_scratch_bytes(int64_t nimg, int h, int w) {
   if (nimg <= 0 || h <= 0 || w <= 0) return 0;
   const int64_t S = ds_side(h, w);
-  return sizeof(float) * (size_t)(nimg * 3 * (int64_t)h * w + nimg * S * S + 2 * nimg);
+  return sizeof(float) * (size_t)(aug_minmax_offset(nimg, (int64_t)h * w, S) + 2 * nimg);
 }
 
 int argus_augment_photometric(int64_t nimg, int h, int w, const uint8_t* src, float* dst, const void* params,
@@ -329,7 +336,11 @@ int argus_augment_photometric(int64_t nimg, int h, int w, const uint8_t* src, fl
   const unsigned g1 = (unsigned)((nimg * hw + 255) / 256), g3 = (unsigned)((nimg * 3 * hw + 255) / 256);
   const int S = ds_side(h, w);
   float* map = scratch + nimg * 3 * hw;
-  float2* mm = reinterpret_cast<float2*>(map + nimg * S * S);
+  float2* mm = reinterpret_cast<float2*>(scratch + aug_minmax_offset(nimg, hw, S));
+  if ((reinterpret_cast<uintptr_t>(scratch) & 15) != 0) {
+    set_error("augment_photometric: scratch must be 16-byte aligned");
+    return ARGUS_ERR_ARG;
+  }
   hipLaunchKernelGGL(aug_color_kernel, dim3(g1), dim3(256), 0, st, nimg, (int)hw, w, src, dst, prm);
   for (int pass = 0; pass < 2; ++pass)
     hipLaunchKernelGGL(aug_blur_kernel, dim3(g3), dim3(256), 0, st, nimg, h, w, dst, scratch, prm, pass);

@@ -27,7 +27,7 @@ using namespace argus;
 
 extern "C" {
 
-int argus_abi_version(void) { return 10; }
+int argus_abi_version(void) { return 11; }
 
 const char* argus_last_error(void) { return g_last_error.c_str(); }
 
@@ -71,8 +71,7 @@ int argus_conv_fwd(const argus_conv_desc* d, int dtype, const void* x, const voi
 
 int argus_conv_fwd_stat_rows(const argus_conv_desc* d, int dtype) { return d ? conv_fwd_stat_rows(*d, dtype) : 0; }
 
-int argus_conv_tuning(int key, int value) { return conv_tuning(key, value); }
-int argus_conv_tuning_get(int key) { return conv_tuning_get(key); }
+int argus_conv_policy_default(int key) { return policy_default(key); }
 
 int argus_conv_launch_info(const argus_conv_desc* d, int dtype, int pass, int64_t* flops) {
   return d ? conv_launch_info(*d, dtype, pass, flops) : -1;

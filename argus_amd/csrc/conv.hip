@@ -942,11 +942,8 @@ __global__ __launch_bounds__(256) void weight_prep_batch_kernel(const WpEntry* _
 // host launchers
 // ------------------------------------------------------------------------------------------------
 
-// argus_conv_wgrad_apply hands its extra arguments to conv_wgrad through this (host, one thread per
-// process: the library's contract)
-static const argus_bn_bwd_prologue* g_wg_apply = nullptr;
-
 static int check_desc(const argus_conv_desc& d) {
+  if (int e = check_tuning(d)) return e;
   if (d.n <= 0 || d.h <= 0 || d.w <= 0 || d.k <= 0 || d.r <= 0 || d.s <= 0 || d.stride <= 0) {
     set_error("conv: non-positive dimension in descriptor");
     return ARGUS_ERR_ARG;
@@ -1019,24 +1016,64 @@ static void dispatch_ig_bwd(const IgParams& p, int maxM, int bm, int bn, hipStre
   else dispatch_ig_bwd1<T, OCC, 0>(p, maxM, bm, bn, st);
 }
 
-extern int g_glds_min_k, g_glds_min_grid;  // conv_glds.hip
-extern int g_bwd_min_px, g_bwd_max_rows, g_ew_target, g_ew_min_ppt, g_fin_div;  // bn.hip
-extern int g_halo64, g_halo_epi_prefetch, g_halo_blocks;  // conv_halo.hip, keys 30, 32 and 37
-extern int g_halo_enable, g_wg_halo_enable, g_wg_halo_target_blocks, g_halo_min_grid,
-    g_wg_halo_max_tiles;  // conv_halo.hip
-// argus_conv_tuning key 7: largest K (elements) served by the single-buffer OCC=3/4 kernel. Swept with
-// tools/convbench.py at B=64: 128 -> 1024 takes the fwd+dgrad conv time from 6.13 to 5.87 ms/step
-// (more resident workgroups hide the global-load latency better than the OCC=2 register ring).
-static int g_smallk_max = 1024;
-// argus_conv_tuning key 18: stem forward kernel, 2 (ring) or 4 (single buffer; convbench B=64:
-// 214 -> 179 us)
-static int g_stem_occ = 4;
-// argus_conv_tuning key 19: the bf16 stem forward on the LDS-patch kernel (stem.hip, 1) or on the
-// implicit GEMM (0)
-static int g_stem_halo = 1;
-// argus_conv_tuning key 34: the bf16 stem weight gradient on the LDS-patch kernel (stem.hip, 1) or on
-// wgrad_kernel's STEM variant (0)
-static int g_stem_wg = 1;
+// ------------------------------------------------------------------------------------------------
+// kernel-selection policy (argus_conv_policy_default): an immutable table + per-call overrides
+// ------------------------------------------------------------------------------------------------
+// Defaults, each the measured best:
+//  7: K <= 1024 on the single-buffer OCC=3/4 kernel (convbench B=64: 128 -> 1024 took fwd+dgrad from
+//     6.13 to 5.87 ms/step: more resident workgroups hide the global-load latency better than the OCC=2
+//     register ring);
+//  6 / 27: weight-gradient split targets 512 (1x1) / 512 (register-staged 3x3, Cout > 64: isolated
+//     sweeps favoured 1024, in the full step 512 wins +0.7 % - fewer fp32 split partials contending with
+//     the main stream for HBM); 3x3 with Cout = 64: 2048;
+//  19 / 34: the bf16 stem forward / weight gradient on the LDS-patch kernels (stem.hip);
+//  35: 128-row forward tiles from 16 K GEMM rows; 36: the glds kernel from 4 256-row tiles.
+static constexpr int kUnset = -1;
+static const Policy kDefaultPolicy = [] {
+  Policy p;
+  for (int& v : p.v) v = kUnset;
+  for (int k = 0; k < 6; ++k) p.v[k] = 0;
+  p.v[kWgradTarget] = 512;
+  p.v[kSmallKMax] = 1024;
+  p.v[kGldsMinK] = 1024;
+  p.v[kGldsMinGrid] = 256;
+  p.v[kHaloEnable] = 1;
+  p.v[kWgHaloEnable] = 1;
+  p.v[kWgHaloTarget] = 256;
+  p.v[kHaloMinGrid] = 256;
+  p.v[kWgHaloMaxTiles] = 4;
+  p.v[kStemLdsFwd] = 1;
+  p.v[kWgradTarget3x3] = 512;
+  p.v[kStemLdsWgrad] = 1;
+  p.v[kFwdBm128Rows] = 16 * 1024;
+  p.v[kGldsMinRows] = 4 * 256;
+  return p;
+}();
+
+int policy_default(int key) {
+  return key >= 0 && key < kNumTuneKeys ? kDefaultPolicy.v[key] : -1;
+}
+
+int check_tuning(const argus_conv_desc& d) {
+  if (d.n_tuning < 0 || (d.n_tuning > 0 && !d.tuning)) {
+    set_error("conv: bad tuning array");
+    return ARGUS_ERR_ARG;
+  }
+  for (int i = 0; i < d.n_tuning; ++i) {
+    const int k = d.tuning[i].key;
+    if (policy_default(k) == kUnset) {
+      set_error("conv: unknown tuning key " + std::to_string(k));
+      return ARGUS_ERR_ARG;
+    }
+  }
+  return ARGUS_OK;
+}
+
+Policy policy_of(const argus_conv_desc& d) {
+  Policy p = kDefaultPolicy;
+  for (int i = 0; i < d.n_tuning; ++i) p.v[d.tuning[i].key] = d.tuning[i].value;
+  return p;
+}
 
 // MX-fp8 operands (ARGUS_FP8) need whole 128-element k-steps inside one filter tap and no staging
 // transform of the A operand; other convs of an fp8 network run the bf16 kernels
@@ -1054,7 +1091,7 @@ static int run_ig(const IgParams& p, hipStream_t st, int bm, int bn) {
     maxM = p.ph[i].M > maxM ? p.ph[i].M : maxM;
     maxK = p.ph[i].K > maxK ? p.ph[i].K : maxK;
   }
-  const bool smallk = maxK <= g_smallk_max;
+  const bool smallk = maxK <= (*p.pol)[kSmallKMax];
   if constexpr (sizeof(T) == 2) {
     if (f8_ok(p)) {  // single-buffered (the staged bf16 pair per chunk doubles the staging registers)
       switch (p.bb.mode ? bwd_variant(p.bb) : 0) {
@@ -1070,8 +1107,7 @@ static int run_ig(const IgParams& p, hipStream_t st, int bm, int bn) {
   }
   if (p.stem) {
     if (p.N != 64 || bm != 128) { set_error("igemm: stem expects 64 output channels"); return ARGUS_ERR_SHAPE; }
-    if (g_stem_occ == 4) launch_ig<T, 128, 64, true, false, 4>(p, maxM, st);
-    else launch_ig<T, 128, 64, true, false, 2>(p, maxM, st);
+    launch_ig<T, 128, 64, true, false, 4>(p, maxM, st);  // single buffer (convbench B=64: 214 -> 179 us)
   } else if (p.pro_scale) {
     if (smallk) dispatch_ig<T, true, 4>(p, maxM, bm, bn, st);
     else dispatch_ig<T, true, 2>(p, maxM, bm, bn, st);
@@ -1085,88 +1121,42 @@ static int run_ig(const IgParams& p, hipStream_t st, int bm, int bn) {
   return check_launch("igemm_kernel");
 }
 
-// Tile policy (argus_conv_tuning): per pass {0 fwd, 1 dgrad, 2 wgrad}, forced tile_m / tile_n
-// (0 = heuristic) and the wgrad split target.
-static int g_force_bm[3] = {0, 0, 0}, g_force_bn[3] = {0, 0, 0};
-static int g_wgrad_target_blocks = 512;
-// key 27: split target of the register-staged 3x3 wgrad (Cout > 64). Isolated sweeps favoured 1024;
-// in the full step 512 wins (+0.7 %): fewer fp32 split partials (for layer 4's 3x3, 7 splits wrote
-// 66 MB of partials against 8 MB of operands), which contend with the main stream for HBM
-static int g_wgrad_target_3x3 = 512;
-static int g_wgrad_split_floor = 1;  // key 33 (A/B): splits = floor(target / tiles) (1) or ceil (0)
-
-static int* tuning_slot(int key) {
-  if (key >= 0 && key < 3) return &g_force_bm[key];
-  if (key >= 3 && key < 6) return &g_force_bn[key - 3];
-  switch (key) {
-    case 6: return &g_wgrad_target_blocks;
-    case 7: return &g_smallk_max;
-    case 8: return &g_glds_min_k;
-    case 9: return &g_glds_min_grid;
-    case 10: return &g_halo_enable;
-    case 11: return &g_wg_halo_enable;
-    case 12: return &g_wg_halo_target_blocks;
-    case 13: return &g_halo_min_grid;
-    case 14: return &g_wg_halo_max_tiles;
-    case 18: return &g_stem_occ;
-    case 19: return &g_stem_halo;
-    case 20: return &g_bwd_min_px;    // bn.hip: BN-backward pixels per block (min)
-    case 21: return &g_bwd_max_rows;  //   ... and blocks per channel group (max)
-    case 22: return &g_ew_target;     //   bn_apply / bwd_apply target blocks
-    case 23: return &g_ew_min_ppt;    //   ... min pixels per thread
-    case 24: return &g_fin_div;       //   BN finalize group-count divisor
-    case 27: return &g_wgrad_target_3x3;
-    case 33: return &g_wgrad_split_floor;
-    case 34: return &g_stem_wg;
-    case 37: return &g_halo_blocks;
-    case 30: return &g_halo64;
-    case 32: return &g_halo_epi_prefetch;
-    default: return nullptr;
-  }
-}
-
-int conv_tuning(int key, int value) {
-  int* slot = tuning_slot(key);
-  if (!slot) return -1;
-  *slot = value;
-  return 0;
-}
-
-int conv_tuning_get(int key) {
-  const int* slot = tuning_slot(key);
-  return slot ? *slot : -1;
-}
-
-static int pick_bn(int pass, int n) {
-  const int f = g_force_bn[pass];
+// column tile of pass {0 fwd, 1 dgrad, 2 wgrad} (policy keys 3..5 force 64 | 128)
+static int pick_bn(const Policy& pol, int pass, int n) {
+  const int f = pol[kForceBn + pass];
   if (f == 64 || (f == 128 && n % 128 == 0)) return f;
   return n % 128 == 0 ? 128 : 64;
 }
 
 // row-tile size of the forward GEMM (drives the BN-statistics partial count)
-static int fwd_bm(const argus_conv_desc& d) {
+static int fwd_bm(const argus_conv_desc& d, const Policy& pol) {
   if (d.stem) return 128;
-  if (g_force_bm[0]) return g_force_bm[0];
+  if (pol[kForceBm]) return pol[kForceBm];
   const long M = (long)d.n * d.ho * d.wo;
-  return M >= 16L * 1024 ? 128 : 64;
+  return M >= pol[kFwdBm128Rows] ? 128 : 64;
 }
 
 int conv_fwd_stat_rows(const argus_conv_desc& d, int) {
-  return cdiv(d.n * d.ho * d.wo, fwd_bm(d));
+  if (check_desc(d)) return 0;
+  return cdiv(d.n * d.ho * d.wo, fwd_bm(d, policy_of(d)));
 }
 
-int conv_fwd_stat_tile(const argus_conv_desc& d, int) { return fwd_bm(d); }
+int conv_fwd_stat_tile(const argus_conv_desc& d, int) {
+  if (check_desc(d)) return 0;
+  return fwd_bm(d, policy_of(d));
+}
 
 // dgrad row tile: 64 (swept: 64-row tiles beat 128 on every non-glds/non-halo dgrad at B=64, the
 // extra workgroups outweigh the re-read weight tile; dgrad has no statistics partials to multiply)
-static int dgrad_bm(const argus_conv_desc&) {
-  if (g_force_bm[1]) return g_force_bm[1];
+static int dgrad_bm(const Policy& pol) {
+  if (pol[kForceBm + 1]) return pol[kForceBm + 1];
   return 64;
 }
 
 // implicit-GEMM parameters of a forward conv (operand pointers left null)
-static void fwd_params(const argus_conv_desc& d, IgParams& p) {
+static void fwd_params(const argus_conv_desc& d, const Policy& pol, IgParams& p) {
   p = IgParams{};
+  p.pol = &pol;
   p.N = d.k; p.H = d.h; p.W = d.w; p.ish = d.stride; p.isw = d.stride;
   p.Ho = d.ho; p.Wo = d.wo; p.osh = 1; p.osw = 1; p.ldc = d.k;
   p.addend = nullptr; p.addend_mask = nullptr; p.stem = d.stem; p.nphase = 1;
@@ -1196,21 +1186,23 @@ int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, 
                         (double)d.n * d.ho * d.wo * d.k) +
                    (stats ? 8.0 * conv_fwd_stat_rows(d, dtype) * d.k : 0.0);
   if (d.stem && sc) { set_error("conv_fwd: stem has no prologue"); return ARGUS_ERR_ARG; }
-  if (d.stem && g_stem_halo && stem_fwd_launch(d, dtype, x, w, y, stats, st))  // stem.hip (bf16)
+  const Policy pol = policy_of(d);
+  if (d.stem && pol[kStemLdsFwd] && stem_fwd_launch(d, dtype, x, w, y, stats, st))  // stem.hip (bf16)
     return check_launch("stem_fwd_kernel");
   IgParams p;
-  fwd_params(d, p);
+  fwd_params(d, pol, p);
   p.a = x; p.b = w; p.c = y; p.pro_scale = sc; p.pro_shift = sh;
   p.stats = reinterpret_cast<float2*>(stats);
-  const int bm = fwd_bm(d), bn = d.stem ? 64 : pick_bn(0, d.k);
+  const int bm = fwd_bm(d, pol), bn = d.stem ? 64 : pick_bn(pol, 0, d.k);
   p.stat_tile = bm;
   p.f8 = f8;
   return dtype == ARGUS_BF16 ? run_ig<bf16>(p, st, bm, bn) : run_ig<float>(p, st, bm, bn);
 }
 
-static void dgrad_params(const argus_conv_desc& d, const void* dy, const void* wt, void* dx, const void* addend,
-                         const uint8_t* addend_mask, IgParams& p) {
+static void dgrad_params(const argus_conv_desc& d, const Policy& pol, const void* dy, const void* wt, void* dx,
+                         const void* addend, const uint8_t* addend_mask, IgParams& p) {
   p = IgParams{};
+  p.pol = &pol;
   p.a = dy; p.b = wt; p.c = dx;
   p.N = d.c; p.Cin = d.k; p.lda = d.k; p.H = d.ho; p.W = d.wo; p.ish = 1; p.isw = 1;
   p.Ho = d.h; p.Wo = d.w; p.osh = d.stride; p.osw = d.stride; p.ldc = d.c; p.ldb = d.r * d.s * d.k;
@@ -1240,7 +1232,7 @@ static void dgrad_params(const argus_conv_desc& d, const void* dy, const void* w
 }
 
 // BN-backward partial rows per phase of the kernel run_ig will choose for these dgrad params
-static int dgrad_prow(const IgParams& p, int dtype, const argus_conv_desc& d) {
+static int dgrad_prow(const IgParams& p, int dtype) {
   int maxM = 0, maxK = 0;
   for (int i = 0; i < p.nphase; ++i) {
     maxM = p.ph[i].M > maxM ? p.ph[i].M : maxM;
@@ -1250,7 +1242,7 @@ static int dgrad_prow(const IgParams& p, int dtype, const argus_conv_desc& d) {
     if (conv3x3_halo_ok(p)) return conv3x3_halo_tiles(p);
     if (igemm_glds_ok(p, maxM, maxK)) return cdiv(maxM, 256);
   }
-  return cdiv(maxM, dgrad_bm(d));
+  return cdiv(maxM, dgrad_bm(*p.pol));
 }
 
 static void dgrad_work(const argus_conv_desc& d, int dtype, bool addend, bool mask, bool bn, bool dual) {
@@ -1270,19 +1262,21 @@ int conv_dgrad(const argus_conv_desc& d, int dtype, const void* dy, const void* 
   if (f8) dtype = ARGUS_BF16;
   dgrad_work(d, dtype, addend != nullptr, addend_mask != nullptr, false, false);
   if (d.stem) { set_error("conv_dgrad: the stem input has no gradient"); return ARGUS_ERR_ARG; }
+  const Policy pol = policy_of(d);
   IgParams p;
-  dgrad_params(d, dy, wt, dx, addend, addend_mask, p);
+  dgrad_params(d, pol, dy, wt, dx, addend, addend_mask, p);
   p.f8 = f8;
-  const int bm = dgrad_bm(d), bn = pick_bn(1, d.c);
+  const int bm = dgrad_bm(pol), bn = pick_bn(pol, 1, d.c);
   return dtype == ARGUS_BF16 ? run_ig<bf16>(p, st, bm, bn) : run_ig<float>(p, st, bm, bn);
 }
 
 int conv_dgrad_bn_rows(const argus_conv_desc& d, int dtype) {
   if (check_desc(d) || d.stem) return -1;
+  const Policy pol = policy_of(d);
   IgParams p;
-  dgrad_params(d, nullptr, nullptr, nullptr, nullptr, nullptr, p);
+  dgrad_params(d, pol, nullptr, nullptr, nullptr, nullptr, nullptr, p);
   p.f8 = dtype == ARGUS_FP8;
-  return p.nphase * dgrad_prow(p, p.f8 ? ARGUS_BF16 : dtype, d);
+  return p.nphase * dgrad_prow(p, p.f8 ? ARGUS_BF16 : dtype);
 }
 
 // Whether argus_conv_dgrad_bn stages the apply prologue inside the (register-staged) dgrad kernel:
@@ -1305,8 +1299,9 @@ static bool dgrad_stages_prologue(const argus_conv_desc& d, int dtype, IgParams&
 
 int conv_dgrad_stages_prologue(const argus_conv_desc& d, int dtype) {
   if (check_desc(d) || d.stem) return 0;
+  const Policy pol = policy_of(d);
   IgParams p;
-  dgrad_params(d, nullptr, nullptr, nullptr, nullptr, nullptr, p);
+  dgrad_params(d, pol, nullptr, nullptr, nullptr, nullptr, nullptr, p);
   p.f8 = dtype == ARGUS_FP8;
   return dgrad_stages_prologue(d, p.f8 ? ARGUS_BF16 : dtype, p) ? 1 : 0;
 }
@@ -1331,8 +1326,9 @@ int conv_dgrad_bn(const argus_conv_desc& d, int dtype, const void* dy, const voi
     set_error("conv_dgrad_bn: bad apply-prologue arguments");
     return ARGUS_ERR_ARG;
   }
+  const Policy pol = policy_of(d);
   IgParams p;
-  dgrad_params(d, dy, wt, dm, addend, nullptr, p);
+  dgrad_params(d, pol, dy, wt, dm, addend, nullptr, p);
   p.f8 = f8;
   if (pro) {
     // the register-staged kernel stages dy = ca*dm + cb*y + cc itself; the halo / glds kernels (LDS
@@ -1359,7 +1355,7 @@ int conv_dgrad_bn(const argus_conv_desc& d, int dtype, const void* dy, const voi
   b.bits = bn->mask_bits; b.y2 = bn->y2; b.mean2 = bn->mean2; b.invstd2 = bn->invstd2;
   b.part = reinterpret_cast<float2*>(bn->part); b.part2 = reinterpret_cast<float2*>(bn->part2);
   b.mode = bn->mask_mode;
-  b.prow = dgrad_prow(p, dtype, d);
+  b.prow = dgrad_prow(p, dtype);
   if (bn->workspace) {  // the BN-backward finalize folded into this launch
     if (!bn->gamma || !bn->ca || !bn->cb || !bn->cc || (bn->y2 && (!bn->gamma2 || !bn->ca2 || !bn->cb2 || !bn->cc2)) ||
         d.c / 64 * 65 * 4 > (int)kBnCounterBytes) {
@@ -1376,7 +1372,7 @@ int conv_dgrad_bn(const argus_conv_desc& d, int dtype, const void* dy, const voi
     f.gamma2 = bn->gamma2; f.bmean2 = bn->mean2; f.binvstd2 = bn->invstd2;
     f.dgamma2 = bn->dgamma2; f.dbeta2 = bn->dbeta2; f.ca2 = bn->ca2; f.cb2 = bn->cb2; f.cc2 = bn->cc2;
   }
-  const int bm = dgrad_bm(d), bn_ = pick_bn(1, d.c);
+  const int bm = dgrad_bm(pol), bn_ = pick_bn(pol, 1, d.c);
   return dtype == ARGUS_BF16 ? run_ig<bf16>(p, st, bm, bn_) : run_ig<float>(p, st, bm, bn_);
 }
 
@@ -1386,10 +1382,11 @@ struct WgPlan {
 };
 
 static WgPlan wgrad_plan(const argus_conv_desc& d, int dtype) {
+  const Policy pol = policy_of(d);
   WgPlan pl;
   pl.N = d.stem ? 256 : d.r * d.s * d.c;
-  pl.bm = (g_force_bm[2] == 64 || d.k % 128) ? 64 : 128;
-  pl.bn = pick_bn(2, pl.N);
+  pl.bm = (pol[kForceBm + 2] == 64 || d.k % 128) ? 64 : 128;
+  pl.bn = pick_bn(pol, 2, pl.N);
   if (d.stem) { pl.bm = 64; pl.bn = 128; }
   pl.mt = d.k / pl.bm;
   pl.nt = pl.N / pl.bn;
@@ -1398,11 +1395,11 @@ static WgPlan wgrad_plan(const argus_conv_desc& d, int dtype) {
   const long tiles = (long)pl.mt * pl.nt;
   // measured (tools/tilesweep.py, MI355X): 1x1 convs peak near 512 workgroups, 3x3 near 1024
   // (2048 when Cout = 64: one row tile, 9 column tiles)
-  long target = g_wgrad_target_blocks;
-  if (target == 512 && d.r == 3) target = d.k <= 64 ? 2048 : g_wgrad_target_3x3;
+  long target = pol[kWgradTarget];
+  if (target == 512 && d.r == 3) target = d.k <= 64 ? 2048 : pol[kWgradTarget3x3];
   // the grid (tiles x splits) stays within the target: a grid just past it (e.g. 36 tiles x 15 splits
   // = 540 for 512 two-per-CU slots) runs a second, nearly empty round of workgroups
-  long splits = g_wgrad_split_floor ? target / tiles : (target + tiles - 1) / tiles;
+  long splits = target / tiles;
   const long max_splits = (P + pl.kstep * 4 - 1) / (pl.kstep * 4);  // >= 4 k-steps per split
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
@@ -1477,9 +1474,12 @@ static void dispatch_wg(const WgParams& p, const WgPlan& pl, hipStream_t st) {
   }
 }
 
-int conv_wgrad(const argus_conv_desc& d, int dtype, const void* x, const float* sc, const float* sh,
-               const void* dy, float* dw, void* ws, size_t ws_bytes, hipStream_t st) {
+// ap != nullptr: argus_conv_wgrad_apply (dy staged as ca*dm + cb*y + cc from dm = `dy`)
+static int conv_wgrad_impl(const argus_conv_desc& d, int dtype, const void* x, const float* sc, const float* sh,
+                           const void* dy, const argus_bn_bwd_prologue* ap, float* dw, void* ws, size_t ws_bytes,
+                           hipStream_t st) {
   if (int e = check_desc(d)) return e;
+  const Policy pol = policy_of(d);
   g_launch_work = 2.0 * d.n * d.ho * d.wo * d.k * d.r * d.s * d.c;  // algorithmic flops / bytes (ktimer)
   const WgPlan pl = wgrad_plan(d, dtype);
   // algorithmic bytes: x + dy read once, the fp32 dW written once (the split partials and their
@@ -1493,8 +1493,8 @@ int conv_wgrad(const argus_conv_desc& d, int dtype, const void* x, const float* 
   }
   WgParams p = {};
   p.x = x; p.dy = dy; p.pro_scale = sc; p.pro_shift = sh; p.part = reinterpret_cast<float*>(ws);
-  if (g_wg_apply) {  // argus_conv_wgrad_apply (stem only)
-    p.ap_y = g_wg_apply->y; p.ap_ca = g_wg_apply->ca; p.ap_cb = g_wg_apply->cb; p.ap_cc = g_wg_apply->cc;
+  if (ap) {
+    p.ap_y = ap->y; p.ap_ca = ap->ca; p.ap_cb = ap->cb; p.ap_cc = ap->cc;
     g_launch_bytes += (dtype == ARGUS_BF16 ? 2.0 : 4.0) * (double)d.n * d.ho * d.wo * d.k;  // y of the apply
   }
   p.M = d.k; p.N = pl.N; p.Cin = d.stem ? 4 : d.c; p.lda = d.stem ? 4 : d.c;
@@ -1506,9 +1506,9 @@ int conv_wgrad(const argus_conv_desc& d, int dtype, const void* x, const float* 
   p.fd_hw = make_fastdiv(d.ho * d.wo); p.fd_w = make_fastdiv(d.wo);
   if (d.stem && sc) { set_error("conv_wgrad: stem has no prologue"); return ARGUS_ERR_ARG; }
   int splits = pl.splits;
-  if (d.stem && g_stem_wg && stem_wgrad_launch(d, dtype, x, dy, g_wg_apply, ws, ws_bytes, &splits, st)) {
+  if (d.stem && pol[kStemLdsWgrad] && stem_wgrad_launch(d, dtype, x, dy, ap, ws, ws_bytes, &splits, st)) {
     if (int e = check_launch("stem_wgrad_kernel")) return e;
-  } else if (g_wg_apply) {  // the register-staged kernel stages the apply; no halo / glds variant does
+  } else if (ap) {  // the register-staged kernel stages the apply; no halo / glds variant does
     if (dtype == ARGUS_BF16) dispatch_wg<bf16>(p, pl, st);
     else dispatch_wg<float>(p, pl, st);
     if (int e = check_launch("wgrad_kernel")) return e;
@@ -1528,22 +1528,24 @@ int conv_wgrad(const argus_conv_desc& d, int dtype, const void* x, const float* 
   return check_launch("wgrad_reduce_kernel");
 }
 
+int conv_wgrad(const argus_conv_desc& d, int dtype, const void* x, const float* sc, const float* sh,
+               const void* dy, float* dw, void* ws, size_t ws_bytes, hipStream_t st) {
+  return conv_wgrad_impl(d, dtype, x, sc, sh, dy, nullptr, dw, ws, ws_bytes, st);
+}
+
 int conv_wgrad_apply(const argus_conv_desc& d, int dtype, const void* x, const void* dm,
                      const argus_bn_bwd_prologue& ap, float* dw, void* ws, size_t ws_bytes, hipStream_t st) {
-  if (int e = check_desc(d)) return e;
   if (!ap.y || !ap.ca || !ap.cb || !ap.cc) { set_error("conv_wgrad_apply: bad apply arguments"); return ARGUS_ERR_ARG; }
-  g_wg_apply = &ap;
-  const int rc = conv_wgrad(d, dtype, x, nullptr, nullptr, dm, dw, ws, ws_bytes, st);
-  g_wg_apply = nullptr;
-  return rc;
+  return conv_wgrad_impl(d, dtype, x, nullptr, nullptr, dm, &ap, dw, ws, ws_bytes, st);
 }
 
 int conv_launch_info(const argus_conv_desc& d, int dtype, int pass, int64_t* flops) {
   if (check_desc(d)) return -1;
+  const Policy pol = policy_of(d);
   if (flops) *flops = 2LL * d.n * d.ho * d.wo * d.k * d.r * d.s * d.c;
   const int dtag = (dtype == ARGUS_BF16 || dtype == ARGUS_FP8) ? 1 : 0;
-  if (pass == 0) return 10000000 + dtag * 1000000 + fwd_bm(d) * 1000 + (d.stem ? 64 : pick_bn(0, d.k));
-  if (pass == 1) return 10000000 + dtag * 1000000 + dgrad_bm(d) * 1000 + pick_bn(1, d.c);
+  if (pass == 0) return 10000000 + dtag * 1000000 + fwd_bm(d, pol) * 1000 + (d.stem ? 64 : pick_bn(pol, 0, d.k));
+  if (pass == 1) return 10000000 + dtag * 1000000 + dgrad_bm(pol) * 1000 + pick_bn(pol, 1, d.c);
   const WgPlan pl = wgrad_plan(d, dtype);
   return 20000000 + dtag * 1000000 + pl.bm * 1000 + pl.bn;
 }

@@ -319,21 +319,19 @@ static void launch_glds(const IgParams& p, int maxM, hipStream_t st) {
   }
 }
 
-// argus_conv_tuning key 8: smallest K (taps*C) served by the glds kernel (0 = off). 512 -> 1024 after
-// the non-temporal epilogue stores (convbench B=64: fwd+dgrad 5.32 -> 5.20 ms)
-int g_glds_min_k = 1024;
-int g_glds_min_grid = 256;  // key 9: fewest workgroups for which it is chosen
-
+// policy key 8: smallest K (taps*C) served by the glds kernel (0 = off); 512 -> 1024 after the
+// non-temporal epilogue stores (convbench B=64: fwd+dgrad 5.32 -> 5.20 ms). Key 9: fewest workgroups.
 bool igemm_glds_ok(const IgParams& p, int maxM, int maxK) {
-  if (g_glds_min_k <= 0 || p.stem || p.pro_scale || maxK < g_glds_min_k || p.Cin % 64 || p.lda % 8 ||
-      p.ldb % 8 || maxM < 4 * 256)
+  const int min_k = (*p.pol)[kGldsMinK];
+  if (min_k <= 0 || p.stem || p.pro_scale || maxK < min_k || p.Cin % 64 || p.lda % 8 ||
+      p.ldb % 8 || maxM < (*p.pol)[kGldsMinRows])
     return false;
   if (p.stats && p.stat_tile != 128 && p.stat_tile != 64) return false;
   for (int i = 0; i < p.nphase; ++i)
     if (p.ph[i].K % 64) return false;
   // measured (tools/convbench.py): a win only with >= one 8-wave workgroup per CU; the 4-wave
   // 256x64 tile and sub-CU-count grids lose to the register-staged kernel
-  return !(p.N % 128 || cdiv(maxM, 256) * (p.N / 128) < g_glds_min_grid);
+  return !(p.N % 128 || cdiv(maxM, 256) * (p.N / 128) < (*p.pol)[kGldsMinGrid]);
 }
 
 bool igemm_glds_launch(const IgParams& p, int maxM, int maxK, hipStream_t st) {

@@ -67,8 +67,7 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_h
   __shared__ __attribute__((aligned(1024))) u32x4 lds[LDS_BYTES / 16];
 
   const IgPhase& ph = p.ph[0];
-  const bool blk = p.hTW > 0;  // hTH x hTW block tiles (dgrad without statistics)
-  const int mtiles = blk ? ph.M / (p.H * p.W) * p.hRT * p.hCT : ph.M / 256;
+  const int mtiles = ph.M / 256;
   const int ntiles = p.N / BN;
   const int nwg = mtiles * ntiles;
   if ((int)blockIdx.x >= nwg) return;
@@ -80,28 +79,15 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_h
   const bf16* __restrict__ Wt = reinterpret_cast<const bf16*>(p.b);
   const uint32_t lds0 = (uint32_t)(uintptr_t)lds;
 
-  // block geometry: NI images x R rows x TW columns of output = input (stride 1), from column c0.
-  // Whole rows / images: 256 consecutive pixels (TW = W). Blocks: slots m >= R * TW, or below the
-  // image, are padding (no store, no BN-backward contribution; their halo rows are valid positions).
+  // tile geometry: NI images x R rows x W columns of output = input (stride 1): 256 consecutive pixels
   const int H = p.H, W = p.W, HWi = H * W;
-  int NI, R, r0, img0, c0 = 0, TW = W;
-  if (blk) {
-    const int tpi = p.hRT * p.hCT;
-    img0 = mt / tpi;
-    const int rem = mt - img0 * tpi, rt = rem / p.hCT;
-    NI = 1; R = p.hTH; TW = p.hTW; r0 = rt * R; c0 = (rem - rt * p.hCT) * TW;
-  } else if (HWi >= 256) { NI = 1; R = 256 / W; img0 = (mt * 256) / HWi; r0 = (mt * 256 - img0 * HWi) / W; }
+  int NI, R, r0, img0;
+  if (HWi >= 256) { NI = 1; R = 256 / W; img0 = (mt * 256) / HWi; r0 = (mt * 256 - img0 * HWi) / W; }
   else { NI = 256 / HWi; R = H; img0 = mt * NI; r0 = 0; }
-  const int HWD = TW + 2, HR = R + 2, IMGP = HR * HWD;
+  const int HWD = W + 2, HR = R + 2, IMGP = HR * HWD;
   const int npos = NI * IMGP;
-  const int RTW = R * TW;
-  // output slot m (0..255) of this tile: its pixel's element offset (in units of ldc) or -1 (padding)
-  auto slot_px = [&](int m) -> long {
-    if (!blk) return (long)mt * 256 + m;
-    const int lr = m / TW, lc = m - lr * TW;
-    if (m >= RTW || r0 + lr >= H) return -1;
-    return ((long)img0 * H + r0 + lr) * W + c0 + lc;
-  };
+  const int RTW = R * W;
+  auto slot_px = [&](int m) -> long { return (long)mt * 256 + m; };  // output pixel of tile slot m
 
   // halo glds sources: position q = 8*(i*NW + wave) + lane/8, channel chunk (lane&7)^swz8(q)
   int h_off[HG];
@@ -111,7 +97,7 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_h
     const int q = 8 * (i * NW + wave) + (lane >> 3);
     const int ii = q / IMGP, rem = q - ii * IMGP;
     const int hr = rem / HWD, hc = rem - hr * HWD;
-    const int ih = r0 + hr - 1, iw = c0 + hc - 1;
+    const int ih = r0 + hr - 1, iw = hc - 1;
     h_ok[i] = q < npos && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
     h_off[i] = h_ok[i] ? (((img0 + ii) * H + ih) * W + iw) * p.lda + ((lane & 7) ^ swz8(q)) * 8 : 0;
   }
@@ -144,10 +130,9 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_h
   int hb[4];
 #pragma unroll
   for (int mi = 0; mi < 4; ++mi) {
-    int m = wm * 64 + mi * 16 + i16;
-    if (m >= NI * RTW) m = 0;  // padding slot (blocks): read a valid position, result discarded
+    const int m = wm * 64 + mi * 16 + i16;
     const int ii = m / RTW, rem = m - ii * RTW;
-    const int lr = rem / TW, lc = rem - lr * TW;
+    const int lr = rem / W, lc = rem - lr * W;
     hb[mi] = ii * IMGP + lr * HWD + lc;
   }
 
@@ -218,7 +203,7 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_h
         for (int i = 0; i < NITP; ++i) {
           const int rr = tid / CPR_ + (NT / CPR_) * i;
           const long px = slot_px(rr);
-          epi_load<bf16, BW>(p, (size_t)(px < 0 ? 0 : px) * p.ldc + nt * BN + (tid % CPR_) * 8, pre[i]);
+          epi_load<bf16, BW>(p, (size_t)px * p.ldc + nt * BN + (tid % CPR_) * 8, pre[i]);
         }
       }
     }
@@ -292,20 +277,16 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_h
 #pragma unroll
   for (int i0 = 0; i0 < NIT; i0 += U) {
     size_t off[U];
-    bool okr[U];
     EpiIn in[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int rr = tid / CPR + RPP * (i0 + u);
-      const long px = slot_px(rr);
-      okr[u] = px >= 0;
-      off[u] = (size_t)(okr[u] ? px : 0) * p.ldc + nt * BN + c * 8;
+      off[u] = (size_t)slot_px(rr) * p.ldc + nt * BN + c * 8;
       if (PRE && p.epi_pre) in[u] = pre[PRE ? i0 + u : 0];
       else epi_load<bf16, BW>(p, off[u], in[u]);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (!okr[u]) continue;
       const int rr = tid / CPR + RPP * (i0 + u);
       const u32x4 v = *reinterpret_cast<const u32x4*>(Cs + rr * LD + c * 8);
       st16_nt(Cg + off[u], epi_apply<bf16, BW>(p, v, in[u], bwd));
@@ -329,15 +310,13 @@ static const char* halo_name() {
   return s.c_str();
 }
 
-// key 32: prefetch the BN-backward epilogue operands of the halo dgrad under its last channel chunk:
-// 1 = on the single-buffer 64-column variant (layer 1: 172 -> 163 us), 2 = every variant (the
-// 128-column one measured 83 -> 100 us, the step within noise), 0 = off
-int g_halo_epi_prefetch = 1;
-
+// The BN-backward epilogue operands of the halo dgrad are prefetched under its last channel chunk on
+// the single-buffer 64-column variant (layer 1: 172 -> 163 us); on the 128-column one it measured
+// 83 -> 100 us (the step within noise), so that variant loads them after the loop.
 template <int BN, int BW, int HB>
 static void launch_halo2(const IgParams& p0, hipStream_t st) {
   IgParams p = p0;
-  p.epi_pre = g_halo_epi_prefetch == 2 || (g_halo_epi_prefetch == 1 && HB == 1);
+  p.epi_pre = HB == 1;
   plan_fin(p, 256);
   dim3 grid(conv3x3_halo_tiles(p) * (p.N / BN));
   timed_launch(halo_name<BN, BW, HB>(), conv3x3_halo_kernel<BN, BW, HB>, grid, dim3(4 * (BN / 64) * 64),
@@ -348,8 +327,7 @@ template <int BN, int BW>
 static void launch_halo1(const IgParams& p, hipStream_t st) {
   if constexpr (BN == 64) {
     const int HWi = p.H * p.W;
-    const int npos = p.hTW ? (p.hTH + 2) * (p.hTW + 2)
-                           : (HWi >= 256 ? (256 / p.W + 2) * (p.W + 2) : (256 / HWi) * (p.H + 2) * (p.W + 2));
+    const int npos = HWi >= 256 ? (256 / p.W + 2) * (p.W + 2) : (256 / HWi) * (p.H + 2) * (p.W + 2);
     if (p.Cin == 64 && npos <= kHaloPos1) {  // one channel chunk: one halo buffer, two workgroups per CU
       launch_halo2<BN, BW, 1>(p, st);
       return;
@@ -368,106 +346,61 @@ static void launch_halo(const IgParams& p, hipStream_t st) {
   }
 }
 
-int g_halo_enable = 1;      // argus_conv_tuning key 10
-int g_halo_min_grid = 256;  // key 13: fewest workgroups for which the fwd/dgrad halo kernel is chosen
-// key 30: 64-channel 3x3 layers (layer 1: Cin = Cout = 64) on the 4-wave, single-halo-buffer variant
-// (two workgroups per CU). B=64 in the full step: fwd 80 -> 71 us, dgrad + BN epilogue 147 -> 132 us
-// per layer; 8245 -> 8302 img/s (two paired runs on one box)
-int g_halo64 = 1;
-// key 37: the dgrad on TH x TW block tiles where the width does not divide 256 (1) or not (0).
-// Off: at 376 x 672, B=128 it moves 11 of 21 dgrads from the 256x128 GEMM to the halo kernel for no
-// net gain (2518.6 vs 2524.4 img/s, paired on one box): the 64-channel 168-wide layer loses what the
-// 128-channel layers win. Kept parity-tested (test_conv3x3_halo_dgrad_block_tiles) for later tuning.
-int g_halo_blocks = 0;
-
-// Block tiles for frames whose width does not divide 256 (the 376 x 672 frame's 168-, 84-, 42- and
-// 21-wide layers), dgrad only (no forward statistics: their finalize assumes full 128-pixel partial
-// rows): TH x TW blocks of one image with TW | W, TH = min(256 / TW, H), the halo within kHaloPos;
-// the most image pixels per 256 slots (ragged last row block), then the fewest halo positions per pixel.
-static bool halo_blocks(const IgParams& p, int& TH, int& TW, int& RT, int& CT) {
-  const int H = p.H, W = p.W;
-  double best = 0.0, best_ov = 1e30;
-  for (int tw = W < 256 ? W : 256; tw >= 8; --tw) {
-    if (W % tw) continue;
-    int th = 256 / tw;
-    if (th > H) th = H;
-    const int npos = (th + 2) * (tw + 2);
-    if (npos > kHaloPos) continue;
-    const int rt = (H + th - 1) / th;
-    const double eff = (double)H * tw / ((double)rt * 256.0), ov = (double)npos / (th * tw);
-    if (eff > best + 1e-9 || (eff > best - 1e-9 && ov < best_ov)) {
-      best = eff; best_ov = ov;
-      TH = th; TW = tw; RT = rt; CT = W / tw;
-    }
-  }
-  return best >= 0.75;
-}
-
-// tile geometry of a halo-eligible conv: false = not servable (hTW = 0: 256 consecutive pixels)
-static bool halo_geom(const IgParams& p, IgParams& g, int& npos, int& tiles) {
+// Tile geometry of a halo-eligible conv: 256 consecutive output pixels = whole rows of one image or
+// whole images (false = not servable). (TH x TW block tiles for frames whose width does not divide 256
+// - the 376 x 672 frame's 168-, 84-, 42- and 21-wide layers - were built and measured: at B=128 they
+// moved 11 of 21 dgrads off the 256 x 128 GEMM for no net gain, 2518.6 vs 2524.4 img/s; removed.)
+static bool halo_geom(const IgParams& p, int& npos, int& tiles) {
   const IgPhase& ph = p.ph[0];
   const int HWi = p.H * p.W;
-  g.hTH = g.hTW = g.hRT = g.hCT = 0;
-  bool rows = ph.M % 256 == 0;
-  if (rows) {
-    if (HWi >= 256) {
-      rows = 256 % p.W == 0 && HWi % 256 == 0;
-      npos = (256 / p.W + 2) * (p.W + 2);
-    } else {
-      rows = 256 % HWi == 0;
-      npos = (256 / HWi) * (p.H + 2) * (p.W + 2);
-    }
-    rows = rows && npos <= kHaloPos;
+  if (ph.M % 256) return false;
+  bool rows;
+  if (HWi >= 256) {
+    rows = 256 % p.W == 0 && HWi % 256 == 0;
+    npos = (256 / p.W + 2) * (p.W + 2);
+  } else {
+    rows = 256 % HWi == 0;
+    npos = (256 / HWi) * (p.H + 2) * (p.W + 2);
   }
-  if (rows) {
-    tiles = ph.M / 256;
-    return true;
-  }
-  if (p.stats || !g_halo_blocks) return false;
-  int TH, TW, RT, CT;
-  if (!halo_blocks(p, TH, TW, RT, CT)) return false;
-  g.hTH = TH; g.hTW = TW; g.hRT = RT; g.hCT = CT;
-  npos = (TH + 2) * (TW + 2);
-  tiles = ph.M / HWi * RT * CT;
+  if (!rows || npos > kHaloPos) return false;
+  tiles = ph.M / 256;
   return true;
 }
 
 // 3x3 / stride 1 / pad 1, same input and output grid, one phase; 256-pixel tiles (whole rows / whole
-// images) or, for the dgrad, TH x TW block tiles
+// images). Policy keys 10 (enable) and 13 (fewest workgroups; 1 also allows the 4-wave 64-column
+// variant on any shape: tests).
 int conv3x3_halo_ok(const IgParams& p) {
-  if (!g_halo_enable || p.stem || p.pro_scale || p.nphase != 1 || p.ish != 1 || p.isw != 1 || p.osh != 1 ||
+  const Policy& pol = *p.pol;
+  if (!pol[kHaloEnable] || p.stem || p.pro_scale || p.nphase != 1 || p.ish != 1 || p.isw != 1 || p.osh != 1 ||
       p.osw != 1)
     return 0;
   const IgPhase& ph = p.ph[0];
   if (ph.K != 9 * p.Cin || p.Cin % 64 || p.lda % 8 || p.ldb % 8 || p.H != p.Ho || p.W != p.Wo) return 0;
   for (int t = 0; t < 9; ++t)
     if (ph.dh[t] < -1 || ph.dh[t] > 1 || ph.dw[t] < -1 || ph.dw[t] > 1) return 0;
-  IgParams g;
   int npos, tiles;
-  if (!halo_geom(p, g, npos, tiles)) return 0;
+  if (!halo_geom(p, npos, tiles)) return 0;
   if (p.stats && p.stat_tile != 64 && p.stat_tile != 128) return 0;
   // measured (tools/convbench.py, B=64): wins only with 8-wave workgroups (N % 128) filling every CU;
-  // the 4-wave BN=64 tile and sub-CU-count grids lose to the register-staged kernel
-  if (p.N % 128 == 0 && tiles * (p.N / 128) >= g_halo_min_grid) return 128;
-  if (g_halo64 && p.N == 64 && p.Cin == 64 && tiles >= g_halo_min_grid) return 64;
-  if (g_halo_min_grid <= 1 && p.N % 64 == 0) return 64;  // forced (tests): the 4-wave variant
+  // the 4-wave BN=64 tile and sub-CU-count grids lose to the register-staged kernel - except the
+  // 64-channel layer-1 3x3 convs on the single-halo-buffer variant (two workgroups per CU; B=64 in the
+  // full step: fwd 80 -> 71 us, dgrad + BN epilogue 147 -> 132 us per layer; 8245 -> 8302 img/s)
+  const int min_grid = pol[kHaloMinGrid];
+  if (p.N % 128 == 0 && tiles * (p.N / 128) >= min_grid) return 128;
+  if (p.N == 64 && p.Cin == 64 && tiles >= min_grid) return 64;
+  if (min_grid <= 1 && p.N % 64 == 0) return 64;  // forced (tests): the 4-wave variant
   return 0;
 }
 
 int conv3x3_halo_tiles(const IgParams& p) {
-  IgParams g;
   int npos, tiles;
-  return halo_geom(p, g, npos, tiles) ? tiles : 0;
+  return halo_geom(p, npos, tiles) ? tiles : 0;
 }
 
-bool conv3x3_halo_launch(const IgParams& p0, hipStream_t st) {
-  const int bn = conv3x3_halo_ok(p0);
+bool conv3x3_halo_launch(const IgParams& p, hipStream_t st) {
+  const int bn = conv3x3_halo_ok(p);
   if (!bn) return false;
-  IgParams p = p0;
-  int npos, tiles;
-  IgParams g;
-  halo_geom(p0, g, npos, tiles);
-  p.hTH = g.hTH; p.hTW = g.hTW; p.hRT = g.hRT; p.hCT = g.hCT;
   if (bn == 128) launch_halo<128>(p, st);
   else launch_halo<64>(p, st);
   return true;
@@ -692,17 +625,13 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(const WgHaloParam
 }
 
 
-int g_wg_halo_enable = 1;          // argus_conv_tuning key 11
-// key 12: split target of the 3x3 halo wgrad. 512 -> 256 once it runs on the side stream beside the
-// main-stream chain (bench B=64: +0.6-0.9 %, two paired runs)
-int g_wg_halo_target_blocks = 256;
-int g_wg_halo_max_tiles = 4;        // key 14
-
 // Tile geometry of the halo weight gradient. H*W < 128: NI = 128 / (H*W) whole images per tile
 // (128 % HW == 0). Otherwise a TH x TW block of one image: over the divisors TW of W (<= 128) with
 // TH = min(128 / TW, H) rows and a (TH+2) x (TW+2) halo within kWgHaloPos, the most useful pixels per
-// 128 slots (ragged last row block included), ties to the wider block. 256 x 256 frames: TW = W
-// (whole rows, as before); 168- and 84-wide frames: 3 x 42.
+// 128 slots (ragged last row block included), ties to the wider block. 256 x 256 frames: the 64-wide
+// layer 1 gets 4 x 32 blocks ((2+2) x (64+2) = 264 positions would exceed kWgHaloPos = 256), the 32-
+// and 16-wide layers whole rows (4 x 32, 8 x 16), the 8 x 8 layer two whole images; 168- and 84-wide
+// frames: 3 x 42.
 struct WgHaloGeom {
   int TH, TW, NI, RT, CT;
   long ptiles;
@@ -736,9 +665,11 @@ static bool wg_halo_geom(const argus_conv_desc& d, WgHaloGeom& gm) {
 }
 
 // Plan for a 3x3 / stride 1 / pad 1 bf16 weight gradient: false when not served. splits * K * 9C
-// fp32 partials.
+// fp32 partials. Policy keys 11 (enable), 12 (split target: 512 -> 256 once it ran on the side stream
+// beside the main-stream chain, bench B=64 +0.6-0.9 %) and 14 (most channel tiles).
 bool wgrad3x3_halo_plan(const argus_conv_desc& d, int dtype, int* splits, int* tps) {
-  if (!g_wg_halo_enable || dtype != ARGUS_BF16 || d.stem || d.r != 3 || d.s != 3 || d.stride != 1 || d.pad != 1 ||
+  const Policy pol = policy_of(d);
+  if (!pol[kWgHaloEnable] || dtype != ARGUS_BF16 || d.stem || d.r != 3 || d.s != 3 || d.stride != 1 || d.pad != 1 ||
       d.c % 64 || d.k % 64 || d.ho != d.h || d.wo != d.w)
     return false;
   WgHaloGeom gm;
@@ -747,8 +678,8 @@ bool wgrad3x3_halo_plan(const argus_conv_desc& d, int dtype, int* splits, int* t
   const long tiles = (long)(d.k / 64) * (d.c / 64);
   // measured: a win for <= 4 (k, c) tiles (the 64- and 128-channel layers); beyond, its two tr16
   // operand streams make it LDS-read-bound and the register-staged wgrad_kernel is faster
-  if (tiles > g_wg_halo_max_tiles) return false;
-  long s = (g_wg_halo_target_blocks + tiles - 1) / tiles;
+  if (tiles > pol[kWgHaloMaxTiles]) return false;
+  long s = (pol[kWgHaloTarget] + tiles - 1) / tiles;
   if (s < 1) s = 1;
   if (s > ptiles) s = ptiles;
   const long per = (ptiles + s - 1) / s;

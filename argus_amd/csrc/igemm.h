@@ -3,6 +3,7 @@
 #pragma once
 #include "common.h"
 #include "bnfin.h"
+#include "internal.h"
 #include "../../include/argus_hip.h"
 
 namespace argus {
@@ -62,10 +63,8 @@ struct IgParams {
   BnFin fin;      // BN finalize folded into this launch (fin.mode != 0)
   BnApplyPro ap;  // dgrad only: the A operand is dm (ap.y != nullptr)
   int f8;         // ARGUS_FP8: MX-fp8 operands where the shape allows (host dispatch only)
-  int epi_pre;    // halo dgrad: prefetch the BN-backward epilogue operands under the last chunk (key 32)
-  // halo fwd/dgrad tile geometry (conv_halo.hip, host-planned): hTW == 0 -> 256 consecutive pixels
-  // (whole rows / whole images); else a hTH x hTW block of one image, hRT x hCT blocks per image
-  int hTH, hTW, hRT, hCT;
+  int epi_pre;    // halo dgrad: prefetch the BN-backward epilogue operands under the last chunk
+  const Policy* pol;  // host only (kernel selection of this call; never read on the device)
 };
 
 // compile-time epilogue/prologue variant of the dgrad kernels: low 3 bits = BN-backward epilogue

@@ -18,8 +18,37 @@ int conv_fwd_stat_rows(const argus_conv_desc& d, int dtype);
 // BN workspace layout (bn.hip): [0, kBnCounterBytes) ticket counters, then double2 group results
 constexpr size_t kBnCounterBytes = 16384;
 int conv_fwd_stat_tile(const argus_conv_desc& d, int dtype);
-int conv_tuning(int key, int value);
-int conv_tuning_get(int key);
+
+// Kernel-selection policy (argus_conv_policy_default): the immutable library table overlaid with one
+// call's overrides (argus_conv_desc.tuning). Host-only; built per call, never stored.
+enum TuneKey : int {
+  kForceBm = 0,         // 0..2: row tile of pass fwd / dgrad / wgrad (0 = heuristic)
+  kForceBn = 3,         // 3..5: column tile
+  kWgradTarget = 6,     // weight-gradient split target (workgroups)
+  kSmallKMax = 7,       // largest K on the single-buffer OCC 3/4 igemm
+  kGldsMinK = 8,        // smallest K on the glds forward / dgrad (0 = off)
+  kGldsMinGrid = 9,     // fewest workgroups for the glds kernel
+  kHaloEnable = 10,     // 3x3 stride-1 forward / dgrad on the LDS-halo kernel
+  kWgHaloEnable = 11,   // 3x3 stride-1 weight gradient on the LDS-halo kernel
+  kWgHaloTarget = 12,   // ... its split target
+  kHaloMinGrid = 13,    // fewest workgroups for the forward / dgrad halo kernel
+  kWgHaloMaxTiles = 14, // most 64 x 64 channel tiles for the halo weight gradient
+  kStemLdsFwd = 19,     // bf16 stem forward on the LDS-patch kernel
+  kWgradTarget3x3 = 27, // split target of the register-staged 3x3 weight gradient (Cout > 64)
+  kStemLdsWgrad = 34,   // bf16 stem weight gradient on the LDS-patch kernel
+  kFwdBm128Rows = 35,   // fewest forward GEMM rows for 128-row tiles
+  kGldsMinRows = 36,    // fewest GEMM rows (largest phase) for the glds kernel
+  kNumTuneKeys = 37
+};
+struct Policy {
+  int v[kNumTuneKeys];
+  int operator[](int key) const { return v[key]; }
+};
+int policy_default(int key);  // -1: not a key
+// The policy of one call: the defaults + d.tuning (the keys were validated by the conv entry point).
+Policy policy_of(const argus_conv_desc& d);
+// ARGUS_OK, or ARGUS_ERR_ARG (+ set_error) when d.tuning holds an unknown key or n_tuning < 0.
+int check_tuning(const argus_conv_desc& d);
 int conv_launch_info(const argus_conv_desc& d, int dtype, int pass, int64_t* flops);
 size_t conv_weight_prep_table_bytes(int count);
 int conv_weight_prep_table(int count, const argus_conv_desc* descs, const float* const* w, const int64_t* strides,

@@ -69,10 +69,14 @@ class _Conv:
 class ResNetEngine:
     """Workspace + launch schedule for one (batch, H, W, dtype) configuration on one device."""
 
-    def __init__(self, n_cams: int, resnet_output_dim: int, dtype: str, device: torch.device):
+    def __init__(self, n_cams: int, resnet_output_dim: int, dtype: str, device: torch.device,
+                 tuning: dict | None = None):
         if dtype not in ("fp32", "bf16", "fp8"):
             raise ValueError(f"compute dtype must be 'fp32', 'bf16' or 'fp8', got {dtype!r}")
         self.L = lib()
+        # per-call overrides of the library's kernel-selection policy, attached to every conv descriptor
+        # of this engine (argus_conv_desc.tuning; None = the library defaults, the benched selection)
+        self.tuning = dict(tuning) if tuning else None
         self.n_cams = n_cams
         self.rdim = resnet_output_dim
         self.dtype = dtype
@@ -130,7 +134,8 @@ class ResNetEngine:
         # the first block's downsample weight gradient runs on the main stream after the stem weight
         # gradient instead of on the side stream: the side stream's last weight gradients otherwise
         # outlast the main stream's stem work (an exposed ~150 us tail before the join; +0.4 % at B=64,
-        # two paired runs)
+        # two paired runs). An attribute, not an environment switch: test_gpu_train.py::
+        # test_side_stream_overlap_is_bit_identical runs both placements.
         self.tail_main = True
         self._tail: list = []
 
@@ -152,7 +157,8 @@ class ResNetEngine:
         convs: dict[str, _Conv] = {}
 
         def add(name, n, h, w, c, k, ks, s, p, stem=False):
-            d = ConvDesc(n, h, w, c, k, ks, ks, s, p, _out(h, ks, s, p), _out(w, ks, s, p), int(stem))
+            d = ConvDesc(n, h, w, c, k, ks, ks, s, p, _out(h, ks, s, p), _out(w, ks, s, p), int(stem)).with_tuning(
+                self.tuning)
             if stem:
                 wf = self._t(k, 256)
                 wd = None

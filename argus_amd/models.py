@@ -128,7 +128,8 @@ def strip_checkpoint_prefixes(state_dict):
 class NCameraCNN(nn.Module):
     """A CNN which assumes N cameras are available in the scene (argus/models.py:26-90)."""
 
-    def __init__(self, cfg: Optional[NCameraCNNConfig] = None, compute_dtype: str = "fp32") -> None:
+    def __init__(self, cfg: Optional[NCameraCNNConfig] = None, compute_dtype: str = "fp32",
+                 kernel_tuning: Optional[dict] = None) -> None:
         super().__init__()
         self.resnet = _ResNet50()
         if cfg is None:
@@ -145,6 +146,9 @@ class NCameraCNN(nn.Module):
             nn.Linear(128, 6),
         )
         self.compute_dtype = compute_dtype
+        # optional kernel-selection overrides ({policy key: value}, argus_conv_policy_default) for this
+        # model's engines - experiments and the kernel-coverage tests; None = the library defaults
+        self.kernel_tuning = dict(kernel_tuning) if kernel_tuning else None
         self._engines: dict = {}
 
     # ---------------------------------------------------------------- engine plumbing
@@ -152,10 +156,11 @@ class NCameraCNN(nn.Module):
         device = torch.device(device)
         if device.type == "cuda" and device.index is None:
             device = torch.device("cuda", torch.cuda.current_device())
-        key = (str(device), self.compute_dtype)
+        tuning = tuple(sorted((self.kernel_tuning or {}).items()))
+        key = (str(device), self.compute_dtype, tuning)
         eng = self._engines.get(key)
         if eng is None:
-            eng = ResNetEngine(self.n_cams, self.resnet_output_dim, self.compute_dtype, device)
+            eng = ResNetEngine(self.n_cams, self.resnet_output_dim, self.compute_dtype, device, dict(tuning))
             self._engines[key] = eng
         return eng
 
@@ -190,6 +195,13 @@ class NCameraCNN(nn.Module):
                 Bf[name + ".eps"] = m.eps
                 Bf[name + ".momentum"] = m.momentum if m.momentum is not None else 1.0 / (counts.get(name, 0) + 1)
         return P, Bf
+
+    def invalidate_bn_counters(self) -> None:
+        """Forget the host shadow of every ``num_batches_tracked`` (momentum=None BN, ``_maps``): the next
+        train-mode forward re-reads the device counters. Writes through ``.data`` (e.g.
+        ``dist.broadcast(b.data)``) do not bump a tensor's version counter, so whoever writes the counters
+        that way calls this (``train.sync_bn_buffers`` and the initial broadcast do)."""
+        self.__dict__.pop("_nbt_shadow", None)
 
     def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
         """``nn.Module.load_state_dict`` that also takes the reference's wrapped checkpoints: keys

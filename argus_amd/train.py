@@ -133,6 +133,9 @@ def sync_bn_buffers(model: torch.nn.Module, src: int = 0, group=None) -> None:
         return
     for b in model.buffers():
         dist.broadcast(b.data, src=src, group=group)
+    invalidate = getattr(model, "invalidate_bn_counters", None)
+    if invalidate is not None:  # .data writes do not bump the counters' version: re-read them
+        invalidate()
 
 
 def _device_for(cfg: TrainConfig, rank: int) -> torch.device:
@@ -195,6 +198,7 @@ def initialize_training(cfg: TrainConfig, rank: int = 0, world: int = 1):
     if distributed:  # DDP's constructor broadcast (train.py:199): every rank starts from rank 0's weights
         for t in list(model.parameters()) + list(model.buffers()):
             dist.broadcast(t.data, src=0)
+        model.invalidate_bn_counters()
     trainer = FusedTrainer(model, lr=cfg.learning_rate, max_grad_norm=cfg.max_grad_norm)
     scheduler = PlateauScheduler(trainer, patience=5, factor=0.5)
     # the reference's kornia augmentations of each training sample (data.py:222-224), on the device

@@ -23,9 +23,12 @@ Also reported:
   cpu_baseline - the CPU oracle (the reference's torch.nn ops on CPU, fp32, B=8) train step timed on
                  this host (rank 0, N=1), a bounded sample of ~15 s.
   val_loss     - mean SE(3) loss (argus/train.py:342) of the trained model in eval mode on a
-                 synthetic validation batch; val_se3_log_rms = sqrt(val_loss) (the RMS norm of the
+                 synthetic held-out batch; val_se3_log_rms = sqrt(val_loss) (the RMS norm of the
                  full se(3) log, translation included); val_rot_err_deg = mean rotation-angle
-                 component |phi| of the geodesic.
+                 component |phi| of the geodesic. The data is synthetic, so the value
+                 itself says nothing about accuracy; val_vs_oracle is the same validation by the CPU
+                 fp32 oracle with the same trained weights (rank 0, first 16 samples): the gap between
+                 the two is the metric's error half (north_star: pose error within 1e-4 at fp32).
 Batch: 64 samples per rank on one GPU (configs[1]); 256 per rank when launched with N > 1 ranks
 (configs[2], cube_unity_data_medium-shaped); --batch overrides.
 """
@@ -103,6 +106,33 @@ def pmc_mfma(kernel: str, B: int, H: int, W: int, dtype: str):
     return None
 
 
+def cpu_model() -> str:
+    """The host CPU's model name (/proc/cpuinfo), as BASELINE.md asks the CPU baseline to state."""
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def oracle_validation(model, vimg: torch.Tensor, vtgt: torch.Tensor) -> dict:
+    """The validation pass of argus/train.py:327-348 (eval mode, running BN statistics, mean SE(3) loss)
+    on the held-out batch, by the CPU fp32 oracle carrying this model's trained weights and buffers:
+    the reference's own numbers for the same weights, beside which the GPU's are reported."""
+    from oracle import se3
+    from oracle.ncamera import build_reference_model
+
+    ref = build_reference_model(42)
+    ref.load_state_dict({k: v.detach().float().cpu() for k, v in model.state_dict().items()})
+    ref.eval()
+    with torch.no_grad():
+        pred = ref(vimg.cpu().float())
+        loss = se3.geometric_loss(pred.double(), vtgt.cpu().double())
+    return {"pred": pred, "loss": loss}
+
+
 def cpu_baseline(batch: int, H: int, W: int, budget_s: float = 15.0) -> dict:
     """Oracle (CPU restatement of the reference model, same torch CPU ops) fwd+loss+bwd+clip+Adam."""
     from oracle import se3
@@ -131,6 +161,7 @@ def cpu_baseline(batch: int, H: int, W: int, budget_s: float = 15.0) -> dict:
         n += 1
     dt = time.perf_counter() - t0
     return {"value": round(2 * batch * n / dt, 3), "unit": "images/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(),
             "sample": f"oracle (reference torch.nn ops on CPU) fp32 train step, batch {batch} samples "
                       f"({2 * batch} images) of {H}x{W}, {n} timed steps after 1 warm-up, {dt:.1f} s"}
 
@@ -150,7 +181,11 @@ def main() -> None:
     ap.add_argument("--kernels", action="store_true", help="print the probe step's per-kernel table to stderr")
     ap.add_argument("--no-isolated", action="store_true",
                     help="skip the two untimed no-overlap steps that measure the dominant kernel alone")
-    ap.add_argument("--tune", nargs="*", default=[], help="dev: argus_conv_tuning key=value pairs")
+    ap.add_argument("--no-val-oracle", action="store_true", help="skip the CPU oracle validation check")
+    ap.add_argument("--val-oracle-batch", type=int, default=16,
+                    help="held-out samples the CPU fp32 oracle validates (rank 0)")
+    ap.add_argument("--tune", nargs="*", default=[],
+                    help="dev: kernel-selection overrides key=value (argus_conv_policy_default keys)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -174,14 +209,10 @@ def main() -> None:
     from argus_amd.step import FusedTrainer
     from argus_amd.losses import geometric_loss_fn
 
-    from argus_amd._lib import lib
-
-    for kv in args.tune:
-        k, v = kv.split("=")
-        assert lib().dll.argus_conv_tuning(int(k), int(v)) == 0, kv
+    tuning = {int(k): int(v) for k, v in (kv.split("=") for kv in args.tune)}
     B, (H, W) = (args.batch or (64 if world == 1 else 256)), args.hw
     torch.manual_seed(42)
-    model = NCameraCNN(compute_dtype=args.dtype).to(dev)
+    model = NCameraCNN(compute_dtype=args.dtype, kernel_tuning=tuning or None).to(dev)
     model.train()
     trainer = FusedTrainer(model, lr=1e-4, max_grad_norm=1.0)
     images, targets = synthetic_batch(B, H, W, 1000 + rank, dev)
@@ -260,7 +291,9 @@ def main() -> None:
     ctimer.stop()
     main_busy_ms = sum(v["total_ms"] for v in msumm.values()) / nprobe
 
-    # validation SE(3) error (eval mode, running BN statistics), synthetic held-out batch
+    # validation SE(3) error (eval mode, running BN statistics) of the trained weights on a synthetic
+    # held-out batch (seed 5000 + rank, never trained on), and the same validation by the CPU fp32 oracle
+    # with the same weights and buffers (rank 0): the metric's error half against the reference
     model.eval()
     vimg, vtgt = synthetic_batch(B, H, W, 5000 + rank, dev)
     from argus_amd.utils import rotation_angle_error
@@ -274,6 +307,22 @@ def main() -> None:
         dist.all_reduce(vsum)
     val_loss = (vsum[0] / vsum[2]).item()
     val_rot = (vsum[1] / vsum[2]).item()
+    val_oracle = None
+    if rank == 0 and not args.no_val_oracle:
+        nv = min(B, args.val_oracle_batch)
+        torch.set_num_threads(min(16, os.cpu_count() or 1))
+        o = oracle_validation(model, vimg[:nv], vtgt[:nv])
+        ours = geometric_loss_fn(vpred[:nv], vtgt[:nv]).double().cpu()
+        val_oracle = {
+            "samples": nv,
+            "val_loss_gpu": round(ours.mean().item(), 6),
+            "val_loss_oracle_fp32": round(o["loss"].mean().item(), 6),
+            "val_loss_abs_diff": float(f"{abs(ours.mean().item() - o['loss'].mean().item()):.3e}"),
+            "pred_max_abs_diff": float(f"{(vpred[:nv].float().cpu() - o['pred']).abs().max().item():.3e}"),
+            "per_sample_loss_max_abs_diff": float(f"{(ours - o['loss']).abs().max().item():.3e}"),
+            "note": f"eval-mode validation (argus/train.py:327-348) of the trained weights on the first {nv} "
+                    f"held-out samples: {args.dtype} HIP path vs the CPU fp32 oracle with the same weights",
+        }
 
     # the dominant kernel's own MFMA roof: MX-fp8 igemm variants (template flag 32) run at the dense
     # fp8 rate; in an "fp8" run the weight gradients and the 64-channel convs stay bf16
@@ -358,6 +407,7 @@ def main() -> None:
         "val_loss": round(val_loss, 6),
         "val_se3_log_rms": round(math.sqrt(max(val_loss, 0.0)), 6),
         "val_rot_err_deg": round(math.degrees(val_rot), 4),
+        "val_vs_oracle": val_oracle,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(8, H, W, args.cpu_seconds)

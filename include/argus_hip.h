@@ -35,6 +35,11 @@ typedef void* argus_stream_t; /* hipStream_t */
 enum { ARGUS_F32 = 0, ARGUS_BF16 = 1, ARGUS_FP8 = 2 };
 enum { ARGUS_OK = 0, ARGUS_ERR_ARG = 1, ARGUS_ERR_SHAPE = 2, ARGUS_ERR_HIP = 3 };
 
+/* One override of the kernel-selection policy (keys: argus_conv_policy_default). */
+typedef struct {
+  int32_t key, value;
+} argus_tuning;
+
 typedef struct {
   int32_t n, h, w; /* images, input spatial */
   int32_t c;       /* input channels (3 for the stem) */
@@ -43,6 +48,11 @@ typedef struct {
   int32_t stride, pad;
   int32_t ho, wo; /* output spatial */
   int32_t stem;   /* 1: the 7x7/2 stem (NHWC4 input, padded weights) */
+  /* Optional per-call overrides of the library's kernel-selection policy (experiments, autotuning and
+   * the kernel-coverage tests): n_tuning entries of `tuning`; 0 / NULL = the library defaults. The
+   * library keeps no mutable selection state: a call sees its own overrides and nothing else. */
+  int32_t n_tuning;
+  const argus_tuning* tuning;
 } argus_conv_desc;
 
 int argus_abi_version(void);
@@ -154,7 +164,9 @@ int argus_conv_dgrad_stages_prologue(const argus_conv_desc* d, int dtype);
 int argus_conv_dgrad_bn(const argus_conv_desc* d, int dtype, const void* dy, const void* w_dgrad,
                         void* dm, const void* addend, const argus_bn_bwd_epilogue* bn,
                         const argus_bn_bwd_prologue* pro, argus_stream_t stream);
-/* Tuning knobs (process-wide; for autotuning / experiments; every default is the measured best):
+/* Kernel-selection policy: the library's immutable default of a key (-1 for an unknown key); a conv
+ * descriptor may override keys for its own call (argus_conv_desc.tuning; an unknown key there makes
+ * the call fail with ARGUS_ERR_ARG). Every default is the measured best.
  * key 0..2 force the row tile (64|128, 0 = heuristic) of pass fwd/dgrad/wgrad, key 3..5 the column
  * tile, key 6 the wgrad split target (workgroups), key 7 the largest K (= taps*C) served by the
  * 4-workgroups-per-CU single-buffer forward/dgrad kernel, key 8 the smallest K served by the bf16
@@ -162,22 +174,14 @@ int argus_conv_dgrad_bn(const argus_conv_desc* d, int dtype, const void* dy, con
  * that kernel is chosen, key 10 enables (1) or disables (0) the LDS-halo kernel for 3x3 stride-1
  * forward/dgrad, key 11 the same for the 3x3 stride-1 weight gradient and key 12 its split target,
  * key 13 the fewest workgroups for the fwd/dgrad halo kernel (1 also allows its 64-channel variant
- * at any size), key 14 the most (64 x 64) channel tiles for the wgrad halo kernel, key 18 the stem
- * forward occupancy (2 | 4) of the implicit GEMM, key 19 the bf16 stem forward on the LDS-patch
- * kernel (1) or the implicit GEMM (0), keys 20-23 the BatchNorm elementwise-kernel geometry (backward min
- * pixels per block, max blocks per channel group; apply target blocks, min pixels per thread), key
- * 24 the BN finalize group-count divisor, key 27 the split target of the register-staged 3x3 weight
- * gradient, key 30 the 64-channel 3x3 stride-1 layers on the LDS-halo kernel's single-halo-buffer
- * variant (1) or on the implicit GEMM (0), key 32 where the 3x3 LDS-halo dgrad with a BN-backward
- * epilogue prefetches its epilogue operands under its last channel chunk (1: the single-halo-buffer
- * variant; 2 every variant; 0 none), key 33 the weight-gradient split count floor(target / tiles)
- * (1) or ceil (0), key 34 the bf16 stem weight gradient on the LDS-patch kernel (1) or on the
- * register-staged weight-gradient kernel (0), key 37 the 3x3 dgrad of frames whose width does not
- * divide 256 on the LDS-halo kernel's TH x TW block tiles (1) or on the implicit GEMM (0, default).
- * Returns 0, or -1 for an unknown key. */
-int argus_conv_tuning(int key, int value);
-/* Current value of a tuning key (-1 for an unknown key). */
-int argus_conv_tuning_get(int key);
+ * at any size), key 14 the most (64 x 64) channel tiles for the wgrad halo kernel, key 19 the bf16
+ * stem forward on the LDS-patch kernel (1) or the implicit GEMM (0), key 27 the split target of the
+ * register-staged 3x3 weight gradient, key 34 the bf16 stem weight gradient on the LDS-patch kernel
+ * (1) or on the register-staged weight-gradient kernel (0), key 35 the fewest GEMM rows (output
+ * pixels) for which the forward uses 128-row tiles (fewer: 64), key 36 the fewest GEMM rows for the
+ * glds kernel. (Keys scaled with the batch keep a smaller batch's kernel selection that of the larger
+ * one: tests/test_gpu_parity.py stage-checks the benched configurations' kernels that way.) */
+int argus_conv_policy_default(int key);
 /* Which tile a pass launches and its algorithmic work: pass 0 fwd, 1 dgrad, 2 wgrad. Returns a
  * tag (kind*10^7 + dtype*10^6 + tile_m*1000 + tile_n; kind 1 igemm, 2 wgrad) and writes
  * 2*P*K*R*S*C flops (P = n*ho*wo output pixels). */

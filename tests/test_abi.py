@@ -41,12 +41,20 @@ def test_bad_arguments_are_reported():
     bad = ConvDesc(2, 8, 8, 64, 64, 3, 3, 1, 1, 7, 8, 0)  # wrong ho
     with pytest.raises(ArgusHipError, match="ho/wo"):
         L.conv_fwd(C.byref(bad), 1, 16, 16, 16, None, None, None, None)
-    assert L.dll.argus_conv_tuning(99, 1) == -1
     fl = C.c_int64(0)
     good = ConvDesc(2, 8, 8, 64, 128, 3, 3, 2, 1, 4, 4, 0)
     tag = L.dll.argus_conv_launch_info(C.byref(good), 1, 0, C.byref(fl))
     assert fl.value == 2 * 2 * 4 * 4 * 128 * 9 * 64 and tag // 10000000 == 1
     assert L.dll.argus_conv_wgrad_workspace_bytes(C.byref(good), 1) > 0
+    # kernel-selection policy: immutable defaults, per-call overrides on the descriptor only
+    assert L.dll.argus_conv_policy_default(99) == -1 and L.dll.argus_conv_policy_default(20) == -1
+    assert L.dll.argus_conv_policy_default(35) == 16384 and L.dll.argus_conv_policy_default(7) == 1024
+    forced = good.with_tuning({1: 128, 4: 64})  # dgrad row / column tiles
+    assert L.dll.argus_conv_launch_info(C.byref(forced), 1, 1, None) % 1000000 == 128 * 1000 + 64
+    assert L.dll.argus_conv_launch_info(C.byref(good), 1, 1, None) % 1000000 == 64 * 1000 + 64
+    unknown = good.with_tuning({37: 1})  # removed key (halo block tiles)
+    with pytest.raises(ArgusHipError, match="unknown tuning key 37"):
+        L.conv_fwd(C.byref(unknown), 1, 16, 16, 16, None, None, None, None)
 
 
 def test_product_path_has_no_cpu_fallback():

@@ -56,16 +56,19 @@ def test_ops_match_restatement(cuda, ops):
     assert err < 2e-5, (ops, err)
 
 
-@pytest.mark.parametrize("hw", [(64, 64), (37, 70)])
-def test_plasma_shadow_matches_restatement(cuda, hw):
+@pytest.mark.parametrize("hw,cams", [((64, 64), 2), ((37, 70), 2), ((64, 64), 3)])
+def test_plasma_shadow_matches_restatement(cuda, hw, cams):
     """Diamond-square plasma map (65 x 65 grid for 64 x 64; 129 x 129 cropped to 37 x 70) and the
-    additive shade, against the float64 restatement."""
+    additive shade, against the float64 restatement. Three cameras: an odd image count, so the
+    per-image min/max scratch follows an odd number of floats (its 16-byte alignment)."""
     g = torch.Generator().manual_seed(2)
     B, (H, W) = 1, hw
-    x = torch.randint(0, 256, (B, 6, H, W), generator=g, dtype=torch.uint8)
-    p = _params(2, plasma_int=[-0.5, -0.3], plasma_q=[0.4, 0.2], plasma_rough=[0.3, 0.15], seed=[12345, 777])
+    x = torch.randint(0, 256, (B, 3 * cams, H, W), generator=g, dtype=torch.uint8)
+    p = _params(cams, plasma_int=[-0.5, -0.3, -0.4][:cams], plasma_q=[0.4, 0.2, 0.3][:cams],
+                plasma_rough=[0.3, 0.15, 0.2][:cams], seed=[12345, 777, 31][:cams])
     out = DeviceAugmentation(AugmentationConfig()).apply(x.to(cuda), p).cpu().double()
-    want = torch.stack([ref.augment_image(x.reshape(2, 3, H, W)[i], p[i]) for i in range(2)]).reshape(B, 6, H, W)
+    want = torch.stack([ref.augment_image(x.reshape(cams, 3, H, W)[i], p[i]) for i in range(cams)]).reshape(
+        B, 3 * cams, H, W)
     bad = ((out - want).abs() > 2e-5).double().mean().item()
     assert bad < 1e-3, bad  # fp32 vs fp64 noise can flip the threshold only at exact ties
     for i, q in ((0, 0.4), (1, 0.2)):

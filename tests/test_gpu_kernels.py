@@ -205,10 +205,10 @@ def test_stem_lds_patch_kernel(cuda):
         for key19 in (1, 0):
             y = torch.empty(n, d.ho, d.wo, 64, dtype=torch.bfloat16, device=cuda)
             stats = torch.full((rows, 64, 2), float("nan"), device=cuda)
-            with _tuned({19: key19}):
-                with KernelTimer() as t:
-                    L.conv_fwd(C.byref(d), BF16, ptr(x4), ptr(wf), ptr(y), None, None, ptr(stats), stream())
-                names = list(t.summary())
+            dk = d.with_tuning({19: key19})
+            with KernelTimer() as t:
+                L.conv_fwd(C.byref(dk), BF16, ptr(x4), ptr(wf), ptr(y), None, None, ptr(stats), stream())
+            names = list(t.summary())
             assert ("argus::stem_fwd_kernel" in names) == (served and key19 == 1), (n, H, W, key19, names)
             assert _rel(y.permute(0, 3, 1, 2), ref) < TOL["bf16"], ("stem fwd", n, H, W, key19)
             assert torch.isfinite(stats).all()
@@ -250,16 +250,16 @@ def test_stem_wgrad_lds_patch_kernel(cuda):
             outs = []
             for key34 in (1, 0):
                 dw = torch.full((64, 7, 7, 3), float("nan"), device=cuda)
-                with _tuned({34: key34}):
-                    with KernelTimer() as t:
-                        if apply:
-                            ap = BnBwdPrologue(ptr(y0), ptr(ca), ptr(cb), ptr(cc), None)
-                            L.conv_wgrad_apply(C.byref(d), BF16, ptr(x4), ptr(dm), C.byref(ap), ptr(dw), ptr(ws),
-                                               ws.numel(), stream())
-                        else:
-                            L.conv_wgrad(C.byref(d), BF16, ptr(x4), None, None, ptr(dm), ptr(dw), ptr(ws),
-                                         ws.numel(), stream())
-                    names = list(t.summary())
+                dk = d.with_tuning({34: key34})
+                with KernelTimer() as t:
+                    if apply:
+                        ap = BnBwdPrologue(ptr(y0), ptr(ca), ptr(cb), ptr(cc), None)
+                        L.conv_wgrad_apply(C.byref(dk), BF16, ptr(x4), ptr(dm), C.byref(ap), ptr(dw), ptr(ws),
+                                           ws.numel(), stream())
+                    else:
+                        L.conv_wgrad(C.byref(dk), BF16, ptr(x4), None, None, ptr(dm), ptr(dw), ptr(ws),
+                                     ws.numel(), stream())
+                names = list(t.summary())
                 want = f"argus::stem_wgrad_kernel<{'true' if apply else 'false'}>"
                 assert (want in names) == (served and key34 == 1), (n, H, W, apply, key34, names)
                 e = _rel(dw.permute(0, 3, 1, 2), ref)
@@ -579,7 +579,7 @@ def test_kernel_timer_records_exact_instantiations(cuda):
     tag = L.dll.argus_conv_launch_info(C.byref(d), BF16, 0, C.byref(fl))
     bm, bn = divmod(tag % 1000000, 1000)
     # K = 576: the single-buffer kernel (OCC 4; 3 for the 128x128 tile) when K <= tuning key 7
-    occ = (3 if bm == bn == 128 else 4) if 576 <= L.dll.argus_conv_tuning_get(7) else 2
+    occ = (3 if bm == bn == 128 else 4) if 576 <= L.dll.argus_conv_policy_default(7) else 2
     assert name == f"argus::igemm_kernel<__bf16, {bm}, {bn}, false, false, {occ}, 0>"
     assert v["launches"] == 3 and v["flops_per_launch"] == fl.value and v["avg_us"] > 0
     assert v["bytes_per_launch"] == 2 * (4 * 32 * 32 * 64 + 128 * 9 * 64 + 4 * 32 * 32 * 128)
@@ -604,47 +604,42 @@ def test_conv_glds_kernel_parity(cuda):
 
     torch.manual_seed(11)
     L = lib()
-    defaults = (L.dll.argus_conv_tuning_get(8), L.dll.argus_conv_tuning_get(9))
-    assert L.dll.argus_conv_tuning(8, 64) == 0 and L.dll.argus_conv_tuning(9, 1) == 0
-    try:
-        for cin, cout, k, s, hin, n in GLDS_SHAPES:
-            d, p = _desc(n, hin, hin, cin, cout, k, s)
-            x = torch.randn(n, hin, hin, cin)
-            w = torch.randn(cout, k, k, cin) * (2.0 / (k * k * cin)) ** 0.5
-            dy = torch.randn(n, d.ho, d.wo, cout)
-            xd, dyd = x.to(cuda, torch.bfloat16), dy.to(cuda, torch.bfloat16)
-            wf, wt = _prep(d, "bf16", w.to(cuda), cuda)
-            y = torch.empty(n, d.ho, d.wo, cout, dtype=torch.bfloat16, device=cuda)
-            rows = L.dll.argus_conv_fwd_stat_rows(C.byref(d), BF16)
-            stats = torch.empty(rows, cout, 2, device=cuda)
-            with KernelTimer("argus::igemm_glds_kernel") as t:
-                L.conv_fwd(C.byref(d), BF16, ptr(xd), ptr(wf), ptr(y), None, None, ptr(stats), stream())
-            M = n * d.ho * d.wo
-            if M >= 1024 and k * k * cin >= 64 and cout % 128 == 0:
-                assert len(t.summary()) == 1, (cin, cout, k, s, hin)
-            xr, wr, dyr = _q(x, "bf16").permute(0, 3, 1, 2), _q(w, "bf16").permute(0, 3, 1, 2), _q(dy, "bf16").permute(0, 3, 1, 2)
-            ref = F.conv2d(xr, wr, stride=s, padding=p)
-            assert _rel(y.permute(0, 3, 1, 2), ref) < TOL["bf16"], ("fwd", cin, cout, k, s)
-            tile = L.dll.argus_conv_fwd_stat_tile(C.byref(d), BF16)
-            mean, var = _merge_stats(stats.double().cpu(), tile, M)
-            yr = ref.permute(0, 2, 3, 1).reshape(-1, cout)
-            assert (mean - yr.mean(0)).abs().max() < 2e-2 * yr.std(0).max(), ("stats mean", cin, cout)
-            assert _rel(var, yr.var(0, unbiased=False)) < 2e-2, ("stats var", cin, cout)
-            # dgrad: plain, in-place accumulate, masked addend from another buffer
-            dx0 = torch.randn(n, hin, hin, cin)
-            dx = dx0.to(cuda, torch.bfloat16)
-            L.conv_dgrad(C.byref(d), BF16, ptr(dyd), ptr(wt), ptr(dx), ptr(dx), None, stream())
-            refd = torch.nn.grad.conv2d_input(xr.shape, wr, dyr, stride=s, padding=p)
-            assert _rel(dx.permute(0, 3, 1, 2), refd + _q(dx0, "bf16").permute(0, 3, 1, 2)) < TOL["bf16"], ("dgrad+", cin)
-            res = _q(torch.randn(n, hin, hin, cin), "bf16")
-            keep = res > 0
-            bits = ((keep.reshape(-1, 8).int() << torch.arange(8)).sum(1)).to(torch.uint8).to(cuda)
-            resg = res.to(cuda, torch.bfloat16)
-            L.conv_dgrad(C.byref(d), BF16, ptr(dyd), ptr(wt), ptr(dx), ptr(resg), ptr(bits), stream())
-            assert _rel(dx.permute(0, 3, 1, 2), refd + (res * keep).permute(0, 3, 1, 2)) < TOL["bf16"], ("dgrad mask", cin)
-    finally:
-        L.dll.argus_conv_tuning(8, defaults[0])
-        L.dll.argus_conv_tuning(9, defaults[1])
+    for cin, cout, k, s, hin, n in GLDS_SHAPES:
+        d, p = _desc(n, hin, hin, cin, cout, k, s)
+        d = d.with_tuning({8: 64, 9: 1})
+        x = torch.randn(n, hin, hin, cin)
+        w = torch.randn(cout, k, k, cin) * (2.0 / (k * k * cin)) ** 0.5
+        dy = torch.randn(n, d.ho, d.wo, cout)
+        xd, dyd = x.to(cuda, torch.bfloat16), dy.to(cuda, torch.bfloat16)
+        wf, wt = _prep(d, "bf16", w.to(cuda), cuda)
+        y = torch.empty(n, d.ho, d.wo, cout, dtype=torch.bfloat16, device=cuda)
+        rows = L.dll.argus_conv_fwd_stat_rows(C.byref(d), BF16)
+        stats = torch.empty(rows, cout, 2, device=cuda)
+        with KernelTimer("argus::igemm_glds_kernel") as t:
+            L.conv_fwd(C.byref(d), BF16, ptr(xd), ptr(wf), ptr(y), None, None, ptr(stats), stream())
+        M = n * d.ho * d.wo
+        if M >= 1024 and k * k * cin >= 64 and cout % 128 == 0:
+            assert len(t.summary()) == 1, (cin, cout, k, s, hin)
+        xr, wr, dyr = _q(x, "bf16").permute(0, 3, 1, 2), _q(w, "bf16").permute(0, 3, 1, 2), _q(dy, "bf16").permute(0, 3, 1, 2)
+        ref = F.conv2d(xr, wr, stride=s, padding=p)
+        assert _rel(y.permute(0, 3, 1, 2), ref) < TOL["bf16"], ("fwd", cin, cout, k, s)
+        tile = L.dll.argus_conv_fwd_stat_tile(C.byref(d), BF16)
+        mean, var = _merge_stats(stats.double().cpu(), tile, M)
+        yr = ref.permute(0, 2, 3, 1).reshape(-1, cout)
+        assert (mean - yr.mean(0)).abs().max() < 2e-2 * yr.std(0).max(), ("stats mean", cin, cout)
+        assert _rel(var, yr.var(0, unbiased=False)) < 2e-2, ("stats var", cin, cout)
+        # dgrad: plain, in-place accumulate, masked addend from another buffer
+        dx0 = torch.randn(n, hin, hin, cin)
+        dx = dx0.to(cuda, torch.bfloat16)
+        L.conv_dgrad(C.byref(d), BF16, ptr(dyd), ptr(wt), ptr(dx), ptr(dx), None, stream())
+        refd = torch.nn.grad.conv2d_input(xr.shape, wr, dyr, stride=s, padding=p)
+        assert _rel(dx.permute(0, 3, 1, 2), refd + _q(dx0, "bf16").permute(0, 3, 1, 2)) < TOL["bf16"], ("dgrad+", cin)
+        res = _q(torch.randn(n, hin, hin, cin), "bf16")
+        keep = res > 0
+        bits = ((keep.reshape(-1, 8).int() << torch.arange(8)).sum(1)).to(torch.uint8).to(cuda)
+        resg = res.to(cuda, torch.bfloat16)
+        L.conv_dgrad(C.byref(d), BF16, ptr(dyd), ptr(wt), ptr(dx), ptr(resg), ptr(bits), stream())
+        assert _rel(dx.permute(0, 3, 1, 2), refd + (res * keep).permute(0, 3, 1, 2)) < TOL["bf16"], ("dgrad mask", cin)
 
 
 HALO_SHAPES = [  # (cin, cout, hw, n): 256-pixel tiles = 4 rows / 8 rows / 1 image / 4 images
@@ -661,18 +656,14 @@ def test_conv3x3_halo_kernel_parity(cuda):
 
     torch.manual_seed(13)
     L = lib()
-    assert L.dll.argus_conv_tuning(13, 1) == 0  # force the halo kernel on every eligible shape
-    try:
-        _halo_cases(L, cuda)
-    finally:
-        L.dll.argus_conv_tuning(13, 256)
+    _halo_cases(L, cuda, {13: 1})  # force the halo kernel on every eligible shape
 
 
 def test_layer1_3x3_on_single_buffer_halo_kernel(cuda):
-    """Default kernel policy (tuning key 30 = 1) for the 64 -> 64 channel 3x3 stride-1 layers of
-    layer 1 at a grid the policy accepts (>= 256 workgroups): forward and dgrad run on the
-    single-halo-buffer 64-column halo kernel and agree with torch (bf16 tolerance) and with the
-    register-staged implicit GEMM the policy replaces (key 30 = 0)."""
+    """Default kernel policy for the 64 -> 64 channel 3x3 stride-1 layers of layer 1 at a grid the
+    policy accepts (>= 256 workgroups): forward and dgrad run on the single-halo-buffer 64-column halo
+    kernel and agree with torch (bf16 tolerance) and with the register-staged implicit GEMM it
+    replaces (policy key 10 = 0: halo kernel off)."""
     from argus_amd.profiling import KernelTimer
 
     torch.manual_seed(31)
@@ -688,30 +679,31 @@ def test_layer1_3x3_on_single_buffer_halo_kernel(cuda):
     ref_y = F.conv2d(xr, wr, padding=1).permute(0, 2, 3, 1)
     ref_dx = torch.nn.grad.conv2d_input(xr.shape, wr, _q(dy, "bf16").permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
     outs = {}
-    for key30, kname in ((1, "conv3x3_halo_kernel<64, 0, 1>"), (0, "igemm_kernel")):
-        with _tuned({30: key30}):
-            rows = L.dll.argus_conv_fwd_stat_rows(C.byref(d), BF16)
-            stats = torch.empty(rows, c, 2, device=cuda)
-            y = torch.empty(n, hw, hw, c, dtype=torch.bfloat16, device=cuda)
-            dx = torch.empty(n, hw, hw, c, dtype=torch.bfloat16, device=cuda)
-            with KernelTimer() as t:
-                L.conv_fwd(C.byref(d), BF16, ptr(xd), ptr(wf), ptr(y), None, None, ptr(stats), stream())
-                L.conv_dgrad(C.byref(d), BF16, ptr(dyd), ptr(wt), ptr(dx), None, None, stream())
-            torch.cuda.synchronize()
+    for key10, kname in ((1, "conv3x3_halo_kernel<64, 0, 1>"), (0, "igemm_kernel")):
+        dk = d.with_tuning({10: key10})
+        rows = L.dll.argus_conv_fwd_stat_rows(C.byref(dk), BF16)
+        stats = torch.empty(rows, c, 2, device=cuda)
+        y = torch.empty(n, hw, hw, c, dtype=torch.bfloat16, device=cuda)
+        dx = torch.empty(n, hw, hw, c, dtype=torch.bfloat16, device=cuda)
+        with KernelTimer() as t:
+            L.conv_fwd(C.byref(dk), BF16, ptr(xd), ptr(wf), ptr(y), None, None, ptr(stats), stream())
+            L.conv_dgrad(C.byref(dk), BF16, ptr(dyd), ptr(wt), ptr(dx), None, None, stream())
+        torch.cuda.synchronize()
         names = list(t.summary())
-        assert any(kname in nm for nm in names), (key30, names)
-        if key30:
+        assert any(kname in nm for nm in names), (key10, names)
+        if key10:
             assert any("conv3x3_halo_kernel<64, 0, 1>" in nm for nm in names) and len(names) == 1, names
-        assert _rel(y, ref_y) < TOL["bf16"] and _rel(dx, ref_dx) < TOL["bf16"], key30
-        outs[key30] = (y.float(), dx.float())
+        assert _rel(y, ref_y) < TOL["bf16"] and _rel(dx, ref_dx) < TOL["bf16"], key10
+        outs[key10] = (y.float(), dx.float())
     assert _rel(outs[1][0], outs[0][0]) < 1e-2 and _rel(outs[1][1], outs[0][1]) < 1e-2
 
 
-def _halo_cases(L, cuda):
+def _halo_cases(L, cuda, tuning):
     from argus_amd.profiling import KernelTimer
 
     for cin, cout, hw, n in HALO_SHAPES:
         d, p = _desc(n, hw, hw, cin, cout, 3, 1)
+        d = d.with_tuning(tuning)
         x = torch.randn(n, hw, hw, cin) * 1.5 + 0.2
         w = torch.randn(cout, 3, 3, cin) * (2.0 / (9 * cin)) ** 0.5
         sc, sh = torch.rand(cin) + 0.5, torch.randn(cin) * 0.5
@@ -750,62 +742,6 @@ def _halo_cases(L, cuda):
         res = dx0.to(cuda, torch.bfloat16)
         L.conv_dgrad(C.byref(d), BF16, ptr(dyd), ptr(wt), ptr(dx), ptr(res), ptr(bits), stream())
         assert _rel(dx.permute(0, 3, 1, 2), refd + (dx0 * keep).permute(0, 3, 1, 2)) < TOL["bf16"], ("dgrad m", cin)
-
-
-def test_conv3x3_halo_dgrad_block_tiles(cuda):
-    """3x3 dgrads of frames whose width does not divide 256 (the 376 x 672 layers' 168-, 84-, 42- and
-    21-wide frames) on the halo kernel's TH x TW block tiles (tuning key 37): ragged last row blocks and
-    padded slots; vs torch (plain dgrad into a non-zero addend) and vs the kernel the shape used before
-    (key 37 = 0) with the BN-backward epilogue (masked dm and the per-channel sums of its partials)."""
-    from argus_amd._lib import BnBwdEpilogue
-    from argus_amd.profiling import KernelTimer
-
-    torch.manual_seed(31)
-    L = lib()
-    keep13, keep37 = L.dll.argus_conv_tuning_get(13), L.dll.argus_conv_tuning_get(37)
-    assert L.dll.argus_conv_tuning(13, 1) == 0  # any grid size (small test shapes)
-    try:
-        for cin, cout, (h, w), n in [(64, 64, (10, 84), 2), (128, 128, (7, 168), 1), (128, 128, (12, 21), 3),
-                                     (256, 256, (12, 42), 2), (64, 64, (13, 168), 1)]:
-            assert L.dll.argus_conv_tuning(37, 1) == 0
-            d, p = _desc(n, h, w, cin, cout, 3, 1)
-            wt_ = torch.randn(cout, 3, 3, cin) * (2.0 / (9 * cin)) ** 0.5
-            _, wt = _prep(d, "bf16", wt_.to(cuda), cuda)
-            wr = _q(wt_, "bf16").permute(0, 3, 1, 2)
-            dy = _q(torch.randn(n, h, w, cout), "bf16")
-            dyd = dy.to(cuda, torch.bfloat16)
-            refd = torch.nn.grad.conv2d_input((n, cin, h, w), wr, dy.permute(0, 3, 1, 2), padding=1)
-            dx0 = _q(torch.randn(n, h, w, cin), "bf16")
-            dx = dx0.to(cuda, torch.bfloat16)
-            with KernelTimer("argus::conv3x3_halo_kernel") as t:
-                L.conv_dgrad(C.byref(d), BF16, ptr(dyd), ptr(wt), ptr(dx), ptr(dx), None, stream())
-            assert len(t.summary()) == 1, ("halo block dgrad not used", cin, cout, h, w, n)
-            assert _rel(dx.permute(0, 3, 1, 2), refd + dx0.permute(0, 3, 1, 2)) < TOL["bf16"], (cin, cout, h, w)
-            # BN-backward epilogue (mask recomputed from y, partials): blocks vs the previous kernel
-            yin = torch.randn(n, h, w, cin, device=cuda).to(torch.bfloat16)
-            mean, invstd = torch.randn(cin, device=cuda) * 0.1, torch.rand(cin, device=cuda) + 0.5
-            sc, sh = torch.randn(cin, device=cuda), torch.randn(cin, device=cuda)
-            outs = []
-            for key37 in (1, 0):
-                assert L.dll.argus_conv_tuning(37, key37) == 0
-                rows = L.dll.argus_conv_dgrad_bn_rows(C.byref(d), BF16)
-                part = torch.zeros(rows, cin, 2, device=cuda)
-                e = BnBwdEpilogue()
-                e.y, e.mean, e.invstd, e.mask_mode, e.scale, e.shift, e.part = ptr(yin), ptr(mean), ptr(invstd), \
-                    2, ptr(sc), ptr(sh), ptr(part)
-                dm = torch.empty(n, h, w, cin, device=cuda, dtype=torch.bfloat16)
-                with KernelTimer("argus::conv3x3_halo_kernel") as t:
-                    rc = L.dll.argus_conv_dgrad_bn(C.byref(d), BF16, ptr(dyd), ptr(wt), ptr(dm), None, C.byref(e),
-                                                   None, stream())
-                assert rc == 0, L.dll.argus_last_error()
-                assert (len(t.summary()) == 1) == (key37 == 1 or (w <= 256 and 256 % w == 0)), (key37, h, w)
-                torch.cuda.synchronize()
-                outs.append((dm.double().cpu(), part.double().sum(0).cpu()))
-            assert _rel(outs[0][0], outs[1][0]) < 1e-2, ("dm", cin, cout, h, w)
-            assert _rel(outs[0][1], outs[1][1]) < 1e-3, ("partial sums", cin, cout, h, w)
-    finally:
-        L.dll.argus_conv_tuning(13, keep13)
-        L.dll.argus_conv_tuning(37, keep37)
 
 
 @pytest.mark.parametrize("dt", ["fp32", "bf16"])
@@ -857,20 +793,14 @@ def test_wgrad3x3_halo_kernel_parity(cuda, pro):
 
     torch.manual_seed(19)
     L = lib()
-    assert L.dll.argus_conv_tuning(14, 1 << 20) == 0  # every channel-tile count
-    target = L.dll.argus_conv_tuning_get(12)
-    try:
-        # default split target (mostly one tile per split) and a target of 3 workgroups per (k, c) tile
-        # (long tile runs: the 3-stage ring's steady state, its drain and ragged run lengths)
-        for tg in (target, 3):
-            assert L.dll.argus_conv_tuning(12, tg) == 0
-            _wgrad_halo_cases(L, cuda, pro)
-    finally:
-        L.dll.argus_conv_tuning(14, 4)
-        L.dll.argus_conv_tuning(12, target)
+    # every channel-tile count (key 14); the default split target (mostly one tile per split) and a
+    # target of 3 workgroups per (k, c) tile (long tile runs: the 3-stage ring's steady state, its
+    # drain and ragged run lengths)
+    for tg in (L.dll.argus_conv_policy_default(12), 3):
+        _wgrad_halo_cases(L, cuda, pro, {14: 1 << 20, 12: tg})
 
 
-def _wgrad_halo_cases(L, cuda, pro):
+def _wgrad_halo_cases(L, cuda, pro, tuning):
     from argus_amd.profiling import KernelTimer
 
     # square frames: whole-row tiles / whole images; 84-, 168- and 21-wide frames (the 376 x 672
@@ -880,6 +810,7 @@ def _wgrad_halo_cases(L, cuda, pro):
                              (128, 128, (47, 84), 1)]:
         hh, ww = hw if isinstance(hw, tuple) else (hw, hw)
         d, p = _desc(n, hh, ww, cin, cout, 3, 1)
+        d = d.with_tuning(tuning)
         x = _q(torch.randn(n, hh, ww, cin) * 1.3 + 0.1, "bf16")
         dy = _q(torch.randn(n, hh, ww, cout), "bf16")
         sc, sh = torch.rand(cin) + 0.5, torch.randn(cin) * 0.5
@@ -946,24 +877,6 @@ def test_images_u8_layout_matches_fp32_path(cuda, dt):
     assert torch.equal(out_f.cpu(), want.to(TDT[dt]))
 
 
-def _tuned(settings):
-    """Context: set argus_conv_tuning keys, restore the defaults after."""
-    import contextlib
-
-    @contextlib.contextmanager
-    def cm():
-        L = lib()
-        old = {k: L.dll.argus_conv_tuning_get(k) for k in settings}
-        for k, v in settings.items():
-            assert L.dll.argus_conv_tuning(k, v) == 0
-        try:
-            yield
-        finally:
-            for k, v in old.items():
-                L.dll.argus_conv_tuning(k, v)
-    return cm()
-
-
 # (cin, cout, k, stride, hin, n, tuning, kernel the dgrad lands on)
 DGRAD_BN_CASES = [
     (64, 64, 3, 1, 16, 2, {13: 1}, "conv3x3_halo_kernel<64"),
@@ -1005,8 +918,8 @@ def test_conv_dgrad_bn_epilogue(cuda, dt):
             yg, y2g = y.to(cuda, TDT[dt]), y2.to(cuda, TDT[dt])
             dm = add.to(cuda, TDT[dt]) if with_add else torch.empty(n, hin, hin, cin, dtype=TDT[dt], device=cuda)
             bitsg = bits_t.to(cuda)
-            with _tuned(tune):  # the row count depends on the kernel the tuning selects
-                rows = L.dll.argus_conv_dgrad_bn_rows(C.byref(d), DT[dt])
+            dk = d.with_tuning(tune)  # the row count depends on the kernel the tuning selects
+            rows = L.dll.argus_conv_dgrad_bn_rows(C.byref(dk), DT[dt])
             part = torch.full((rows, cin, 2), float("nan"), device=cuda)
             part2 = torch.full((rows, cin, 2), float("nan"), device=cuda)
             e = BnBwdEpilogue()
@@ -1018,8 +931,8 @@ def test_conv_dgrad_bn_epilogue(cuda, dt):
             if dual:
                 e.y2, e.mean2, e.invstd2, e.part2 = ptr(y2g), ptr(g["mean2"]), ptr(g["invstd2"]), ptr(part2)
             dyg = dy.to(cuda, TDT[dt])
-            with _tuned(tune), KernelTimer() as kt:
-                L.conv_dgrad_bn(C.byref(d), DT[dt], ptr(dyg), ptr(wt), ptr(dm), ptr(dm) if with_add else None,
+            with KernelTimer() as kt:
+                L.conv_dgrad_bn(C.byref(dk), DT[dt], ptr(dyg), ptr(wt), ptr(dm), ptr(dm) if with_add else None,
                                 C.byref(e), None, stream())
             torch.cuda.synchronize()
             assert any(kname in nm for nm in kt.summary()), (kname, list(kt.summary()))
@@ -1087,26 +1000,26 @@ def test_folded_bn_finalize_matches_separate_kernels(cuda, dt):
         sc, sh = torch.randn(cin, device=cuda), torch.randn(cin, device=cuda)
         g_in = torch.rand(cin, device=cuda) + 0.5
         res = []
-        with _tuned(tune):
-            brows = L.dll.argus_conv_dgrad_bn_rows(C.byref(d), DT[dt])
-            for folded in (False, True):
-                ws = torch.zeros(ws_bytes, dtype=torch.uint8, device=cuda)
-                part = torch.empty(brows, cin, 2, device=cuda)
-                dm = torch.empty(n, hin, hin, cin, dtype=TDT[dt], device=cuda)
-                co = torch.zeros(5, cin, device=cuda)
-                e = BnBwdEpilogue()
-                e.y, e.mean, e.invstd, e.mask_mode, e.scale, e.shift, e.part = ptr(yb), ptr(mean), ptr(invstd), 2, \
-                    ptr(sc), ptr(sh), ptr(part)
-                if folded:
-                    e.workspace, e.gamma, e.dgamma, e.dbeta = ptr(ws), ptr(g_in), ptr(co[3]), ptr(co[4])
-                    e.ca, e.cb, e.cc = ptr(co[0]), ptr(co[1]), ptr(co[2])
-                L.conv_dgrad_bn(C.byref(d), DT[dt], ptr(dy), ptr(wt), ptr(dm), None, C.byref(e), None, stream())
-                if not folded:
-                    L.bn_bwd_finalize(cin, brows, ptr(part), n * hin * hin, ptr(g_in), ptr(mean), ptr(invstd),
-                                      ptr(co[3]), ptr(co[4]), ptr(co[0]), ptr(co[1]), ptr(co[2]), ptr(ws), stream())
-                torch.cuda.synchronize()
-                assert int(ws[:16384].view(torch.int32).abs().sum()) == 0
-                res.append((dm.cpu(), co.cpu()))
+        dk = d.with_tuning(tune)
+        brows = L.dll.argus_conv_dgrad_bn_rows(C.byref(dk), DT[dt])
+        for folded in (False, True):
+            ws = torch.zeros(ws_bytes, dtype=torch.uint8, device=cuda)
+            part = torch.empty(brows, cin, 2, device=cuda)
+            dm = torch.empty(n, hin, hin, cin, dtype=TDT[dt], device=cuda)
+            co = torch.zeros(5, cin, device=cuda)
+            e = BnBwdEpilogue()
+            e.y, e.mean, e.invstd, e.mask_mode, e.scale, e.shift, e.part = ptr(yb), ptr(mean), ptr(invstd), 2, \
+                ptr(sc), ptr(sh), ptr(part)
+            if folded:
+                e.workspace, e.gamma, e.dgamma, e.dbeta = ptr(ws), ptr(g_in), ptr(co[3]), ptr(co[4])
+                e.ca, e.cb, e.cc = ptr(co[0]), ptr(co[1]), ptr(co[2])
+            L.conv_dgrad_bn(C.byref(dk), DT[dt], ptr(dy), ptr(wt), ptr(dm), None, C.byref(e), None, stream())
+            if not folded:
+                L.bn_bwd_finalize(cin, brows, ptr(part), n * hin * hin, ptr(g_in), ptr(mean), ptr(invstd),
+                                  ptr(co[3]), ptr(co[4]), ptr(co[0]), ptr(co[1]), ptr(co[2]), ptr(ws), stream())
+            torch.cuda.synchronize()
+            assert int(ws[:16384].view(torch.int32).abs().sum()) == 0
+            res.append((dm.cpu(), co.cpu()))
         assert torch.equal(res[0][0], res[1][0])
         assert _rel(res[0][1], res[1][1]) < 1e-6, (cin, cout, k, s, dt)
 
@@ -1137,26 +1050,26 @@ def test_dgrad_apply_prologue_matches_apply_pass(cuda, dt):
         for with_epi in (False, True):
             outs = []
             for fused in (False, True):
-                with _tuned(tune):
-                    rows = L.dll.argus_conv_dgrad_bn_rows(C.byref(d), DT[dt])
-                    part = torch.zeros(rows, cin, 2, device=cuda)
-                    e = BnBwdEpilogue()
-                    e.y, e.mean, e.invstd, e.mask_mode, e.scale, e.shift, e.part = ptr(yin), ptr(mean), ptr(invstd), \
-                        2, ptr(sc), ptr(sh), ptr(part)
-                    dy = torch.zeros(n, d.ho, d.wo, cout, device=cuda, dtype=TDT[dt])
-                    dx = torch.empty(n, hin, hin, cin, device=cuda, dtype=TDT[dt])
-                    if fused:
-                        pro = BnBwdPrologue(ptr(yb), ptr(ca), ptr(cb), ptr(cc), ptr(dy))
-                        L.conv_dgrad_bn(C.byref(d), DT[dt], ptr(dm), ptr(wt), ptr(dx), None,
-                                        C.byref(e) if with_epi else None, C.byref(pro), stream())
+                dk = d.with_tuning(tune)
+                rows = L.dll.argus_conv_dgrad_bn_rows(C.byref(dk), DT[dt])
+                part = torch.zeros(rows, cin, 2, device=cuda)
+                e = BnBwdEpilogue()
+                e.y, e.mean, e.invstd, e.mask_mode, e.scale, e.shift, e.part = ptr(yin), ptr(mean), ptr(invstd), \
+                    2, ptr(sc), ptr(sh), ptr(part)
+                dy = torch.zeros(n, d.ho, d.wo, cout, device=cuda, dtype=TDT[dt])
+                dx = torch.empty(n, hin, hin, cin, device=cuda, dtype=TDT[dt])
+                if fused:
+                    pro = BnBwdPrologue(ptr(yb), ptr(ca), ptr(cb), ptr(cc), ptr(dy))
+                    L.conv_dgrad_bn(C.byref(dk), DT[dt], ptr(dm), ptr(wt), ptr(dx), None,
+                                    C.byref(e) if with_epi else None, C.byref(pro), stream())
+                else:
+                    L.bn_bwd_apply(DT[dt], n * d.ho * d.wo, cout, ptr(dm), 0, None, ptr(yb), None, None, ptr(ca),
+                                   ptr(cb), ptr(cc), ptr(dy), None, None, None, None, None, None, stream())
+                    if with_epi:
+                        L.conv_dgrad_bn(C.byref(dk), DT[dt], ptr(dy), ptr(wt), ptr(dx), None, C.byref(e), None,
+                                        stream())
                     else:
-                        L.bn_bwd_apply(DT[dt], n * d.ho * d.wo, cout, ptr(dm), 0, None, ptr(yb), None, None, ptr(ca),
-                                       ptr(cb), ptr(cc), ptr(dy), None, None, None, None, None, None, stream())
-                        if with_epi:
-                            L.conv_dgrad_bn(C.byref(d), DT[dt], ptr(dy), ptr(wt), ptr(dx), None, C.byref(e), None,
-                                            stream())
-                        else:
-                            L.conv_dgrad(C.byref(d), DT[dt], ptr(dy), ptr(wt), ptr(dx), None, None, stream())
+                        L.conv_dgrad(C.byref(dk), DT[dt], ptr(dy), ptr(wt), ptr(dx), None, None, stream())
                 torch.cuda.synchronize()
                 outs.append((dy.cpu(), dx.cpu(), part.cpu()))
             (y0, x0, p0), (y1, x1, p1) = outs

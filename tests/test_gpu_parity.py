@@ -167,48 +167,74 @@ def _conv_kernels(fn):
 
     with KernelTimer() as kt:
         fn()
-    return {n for n in kt.summary() if "igemm" in n or "conv3x3" in n or "wgrad" in n}
+    return {n for n in kt.summary() if "igemm" in n or "conv3x3" in n or "wgrad" in n or "stem" in n}
 
 
-def test_bf16_b64_kernel_selection_block_backward_stages(cuda, golden):
-    """The kernel selection of the benched B=64 step, stage by stage: at B=4 (256x256) with the grid
-    thresholds of the LDS-halo and global->LDS kernels lowered (tuning keys 13 and 9), every conv
-    kernel instantiation the B=64 fused step launches also runs here, and every backward stage of
-    every block is re-derived in fp64 from the engine's own bf16 tensors (max-relative 1e-2)."""
+# (id, the benched configuration (B, H, W, dtype), the small batch its stages are re-derived at,
+# per-stage tolerances beyond the default 1e-2)
+SELECTION_CASES = [
+    ("configs1_b64_256", (64, 256, 256, "bf16"), 4, {}),
+    ("configs3_b128_376x672", (128, 376, 672, "bf16"), 2, {}),
+    # fp8 GEMM outputs (the dgrads: dz2, dz1, dout) carry the MX-fp8 operand rounding: the bar of
+    # test_gpu_kernels.py::test_fp8_mx_conv_fwd_dgrad (6e-2 of the output's max magnitude)
+    ("configs4_b512_fp8", (512, 256, 256, "fp8"), 8, {"dz2": 6e-2, "dz1": 6e-2, "dout": 6e-2}),
+]
+
+
+def _scaled_policy(r):
+    """Kernel-selection overrides that keep a batch r x smaller on the larger batch's kernels: the
+    thresholds that compare a GEMM row count or a grid size (both linear in the batch) scaled by r
+    (policy keys 35: 128-row forward tiles, 36 / 9: glds rows / workgroups, 13: halo workgroups)."""
     from argus_amd._lib import lib
+
+    L = lib()
+    return {k: max(1, round(L.dll.argus_conv_policy_default(k) * r)) for k in (35, 36, 9, 13)}
+
+
+@pytest.mark.parametrize("case", SELECTION_CASES, ids=[c[0] for c in SELECTION_CASES])
+def test_benched_kernel_selection_block_backward_stages(cuda, case):
+    """The kernel selection of a benched configuration, stage by stage: one fused step at the benched
+    size records the conv kernel instantiations it launches; a small batch then runs with the
+    size-dependent selection thresholds scaled by the batch ratio (_scaled_policy), every one of those
+    instantiations must run there too, and every backward stage of every block (dW1..dW3, the
+    downsample dW, dgrads with their BN epilogues, BN backward, the materialised a1 / a2) is re-derived
+    in fp64 from the engine's own tensors (max-relative 1e-2; fp8 GEMM outputs 6e-2)."""
     from argus_amd.losses import geometric_loss_fn
     from argus_amd.step import FusedTrainer
 
-    x64 = mg.synthetic_images(64, 256, 256, seed=3).to(cuda)
-    T64 = mg.synthetic_targets(64, seed=4).to(cuda)
-    m = _product(cuda, "bf16")
+    _, (B, H, W, dt), b, tol = case
+    gen = torch.Generator(device=cuda).manual_seed(3)
+    xb = torch.randint(0, 256, (B, 6, H, W), generator=gen, device=cuda, dtype=torch.uint8).float() / 255.0
+    Tb = mg.synthetic_targets(B, seed=4).to(cuda)
+    m = _product(cuda, dt)
     tr = FusedTrainer(m, lr=1e-4, max_grad_norm=1.0)
-    want = _conv_kernels(lambda: tr.step(x64, T64))
-    del m, tr, x64
+    want = _conv_kernels(lambda: tr.step(xb, Tb))
+    del m, tr, xb
     torch.cuda.empty_cache()
-    L = lib()
-    keys = {13: L.dll.argus_conv_tuning_get(13), 9: L.dll.argus_conv_tuning_get(9)}
-    assert L.dll.argus_conv_tuning(13, 1) == 0 and L.dll.argus_conv_tuning(9, 1) == 0
-    try:
-        x = mg.synthetic_images(4, 256, 256, seed=1234)
-        T = mg.synthetic_targets(4, seed=2000)
-        m = _product(cuda, "bf16")
-        eng = m._engine(cuda)
 
-        def run():
-            eng.debug = {}
-            geometric_loss_fn(m(x.to(cuda)), T.to(cuda)).mean().backward()
-            torch.cuda.synchronize()
+    x = torch.randint(0, 256, (b, 6, H, W), generator=torch.Generator().manual_seed(1234), dtype=torch.uint8)
+    x = x.float() / 255.0
+    T = mg.synthetic_targets(b, seed=2000)
+    torch.manual_seed(42)
+    from argus_amd.models import NCameraCNN
 
-        got = _conv_kernels(run)
-        debug, eng.debug = eng.debug, None
-    finally:
-        for k, v in keys.items():
-            L.dll.argus_conv_tuning(k, v)
+    m = NCameraCNN(compute_dtype=dt, kernel_tuning=_scaled_policy(b / B)).to(cuda).train()
+    eng = m._engine(cuda)
+    assert eng.materialize and eng.cdt == (2 if dt == "fp8" else 1)
+
+    def run():
+        eng.debug = {}
+        geometric_loss_fn(m(x.to(cuda)), T.to(cuda)).mean().backward()
+        torch.cuda.synchronize()
+
+    got = _conv_kernels(run)
+    debug, eng.debug = eng.debug, None
     missing = sorted(want - got)
-    assert not missing, f"B=64 kernels not covered by the stage-checked run: {missing}"
-    worst = stage_checks(eng, dict(m.named_parameters()), debug, 1e-2)
-    print(f"{len(want)} conv kernel instantiations at B=64, all stage-checked; worst per stage:",
+    assert not missing, f"{case[0]}: kernels of the benched step not covered by the stage-checked run: {missing}"
+    tols = {**{k: 1e-2 for k in ("a1", "a2", "dy3", "dz2", "dy2", "dz1", "dy1", "dout", "dW1", "dW2", "dW3", "dWd")},
+            **tol}
+    worst = stage_checks(eng, dict(m.named_parameters()), debug, tols)
+    print(f"{case[0]}: {len(want)} conv kernel instantiations, all stage-checked; worst per stage:",
           {k: f"{v:.2e}" for k, v in worst.items()})
 
 

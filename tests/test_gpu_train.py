@@ -138,8 +138,9 @@ def test_forward_latency_graph_replay(cuda):
 
 
 def test_side_stream_overlap_is_bit_identical(cuda):
-    """The weight-gradient / downsample side stream (engine.wgrad_overlap) only reorders independent
-    launches: three bf16 training steps with and without it must give bitwise-identical parameters,
+    """The weight-gradient / downsample side stream (engine.wgrad_overlap) and the first block's
+    downsample weight gradient moved to the main stream's tail (engine.tail_main) only reorder
+    independent launches: three bf16 training steps with and without them must give bitwise-identical parameters,
     Adam moments, BN running statistics and losses (a missed event would show up as a race here)."""
     from argus_amd.models import NCameraCNN
     from argus_amd.step import FusedTrainer
@@ -149,18 +150,21 @@ def test_side_stream_overlap_is_bit_identical(cuda):
     x = (torch.randint(0, 256, (8, 6, 128, 128), generator=g, dtype=torch.uint8).float() / 255.0).to(cuda)
     T = se3.random_targets(8, generator=g).float().to(cuda)
     runs = []
-    for overlap in (True, False):
+    # (side stream, first block's downsample weight gradient on the main stream's tail)
+    for overlap, tail in ((True, True), (True, False), (False, True)):
         torch.manual_seed(42)
         model = NCameraCNN(compute_dtype="bf16").to(cuda).train()
         tr = FusedTrainer(model, lr=1e-3, max_grad_norm=1.0)
-        model._engine(cuda).wgrad_overlap = overlap
+        eng = model._engine(cuda)
+        eng.wgrad_overlap, eng.tail_main = overlap, tail
         losses = [tr.step(x, T).clone() for _ in range(3)]
         torch.cuda.synchronize()
         runs.append((torch.stack(losses).cpu(), tr.flat.param.cpu(), tr.exp_avg_sq.cpu(),
                      {k: v.cpu() for k, v in model.state_dict().items()}))
-    (l1, p1, v1, s1), (l0, p0, v0, s0) = runs
-    assert torch.equal(l1, l0) and torch.equal(p1, p0) and torch.equal(v1, v0)
-    assert all(torch.equal(s1[k], s0[k]) for k in s1)
+    (l1, p1, v1, s1) = runs[0]
+    for l0, p0, v0, s0 in runs[1:]:
+        assert torch.equal(l1, l0) and torch.equal(p1, p0) and torch.equal(v1, v0)
+        assert all(torch.equal(s1[k], s0[k]) for k in s1)
 
 
 def test_rotation_angle_error_matches_oracle(cuda):

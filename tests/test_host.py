@@ -102,6 +102,11 @@ def test_bn_momentum_none_is_cumulative_average():
     assert m._maps()[1]["resnet.bn1.momentum"] == 1 / 6
     m.resnet.bn1.num_batches_tracked.fill_(10)
     assert m._maps()[1]["resnet.bn1.momentum"] == 1 / 11
+    # a .data write (dist.broadcast(b.data) in sync_bn_buffers) does not bump the version: the writer
+    # invalidates the shadow, and the next forward re-reads the counter
+    m.resnet.bn1.num_batches_tracked.data.fill_(20)
+    m.invalidate_bn_counters()
+    assert m._maps()[1]["resnet.bn1.momentum"] == 1 / 21
 
 
 def test_spaghetti_draws_reference_arcs():

@@ -20,13 +20,11 @@ def main():
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--filter", default="")
-    ap.add_argument("--tune", nargs="*", default=[], help="argus_conv_tuning key=value pairs")
+    ap.add_argument("--tune", nargs="*", default=[], help="kernel-selection overrides key=value")
     a = ap.parse_args()
-    for kv in a.tune:
-        k, v = kv.split("=")
-        assert lib().dll.argus_conv_tuning(int(k), int(v)) == 0
+    tuning = {int(k): int(v) for k, v in (kv.split("=") for kv in a.tune)}
     dev = torch.device("cuda", 0)
-    eng = ResNetEngine(2, 1024, a.dtype, dev)
+    eng = ResNetEngine(2, 1024, a.dtype, dev, tuning)
     eng.ensure(a.batch, *a.hw)
     L = lib()
     dt = eng.dt

@@ -34,11 +34,9 @@ def main():
     ap.add_argument("--tune", nargs="*", default=[])
     a = ap.parse_args()
     L = lib()
-    for kv in a.tune:
-        k, v = kv.split("=")
-        assert L.dll.argus_conv_tuning(int(k), int(v)) == 0
+    tuning = {int(k): int(v) for k, v in (kv.split("=") for kv in a.tune)}
     dev = torch.device("cuda", 0)
-    eng = ResNetEngine(2, 1024, "bf16", dev)
+    eng = ResNetEngine(2, 1024, "bf16", dev, tuning)
     eng.ensure(a.batch, *a.hw)
     bf = torch.bfloat16
     ws = torch.zeros(L.dll.argus_bn_workspace_bytes(2048), dtype=torch.uint8, device=dev)

@@ -14,28 +14,34 @@ mkdir -p $O
 export TMPDIR=/tmp
 cd $R
 if [ "$PART" = a ]; then
-  timeout -k 10 240 python3 -u bench.py > $O/bench.json 2> $O/bench.err
-  timeout -k 10 180 python3 -u bench.py --batch 256 --no-cpu-baseline > $O/bench_b256.json 2> $O/bench_b256.err
+  # counters first, so the bench lines below cite this round's PMC summaries (bench.py reads the newest
+  # committed/copied profiles/*_pmc_*.json of the same workload)
   bash tools/profile_round.sh $TAG
   python3 tools/pmc_traffic.py gpurun_out/prof_$TAG/pmc_fetch gpurun_out/prof_$TAG/pmc_write $O/pmc_traffic.json 64 256 256 bf16
-  python3 tools/profsum.py $(find gpurun_out/prof_$TAG/stats -name "*kernel_stats.csv" | head -1) 28 40 > $O/kernel_summary.txt
+  python3 tools/profsum.py $(find gpurun_out/prof_$TAG/stats -name "*kernel_stats.csv" | head -1) 40 > $O/kernel_summary.txt
   cp $(find gpurun_out/prof_$TAG/stats -name "*kernel_stats.csv" | head -1) $O/kernel_stats.csv
   bash tools/prof_timeline.sh $TAG
   cp gpurun_out/tl_$TAG/timeline.txt $O/timeline.txt
   WORKLOAD="64 256 256 bf16" bash tools/prof_pmc.sh $TAG
   cp gpurun_out/pmc_$TAG/summary.json $O/pmc_mfma_summary.json
   cp gpurun_out/pmc_$TAG/summary.txt $O/pmc_mfma_summary.txt
+  cp $O/pmc_traffic.json profiles/${TAG}_pmc_traffic.json
+  cp $O/pmc_mfma_summary.json profiles/${TAG}_pmc_mfma_summary.json
+  timeout -k 10 240 python3 -u bench.py > $O/bench.json 2> $O/bench.err
+  timeout -k 10 180 python3 -u bench.py --batch 256 --no-cpu-baseline > $O/bench_b256.json 2> $O/bench_b256.err
 else
+  bash tools/profile_round.sh ${TAG}_376 --hw 376 672 --batch 128 --steps 5 --warmup 2
+  python3 tools/pmc_traffic.py gpurun_out/prof_${TAG}_376/pmc_fetch gpurun_out/prof_${TAG}_376/pmc_write $O/pmc_traffic_376x672.json 128 376 672 bf16
+  WORKLOAD="128 376 672 bf16" bash tools/prof_pmc.sh ${TAG}_376 --hw 376 672 --batch 128
+  cp gpurun_out/pmc_${TAG}_376/summary.json $O/376x672_pmc_mfma_summary.json
+  cp gpurun_out/pmc_${TAG}_376/summary.txt $O/376x672_pmc_mfma_summary.txt
+  cp $O/pmc_traffic_376x672.json profiles/${TAG}_376x672_pmc_traffic.json
+  cp $O/376x672_pmc_mfma_summary.json profiles/${TAG}_376x672_pmc_mfma_summary.json
   timeout -k 10 240 python3 -u bench.py --hw 376 672 --batch 128 --no-cpu-baseline --kernels \
     > $O/bench_376x672.json 2> $O/bench_376x672_kernels.txt
   timeout -k 10 240 python3 -u bench.py --dtype fp8 --batch 512 --no-cpu-baseline --steps 5 --warmup 2 \
     > $O/bench_b512_fp8.json 2> $O/bench_b512_fp8.err
   timeout -k 10 240 python3 -u bench.py --batch 512 --no-cpu-baseline --no-isolated --steps 5 --warmup 2 \
     > $O/bench_b512_bf16.json 2> $O/bench_b512_bf16.err
-  bash tools/profile_round.sh ${TAG}_376 --hw 376 672 --batch 128 --steps 5 --warmup 2
-  python3 tools/pmc_traffic.py gpurun_out/prof_${TAG}_376/pmc_fetch gpurun_out/prof_${TAG}_376/pmc_write $O/pmc_traffic_376x672.json 128 376 672 bf16
-  WORKLOAD="128 376 672 bf16" bash tools/prof_pmc.sh ${TAG}_376 --hw 376 672 --batch 128
-  cp gpurun_out/pmc_${TAG}_376/summary.json $O/376x672_pmc_mfma_summary.json
-  cp gpurun_out/pmc_${TAG}_376/summary.txt $O/376x672_pmc_mfma_summary.txt
 fi
 echo "measure $PART done"

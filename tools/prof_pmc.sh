@@ -14,7 +14,7 @@ i=0
 for P in "$P1" "$P2"; do
   i=$((i+1))
   timeout -s KILL 150 rocprofv3 --pmc $P --output-format csv -d $O/p$i -o run -- \
-    python3 bench.py --no-cpu-baseline --no-isolated --steps 2 --warmup 1 "$@" > $O/p$i.log 2>&1
+    python3 bench.py --no-cpu-baseline --no-val-oracle --no-isolated --steps 2 --warmup 1 "$@" > $O/p$i.log 2>&1
 done
 python3 tools/pmc_summary.py $O/summary.json $O/p1 $O/p2 --workload ${WORKLOAD:-64 256 256 bf16} > $O/summary.txt
 echo pmc done

@@ -10,9 +10,9 @@ mkdir -p $O
 export TMPDIR=/tmp
 cd $R
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- \
-  python3 bench.py --no-cpu-baseline "$@" > $O/stats_bench.log 2>&1
+  python3 bench.py --no-cpu-baseline --no-val-oracle "$@" > $O/stats_bench.log 2>&1
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- \
-  python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 "$@" > $O/fetch.log 2>&1
+  python3 bench.py --no-cpu-baseline --no-val-oracle --steps 3 --warmup 1 "$@" > $O/fetch.log 2>&1
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- \
-  python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 "$@" > $O/write.log 2>&1
+  python3 bench.py --no-cpu-baseline --no-val-oracle --steps 3 --warmup 1 "$@" > $O/write.log 2>&1
 echo profile done

@@ -1,4 +1,4 @@
-"""Sweep conv tile configs per layer/pass (dev tool, GPU) via argus_conv_tuning.
+"""Sweep conv tile configs per layer/pass (dev tool, GPU) via per-call kernel-selection overrides (ConvDesc.with_tuning).
 python tools/tilesweep.py [--batch 64]"""
 import argparse
 import ctypes as C
@@ -57,11 +57,12 @@ def main():
                 cfgs = list(itertools.product((64, 128), (64, 128)))
                 if ps == 2:
                     cfgs = [(bm, bn, tb) for bm, bn in cfgs for tb in (256, 512, 1024, 2048)]
+                d0 = d
                 for cfg in cfgs:
-                    L.dll.argus_conv_tuning(ps, cfg[0])
-                    L.dll.argus_conv_tuning(3 + ps, cfg[1])
+                    tun = {ps: cfg[0], 3 + ps: cfg[1]}
                     if ps == 2:
-                        L.dll.argus_conv_tuning(6, cfg[2])
+                        tun[6] = cfg[2]
+                    d = d0.with_tuning(tun)
                     if d.stem and ps == 0 and cfg != (128, 64):
                         continue
                     if ps == 0:
@@ -74,8 +75,7 @@ def main():
                         fn = lambda: L.conv_wgrad(C.byref(d), dt, ptr(x), None, None, ptr(dy), ptr(dw), ptr(ws), wsb,
                                                   stream())
                     opts[cfg] = timeit(fn)
-                for k in range(7):
-                    L.dll.argus_conv_tuning(k, 0 if k < 6 else 512)
+                d = d0
                 res[ps] = opts
             seen[key] = res
         line = f"{name:30s} {d.h:3d} {d.c:4d}->{d.k:4d} k{d.r}s{d.stride} "
