@@ -98,14 +98,17 @@ __global__ __launch_bounds__(256) void stats_finalize_kernel(const BnFinArgs a) 
   const int lane_r = threadIdx.x >> 6;
   const int g = blockIdx.y;
   const int r0 = g * a.rpg, r1 = min(a.rows, r0 + a.rpg);
-  const double inv_full = 1.0 / (double)a.tile_rows;
+  // tile_rows < 0: every row is merged as a full row of |tile_rows| elements (ragged producers store
+  // {sum, M2 + sum^2 (1/n - 1/|tile_rows|)} for their n-element rows)
+  const int tr = a.tile_rows < 0 ? -a.tile_rows : a.tile_rows;
+  const double inv_full = 1.0 / (double)tr;
   double S = 0.0, Q = 0.0;
   if (c < a.C)
 #pragma unroll 8
     for (int r = r0 + lane_r; r < r1; r += 4) {
       const float2 v = a.part[(size_t)r * a.C + c];
-      const int64_t left = a.count - (int64_t)r * a.tile_rows;
-      const double inv = left >= a.tile_rows ? inv_full : 1.0 / (double)left;
+      const int64_t left = a.count - (int64_t)r * tr;
+      const double inv = (a.tile_rows < 0 || left >= tr) ? inv_full : 1.0 / (double)left;
       S += (double)v.x;
       Q += (double)v.y + (double)v.x * (double)v.x * inv;
     }
@@ -597,14 +600,18 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(int n, int H, int W, i
     st16_nt(dz + off, pack(acc));  // 268 MB written once, read by the stem BN backward / wgrad later
   }
   if constexpr (BNE) {
+    // element planes red[j][lane row][chunk]: the 8-byte writes of consecutive threads (consecutive
+    // chunks) are contiguous, no bank conflicts (a [lane row][channel] layout put lanes 8 float2 apart:
+    // SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE 0.82 at 376 x 672); the lane rows are summed in order
     __shared__ float2 red[256 * E];
     const int lanes = 256 / CH, ln = threadIdx.x / CH;
 #pragma unroll
-    for (int j = 0; j < E; ++j) red[ln * C + ch0 * E + j] = make_float2(s[j], t[j]);
+    for (int j = 0; j < E; ++j) red[(j * lanes + ln) * CH + ch0] = make_float2(s[j], t[j]);
     __syncthreads();
     for (int col = threadIdx.x; col < C; col += 256) {
-      float2 a = red[col];
-      for (int l = 1; l < lanes; ++l) { a.x += red[l * C + col].x; a.y += red[l * C + col].y; }
+      const float2* plane = red + (col % E) * lanes * CH + col / E;  // channel col = chunk * E + j
+      float2 a = plane[0];
+      for (int l = 1; l < lanes; ++l) { a.x += plane[l * CH].x; a.y += plane[l * CH].y; }
       part[(size_t)blockIdx.x * C + col] = a;
     }
   }
@@ -673,8 +680,8 @@ size_t argus_bn_workspace_bytes(int channels) { return kBnCounterBytes + (size_t
 int argus_bn_finalize(int C, int rows, int tile_rows, const float* part, int64_t count, const float* gamma,
                       const float* beta, float eps, float momentum, float* rm, float* rv, int64_t* nbt, float* mean,
                       float* invstd, float* scale, float* shift, void* ws, argus_stream_t stream) {
-  if (C <= 0 || rows <= 0 || tile_rows <= 0 || count <= 0 || !part || !gamma || !beta || !ws ||
-      (int64_t)rows * tile_rows < count) {
+  if (C <= 0 || rows <= 0 || tile_rows == 0 || count <= 0 || !part || !gamma || !beta || !ws ||
+      (int64_t)rows * (tile_rows < 0 ? -tile_rows : tile_rows) < count) {
     set_error("bn_finalize: bad arguments");
     return ARGUS_ERR_ARG;
   }

@@ -84,8 +84,8 @@ template <typename T, int BM, int BN, bool STEM, bool PRO, int OCC, int BWX>
 __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
   constexpr int BW = BWX & 7;                   // BN-backward epilogue variant
   constexpr bool AP = (BWX & kApplyBit) != 0;   // BN-backward apply prologue
-  constexpr bool F8 = (BWX & kFp8Bit) != 0;     // MX-fp8 operands (bf16 storage)
-  static_assert(!F8 || (sizeof(T) == 2 && !STEM && !PRO && !AP), "fp8: bf16 tensors, no staging transforms");
+  constexpr bool F8 = (BWX & kFp8Bit) != 0;     // MX-fp8 operands (bf16 activations, fp8 weights)
+  static_assert(!F8 || (sizeof(T) == 2 && !STEM && !PRO), "fp8: bf16 tensors, no BN+ReLU prologue");
   constexpr int E = Chunk<T>::E;
   constexpr int EF = F8 ? 2 * E : E;  // elements one thread stages per row per k-step
   constexpr int BKE = 8 * EF;  // K elements per k-step (8 chunks of 16 B per LDS row)
@@ -168,6 +168,19 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
 #pragma unroll
   for (int i = 0; i < BR; ++i)
     b_row[i] = B + (size_t)(nt * BN + (tid >> 3) + 32 * i) * p.ldb + cidx * EF;
+  // fp8: B is the pre-quantized weight copy (argus_conv_weight_prep, ARGUS_FP8): e4m3 rows of ldb bytes,
+  // then the E8M0 scales [N][ldb / 32]
+  const uint8_t* b8_row[F8 ? BR : 1];
+  const uint8_t* b8_sc[F8 ? BR : 1];
+  if constexpr (F8) {
+    const uint8_t* B8 = reinterpret_cast<const uint8_t*>(p.b);
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const size_t row = (size_t)(nt * BN + (tid >> 3) + 32 * i);
+      b8_row[i] = B8 + row * p.ldb + cidx * 16;
+      b8_sc[i] = B8 + (size_t)p.N * p.ldb + row * (p.ldb / 32) + (cidx >> 1);
+    }
+  }
 
   f32x4 acc[MI][NI];
 #pragma unroll
@@ -178,8 +191,10 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
   // one k-step of staged operands (two named copies form the 2-deep prefetch ring)
   struct Stage {
     u32x4 a[AR], b[BR];
-    u32x4 a2[F8 ? AR : 1], b2[F8 ? BR : 1];  // fp8: the second bf16 chunk of the thread's 16 elements
+    u32x4 a2[F8 ? AR : 1];  // fp8: the second bf16 chunk of the thread's 16 A elements
+    uint8_t sb[F8 ? BR : 1];  // fp8: the E8M0 scale of the thread's B block (even cidx)
     u32x4 y[AP ? AR : 1];  // apply prologue: the BN input rows beside the dm rows
+    u32x4 y2[(AP && F8) ? AR : 1];
     bool ok[AR];
     int ch, tap0;  // tap0: this k-step is the center tap of phase 0 (the dy store)
   };
@@ -220,15 +235,23 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
         const int ih = a_ih[i] + dh, iw = a_iw[i] + dw;
         const bool ok = a_ok[i] && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
         S.a[i] = ld16(A + (ok ? a_off[i] + tap : ch));
-        if constexpr (F8) S.a2[i] = sel(ok, ld16(A + (ok ? a_off[i] + tap + E : ch)));
+        if constexpr (F8) S.a2[i] = ld16(A + (ok ? a_off[i] + tap + E : ch));
         if constexpr (AP) S.y[i] = ld16(reinterpret_cast<const T*>(p.ap.y) + (ok ? a_off[i] + tap : ch));
-        if constexpr (!PRO && !AP) S.a[i] = sel(ok, S.a[i]);
+        if constexpr (AP && F8) S.y2[i] = ld16(reinterpret_cast<const T*>(p.ap.y) + (ok ? a_off[i] + tap + E : ch));
+        if constexpr (!PRO && !AP) {
+          S.a[i] = sel(ok, S.a[i]);
+          if constexpr (F8) S.a2[i] = sel(ok, S.a2[i]);
+        }
         S.ok[i] = ok;
       }
 #pragma unroll
       for (int i = 0; i < BR; ++i) {
-        S.b[i] = ld16(b_row[i] + boff + ci0);
-        if constexpr (F8) S.b2[i] = ld16(b_row[i] + boff + ci0 + E);
+        if constexpr (F8) {
+          S.b[i] = ld16(b8_row[i] + boff + ci0);
+          if ((cidx & 1) == 0) S.sb[i] = b8_sc[i][(boff + ci0) / 32];
+        } else {
+          S.b[i] = ld16(b_row[i] + boff + ci0);
+        }
       }
       S.ch = ch;
       if constexpr (AP) S.tap0 = dh == 0 && dw == 0 && blockIdx.z == 0 && nt == 0;
@@ -245,22 +268,26 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
       for (int i = 0; i < AR; ++i) S.a[i] = sel(S.ok[i], pc.apply(S.a[i]));
     }
     if constexpr (AP) {  // dy = ca*dm + cb*y + cc; zero outside the image (dgrad's zero padding of dy)
-      float ca[E], cb[E], cc[E];
-      BwdEpiAcc<T, 3>::ld(ca, p.ap.ca + S.ch);
-      BwdEpiAcc<T, 3>::ld(cb, p.ap.cb + S.ch);
-      BwdEpiAcc<T, 3>::ld(cc, p.ap.cc + S.ch);
 #pragma unroll
-      for (int i = 0; i < AR; ++i) {
-        float d[E], yv[E];
-        unpack(S.a[i], d);
-        unpack(S.y[i], yv);
+      for (int h = 0; h < (F8 ? 2 : 1); ++h) {  // fp8: the thread's two chunks
+        float ca[E], cb[E], cc[E];
+        BwdEpiAcc<T, 3>::ld(ca, p.ap.ca + S.ch + h * E);
+        BwdEpiAcc<T, 3>::ld(cb, p.ap.cb + S.ch + h * E);
+        BwdEpiAcc<T, 3>::ld(cc, p.ap.cc + S.ch + h * E);
 #pragma unroll
-        for (int j = 0; j < E; ++j) d[j] = fmaf(ca[j], d[j], fmaf(cb[j], yv[j], cc[j]));
-        S.a[i] = sel(S.ok[i], pack(d));
-        if (p.ap.out && S.tap0 && S.ok[i]) st16(reinterpret_cast<T*>(p.ap.out) + a_off[i] + S.ch, S.a[i]);
+        for (int i = 0; i < AR; ++i) {
+          u32x4& av = h == 0 ? S.a[i] : S.a2[F8 ? i : 0];
+          float d[E], yv[E];
+          unpack(av, d);
+          unpack(h == 0 ? S.y[i] : S.y2[(AP && F8) ? i : 0], yv);
+#pragma unroll
+          for (int j = 0; j < E; ++j) d[j] = fmaf(ca[j], d[j], fmaf(cb[j], yv[j], cc[j]));
+          av = sel(S.ok[i], pack(d));
+          if (p.ap.out && S.tap0 && S.ok[i]) st16(reinterpret_cast<T*>(p.ap.out) + a_off[i] + S.ch + h * E, av);
+        }
       }
     }
-    if constexpr (F8) {  // 16 bf16 -> 16 e4m3 with the 32-element block scale shared with lane ^ 1
+    if constexpr (F8) {  // A: 16 bf16 -> 16 e4m3 with the 32-element block scale shared with lane ^ 1
 #pragma unroll
       for (int i = 0; i < AR; ++i) {
         const int row = (tid >> 3) + 32 * i;
@@ -269,11 +296,10 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
         if ((cidx & 1) == 0) lds_sc[buf][row][cidx >> 1] = (uint8_t)(127 + e);
       }
 #pragma unroll
-      for (int i = 0; i < BR; ++i) {
+      for (int i = 0; i < BR; ++i) {  // B: pre-quantized
         const int row = (tid >> 3) + 32 * i;
-        int e;
-        L[BM * 8 + row * 8 + (cidx ^ swz8(row))] = mx_fp8_quant(S.b[i], S.b2[i], e);
-        if ((cidx & 1) == 0) lds_sc[buf][BM + row][cidx >> 1] = (uint8_t)(127 + e);
+        L[BM * 8 + row * 8 + (cidx ^ swz8(row))] = S.b[i];
+        if ((cidx & 1) == 0) lds_sc[buf][BM + row][cidx >> 1] = S.sb[i];
       }
       return;
     }
@@ -866,6 +892,7 @@ struct WpEntry {
   void* wf;
   void* wd;
   int K, R, S, C, stem, blk0;  // blk0: first workgroup of this entry
+  int f8f, f8d;                 // ARGUS_FP8: the MX-fp8 layout for w_fwd / w_dgrad (wp_f8_layouts)
 };
 constexpr int kWpChunk = 4096;
 
@@ -873,18 +900,40 @@ ARGUS_HOST_DEV inline int wp_blocks(int K, int R, int S, int C, int stem) {
   return stem ? (K * 256 + kWpChunk - 1) / kWpChunk : (K / 64) * (C / 64) * R * S;
 }
 
-template <typename T>
-__global__ __launch_bounds__(256) void weight_prep_batch_kernel(const WpEntry* __restrict__ tab, int count) {
-  int lo = 0, hi = count - 1;
-  const int b = blockIdx.x;
-  while (lo < hi) {  // last entry with blk0 <= b
-    const int mid = (lo + hi + 1) >> 1;
-    if (tab[mid].blk0 <= b) lo = mid; else hi = mid - 1;
-  }
-  const WpEntry e = tab[lo];
+// MX-fp8 weight layout (argus_conv_weight_prep with ARGUS_FP8, for the passes whose reduction channels
+// are multiples of 128: forward when C % 128 == 0, dgrad when K % 128 == 0): in the buffer of the bf16
+// copy, bytes [0, rows * cols) hold the e4m3 values row-major, followed by one E8M0 scale byte per 32
+// consecutive elements of a row ([rows][cols / 32]). The values are the bf16-rounded weights quantized
+// exactly as the conv kernel would quantize them while staging (mx_fp8_quant): pre-quantizing only
+// moves that work out of every forward / dgrad launch.
+// policy key 37 bit of a pass: 1 forward, 2 data gradient of a 3x3 conv, 4 data gradient of a 1x1 conv
+// (with or without the apply prologue: one weight copy serves both)
+static int fp8_pass_bits(int fwd, int ksz) { return fwd ? 1 : (ksz == 1 ? 4 : 2); }
+
+// the passes of conv d that take fp8 operands under its policy: their weight copies get the fp8 layout
+static void wp_f8_layouts(const argus_conv_desc& d, int& f8f, int& f8d) {
+  const int passes = policy_of(d)[kFp8Passes];
+  f8f = !d.stem && d.c % 128 == 0 && (passes & fp8_pass_bits(1, d.r));
+  f8d = !d.stem && d.k % 128 == 0 && (passes & fp8_pass_bits(0, d.r));
+}
+
+// 16 fp32 weights of one row -> bf16 (as the bf16 copy) -> 16 e4m3 + the 32-element block's scale
+// (shared with lane ^ 1, which holds the other half of the block); returns the scale byte.
+ARGUS_DEV unsigned wp_quant16(const float (&f)[16], uint8_t* dst) {
+  float lo[8], hi[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { lo[j] = f[j]; hi[j] = f[8 + j]; }
+  int e;
+  st16(dst, mx_fp8_quant(pack(lo), pack(hi), e));
+  return (unsigned)(127 + e);
+}
+
+// One 64 (k) x 64 (c) tile of one tap (or a stem chunk) of entry e: workgroup `local` of the entry.
+// F8: fp8 layout for the passes wp_f8_fwd / wp_f8_dgrad select, bf16 otherwise (T = bf16).
+template <typename T, bool F8>
+ARGUS_DEV void weight_prep_tile(const WpEntry& e, int local) {
   T* __restrict__ wf = reinterpret_cast<T*>(e.wf);
   T* __restrict__ wd = reinterpret_cast<T*>(e.wd);
-  const int local = b - e.blk0;
   if (e.stem) {
     const int total = e.K * 256;
     for (int i = local * kWpChunk + threadIdx.x; i < (local + 1) * kWpChunk && i < total; i += 256) {
@@ -902,9 +951,9 @@ __global__ __launch_bounds__(256) void weight_prep_batch_kernel(const WpEntry* _
   const int r = rs / e.S, s = rs - r * e.S;
   __shared__ T tile[64][65];
   const int row = threadIdx.x >> 2, cq = (threadIdx.x & 3) * 16;  // 4 threads x 16 elements per row
+  const bool f8f = F8 && e.f8f, f8d = F8 && e.f8d;
   {
     const float* src = e.w + (long long)(k0 + row) * e.sk + r * e.sr + s * e.ss + (long long)(c0 + cq) * e.sc;
-    T* dst = wf + ((size_t)(k0 + row) * RS + rs) * e.C + c0 + cq;
     float f[16];
     if (e.sc == 1 && ((uintptr_t)src & 15) == 0) {  // channel-contiguous master (OHWI storage): 16-byte loads
 #pragma unroll
@@ -918,24 +967,61 @@ __global__ __launch_bounds__(256) void weight_prep_batch_kernel(const WpEntry* _
     }
     constexpr int E = Chunk<T>::E;
 #pragma unroll
-    for (int j = 0; j < 16; j += E) {
-      float g[E];
+    for (int j = 0; j < 16; ++j) tile[row][cq + j] = from_f32<T>(f[j]);
+    if (f8f) {  // e4m3 row [k][RS*C] + scales [k][RS*C/32]
+      const long long cols = (long long)RS * e.C, at = (long long)(k0 + row) * cols + rs * e.C + c0 + cq;
+      uint8_t* base = reinterpret_cast<uint8_t*>(e.wf);
+      const unsigned sb = wp_quant16(f, base + at);
+      if ((threadIdx.x & 1) == 0) base[(long long)e.K * cols + at / 32] = (uint8_t)sb;
+    } else {
+      T* dst = wf + ((size_t)(k0 + row) * RS + rs) * e.C + c0 + cq;
 #pragma unroll
-      for (int u = 0; u < E; ++u) { g[u] = f[j + u]; tile[row][cq + j + u] = from_f32<T>(f[j + u]); }
-      st16(dst + j, pack(g));
+      for (int j = 0; j < 16; j += E) {
+        float g[E];
+#pragma unroll
+        for (int u = 0; u < E; ++u) g[u] = f[j + u];
+        st16(dst + j, pack(g));
+      }
     }
   }
   if (!wd) return;
   __syncthreads();
-  T* dst = wd + ((size_t)(c0 + row) * RS + rs) * e.K + k0 + cq;  // row = c, 16 consecutive k
   constexpr int E = Chunk<T>::E;
+  float g16[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) g16[j] = to_f32(tile[cq + j][row]);  // row = c, 16 consecutive k
+  if (f8d) {  // e4m3 row [c][RS*K] + scales [c][RS*K/32]
+    const long long cols = (long long)RS * e.K, at = (long long)(c0 + row) * cols + rs * e.K + k0 + cq;
+    uint8_t* base = reinterpret_cast<uint8_t*>(e.wd);
+    const unsigned sb = wp_quant16(g16, base + at);
+    if ((threadIdx.x & 1) == 0) base[(long long)e.C * cols + at / 32] = (uint8_t)sb;
+    return;
+  }
+  T* dst = wd + ((size_t)(c0 + row) * RS + rs) * e.K + k0 + cq;
 #pragma unroll
   for (int j = 0; j < 16; j += E) {
     float g[E];
 #pragma unroll
-    for (int u = 0; u < E; ++u) g[u] = to_f32(tile[cq + j + u][row]);
+    for (int u = 0; u < E; ++u) g[u] = g16[j + u];
     st16(dst + j, pack(g));
   }
+}
+
+template <typename T, bool F8>
+__global__ __launch_bounds__(256) void weight_prep_batch_kernel(const WpEntry* __restrict__ tab, int count) {
+  int lo = 0, hi = count - 1;
+  const int b = blockIdx.x;
+  while (lo < hi) {  // last entry with blk0 <= b
+    const int mid = (lo + hi + 1) >> 1;
+    if (tab[mid].blk0 <= b) lo = mid; else hi = mid - 1;
+  }
+  const WpEntry e = tab[lo];
+  weight_prep_tile<T, F8>(e, b - e.blk0);
+}
+
+// one conv (argus_conv_weight_prep with ARGUS_FP8): the entry by value
+__global__ __launch_bounds__(256) void weight_prep_one_f8_kernel(const WpEntry e) {
+  weight_prep_tile<bf16, true>(e, blockIdx.x);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1027,7 +1113,14 @@ static void dispatch_ig_bwd(const IgParams& p, int maxM, int bm, int bn, hipStre
 //     sweeps favoured 1024, in the full step 512 wins +0.7 % - fewer fp32 split partials contending with
 //     the main stream for HBM); 3x3 with Cout = 64: 2048;
 //  19 / 34: the bf16 stem forward / weight gradient on the LDS-patch kernels (stem.hip);
-//  35: 128-row forward tiles from 16 K GEMM rows; 36: the glds kernel from 4 256-row tiles.
+//  35: 128-row forward tiles from 16 K GEMM rows; 36: the glds kernel from 4 256-row tiles;
+//  37: ARGUS_FP8 runs the MX-fp8 MFMA on the 3x3 data gradients only (2). Full B=512 steps per
+//      setting (profiles/r04_b512_fp8_policy.txt): 2 -> 10203 img/s, 0 (no fp8) 10170, 4 (1x1 dgrads,
+//      apply prologue staged then quantized) 9583, 6 9668, 7 (every pass) 9486; bf16 10190. Per layer
+//      (tools/convbench.py, profiles/r04_convbench_b512_*.txt) the register-staged fp8 kernel loses to
+//      the bf16 kernels on every forward but one (OCC 2 against OCC 3-4 or LDS-DMA staging, plus the
+//      per-row quantization of the activation operand) and the 1x1 data gradients with the apply
+//      prologue (four staged chunks per row: OCC 2) take 1.4 ms where the bf16 kernel takes 1.0 ms.
 static constexpr int kUnset = -1;
 static const Policy kDefaultPolicy = [] {
   Policy p;
@@ -1047,6 +1140,7 @@ static const Policy kDefaultPolicy = [] {
   p.v[kStemLdsWgrad] = 1;
   p.v[kFwdBm128Rows] = 16 * 1024;
   p.v[kGldsMinRows] = 4 * 256;
+  p.v[kFp8Passes] = 2;
   return p;
 }();
 
@@ -1075,10 +1169,13 @@ Policy policy_of(const argus_conv_desc& d) {
   return p;
 }
 
-// MX-fp8 operands (ARGUS_FP8) need whole 128-element k-steps inside one filter tap and no staging
-// transform of the A operand; other convs of an fp8 network run the bf16 kernels
+// MX-fp8 operands (ARGUS_FP8) need whole 128-element k-steps inside one filter tap and no BN+ReLU
+// prologue (the BN-backward apply prologue is staged before the quantization); other convs of an fp8
+// network run the bf16 kernels. The weights are then the pre-quantized copy (argus_conv_weight_prep
+// with ARGUS_FP8: wp_f8_fwd / wp_f8_dgrad pick the same convs).
 static bool f8_ok(const IgParams& p) {
-  if (!p.f8 || p.stem || p.pro_scale || p.ap.y || p.Cin % 128) return false;
+  if (!p.f8 || p.stem || p.pro_scale || p.Cin % 128) return false;
+  if (!(fp8_pass_bits(p.fwd, p.ksz) & (*p.pol)[kFp8Passes])) return false;
   for (int i = 0; i < p.nphase; ++i)
     if (p.ph[i].K % 128) return false;
   return true;
@@ -1094,12 +1191,8 @@ static int run_ig(const IgParams& p, hipStream_t st, int bm, int bn) {
   const bool smallk = maxK <= (*p.pol)[kSmallKMax];
   if constexpr (sizeof(T) == 2) {
     if (f8_ok(p)) {  // single-buffered (the staged bf16 pair per chunk doubles the staging registers)
-      switch (p.bb.mode ? bwd_variant(p.bb) : 0) {
-        case 2: dispatch_ig<T, false, 2, 2 | kFp8Bit>(p, maxM, bm, bn, st); break;
-        case 3: dispatch_ig<T, false, 2, 3 | kFp8Bit>(p, maxM, bm, bn, st); break;
-        case 4: dispatch_ig<T, false, 2, 4 | kFp8Bit>(p, maxM, bm, bn, st); break;
-        default: dispatch_ig<T, false, 2, kFp8Bit>(p, maxM, bm, bn, st);
-      }
+      if (p.ap.y) dispatch_ig_bwd1<T, 2, kFp8Bit | kApplyBit>(p, maxM, bm, bn, st);
+      else dispatch_ig_bwd1<T, 2, kFp8Bit>(p, maxM, bm, bn, st);
       return check_launch("igemm_kernel");
     }
     if (conv3x3_halo_launch(p, st)) return check_launch("conv3x3_halo_kernel");
@@ -1136,14 +1229,25 @@ static int fwd_bm(const argus_conv_desc& d, const Policy& pol) {
   return M >= pol[kFwdBm128Rows] ? 128 : 64;
 }
 
-int conv_fwd_stat_rows(const argus_conv_desc& d, int) {
-  if (check_desc(d)) return 0;
-  return cdiv(d.n * d.ho * d.wo, fwd_bm(d, policy_of(d)));
+// the stem forward runs on the LDS-patch kernel (stem.hip)
+static bool stem_lds_fwd(const argus_conv_desc& d, int dtype, const Policy& pol) {
+  return d.stem && pol[kStemLdsFwd] && stem_fwd_ok(d, dtype == ARGUS_FP8 ? ARGUS_BF16 : dtype);
 }
 
-int conv_fwd_stat_tile(const argus_conv_desc& d, int) {
+int conv_fwd_stat_rows(const argus_conv_desc& d, int dtype) {
   if (check_desc(d)) return 0;
-  return fwd_bm(d, policy_of(d));
+  const Policy pol = policy_of(d);
+  if (stem_lds_fwd(d, dtype, pol)) return stem_stat_rows(d);
+  return cdiv(d.n * d.ho * d.wo, fwd_bm(d, pol));
+}
+
+// rows of the forward statistics partials; negative when every partial row is to be merged as a full
+// one (the ragged LDS-patch stem: argus_bn_finalize)
+int conv_fwd_stat_tile(const argus_conv_desc& d, int dtype) {
+  if (check_desc(d)) return 0;
+  const Policy pol = policy_of(d);
+  if (stem_lds_fwd(d, dtype, pol)) return stem_ragged(d) ? -128 : 128;
+  return fwd_bm(d, pol);
 }
 
 // dgrad row tile: 64 (swept: 64-row tiles beat 128 on every non-glds/non-halo dgrad at B=64, the
@@ -1157,6 +1261,8 @@ static int dgrad_bm(const Policy& pol) {
 static void fwd_params(const argus_conv_desc& d, const Policy& pol, IgParams& p) {
   p = IgParams{};
   p.pol = &pol;
+  p.fwd = 1;
+  p.ksz = d.r;
   p.N = d.k; p.H = d.h; p.W = d.w; p.ish = d.stride; p.isw = d.stride;
   p.Ho = d.ho; p.Wo = d.wo; p.osh = 1; p.osw = 1; p.ldc = d.k;
   p.addend = nullptr; p.addend_mask = nullptr; p.stem = d.stem; p.nphase = 1;
@@ -1187,7 +1293,12 @@ int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, 
                    (stats ? 8.0 * conv_fwd_stat_rows(d, dtype) * d.k : 0.0);
   if (d.stem && sc) { set_error("conv_fwd: stem has no prologue"); return ARGUS_ERR_ARG; }
   const Policy pol = policy_of(d);
-  if (d.stem && pol[kStemLdsFwd] && stem_fwd_launch(d, dtype, x, w, y, stats, st))  // stem.hip (bf16)
+  if (f8 && sc) {
+    int f8f, f8d;
+    wp_f8_layouts(d, f8f, f8d);
+    if (f8f) { set_error("conv_fwd: an fp8 forward takes no BN+ReLU prologue"); return ARGUS_ERR_ARG; }
+  }
+  if (stem_lds_fwd(d, dtype, pol) && stem_fwd_launch(d, dtype, x, w, y, stats, st))  // stem.hip (bf16)
     return check_launch("stem_fwd_kernel");
   IgParams p;
   fwd_params(d, pol, p);
@@ -1203,6 +1314,7 @@ static void dgrad_params(const argus_conv_desc& d, const Policy& pol, const void
                          const void* addend, const uint8_t* addend_mask, IgParams& p) {
   p = IgParams{};
   p.pol = &pol;
+  p.ksz = d.r;
   p.a = dy; p.b = wt; p.c = dx;
   p.N = d.c; p.Cin = d.k; p.lda = d.k; p.H = d.ho; p.W = d.wo; p.ish = 1; p.isw = 1;
   p.Ho = d.h; p.Wo = d.w; p.osh = d.stride; p.osw = d.stride; p.ldc = d.c; p.ldb = d.r * d.s * d.k;
@@ -1285,10 +1397,7 @@ int conv_dgrad_bn_rows(const argus_conv_desc& d, int dtype) {
 // than the separate pass), so only 1x1 dgrads on the register-staged kernel stage it.
 static bool dgrad_stages_prologue(const argus_conv_desc& d, int dtype, IgParams& p) {
   if (d.r != 1 || d.s != 1) return false;
-  if (p.f8) {  // the fp8 kernels stage no transform: eligible convs get dy materialised
-    p.ap.y = nullptr;
-    if (f8_ok(p)) return false;
-  }
+  if (f8_ok(p)) return true;  // the fp8 register-staged kernel stages the apply, then quantizes
   int maxM = 0, maxK = 0;
   for (int i = 0; i < p.nphase; ++i) {
     maxM = p.ph[i].M > maxM ? p.ph[i].M : maxM;
@@ -1560,6 +1669,13 @@ int conv_weight_prep(const argus_conv_desc& d, int dtype, const float* w, const 
     ws = {(long long)d.r * d.s * d.c, 1, (long long)d.s * d.c, d.c};
   }
   if (d.stem && !wf) { set_error("weight_prep: stem needs w_fwd"); return ARGUS_ERR_ARG; }
+  if (dtype == ARGUS_FP8) {  // the MX-fp8 layout where a pass takes fp8 operands (weight_prep_tile)
+    if (!wf) { set_error("weight_prep: fp8 needs w_fwd"); return ARGUS_ERR_ARG; }
+    WpEntry e{w, ws.sk, ws.sc, ws.sr, ws.ss, wf, d.stem ? nullptr : wd, d.k, d.r, d.s, d.c, d.stem, 0, 0, 0};
+    wp_f8_layouts(d, e.f8f, e.f8d);
+    hipLaunchKernelGGL(weight_prep_one_f8_kernel, dim3(wp_blocks(d.k, d.r, d.s, d.c, d.stem)), dim3(256), 0, st, e);
+    return check_launch("weight_prep_one_f8_kernel");
+  }
   const int total = d.stem ? d.k * 256 : d.k * d.r * d.s * d.c;
   const int blocks = std::min(cdiv(total, 256), 4096);
   if (dtype == ARGUS_BF16)
@@ -1592,6 +1708,7 @@ int conv_weight_prep_table(int count, const argus_conv_desc* descs, const float*
     t.wf = wf[i];
     t.wd = (d.stem || !wd) ? nullptr : wd[i];
     t.K = d.k; t.R = d.r; t.S = d.s; t.C = d.c; t.stem = d.stem; t.blk0 = blk;
+    wp_f8_layouts(d, t.f8f, t.f8d);  // used by the ARGUS_FP8 batch only
     if (!d.stem && (d.k % 64 || d.c % 64)) { set_error("conv_weight_prep_table: channels must be multiples of 64"); return ARGUS_ERR_SHAPE; }
     blk += wp_blocks(d.k, d.r, d.s, d.c, d.stem);
   }
@@ -1602,12 +1719,13 @@ int conv_weight_prep_table(int count, const argus_conv_desc* descs, const float*
 int conv_weight_prep_batch(int dtype, int count, const void* device_table, int nblocks, hipStream_t st) {
   if (count <= 0 || nblocks <= 0 || !device_table) { set_error("conv_weight_prep_batch: bad arguments"); return ARGUS_ERR_ARG; }
   g_launch_work = 0.0;
-  if (dtype == ARGUS_BF16)
-    hipLaunchKernelGGL(weight_prep_batch_kernel<bf16>, dim3(nblocks), dim3(256), 0, st,
-                       reinterpret_cast<const WpEntry*>(device_table), count);
+  const WpEntry* tab = reinterpret_cast<const WpEntry*>(device_table);
+  if (dtype == ARGUS_FP8)
+    hipLaunchKernelGGL((weight_prep_batch_kernel<bf16, true>), dim3(nblocks), dim3(256), 0, st, tab, count);
+  else if (dtype == ARGUS_BF16)
+    hipLaunchKernelGGL((weight_prep_batch_kernel<bf16, false>), dim3(nblocks), dim3(256), 0, st, tab, count);
   else
-    hipLaunchKernelGGL(weight_prep_batch_kernel<float>, dim3(nblocks), dim3(256), 0, st,
-                       reinterpret_cast<const WpEntry*>(device_table), count);
+    hipLaunchKernelGGL((weight_prep_batch_kernel<float, false>), dim3(nblocks), dim3(256), 0, st, tab, count);
   return check_launch("weight_prep_batch_kernel");
 }
 

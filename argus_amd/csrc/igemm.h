@@ -63,6 +63,8 @@ struct IgParams {
   BnFin fin;      // BN finalize folded into this launch (fin.mode != 0)
   BnApplyPro ap;  // dgrad only: the A operand is dm (ap.y != nullptr)
   int f8;         // ARGUS_FP8: MX-fp8 operands where the shape allows (host dispatch only)
+  int fwd;        // host: forward params (1) or data gradient (0) - the fp8 pass policy (key 37)
+  int ksz;        // host: filter size of the conv (1 or 3; the fp8 pass policy)
   int epi_pre;    // halo dgrad: prefetch the BN-backward epilogue operands under the last chunk
   const Policy* pol;  // host only (kernel selection of this call; never read on the device)
 };
@@ -288,6 +290,9 @@ bool conv3x3_halo_launch(const IgParams& p, hipStream_t st);
 bool wgrad3x3_halo_plan(const argus_conv_desc& d, int dtype, int* splits, int* tiles_per_split);
 // stem forward on an LDS input patch (stem.hip): false = shape / dtype not served
 bool stem_fwd_ok(const argus_conv_desc& d, int dtype);
+// its BN-statistics partial rows, and whether its tiling is ragged (stat tile -128: argus_bn_finalize)
+int stem_stat_rows(const argus_conv_desc& d);
+bool stem_ragged(const argus_conv_desc& d);
 bool stem_fwd_launch(const argus_conv_desc& d, int dtype, const void* x, const void* w, void* y, float* stats,
                      hipStream_t st);
 // stem weight gradient on the LDS patch + dy tile (stem.hip): split plan and launch of the fp32

@@ -38,7 +38,8 @@ enum TuneKey : int {
   kStemLdsWgrad = 34,   // bf16 stem weight gradient on the LDS-patch kernel
   kFwdBm128Rows = 35,   // fewest forward GEMM rows for 128-row tiles
   kGldsMinRows = 36,    // fewest GEMM rows (largest phase) for the glds kernel
-  kNumTuneKeys = 37
+  kFp8Passes = 37,      // ARGUS_FP8: which passes take MX-fp8 operands (1 fwd | 2 dgrad | 4 dgrad with apply)
+  kNumTuneKeys = 38
 };
 struct Policy {
   int v[kNumTuneKeys];

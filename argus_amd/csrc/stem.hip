@@ -12,7 +12,11 @@
 //
 // Epilogue as igemm_kernel's forward: BN statistics {sum, M2} per 128 output pixels (the tile's two
 // halves: rows 0-3 and 4-7), the C tile staged through LDS and written as 16-byte non-temporal stores.
-// Served: bf16, output H and W multiples of 8 and 32 (256 x 256 inputs); other shapes keep conv.hip.
+// Served: bf16, any output size whose 8 x 32 tiling is >= 75 % useful. Ragged edge tiles (the 376 x 672
+// frame's 188 x 336 output: 4 spare rows, 16 spare columns) compute their spare pixels but neither
+// store them nor count them: such a half-tile's partial is {sum, M2 + sum^2 (1/n - 1/128)} over its n
+// valid pixels, i.e. sum x^2 - sum^2 / 128, which the finalize merges as a full 128-pixel row
+// (stat tile -128, argus_bn_finalize); full tiles' partials are unchanged.
 //
 // The weight gradient (stem_wgrad_kernel) uses the same tile: dW[oc][(r, s, c)] = sum over pixels of
 // dy[px][oc] * patch(2i + r, 2j + s)[c]. Both MFMA operands need 8 consecutive PIXELS per lane, which
@@ -48,12 +52,15 @@ struct StemParams {
   int n, H, W, Ho, Wo;
 };
 
+ARGUS_HOST_DEV inline int stem_tpr(int wo) { return (wo + kTW - 1) / kTW; }
+ARGUS_HOST_DEV inline int stem_tpi(int ho, int wo) { return ((ho + kTH - 1) / kTH) * stem_tpr(wo); }
+
 __global__ __launch_bounds__(256, 3) void stem_fwd_kernel(const StemParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsB];
   uint2* patch = reinterpret_cast<uint2*>(lds);
   bf16* wl = reinterpret_cast<bf16*>(lds + kPatchB);
 
-  const int tpr = p.Wo / kTW, tpi = (p.Ho / kTH) * tpr;  // tiles per tile-row, per image
+  const int tpr = stem_tpr(p.Wo), tpi = stem_tpi(p.Ho, p.Wo);  // tiles per tile-row, per image
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int img = tile / tpi, rem = tile - img * tpi;
   const int oh0 = (rem / tpr) * kTH, ow0 = (rem % tpr) * kTW;
@@ -122,25 +129,34 @@ __global__ __launch_bounds__(256, 3) void stem_fwd_kernel(const StemParams p) {
 
   // ---- BN statistics: {sum, M2} per 64-pixel wave, merged per 128-pixel half (waves 2h, 2h+1) ----
   const size_t tile_lin = (size_t)img * tpi + rem;
+  // valid output rows / columns of this tile (ragged edge tiles: fewer than 8 / 32)
+  const int vr = min(kTH, p.Ho - oh0), vc = min(kTW, p.Wo - ow0);
+  const bool full = vr == kTH && vc == kTW;
   if (p.stats) {
     float2* red = reinterpret_cast<float2*>(lds);  // [4 waves][64]
+    // this wave's tile rows 2w, 2w+1: valid pixels, and which of its accumulator rows are valid
+    const int nw = (min(max(vr - 2 * wave, 0), 2)) * vc;
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) {
       float s = 0.f;
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) s += acc[mi][ni][r];
+        for (int r = 0; r < 4; ++r) {
+          const bool ok = full || (2 * wave + (mi >> 1) < vr && (mi & 1) * 16 + g * 4 + r < vc);
+          s += ok ? acc[mi][ni][r] : 0.f;
+        }
       s += __shfl_xor(s, 16, 64);
       s += __shfl_xor(s, 32, 64);
-      const float mean_w = s * (1.f / 64.f);
+      const float mean_w = full ? s * (1.f / 64.f) : (nw > 0 ? s / (float)nw : 0.f);
       float q = 0.f;
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
+          const bool ok = full || (2 * wave + (mi >> 1) < vr && (mi & 1) * 16 + g * 4 + r < vc);
           const float d = acc[mi][ni][r] - mean_w;
-          q = fmaf(d, d, q);
+          q = ok ? fmaf(d, d, q) : q;
         }
       q += __shfl_xor(q, 16, 64);
       q += __shfl_xor(q, 32, 64);
@@ -150,8 +166,22 @@ __global__ __launch_bounds__(256, 3) void stem_fwd_kernel(const StemParams p) {
     if (tid < 128) {
       const int h = tid >> 6, col = tid & 63;
       const float2 a0 = red[(2 * h) * 64 + col], a1 = red[(2 * h + 1) * 64 + col];
-      const float d = (a0.x - a1.x) * (1.f / 64.f);
-      store_part(p.stats + (tile_lin * 2 + h) * 64 + col, make_float2(a0.x + a1.x, a0.y + a1.y + d * d * 32.f));
+      float2 o;
+      if (full) {
+        const float d = (a0.x - a1.x) * (1.f / 64.f);
+        o = make_float2(a0.x + a1.x, a0.y + a1.y + d * d * 32.f);
+      } else {  // Chan's merge over the valid counts, then re-centred to a 128-pixel row
+        const int na = min(max(vr - 4 * h, 0), 2) * vc, nb = min(max(vr - 4 * h - 2, 0), 2) * vc;
+        const int n = na + nb;
+        float m2 = a0.y + a1.y;
+        if (na > 0 && nb > 0) {
+          const float d = a0.x / (float)na - a1.x / (float)nb;
+          m2 += d * d * ((float)na * (float)nb / (float)n);
+        }
+        const float S = a0.x + a1.x;
+        o = n > 0 ? make_float2(S, m2 + S * S * (1.f / (float)n - 1.f / 128.f)) : make_float2(0.f, 0.f);
+      }
+      store_part(p.stats + (tile_lin * 2 + h) * 64 + col, o);
     }
     __syncthreads();
   }
@@ -170,6 +200,7 @@ __global__ __launch_bounds__(256, 3) void stem_fwd_kernel(const StemParams p) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int m = (tid >> 3) + 32 * i;  // C row: tile row m / 32, column m % 32
+    if ((m >> 5) >= vr || (m & 31) >= vc) continue;  // a ragged tile's spare pixel
     const int oh = oh0 + (m >> 5), ow = ow0 + (m & 31);
     const u32x4 v = *reinterpret_cast<const u32x4*>(Cs + m * kLD + c * 8);
     st16_nt(p.y + (((size_t)img * p.Ho + oh) * p.Wo + ow) * 64 + c * 8, v);
@@ -205,7 +236,7 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_kernel(const StemWgParams p
 
   const int split = blockIdx.x;
   const int t0 = split * p.tps, t1 = min(p.tiles, t0 + p.tps);
-  const int tpr = p.Wo / kTW, tpi = (p.Ho / kTH) * tpr;
+  const int tpr = stem_tpr(p.Wo), tpi = stem_tpi(p.Ho, p.Wo);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int c8 = tid & 7;  // this thread's 8-channel chunk of every dy row it stages
 
@@ -218,16 +249,20 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_kernel(const StemWgParams p
   struct Stage {
     u32x4 d[8], y[AP ? 8 : 1];
     uint2 x[kPatchPT];
+    unsigned ok;  // bit i: staged dy row i is a pixel of the image (ragged edge tiles: spare ones are 0)
   } S;
   auto load = [&](int tile) {
     const int img = tile / tpi, rem = tile - img * tpi;
     const int oh0 = (rem / tpr) * kTH, ow0 = (rem % tpr) * kTW;
+    S.ok = 0u;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int row = (tid >> 3) + 32 * i;  // tile pixel: row i of the tile, column tid >> 3
-      const size_t off = (((size_t)img * p.Ho + oh0 + (row >> 5)) * p.Wo + ow0 + (row & 31)) * 64 + c8 * 8;
+      const bool ok = oh0 + (row >> 5) < p.Ho && ow0 + (row & 31) < p.Wo;
+      const size_t off = ok ? (((size_t)img * p.Ho + oh0 + (row >> 5)) * p.Wo + ow0 + (row & 31)) * 64 + c8 * 8 : 0;
       S.d[i] = ld16(p.dm + off);
       if constexpr (AP) S.y[i] = ld16(p.y + off);
+      S.ok |= ok ? 1u << i : 0u;
     }
     const uint2* X = reinterpret_cast<const uint2*>(p.x) + (size_t)img * p.H * p.W;
     const int ih0 = 2 * oh0 - 3, iw0 = 2 * ow0 - 3;
@@ -254,6 +289,7 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_kernel(const StemWgParams p
         for (int j = 0; j < 8; ++j) d[j] = fmaf(ca[j], d[j], fmaf(cb[j], yv[j], cc[j]));
         v = pack(d);
       }
+      if (!((S.ok >> i) & 1u)) v = u32x4{0u, 0u, 0u, 0u};  // a spare pixel's dy is zero (after the apply)
       *reinterpret_cast<u32x4*>(dyl + row * 128 + (((c8 >> 1) ^ dswz(row)) << 5) + (c8 & 1) * 16) = v;
     }
 #pragma unroll
@@ -326,14 +362,20 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_kernel(const StemWgParams p
         out[(16 * (2 * wm + m2) + 4 * g + e) * 256 + 16 * (7 * wn + t7) + i16] = acc[m2][t7][e];
 }
 
-static bool stem_wg_shape_ok(const argus_conv_desc& d, int dtype) {
-  return dtype == ARGUS_BF16 && d.stem && d.k == 64 && d.ho % kTH == 0 && d.wo % kTW == 0;
+// bf16, 64 output channels, and an 8 x 32 tiling of the output that is >= 75 % pixels of the image
+static bool stem_shape_ok(const argus_conv_desc& d, int dtype) {
+  if (dtype != ARGUS_BF16 || !d.stem || d.k != 64) return false;
+  const long tiled = (long)stem_tpi(d.ho, d.wo) * kTH * kTW;
+  return 4L * d.ho * d.wo >= 3L * tiled;
 }
+
+int stem_stat_rows(const argus_conv_desc& d) { return 2 * d.n * stem_tpi(d.ho, d.wo); }
+bool stem_ragged(const argus_conv_desc& d) { return d.ho % kTH != 0 || d.wo % kTW != 0; }
 
 // splits: ~2 workgroups per CU (the LDS of two 43.5 KB tiles), each a run of whole tiles
 bool stem_wgrad_plan(const argus_conv_desc& d, int dtype, int* splits, int* tps) {
-  if (!stem_wg_shape_ok(d, dtype)) return false;
-  const int tiles = d.n * (d.ho / kTH) * (d.wo / kTW);
+  if (!stem_shape_ok(d, dtype)) return false;
+  const int tiles = d.n * stem_tpi(d.ho, d.wo);
   int t = (tiles + 511) / 512;
   *tps = t;
   *splits = (tiles + t - 1) / t;
@@ -352,18 +394,17 @@ bool stem_wgrad_launch(const argus_conv_desc& d, int dtype, const void* x, const
   p.ca = ap ? ap->ca : nullptr; p.cb = ap ? ap->cb : nullptr; p.cc = ap ? ap->cc : nullptr;
   p.part = reinterpret_cast<float*>(ws);
   p.n = d.n; p.H = d.h; p.W = d.w; p.Ho = d.ho; p.Wo = d.wo;
-  p.tiles = d.n * (d.ho / kTH) * (d.wo / kTW); p.tps = tps;
+  p.tiles = d.n * stem_tpi(d.ho, d.wo); p.tps = tps;
   if (ap) timed_launch("argus::stem_wgrad_kernel<true>", stem_wgrad_kernel<true>, dim3(s), dim3(256), st, p);
   else timed_launch("argus::stem_wgrad_kernel<false>", stem_wgrad_kernel<false>, dim3(s), dim3(256), st, p);
   *splits = s;
   return true;
 }
 
-bool stem_fwd_ok(const argus_conv_desc& d, int dtype) {
-  return dtype == ARGUS_BF16 && d.stem && d.k == 64 && d.ho % kTH == 0 && d.wo % kTW == 0;
-}
+bool stem_fwd_ok(const argus_conv_desc& d, int dtype) { return stem_shape_ok(d, dtype); }
 
-// The partial-row layout this kernel writes equals argus_conv_fwd_stat_rows / _stat_tile (128)
+// The partial-row layout this kernel writes is argus_conv_fwd_stat_rows / _stat_tile: stem_stat_rows
+// rows of 128 pixels (-128 when ragged: every row merged as a full one)
 bool stem_fwd_launch(const argus_conv_desc& d, int dtype, const void* x, const void* w, void* y, float* stats,
                      hipStream_t st) {
   if (!stem_fwd_ok(d, dtype)) return false;
@@ -373,7 +414,7 @@ bool stem_fwd_launch(const argus_conv_desc& d, int dtype, const void* x, const v
   p.y = reinterpret_cast<bf16*>(y);
   p.stats = reinterpret_cast<float2*>(stats);
   p.n = d.n; p.H = d.h; p.W = d.w; p.Ho = d.ho; p.Wo = d.wo;
-  const int grid = d.n * (d.ho / kTH) * (d.wo / kTW);
+  const int grid = d.n * stem_tpi(d.ho, d.wo);
   timed_launch("argus::stem_fwd_kernel", stem_fwd_kernel, dim3(grid), dim3(256), st, p);
   return true;
 }

@@ -23,7 +23,6 @@ from __future__ import annotations
 
 import ctypes as C
 import contextlib
-import os
 from dataclasses import dataclass
 
 import torch
@@ -89,9 +88,12 @@ class ResNetEngine:
         self.E = 8 if low else 4  # elements per 16-byte chunk
         # materialize a = relu(bn(y)) of bn1/bn2 once per forward (one extra HBM pass each) so that
         # conv2/conv3 forward and weight gradients run without the BN prologue, on the global->LDS
-        # kernels; fp32 (parity path) keeps the fused prologue. ARGUS_MATERIALIZE=0/1 overrides.
-        env = os.environ.get("ARGUS_MATERIALIZE")
-        self.materialize = low if env is None else env == "1"
+        # kernels; fp32 (parity path) keeps the fused prologue.
+        self.materialize = low
+        # a2 = relu(bn2(y2)) is materialised only for blocks with at least this many output pixels;
+        # smaller blocks' conv3 stages bn2 + ReLU in its forward (and weight gradient) prologue instead
+        # (0: every block; set before the first forward)
+        self.a2_min_px = 20000  # B=64: layer 4's three blocks (8192 px; A/B +0.7 %, profiles/r04_ab_a2.txt)
         self.device = torch.device(device)
         self.blocks = resnet50_blocks()
         self.shape = None
@@ -101,21 +103,21 @@ class ResNetEngine:
         # main stream (they only feed the gradient buffer). Events order them after their dy and
         # before any main-stream overwrite of that dy buffer; each bucket all-reduce is issued on the
         # side stream after both streams' work (on_ready's comm) and backward() joins it at its end.
-        # ARGUS_WGRAD_STREAM=0 keeps everything on the caller's stream.
-        self.wgrad_overlap = os.environ.get("ARGUS_WGRAD_STREAM", "1") != "0"
+        # False keeps everything on the caller's stream.
+        self.wgrad_overlap = True
         # BN-backward apply (dy = ca*dm + cb*y + cc) staged by the consuming dgrad, which also stores dy for
-        # the weight gradient (argus_conv_dgrad_bn with a prologue); ARGUS_FUSE_APPLY=0 runs the apply pass
-        self.fuse_apply = os.environ.get("ARGUS_FUSE_APPLY", "1") != "0"
+        # the weight gradient (argus_conv_dgrad_bn with a prologue); False runs the apply pass
+        self.fuse_apply = True
         # ... and where that dgrad stages the apply inside its kernel (1x1, register-staged:
         # argus_conv_dgrad_stages_prologue), dy is not stored at all: the side-stream weight gradient
         # stages the same apply from dm and y (argus_conv_wgrad_apply). Moves the dy write off the main
-        # stream (one more read on the side stream). ARGUS_WGRAD_APPLY=0 stores dy as before.
-        self.wgrad_apply = os.environ.get("ARGUS_WGRAD_APPLY", "1") != "0"
+        # stream (one more read on the side stream). False stores dy.
+        self.wgrad_apply = True
         # BN-backward finalize (dgamma, dbeta, ca / cb / cc) folded into the dgrad launch that produces
-        # its partial sums (argus_conv_dgrad_bn with a workspace; +0.3 % at B=64); ARGUS_FOLD_FIN=0 runs
-        # the separate bwd_finalize kernels (A/B measurements). The forward statistics keep their own
+        # its partial sums (argus_conv_dgrad_bn with a workspace; +0.3 % at B=64); False runs
+        # the separate bwd_finalize kernels. The forward statistics keep their own
         # finalize launch (folding it into the conv measured neutral).
-        self.fold_fin = os.environ.get("ARGUS_FOLD_FIN", "1") != "0"
+        self.fold_fin = True
         self._side: torch.cuda.Stream | None = None
         self._pending: dict = {}  # buffer data_ptr -> (seq, event) of the last side-stream wgrad reading it
         self._last_side = None
@@ -123,14 +125,14 @@ class ResNetEngine:
         # record on the main stream per block instead of one per weight gradient (each cross-stream
         # event costs the main stream a dispatch gap; +0.6 % at B=64). A single wait per block for the
         # ring buffers it reuses was measured too (-2.5 %: it waits earlier than the per-buffer guards).
-        # ARGUS_SIDE_BATCH=0 issues every weight gradient as soon as its dy is ready.
-        self.side_batch = os.environ.get("ARGUS_SIDE_BATCH", "1") != "0"
+        # False issues every weight gradient as soon as its dy is ready.
+        self.side_batch = True
         self._deferred: list = []  # (cv, fn, buffer data_ptrs)
         self._side_seq = 0
         self._waited_seq = 0
         # the stem weight gradient (main stream, its own split workspace) is issued before the final
-        # join, beside the side stream's last weight gradients (+0.2 %); ARGUS_STEM_OVERLAP=0 after it
-        self._stem_overlap = os.environ.get("ARGUS_STEM_OVERLAP", "1") == "1"
+        # join, beside the side stream's last weight gradients (+0.2 %); False: after it
+        self._stem_overlap = True
         # the first block's downsample weight gradient runs on the main stream after the stem weight
         # gradient instead of on the side stream: the side stream's last weight gradients otherwise
         # outlast the main stream's stem work (an exposed ~150 us tail before the join; +0.4 % at B=64,
@@ -138,6 +140,9 @@ class ResNetEngine:
         # test_side_stream_overlap_is_bit_identical runs both placements.
         self.tail_main = True
         self._tail: list = []
+        self.dy_ring = 12  # dy ring buffers (set before the first forward)
+        # (the schedule switches above are attributes, not environment variables: tools/engine_ab.py
+        # A/B-measures them; test_gpu_train.py runs the overlap / tail placements against each other)
 
     # ------------------------------------------------------------------ allocation
     def _t(self, *shape, dtype=None):
@@ -195,7 +200,7 @@ class ResNetEngine:
                 "y3": self._t(N, ho, wo, b.cout), "out": self._t(N, ho, wo, b.cout),
                 "yd": self._t(N, ho, wo, b.cout) if b.has_ds else None,
                 "a1": self._t(N, h, w, b.width) if self.materialize else None,
-                "a2": self._t(N, ho, wo, b.width) if self.materialize else None,
+                "a2": self._t(N, ho, wo, b.width) if self.materialize and N * ho * wo >= self.a2_min_px else None,
                 # ReLU mask of `out`, one byte per 16-byte chunk (argus_bn_apply mask_out)
                 "bits": torch.empty(N * ho * wo * b.cout // self.E, dtype=torch.uint8, device=self.device),
             }
@@ -257,8 +262,8 @@ class ResNetEngine:
         self.gbuf = [self._t(max_elems) for _ in range(3)]  # avgpool dh; dza / dzb (the dz of bn2 / bn1)
         # dy operands of the side-stream weight gradients come from a ring, so the main stream can
         # run ahead of the wgrad stream by several layers before it must wait to reuse a buffer
-        # (ARGUS_DY_RING buffers; a reuse waits on the event of the wgrad that last read it)
-        nring = max(8, int(os.environ.get("ARGUS_DY_RING", "12")))  # >= 2 blocks of takes
+        # (a reuse waits on the event of the wgrad that last read it; 16 buffers measured no better)
+        nring = max(8, self.dy_ring)  # >= 2 blocks of takes
         self.dyring = [self._t(max_elems) for _ in range(nring)]
         self._ring_i = 0
 
@@ -342,7 +347,8 @@ class ResNetEngine:
             self.L.conv_weight_prep_table(n, descs, masters, strides, wfs, wds, host, nbytes, C.byref(nblk))
             self._wp_table = torch.frombuffer(bytearray(host), dtype=torch.uint8).to(self.device)
             self._wp_n, self._wp_blocks, self._wp_key = n, nblk.value, key
-        self.L.conv_weight_prep_batch(self.dt, self._wp_n, ptr(self._wp_table), self._wp_blocks, stream())
+        # fp8: the pre-quantized MX-fp8 copies of the convs whose passes take fp8 operands (cdt = FP8)
+        self.L.conv_weight_prep_batch(self.cdt, self._wp_n, ptr(self._wp_table), self._wp_blocks, stream())
 
     # ------------------------------------------------------------------ forward
     def forward(self, x: torch.Tensor, P: dict, Bf: dict, training: bool) -> torch.Tensor:
@@ -379,8 +385,11 @@ class ResNetEngine:
             if self.materialize:
                 self._act(pf + ".bn1", a["y1"], a["a1"], N * a["hw_in"][0] * a["hw_in"][1], b.width)
                 self._conv_bn(P, Bf, pf + ".conv2", pf + ".bn2", a["a1"], a["y2"], None, training)
-                self._act(pf + ".bn2", a["y2"], a["a2"], N * a["hw"][0] * a["hw"][1], b.width)
-                self._conv_bn(P, Bf, pf + ".conv3", pf + ".bn3", a["a2"], a["y3"], None, training)
+                if a["a2"] is not None:
+                    self._act(pf + ".bn2", a["y2"], a["a2"], N * a["hw"][0] * a["hw"][1], b.width)
+                    self._conv_bn(P, Bf, pf + ".conv3", pf + ".bn3", a["a2"], a["y3"], None, training)
+                else:  # bn2 + ReLU staged by conv3's forward (register-staged kernel)
+                    self._conv_bn(P, Bf, pf + ".conv3", pf + ".bn3", a["y2"], a["y3"], pf + ".bn2", training)
             else:
                 self._conv_bn(P, Bf, pf + ".conv2", pf + ".bn2", a["y1"], a["y2"], pf + ".bn1", training)
                 self._conv_bn(P, Bf, pf + ".conv3", pf + ".bn3", a["y2"], a["y3"], pf + ".bn2", training)
@@ -491,7 +500,7 @@ class ResNetEngine:
             dbg = self.debug
             # weight gradients that stage the BN-backward apply from dm themselves (dy never stored;
             # the debug capture keeps storing it for the stage checks)
-            wg3_apply = (rows3 is not None and self.fuse_apply and self.wgrad_apply and self.materialize
+            wg3_apply = (rows3 is not None and self.fuse_apply and self.wgrad_apply and a["a2"] is not None
                          and self.stages_pro[pf + ".conv3"])
             wg1_apply = idx > 0 and self.fuse_apply and self.wgrad_apply and self.stages_pro[pf + ".conv1"]
             dy3 = None if wg3_apply and dbg is None else self._next_dy()
@@ -537,7 +546,7 @@ class ResNetEngine:
             s2 = self.bn_state[pf + ".bn2"]
             if wg3_apply:  # dh holds dm3 (read by the side stream until its event: dh is not reused)
                 self._wgrad_apply(pf + ".conv3", a["a2"], dh, pf + ".bn3", a["y3"], G)
-            elif self.materialize:
+            elif a["a2"] is not None:
                 self._wgrad(pf + ".conv3", a["a2"], None, dy3, G)
             else:
                 self._wgrad(pf + ".conv3", a["y2"], s2, dy3, G)

@@ -28,10 +28,13 @@ extern "C" {
 
 typedef void* argus_stream_t; /* hipStream_t */
 
-/* ARGUS_FP8 (conv fwd / dgrad entry points only): bf16 tensors, GEMM operands quantized while
- * staging to OCP MX-fp8 (e4m3 + one E8M0 scale per 32 K-elements of a row) for the MFMA
- * v_mfma_scale_f32_16x16x128_f8f6f4, where the conv allows it (reduction channels % 128 == 0,
- * not the stem); the other convs, and every non-conv entry point (pass ARGUS_BF16), run bf16. */
+/* ARGUS_FP8 (conv fwd / dgrad and weight-prep entry points): bf16 activations, GEMM operands in OCP
+ * MX-fp8 (e4m3 + one E8M0 scale per 32 K-elements of a row) for the MFMA
+ * v_mfma_scale_f32_16x16x128_f8f6f4 where the conv pass allows it (reduction channels % 128 == 0, not
+ * the stem): the activation operand (and a BN-backward apply prologue) is quantized while staging, the
+ * weights are the pre-quantized copies argus_conv_weight_prep(_batch) writes with ARGUS_FP8 (e4m3 rows
+ * [rows][cols] then scales [rows][cols/32], in the bf16 copy's buffer). The other passes and every
+ * non-conv entry point (pass ARGUS_BF16) run bf16. */
 enum { ARGUS_F32 = 0, ARGUS_BF16 = 1, ARGUS_FP8 = 2 };
 enum { ARGUS_OK = 0, ARGUS_ERR_ARG = 1, ARGUS_ERR_SHAPE = 2, ARGUS_ERR_HIP = 3 };
 
@@ -179,7 +182,8 @@ int argus_conv_dgrad_bn(const argus_conv_desc* d, int dtype, const void* dy, con
  * register-staged 3x3 weight gradient, key 34 the bf16 stem weight gradient on the LDS-patch kernel
  * (1) or on the register-staged weight-gradient kernel (0), key 35 the fewest GEMM rows (output
  * pixels) for which the forward uses 128-row tiles (fewer: 64), key 36 the fewest GEMM rows for the
- * glds kernel. (Keys scaled with the batch keep a smaller batch's kernel selection that of the larger
+ * glds kernel, key 37 which ARGUS_FP8 passes take MX-fp8 operands (bits: 1 forward, 2 data gradient of
+ * a 3x3 conv, 4 data gradient of a 1x1 conv; argus_conv_weight_prep follows the same key). (Keys scaled with the batch keep a smaller batch's kernel selection that of the larger
  * one: tests/test_gpu_parity.py stage-checks the benched configurations' kernels that way.) */
 int argus_conv_policy_default(int key);
 /* Which tile a pass launches and its algorithmic work: pass 0 fwd, 1 dgrad, 2 wgrad. Returns a
@@ -225,7 +229,9 @@ int argus_ktimer_get(int index, char* name, int name_len, int64_t* launches, dou
 size_t argus_bn_workspace_bytes(int channels);
 /* From tile partials float2[rows][C] = {sum, M2 (sum of squared deviations from the tile mean)},
  * tile t holding min(tile_rows, count - t*tile_rows) elements per channel (as argus_conv_fwd
- * writes them): merged in fp64 (Chan), gives mean, invstd, the fused apply coefficients
+ * writes them; tile_rows < 0, as argus_conv_fwd_stat_tile reports for a producer with ragged tiles:
+ * every row is merged as |tile_rows| elements, its M2 stored as sum x^2 - sum^2/|tile_rows|): merged
+ * in fp64 (Chan), gives mean, invstd, the fused apply coefficients
  * scale = gamma*invstd, shift = beta - mean*scale; updates running stats (momentum, unbiased
  * variance) and num_batches_tracked when those pointers are non-NULL. */
 int argus_bn_finalize(int channels, int rows, int tile_rows, const float* part, int64_t count,

@@ -11,13 +11,13 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from argus_amd._lib import BF16, F32, ConvDesc, lib, ptr, stream
+from argus_amd._lib import BF16, F32, FP8, ConvDesc, lib, ptr, stream
 
 pytestmark = pytest.mark.gpu
 
 TOL = {"fp32": 2e-5, "bf16": 1.5e-2}
-TDT = {"fp32": torch.float32, "bf16": torch.bfloat16}
-DT = {"fp32": F32, "bf16": BF16}
+TDT = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp8": torch.bfloat16}  # fp8: bf16 tensors
+DT = {"fp32": F32, "bf16": BF16, "fp8": FP8}
 
 # (cin, cout, k, stride, input size) — every distinct conv shape of SURVEY.md Appendix B at small
 # spatial sizes (odd sizes exercise partial tiles and the 376x672 rounding).
@@ -60,12 +60,16 @@ def _q(t, dt):  # round to the compute dtype (reference inputs)
 
 
 def _merge_stats(part, tile, count):
-    """Chan-merge per-tile {sum, M2} partials (rows, C, 2) -> per-channel (mean, biased var)."""
-    n = torch.tensor([min(tile, count - t * tile) for t in range(part.shape[0])], dtype=torch.float64)
+    """Chan-merge per-tile {sum, M2} partials (rows, C, 2) -> per-channel (mean, biased var). tile < 0
+    (argus_conv_fwd_stat_tile of a ragged producer): every row is merged as |tile| elements."""
+    if tile < 0:
+        n = torch.full((part.shape[0],), float(-tile), dtype=torch.float64)
+    else:
+        n = torch.tensor([min(tile, count - t * tile) for t in range(part.shape[0])], dtype=torch.float64)
     mean_t = part[..., 0] / n[:, None]
     mean = part[..., 0].sum(0) / count
-    m2 = part[..., 1].sum(0) + (n[:, None] * (mean_t - mean) ** 2).sum(0)
-    return mean, m2 / count
+    q = (part[..., 1] + part[..., 0] * mean_t).sum(0)  # sum of x^2
+    return mean, q / count - mean * mean
 
 
 @pytest.mark.parametrize("dt", ["fp32", "bf16"])
@@ -181,12 +185,15 @@ def test_stem_lds_patch_kernel(cuda):
     """bf16 stem forward on the LDS-patch kernel (stem.hip: 8 x 32 output tiles, K = 7 filter rows x 32)
     vs torch (bf16 tolerance) and vs the implicit GEMM it replaces (tuning key 19 = 0): outputs within
     the bf16 tolerance of each other, BN statistics partials (one per 128 pixels) merging to the same
-    mean / variance; shapes whose output does not tile (19 x 15) keep the implicit GEMM."""
+    mean / variance (ragged edge tiles: partial rows merged as full ones, stat tile -128); shapes whose
+    8 x 32 tiling is mostly padding (19 x 15) keep the implicit GEMM."""
     from argus_amd.profiling import KernelTimer
 
     torch.manual_seed(33)
     L = lib()
-    for n, H, W, served in ((2, 64, 128, True), (1, 256, 256, True), (3, 38, 30, False)):
+    # 376 x 672 (188 x 336 output) and 100 x 248 (50 x 124): ragged edge tiles in both dimensions
+    for n, H, W, served in ((2, 64, 128, True), (1, 256, 256, True), (3, 38, 30, False), (1, 376, 672, True),
+                            (2, 100, 248, True)):
         d, p = _desc(n, H, W, 3, 64, 7, 2, stem=True)
         img = torch.rand(n, 3, H, W)
         x4 = torch.empty(n, H, W, 4, dtype=torch.bfloat16, device=cuda)
@@ -198,14 +205,15 @@ def test_stem_lds_patch_kernel(cuda):
         strides = (C.c_int64 * 4)(*wmaster.stride())
         L.conv_weight_prep(C.byref(d), BF16, ptr(wmaster), strides, ptr(wf), None, stream())
         ref = F.conv2d(_q(img, "bf16"), _q(w, "bf16").permute(0, 3, 1, 2), stride=2, padding=3)
-        rows = L.dll.argus_conv_fwd_stat_rows(C.byref(d), BF16)
-        tile = L.dll.argus_conv_fwd_stat_tile(C.byref(d), BF16)
         M = n * d.ho * d.wo
         outs = []
         for key19 in (1, 0):
+            dk = d.with_tuning({19: key19})
+            rows = L.dll.argus_conv_fwd_stat_rows(C.byref(dk), BF16)
+            tile = L.dll.argus_conv_fwd_stat_tile(C.byref(dk), BF16)
+            assert tile == (-128 if served and key19 and (d.ho % 8 or d.wo % 32) else 128), (n, H, W, key19, tile)
             y = torch.empty(n, d.ho, d.wo, 64, dtype=torch.bfloat16, device=cuda)
             stats = torch.full((rows, 64, 2), float("nan"), device=cuda)
-            dk = d.with_tuning({19: key19})
             with KernelTimer() as t:
                 L.conv_fwd(C.byref(dk), BF16, ptr(x4), ptr(wf), ptr(y), None, None, ptr(stats), stream())
             names = list(t.summary())
@@ -232,7 +240,8 @@ def test_stem_wgrad_lds_patch_kernel(cuda):
 
     torch.manual_seed(34)
     L = lib()
-    for n, H, W, served in ((2, 64, 128, True), (1, 304, 1856, True), (3, 38, 30, False)):
+    for n, H, W, served in ((2, 64, 128, True), (1, 304, 1856, True), (3, 38, 30, False), (1, 376, 672, True),
+                            (2, 100, 248, True)):
         d, _ = _desc(n, H, W, 3, 64, 7, 2, stem=True)
         img = torch.rand(n, 3, H, W)
         x4 = torch.empty(n, H, W, 4, dtype=torch.bfloat16, device=cuda)
@@ -744,12 +753,12 @@ def _halo_cases(L, cuda, tuning):
         assert _rel(dx.permute(0, 3, 1, 2), refd + (dx0 * keep).permute(0, 3, 1, 2)) < TOL["bf16"], ("dgrad m", cin)
 
 
-@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+@pytest.mark.parametrize("dt", ["fp32", "bf16", "fp8"])
 def test_weight_prep_batch_matches_single(cuda, dt):
     L = lib()
     torch.manual_seed(17)
     convs = [_desc(2, 16, 16, 3, 64, 7, 2, stem=True)[0], _desc(2, 8, 8, 64, 128, 3, 1)[0],
-             _desc(2, 8, 8, 256, 64, 1, 1)[0], _desc(2, 8, 8, 128, 128, 3, 2)[0]]
+             _desc(2, 8, 8, 256, 64, 1, 1)[0], _desc(2, 8, 8, 128, 128, 3, 2)[0]]  # fp8: fwd / dgrad / both
     masters, single, batch = [], [], []
     for i, d in enumerate(convs):
         w = torch.randn(d.k, d.c, d.r, d.s, device=cuda)  # OIHW contiguous (strided as OHWI)
@@ -779,7 +788,17 @@ def test_weight_prep_batch_matches_single(cuda, dt):
     table = torch.frombuffer(bytearray(host), dtype=torch.uint8).to(cuda)
     L.conv_weight_prep_batch(DT[dt], n, ptr(table), nblk.value, stream())
     torch.cuda.synchronize()
-    for (sf, sd), (bf, bd) in zip(single, batch):
+    for d, (sf, sd), (bf, bd) in zip(convs, single, batch):
+        if dt == "fp8":  # bytes in use: e4m3 values + E8M0 scales of the fp8 passes, bf16 otherwise
+            def used(t, rows, cols, f8):
+                return t.view(torch.uint8).reshape(-1)[: rows * cols + rows * cols // 32] if f8 else t.view(torch.uint8)
+            cols_f = 256 if d.stem else d.r * d.s * d.c
+            assert torch.equal(used(sf, d.k, cols_f, not d.stem and d.c % 128 == 0),
+                               used(bf, d.k, cols_f, not d.stem and d.c % 128 == 0))
+            if sd is not None:
+                f8d = d.k % 128 == 0
+                assert torch.equal(used(sd, d.c, d.r * d.s * d.k, f8d), used(bd, d.c, d.r * d.s * d.k, f8d))
+            continue
         assert torch.equal(sf, bf)
         assert (sd is None and bd is None) or torch.equal(sd, bd)
 
@@ -1205,19 +1224,23 @@ FP8_CASES = [  # (cin, cout, k, stride, hin, n): reduction channels % 128 == 0 i
 def test_fp8_mx_conv_fwd_dgrad(cuda):
     """ARGUS_FP8: conv fwd (+ BN statistics) and dgrad (+ BN-backward epilogue) with the A and B
     operands quantized to OCP MX-fp8 (e4m3, E8M0 scale per 32 K-elements) on the scaled MFMA, vs
-    the fp64 reference on the bf16 inputs. Stated fp8 tolerance: max error <= 6e-2 of the output's
-    max magnitude (e4m3 keeps 3 mantissa bits: 2^-4 relative per operand element)."""
-    from argus_amd._lib import FP8, BnBwdEpilogue
+    the fp64 reference on the bf16 inputs (policy key 37 = 7: every pass in fp8, the weights from the
+    fp8 weight prep), and a 1x1 dgrad staging the BN-backward apply before the quantization. Stated fp8
+    tolerance: max error <= 6e-2 of the output's max magnitude (e4m3 keeps 3 mantissa bits: 2^-4
+    relative per operand element)."""
+    from argus_amd._lib import BnBwdEpilogue, BnBwdPrologue
     from argus_amd.profiling import KernelTimer
 
     torch.manual_seed(17)
     L = lib()
     for cin, cout, k, s, hin, n in FP8_CASES:
         d, p = _desc(n, hin, hin, cin, cout, k, s)
+        d = d.with_tuning({37: 7})  # every pass on the fp8 kernel (the default takes the dgrads only)
         x = _q(torch.randn(n, hin, hin, cin), "bf16")
         w = torch.randn(cout, k, k, cin) * (2.0 / (k * k * cin)) ** 0.5
         dy = _q(torch.randn(n, d.ho, d.wo, cout), "bf16")
-        wf, wt = _prep(d, "bf16", w.to(cuda), cuda)
+        wf, wt = _prep(d, "fp8", w.to(cuda), cuda)  # the pre-quantized MX-fp8 weight copies
+        _check_fp8_weight_layout(wf, w.reshape(cout, -1), k * k * cin)
         y = torch.empty(n, d.ho, d.wo, cout, dtype=torch.bfloat16, device=cuda)
         rows = L.dll.argus_conv_fwd_stat_rows(C.byref(d), FP8)
         stats = torch.empty(rows, cout, 2, device=cuda)
@@ -1249,3 +1272,39 @@ def test_fp8_mx_conv_fwd_dgrad(cuda):
         assert e < 6e-2, ("fp8 dgrad", cin, cout, k, s, e)
         colsum = part.double().sum(0)[:, 0].cpu()
         assert _rel(colsum, dm.double().cpu().reshape(-1, cin).sum(0)) < 1e-3  # partials sum what was stored
+        if k == 1:  # the BN-backward apply staged before the quantization (dy never stored)
+            dmg = _q(torch.randn(n, d.ho, d.wo, cout), "bf16")
+            yb = _q(torch.randn(n, d.ho, d.wo, cout), "bf16")
+            ca, cb, cc = (torch.randn(cout) * 0.3 for _ in range(3))
+            assert L.dll.argus_conv_dgrad_stages_prologue(C.byref(d), FP8) == 1
+            pro = BnBwdPrologue(ptr(ybg := yb.to(cuda, torch.bfloat16)), ptr(cag := ca.to(cuda)), ptr(cbg := cb.to(cuda)),
+                                ptr(ccg := cc.to(cuda)), None)
+            dx = torch.empty(n, hin, hin, cin, device=cuda, dtype=torch.bfloat16)
+            with KernelTimer("argus::igemm_kernel") as t:
+                L.conv_dgrad_bn(C.byref(d), FP8, ptr(dmg.to(cuda, torch.bfloat16)), ptr(wt), ptr(dx), None, None,
+                                C.byref(pro), stream())
+            assert any(nm.endswith(", 48>") for nm in t.summary()), list(t.summary())  # fp8 | apply prologue
+            dyr = _q(ca * dmg + (cb * yb + cc), "bf16")
+            refa = torch.nn.grad.conv2d_input(x.permute(0, 3, 1, 2).shape, wr, dyr.permute(0, 3, 1, 2), stride=s,
+                                              padding=p)
+            e = _rel(dx.permute(0, 3, 1, 2), refa)
+            assert e < 6e-2, ("fp8 dgrad + apply prologue", cin, cout, k, s, e)
+
+
+def _check_fp8_weight_layout(buf, w_fp32, cols):
+    """argus_conv_weight_prep(ARGUS_FP8) layout of a forward copy: e4m3 rows [K][cols] then E8M0 scales
+    [K][cols / 32]; the block scale 2^e is the smallest with amax(bf16 block) * 2^-e < 448 (e4m3 max), and
+    dequantized values are the bf16 weights to e4m3's 3-bit mantissa (2^-4 relative, 2^-10 absolute
+    under the block scale for subnormals) - the same as torch's float8_e4m3fn rounding of w / 2^e."""
+    K = w_fp32.shape[0]
+    raw = buf.view(torch.uint8).reshape(-1)[: K * cols + K * cols // 32].cpu()
+    vals = raw[: K * cols].view(torch.float8_e4m3fn).float().reshape(K, cols)
+    e = raw[K * cols:].to(torch.int32).reshape(K, cols // 32) - 127
+    scale = torch.pow(2.0, e.double()).repeat_interleave(32, dim=1)
+    wb = w_fp32.to(torch.bfloat16).double()  # OHWI flattening = the kernel's K order
+    amax = wb.abs().reshape(K, cols // 32, 32).amax(-1).repeat_interleave(32, dim=1)
+    assert (amax / scale < 448).all() and ((amax / scale >= 224) | (amax == 0)).all()  # tightest E8M0 scale
+    deq = vals.double() * scale
+    assert ((deq - wb).abs() <= wb.abs() * 2.0 ** -4 + scale * 2.0 ** -10).all()
+    same = (vals == (wb / scale).float().to(torch.float8_e4m3fn).float()).double().mean().item()
+    assert same > 0.999, same  # round-to-nearest-even ties may differ

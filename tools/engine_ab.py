@@ -1,0 +1,56 @@
+"""A/B of engine schedule attributes on full bf16 train steps (dev tool, GPU): configurations run
+interleaved (A B A B ...) on one box so drift between them cancels.
+
+    python tools/engine_ab.py --batch 64 --cfg "" --cfg "a2_min_px=100000" [--rounds 3 --steps 20]
+"""
+import argparse
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, ".")
+from bench import synthetic_batch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--hw", type=int, nargs=2, default=(256, 256))
+    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--cfg", action="append", default=[], help="attr=value[,attr=value] (\"\" = defaults)")
+    a = ap.parse_args()
+    from argus_amd.models import NCameraCNN
+    from argus_amd.step import FusedTrainer
+
+    dev = torch.device("cuda", 0)
+    images, targets = synthetic_batch(a.batch, *a.hw, 1000, dev)
+    runs = []
+    for cfg in a.cfg or [""]:
+        torch.manual_seed(42)
+        m = NCameraCNN(compute_dtype=a.dtype).to(dev).train()
+        eng = m._engine(dev)
+        for kv in filter(None, cfg.split(",")):
+            k, v = kv.split("=")
+            setattr(eng, k, type(getattr(eng, k))(int(v)) if not isinstance(getattr(eng, k), bool) else v == "1")
+        tr = FusedTrainer(m, lr=1e-4, max_grad_norm=1.0)
+        for _ in range(3):
+            tr.step(images, targets)
+        runs.append((cfg, tr, []))
+    for _ in range(a.rounds):
+        for cfg, tr, res in runs:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(a.steps):
+                tr.step(images, targets)
+            torch.cuda.synchronize()
+            res.append(1e3 * (time.perf_counter() - t0) / a.steps)
+    for cfg, _, res in runs:
+        print(f"{cfg or 'defaults':40s} ms/step " + " ".join(f"{r:7.3f}" for r in res) +
+              f"   img/s best {2 * a.batch / min(res) * 1e3:8.1f}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
