@@ -90,10 +90,6 @@ class ResNetEngine:
         # conv2/conv3 forward and weight gradients run without the BN prologue, on the global->LDS
         # kernels; fp32 (parity path) keeps the fused prologue.
         self.materialize = low
-        # a2 = relu(bn2(y2)) is materialised only for blocks with at least this many output pixels;
-        # smaller blocks' conv3 stages bn2 + ReLU in its forward (and weight gradient) prologue instead
-        # (0: every block; set before the first forward)
-        self.a2_min_px = 20000  # B=64: layer 4's three blocks (8192 px; A/B +0.7 %, profiles/r04_ab_a2.txt)
         self.device = torch.device(device)
         self.blocks = resnet50_blocks()
         self.shape = None
@@ -200,7 +196,7 @@ class ResNetEngine:
                 "y3": self._t(N, ho, wo, b.cout), "out": self._t(N, ho, wo, b.cout),
                 "yd": self._t(N, ho, wo, b.cout) if b.has_ds else None,
                 "a1": self._t(N, h, w, b.width) if self.materialize else None,
-                "a2": self._t(N, ho, wo, b.width) if self.materialize and N * ho * wo >= self.a2_min_px else None,
+                "a2": self._t(N, ho, wo, b.width) if self.materialize else None,
                 # ReLU mask of `out`, one byte per 16-byte chunk (argus_bn_apply mask_out)
                 "bits": torch.empty(N * ho * wo * b.cout // self.E, dtype=torch.uint8, device=self.device),
             }
@@ -385,11 +381,8 @@ class ResNetEngine:
             if self.materialize:
                 self._act(pf + ".bn1", a["y1"], a["a1"], N * a["hw_in"][0] * a["hw_in"][1], b.width)
                 self._conv_bn(P, Bf, pf + ".conv2", pf + ".bn2", a["a1"], a["y2"], None, training)
-                if a["a2"] is not None:
-                    self._act(pf + ".bn2", a["y2"], a["a2"], N * a["hw"][0] * a["hw"][1], b.width)
-                    self._conv_bn(P, Bf, pf + ".conv3", pf + ".bn3", a["a2"], a["y3"], None, training)
-                else:  # bn2 + ReLU staged by conv3's forward (register-staged kernel)
-                    self._conv_bn(P, Bf, pf + ".conv3", pf + ".bn3", a["y2"], a["y3"], pf + ".bn2", training)
+                self._act(pf + ".bn2", a["y2"], a["a2"], N * a["hw"][0] * a["hw"][1], b.width)
+                self._conv_bn(P, Bf, pf + ".conv3", pf + ".bn3", a["a2"], a["y3"], None, training)
             else:
                 self._conv_bn(P, Bf, pf + ".conv2", pf + ".bn2", a["y1"], a["y2"], pf + ".bn1", training)
                 self._conv_bn(P, Bf, pf + ".conv3", pf + ".bn3", a["y2"], a["y3"], pf + ".bn2", training)

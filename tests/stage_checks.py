@@ -41,11 +41,8 @@ def stage_checks(eng, P, debug, tol_max):
                 z1 = nchw(a["a1"])
             else:  # conv2 on the halo kernel: bn1 + ReLU applied in LDS, rounded to the compute dtype
                 z1 = z1.to(a["y1"].dtype).double()
-            if a["a2"] is not None:
-                checks["a2"] = (nchw(a["a2"]), z2)
-                z2 = nchw(a["a2"])
-            else:  # conv3 staged bn2 + ReLU (register-staged prologue), rounded to the compute dtype
-                z2 = z2.to(a["y2"].dtype).double()
+            checks["a2"] = (nchw(a["a2"]), z2)
+            z2 = nchw(a["a2"])
         dm3 = D["b_dout"] * (out > 0)
         checks["dy3"] = (D["b_dy3"], bn_bwd(dm3, y3, st[".bn3"][0], st[".bn3"][1], gm[".bn3"]))
         w3 = P[pf + ".conv3.weight"].double().cpu()
