@@ -68,10 +68,16 @@ ARGUS_DEV double2 merge_groups(const double2* red, int G, int C, int c, double2 
   const int lane_r = threadIdx.x >> 6, cl = threadIdx.x & 63;
   double S = 0.0, Q = 0.0;
   if (c < C)
-    for (int g = lane_r; g < G; g += 4) {
-      const double2 v = red[(size_t)g * C + c];
-      S += v.x;
-      Q += v.y;
+    for (int gb = lane_r; gb < G; gb += 4 * 4) {
+      double2 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = red[(size_t)min(gb + 4 * u, G - 1) * C + c];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const bool ok = gb + 4 * u < G;
+        S += ok ? v[u].x : 0.0;
+        Q += ok ? v[u].y : 0.0;
+      }
     }
   lds[lane_r][cl] = make_double2(S, Q);
   __syncthreads();
@@ -104,13 +110,19 @@ __global__ __launch_bounds__(256) void stats_finalize_kernel(const BnFinArgs a) 
   const double inv_full = 1.0 / (double)tr;
   double S = 0.0, Q = 0.0;
   if (c < a.C)
-#pragma unroll 8
-    for (int r = r0 + lane_r; r < r1; r += 4) {
-      const float2 v = a.part[(size_t)r * a.C + c];
-      const int64_t left = a.count - (int64_t)r * tr;
-      const double inv = (a.tile_rows < 0 || left >= tr) ? inv_full : 1.0 / (double)left;
-      S += (double)v.x;
-      Q += (double)v.y + (double)v.x * (double)v.x * inv;
+    for (int rb = r0 + lane_r; rb < r1; rb += 4 * kLoadBatch) {
+      float2 v[kLoadBatch];  // the batch's loads in flight together (clamped rows, masked below)
+#pragma unroll
+      for (int u = 0; u < kLoadBatch; ++u) v[u] = a.part[(size_t)min(rb + 4 * u, r1 - 1) * a.C + c];
+#pragma unroll
+      for (int u = 0; u < kLoadBatch; ++u) {
+        const int r = rb + 4 * u;
+        const int64_t left = a.count - (int64_t)r * tr;
+        const double inv = (a.tile_rows < 0 || left >= tr) ? inv_full : 1.0 / (double)left;
+        const bool ok = r < r1;  // selects, not branches: a branch lets the compiler sink the loads
+        S += ok ? (double)v[u].x : 0.0;
+        Q += ok ? (double)v[u].y + (double)v[u].x * (double)v[u].x * inv : 0.0;
+      }
     }
   __shared__ double2 red[4][64];
   __shared__ int flag;
@@ -370,11 +382,16 @@ __global__ __launch_bounds__(256) void bwd_finalize_kernel(const BnBwdFinArgs a)
   const int r0 = g * a.rpg, r1 = min(a.rows, r0 + a.rpg);
   double s = 0.0, q = 0.0;
   if (c < a.C)
-#pragma unroll 8
-    for (int r = r0 + lane_r; r < r1; r += 4) {
-      const float2 v = a.part[(size_t)r * a.C + c];
-      s += v.x;
-      q += v.y;
+    for (int rb = r0 + lane_r; rb < r1; rb += 4 * kLoadBatch) {
+      float2 v[kLoadBatch];
+#pragma unroll
+      for (int u = 0; u < kLoadBatch; ++u) v[u] = a.part[(size_t)min(rb + 4 * u, r1 - 1) * a.C + c];
+#pragma unroll
+      for (int u = 0; u < kLoadBatch; ++u) {
+        const bool ok = rb + 4 * u < r1;
+        s += ok ? (double)v[u].x : 0.0;
+        q += ok ? (double)v[u].y : 0.0;
+      }
     }
   __shared__ double2 red[4][64];
   __shared__ int flag;

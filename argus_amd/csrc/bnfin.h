@@ -112,17 +112,15 @@ ARGUS_DEV void bn_fin_arrive(const BnFin& f, int t, int nt, double2* scratch, in
       f32x4 v[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int r = rb + u * LR;
-        v[u] = r < r1 ? *reinterpret_cast<const f32x4*>(part + (size_t)r * f.C + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+        v[u] = *reinterpret_cast<const f32x4*>(part + (size_t)min(rb + u * LR, r1 - 1) * f.C + c);
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int r = rb + u * LR;
-        if (r >= r1) break;
-        S0 += (double)v[u].x;
-        S1 += (double)v[u].z;
-        Q0 += (double)v[u].y;
-        Q1 += (double)v[u].w;
+        const bool ok = rb + u * LR < r1;  // selects, not branches (common.h kLoadBatch)
+        S0 += ok ? (double)v[u].x : 0.0;
+        S1 += ok ? (double)v[u].z : 0.0;
+        Q0 += ok ? (double)v[u].y : 0.0;
+        Q1 += ok ? (double)v[u].w : 0.0;
       }
     }
     scratch[2 * (lr * CP + cp)] = make_double2(S0, Q0);
@@ -147,10 +145,19 @@ ARGUS_DEV void bn_fin_arrive(const BnFin& f, int t, int nt, double2* scratch, in
     if (br == 1 && !dual) break;
     const double2* red = f.red + (size_t)br * f.ng * f.C;
     double S0 = 0.0, Q0 = 0.0, S1 = 0.0, Q1 = 0.0;
-#pragma unroll 4
-    for (int q = lr; q < f.ng; q += LR) {
-      const double2 a = red[(size_t)q * f.C + c], b = red[(size_t)q * f.C + c + 1];
-      S0 += a.x; Q0 += a.y; S1 += b.x; Q1 += b.y;
+    for (int qb = lr; qb < f.ng; qb += 4 * LR) {
+      double2 a[4], b[4];  // four group results in flight (clamped, masked below: common.h kLoadBatch)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const size_t q = (size_t)min(qb + u * LR, f.ng - 1);
+        a[u] = red[q * f.C + c];
+        b[u] = red[q * f.C + c + 1];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const bool ok = qb + u * LR < f.ng;
+        S0 += ok ? a[u].x : 0.0; Q0 += ok ? a[u].y : 0.0; S1 += ok ? b[u].x : 0.0; Q1 += ok ? b[u].y : 0.0;
+      }
     }
     scratch[2 * (lr * CP + cp)] = make_double2(S0, Q0);
     scratch[2 * (lr * CP + cp) + 1] = make_double2(S1, Q1);

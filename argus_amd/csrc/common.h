@@ -18,6 +18,15 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 
 namespace argus {
 
+// Loads issued together by the small cross-workgroup reductions (finalize merges, split-K sums): in a
+// plain `for (...) s += p[i]` loop the compiler waits for each load (s_waitcnt vmcnt(0)) before
+// issuing the next, so a 16-row merge paid 16 memory latencies in series (tools/isa_loopmix.py-style
+// ISA check: tests/test_isa.py::test_reductions_batch_their_loads). These loops load a batch of
+// kLoadBatch into registers (addresses clamped to a valid element), then accumulate in the same fixed
+// order as before with selects (x + 0 = x), not branches: a branch per element lets the compiler sink
+// each load into its branch and the waits come back.
+constexpr int kLoadBatch = 8;
+
 constexpr int kWave = 64;
 
 static inline __host__ __device__ int cdiv(int a, int b) { return (a + b - 1) / b; }

@@ -797,37 +797,6 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgParams p) {
     }
 }
 
-// dw[e] = sum_s part[s][e] (fixed order: deterministic). Block = CW float4-columns x SL split lanes;
-// lane l sums splits l, l+SL, ... then the SL lanes combine through LDS in lane order. For the stem
-// the padded (r8, s8, c4) columns are scattered to OHWI 7x7x3.
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int splits, int M, int N,
-                                                           int stem, int CW, float* __restrict__ dw) {
-  const int SL = 256 / CW;
-  const int col = threadIdx.x % CW, sl = threadIdx.x / CW;
-  const size_t e4 = (size_t)blockIdx.x * CW + col;
-  const size_t total4 = (size_t)M * N / 4;
-  const size_t stride = (size_t)M * N;
-  f32x4 s = {0.f, 0.f, 0.f, 0.f};
-  if (e4 < total4)
-    for (int k = sl; k < splits; k += SL) s += *reinterpret_cast<const f32x4*>(part + k * stride + e4 * 4);
-  __shared__ f32x4 red[256];
-  red[threadIdx.x] = s;
-  __syncthreads();
-  if (sl != 0 || e4 >= total4) return;
-  for (int l = 1; l < SL; ++l) s += red[l * CW + col];
-  if (!stem) {
-    *reinterpret_cast<f32x4*>(dw + e4 * 4) = s;
-  } else {
-    const size_t e = e4 * 4;
-    const int m = (int)(e / N), c = (int)(e - (size_t)m * N);
-    const int r = c >> 5, sp = (c & 31) >> 2;  // 4 consecutive cols = channels 0..3 of one (r, s)
-    if (r < 7 && sp < 7) {
-      float* o = dw + (size_t)m * 147 + (r * 7 + sp) * 3;
-      o[0] = s.x; o[1] = s.y; o[2] = s.z;
-    }
-  }
-}
-
 // ------------------------------------------------------------------------------------------------
 // layout kernels
 // ------------------------------------------------------------------------------------------------
@@ -1628,13 +1597,7 @@ static int conv_wgrad_impl(const argus_conv_desc& d, int dtype, const void* x, c
     else dispatch_wg<float>(p, pl, st);
     if (int e = check_launch("wgrad_kernel")) return e;
   }
-  const size_t total4 = (size_t)d.k * pl.N / 4;
-  int cw = 64;  // float4 columns per block: aim for >= 512 blocks, more split lanes when few columns
-  while (cw > 4 && (total4 + cw - 1) / cw < 512) cw >>= 1;
-  const int blocks = (int)((total4 + cw - 1) / cw);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, reinterpret_cast<const float*>(ws),
-                     splits, d.k, pl.N, d.stem, cw, dw);
-  return check_launch("wgrad_reduce_kernel");
+  return wgrad_reduce_launch(reinterpret_cast<const float*>(ws), splits, d.k, pl.N, d.stem, dw, st);
 }
 
 int conv_wgrad(const argus_conv_desc& d, int dtype, const void* x, const float* sc, const float* sh,

@@ -14,7 +14,10 @@ ARGUS_DEV float gelu_grad(float x) {
   return cdf + x * pdf;
 }
 
-// 64x64 output tile, 256 threads (4 waves, 2x2, each 32x32 = 2x2 MFMA blocks), K-step 16.
+// 64x64 output tile, 256 threads (4 waves, 2x2, each 32x32 = 2x2 MFMA blocks), K-tile 32. The next
+// K-tile's global loads are issued into registers before the current one's MFMAs (one exposed global
+// latency per K-tile: these GEMMs have few tiles and are latency-bound, so the split heuristic below
+// keeps every slice at <= 4 K-tiles).
 ARGUS_DEV void epilogue_store(float v, int m, int n, float* __restrict__ C, int ldc, const float* __restrict__ bias,
                                int epi, float* __restrict__ aux) {
   float* dst = C + (size_t)m * ldc + n;
@@ -27,6 +30,15 @@ ARGUS_DEV void epilogue_store(float v, int m, int n, float* __restrict__ C, int 
   }
 }
 
+constexpr int kGemmKT = 32;
+
+// element e (0..7) of this thread's share of a 64 x 32 operand tile: (row 0..63, k 0..31); `t` = the
+// operand is stored [k][row] (k-major: consecutive threads walk rows) instead of [row][k]
+ARGUS_DEV void gemm_tile_pos(int tid, int e, int t, int& row, int& kk) {
+  const int idx = tid + 256 * e;
+  if (t) { kk = idx >> 6; row = idx & 63; } else { row = idx >> 5; kk = idx & 31; }
+}
+
 // split-K slice z covers k in [z*kc, min(K, (z+1)*kc)); with splits > 1 the raw partial tile goes to
 // ws[z][M][N] and gemm_reduce_kernel applies the epilogue after a fixed-order sum.
 __global__ __launch_bounds__(256) void gemm_f32_kernel(int M, int N, int K, const float* __restrict__ A, int lda,
@@ -34,8 +46,8 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(int M, int N, int K, cons
                                                        float* __restrict__ C, int ldc, const float* __restrict__ bias,
                                                        int epi, float* __restrict__ aux, int kc,
                                                        float* __restrict__ ws) {
-  __shared__ float As[16][65];  // [k][m]
-  __shared__ float Bs[16][65];  // [k][n]
+  __shared__ float As[kGemmKT][65];  // [k][m]
+  __shared__ float Bs[kGemmKT][65];  // [k][n]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
@@ -45,27 +57,34 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(int M, int N, int K, cons
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int kbeg = blockIdx.z * kc, kend = min(K, kbeg + kc);
-  for (int k0 = kbeg; k0 < kend; k0 += 16) {
-    // stage 16 x 64 of A (as [k][m]) and B (as [k][n]): 1024 elements each, 4 per thread
+  float ra[8], rb[8];
+  auto load = [&](int k0) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int idx = tid + 256 * e;
-      int kk, mm;
-      if (ta) { kk = idx >> 6; mm = idx & 63; } else { mm = idx >> 4; kk = idx & 15; }
+    for (int e = 0; e < 8; ++e) {
+      int mm, kk;
+      gemm_tile_pos(tid, e, ta, mm, kk);
       const int gm = m0 + mm, gk = k0 + kk;
-      float v = 0.f;
-      if (gm < M && gk < kend) v = ta ? A[(size_t)gk * lda + gm] : A[(size_t)gm * lda + gk];
-      As[kk][mm] = v;
-      int kb, nn;
-      if (tb) { nn = idx >> 4; kb = idx & 15; } else { kb = idx >> 6; nn = idx & 63; }
+      ra[e] = (gm < M && gk < kend) ? (ta ? A[(size_t)gk * lda + gm] : A[(size_t)gm * lda + gk]) : 0.f;
+      int nn, kb;
+      gemm_tile_pos(tid, e, tb ? 0 : 1, nn, kb);
       const int gn = n0 + nn, gk2 = k0 + kb;
-      float w = 0.f;
-      if (gn < N && gk2 < kend) w = tb ? B[(size_t)gn * ldb + gk2] : B[(size_t)gk2 * ldb + gn];
-      Bs[kb][nn] = w;
+      rb[e] = (gn < N && gk2 < kend) ? (tb ? B[(size_t)gn * ldb + gk2] : B[(size_t)gk2 * ldb + gn]) : 0.f;
+    }
+  };
+  if (kbeg < kend) load(kbeg);
+  for (int k0 = kbeg; k0 < kend; k0 += kGemmKT) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      int mm, kk, nn, kb;
+      gemm_tile_pos(tid, e, ta, mm, kk);
+      gemm_tile_pos(tid, e, tb ? 0 : 1, nn, kb);
+      As[kk][mm] = ra[e];
+      Bs[kb][nn] = rb[e];
     }
     __syncthreads();
+    if (k0 + kGemmKT < kend) load(k0 + kGemmKT);  // in flight during this tile's MFMAs
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < kGemmKT / 4; ++s) {
       const int kk = 4 * s + (lane >> 4);
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
@@ -100,7 +119,13 @@ __global__ __launch_bounds__(256) void gemm_reduce_kernel(int M, int N, int spli
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= (int64_t)M * N) return;
   float v = 0.f;
-  for (int z = 0; z < splits; ++z) v += ws[(size_t)z * M * N + e];
+  for (int zb = 0; zb < splits; zb += kLoadBatch) {
+    float t[kLoadBatch];  // in flight together (common.h kLoadBatch); clamped, masked below
+#pragma unroll
+    for (int u = 0; u < kLoadBatch; ++u) t[u] = ws[(size_t)min(zb + u, splits - 1) * M * N + e];
+#pragma unroll
+    for (int u = 0; u < kLoadBatch; ++u) v += zb + u < splits ? t[u] : 0.f;
+  }
   const int m = (int)(e / N), n = (int)(e - (int64_t)m * N);
   epilogue_store(v, m, n, C, ldc, bias, epi, aux);
 }
@@ -109,7 +134,13 @@ __global__ void colsum_kernel(int M, int N, const float* __restrict__ x, int ld,
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
   float s = 0.f;
-  for (int m = 0; m < M; ++m) s += x[(size_t)m * ld + n];
+  for (int mb = 0; mb < M; mb += kLoadBatch) {
+    float t[kLoadBatch];
+#pragma unroll
+    for (int u = 0; u < kLoadBatch; ++u) t[u] = x[(size_t)min(mb + u, M - 1) * ld + n];
+#pragma unroll
+    for (int u = 0; u < kLoadBatch; ++u) s += mb + u < M ? t[u] : 0.f;
+  }
   out[n] = s;
 }
 
@@ -128,10 +159,16 @@ using namespace argus;
 
 extern "C" {
 
-size_t argus_gemm_f32_workspace_bytes(int m, int n, int k) {
+// split-K slices: up to 512 workgroups, each slice >= 128 of K (<= 4 K-tiles once K allows)
+static int gemm_splits(int m, int n, int k) {
   const int tiles = ((m + 63) / 64) * ((n + 63) / 64);
   int splits = 1;
-  while (tiles * splits < 256 && k / (splits * 2) >= 128) splits *= 2;
+  while (tiles * splits < 512 && k / (splits * 2) >= 128) splits *= 2;
+  return splits;
+}
+
+size_t argus_gemm_f32_workspace_bytes(int m, int n, int k) {
+  const int splits = gemm_splits(m, n, k);
   return splits > 1 ? (size_t)splits * m * n * sizeof(float) : 0;
 }
 
@@ -142,11 +179,9 @@ int argus_gemm_f32(int m, int n, int k, const float* a, int lda, int ta, const f
     set_error("gemm_f32: bad arguments");
     return ARGUS_ERR_ARG;
   }
-  const int tiles = ((m + 63) / 64) * ((n + 63) / 64);
-  int splits = 1;
-  while (tiles * splits < 256 && k / (splits * 2) >= 128) splits *= 2;
+  int splits = gemm_splits(m, n, k);
   if (splits > 1 && (!ws || ws_bytes < (size_t)splits * m * n * sizeof(float))) splits = 1;  // no workspace
-  const int kc = ((k + splits - 1) / splits + 15) / 16 * 16;
+  const int kc = ((k + splits - 1) / splits + kGemmKT - 1) / kGemmKT * kGemmKT;
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((n + 63) / 64, (m + 63) / 64, splits);
   hipLaunchKernelGGL(gemm_f32_kernel, grid, dim3(256), 0, st, m, n, k, a, lda, ta, b, ldb, tb, c, ldc, bias, epi, aux,

@@ -275,6 +275,10 @@ ARGUS_DEV u32x4 sel(bool ok, u32x4 v) {
 }
 
 
+// dW = fixed-order sum of the fp32 split partials [splits][M][N] (reduce.hip); the stem's padded
+// (r8, s8, c4) columns are scattered to OHWI 7x7x3
+int wgrad_reduce_launch(const float* part, int splits, int M, int N, int stem, float* dw, hipStream_t st);
+
 // forward / dgrad launchers of the glds kernel (conv_glds.hip); return false when the shape is not
 // served by it (then conv.hip's kernel runs). _ok: the same choice without launching.
 bool igemm_glds_ok(const IgParams& p, int maxM, int maxK);

@@ -137,6 +137,9 @@ class ResNetEngine:
         self.tail_main = True
         self._tail: list = []
         self.dy_ring = 12  # dy ring buffers (set before the first forward)
+        # HIP priority of the side stream (torch convention: lower = higher priority; 0 = the main
+        # stream's); set before the first backward
+        self.side_priority = 0
         # (the schedule switches above are attributes, not environment variables: tools/engine_ab.py
         # A/B-measures them; test_gpu_train.py runs the overlap / tail placements against each other)
 
@@ -787,7 +790,7 @@ class ResNetEngine:
         side-stream event that marks their completion."""
         main = torch.cuda.current_stream()
         if self._side is None:
-            self._side = torch.cuda.Stream(device=self.device)
+            self._side = torch.cuda.Stream(device=self.device, priority=self.side_priority)
         ready = torch.cuda.Event()
         ready.record(main)
         self._side.wait_event(ready)

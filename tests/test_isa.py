@@ -113,3 +113,88 @@ def test_inline_asm_lds_reads_are_waited_for(tmp_path, src):
     assert n_reads > 0, "no transposed LDS reads found: the check would be vacuous"
     bad = check_asm_lds_reads(asm)
     assert not bad, "\n".join(f"{f}:{ln}: {ins}  (registers {regs})" for f, ln, ins, regs in bad[:20])
+
+
+# ---- batched loads in the small cross-workgroup reductions (common.h kLoadBatch) ------------------
+# kernel (mangled-name fragment) -> source; each is a reduction over a runtime-length loop of loads
+REDUCTIONS = {
+    "stats_finalize_kernel": "bn.hip",
+    "bwd_finalize_kernel": "bn.hip",
+    "wgrad_reduce_kernel": "reduce.hip",
+    "gemm_reduce_kernel": "head.hip",
+    "colsum_kernel": "head.hip",
+    # the folded BN-backward finalize's group merges (bnfin.h) inside a BN-epilogue dgrad
+    "igemm_glds_kernelILi256ELi128ELi2E": "conv_glds.hip",
+}
+
+
+def _function_bodies(asm):
+    """name -> instruction lines; a loop header label keeps the compiler's "Loop Header" marker as a
+    trailing " LOOP" (the compiler's own loop analysis, not a guess from branch directions)."""
+    fns, cur = {}, None
+    for raw in asm.splitlines():
+        s = raw.split(";")[0].rstrip()
+        if s and not raw.startswith((" ", "\t")) and s.endswith(":") and not s.startswith("."):
+            cur = fns.setdefault(s[:-1], [])
+            continue
+        if cur is not None and s.strip():
+            cur.append(s.strip() + (" LOOP" if "Loop Header" in raw else ""))
+    return fns
+
+
+def loop_load_runs(body):
+    """For each loop (a "Loop Header" label .. the last backward branch to it) holding global loads: the
+    most loads a trip has in flight at once (each load adds one, s_waitcnt vmcnt(N) leaves N)."""
+    labels = {s[:-6]: i for i, s in enumerate(body) if s.endswith(": LOOP")}
+    ends = {}
+    for i, s in enumerate(body):
+        m = re.match(r"s_(?:cbranch_\w+|branch)\s+(\.L\w+)", s)
+        if m and m.group(1) in labels and labels[m.group(1)] < i:
+            ends[m.group(1)] = i
+    runs = []
+    for lab, i in ends.items():
+        seg = body[labels[lab]:i + 1]
+        out = most = 0  # loads outstanding (vmcnt(N) leaves at most N), and their maximum in a trip
+        for ins in seg:
+            if ins.startswith(("global_load", "buffer_load")):
+                out += 1
+                most = max(most, out)
+            else:
+                w = re.match(r"s_waitcnt\b.*vmcnt\((\d+)\)", ins)
+                if w:
+                    out = min(out, int(w.group(1)))
+        if any(ins.startswith(("global_load", "buffer_load")) for ins in seg):
+            runs.append(most)
+    return runs
+
+
+def test_loop_load_runs_self_test():
+    serial = ["x:", ".LBB0_1: LOOP", "global_load_dwordx2 v[0:1], v[2:3], off", "s_waitcnt vmcnt(0)",
+              "v_add_f64 v[4:5], v[4:5], v[0:1]", "s_cbranch_scc1 .LBB0_1"]
+    batched = ["x:", ".LBB0_1: LOOP"] + [f"global_load_dwordx2 v[{2*i}:{2*i+1}], v[20:21], off" for i in range(8)] + \
+        ["s_waitcnt vmcnt(7)", "s_waitcnt vmcnt(0)", "s_cbranch_scc1 .LBB0_1"]
+    assert loop_load_runs(serial) == [1]
+    assert loop_load_runs(batched) == [8]
+
+
+@pytest.mark.parametrize("src", sorted(set(REDUCTIONS.values())))
+def test_reductions_batch_their_loads(tmp_path, src):
+    """Every load loop of these reduction kernels keeps >= 4 loads in flight per trip (a plain
+    accumulate loop compiles to load / s_waitcnt vmcnt(0) / add per element: one memory latency each)."""
+    from argus_amd.build import CSRC, FLAGS, HIPCC
+
+    out = tmp_path / (src + ".s")
+    cmd = [HIPCC, *[f for f in FLAGS if f != "-fPIC"], "--cuda-device-only", "-S", str(CSRC / src), "-o", str(out)]
+    r = subprocess.run(cmd, capture_output=True, text=True, cwd=tmp_path)
+    assert r.returncode == 0, r.stderr[-2000:]
+    fns = _function_bodies(out.read_text())
+    for frag, s in REDUCTIONS.items():
+        if s != src:
+            continue
+        hits = [name for name in fns if frag in name]
+        assert hits, f"{frag} not found in {src}"
+        for name in hits:
+            runs = loop_load_runs(fns[name])
+            assert runs, f"{name}: no load loop found (the check would be vacuous)"
+            # the glds kernel's main loop (LDS DMA) is not a global_load loop; its bnfin merges are
+            assert max(runs) >= 4 and all(n >= 4 for n in runs if n), f"{name}: loads in flight per loop trip {runs}"

@@ -1,7 +1,10 @@
 """A/B of engine schedule attributes on full bf16 train steps (dev tool, GPU): configurations run
 interleaved (A B A B ...) on one box so drift between them cancels.
 
-    python tools/engine_ab.py --batch 64 --cfg "" --cfg "a2_min_px=100000" [--rounds 3 --steps 20]
+    python tools/engine_ab.py --batch 64 --cfg "" --cfg "side_priority=-1" --cfg "tune:6=256" [--rounds 3]
+
+Model instances differ by about 1 % on their own (allocation placement): repeat a configuration
+(e.g. defaults first and last) to see that spread.
 """
 import argparse
 import sys
@@ -29,12 +32,19 @@ def main():
     images, targets = synthetic_batch(a.batch, *a.hw, 1000, dev)
     runs = []
     for cfg in a.cfg or [""]:
-        torch.manual_seed(42)
-        m = NCameraCNN(compute_dtype=a.dtype).to(dev).train()
-        eng = m._engine(dev)
+        tune, attrs = {}, {}
         for kv in filter(None, cfg.split(",")):
             k, v = kv.split("=")
-            setattr(eng, k, type(getattr(eng, k))(int(v)) if not isinstance(getattr(eng, k), bool) else v == "1")
+            if k.startswith("tune:"):  # a kernel-selection policy override (argus_conv_policy_default key)
+                tune[int(k[5:])] = int(v)
+            else:
+                attrs[k] = v
+        torch.manual_seed(42)
+        m = NCameraCNN(compute_dtype=a.dtype, kernel_tuning=tune or None).to(dev).train()
+        eng = m._engine(dev)
+        for k, v in attrs.items():
+            cur = getattr(eng, k)
+            setattr(eng, k, v == "1" if isinstance(cur, bool) else type(cur)(int(v)))
         tr = FusedTrainer(m, lr=1e-4, max_grad_norm=1.0)
         for _ in range(3):
             tr.step(images, targets)
