@@ -63,18 +63,24 @@ ARGUS_DEV bool ticket_last(unsigned* cnt_, int G, int* flag) {
   return *flag != 0;
 }
 
-// fixed-order sum over the G group results of this block's 64 channels: 4 row lanes, then lanes 0..3
+// fixed-order sum over the G group results of this block's 64 channels: kFinLanes row lanes, then the lanes in order
+// Finalize blocks: 64 channels x kFinLanes row lanes. 16 lanes (1024 threads: one batch of loads per
+// lane per level) measured slower in the step, 0.42 -> 0.57 ms/step of finalize (profiles/
+// r04p_timeline.txt): a 16-wave workgroup waits for a CU with 16 free wave slots while the side
+// stream's weight gradients hold them (one launch took 68 us).
+constexpr int kFinLanes = 4;
+
 ARGUS_DEV double2 merge_groups(const double2* red, int G, int C, int c, double2 (*lds)[64]) {
   const int lane_r = threadIdx.x >> 6, cl = threadIdx.x & 63;
   double S = 0.0, Q = 0.0;
   if (c < C)
-    for (int gb = lane_r; gb < G; gb += 4 * 4) {
+    for (int gb = lane_r; gb < G; gb += kFinLanes * 4) {
       double2 v[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = red[(size_t)min(gb + 4 * u, G - 1) * C + c];
+      for (int u = 0; u < 4; ++u) v[u] = red[(size_t)min(gb + kFinLanes * u, G - 1) * C + c];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const bool ok = gb + 4 * u < G;
+        const bool ok = gb + kFinLanes * u < G;
         S += ok ? v[u].x : 0.0;
         Q += ok ? v[u].y : 0.0;
       }
@@ -82,7 +88,7 @@ ARGUS_DEV double2 merge_groups(const double2* red, int G, int C, int c, double2 
   lds[lane_r][cl] = make_double2(S, Q);
   __syncthreads();
   double2 a = lds[0][cl];
-  for (int i = 1; i < 4; ++i) { a.x += lds[i][cl].x; a.y += lds[i][cl].y; }
+  for (int i = 1; i < kFinLanes; ++i) { a.x += lds[i][cl].x; a.y += lds[i][cl].y; }
   return a;
 }
 
@@ -99,7 +105,7 @@ struct BnFinArgs {
   float *mean_o, *invstd_o, *scale_o, *shift_o;
 };
 
-__global__ __launch_bounds__(256) void stats_finalize_kernel(const BnFinArgs a) {
+__global__ __launch_bounds__(64 * kFinLanes) void stats_finalize_kernel(const BnFinArgs a) {
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int lane_r = threadIdx.x >> 6;
   const int g = blockIdx.y;
@@ -110,13 +116,13 @@ __global__ __launch_bounds__(256) void stats_finalize_kernel(const BnFinArgs a) 
   const double inv_full = 1.0 / (double)tr;
   double S = 0.0, Q = 0.0;
   if (c < a.C)
-    for (int rb = r0 + lane_r; rb < r1; rb += 4 * kLoadBatch) {
+    for (int rb = r0 + lane_r; rb < r1; rb += kFinLanes * kLoadBatch) {
       float2 v[kLoadBatch];  // the batch's loads in flight together (clamped rows, masked below)
 #pragma unroll
-      for (int u = 0; u < kLoadBatch; ++u) v[u] = a.part[(size_t)min(rb + 4 * u, r1 - 1) * a.C + c];
+      for (int u = 0; u < kLoadBatch; ++u) v[u] = a.part[(size_t)min(rb + kFinLanes * u, r1 - 1) * a.C + c];
 #pragma unroll
       for (int u = 0; u < kLoadBatch; ++u) {
-        const int r = rb + 4 * u;
+        const int r = rb + kFinLanes * u;
         const int64_t left = a.count - (int64_t)r * tr;
         const double inv = (a.tile_rows < 0 || left >= tr) ? inv_full : 1.0 / (double)left;
         const bool ok = r < r1;  // selects, not branches: a branch lets the compiler sink the loads
@@ -124,13 +130,13 @@ __global__ __launch_bounds__(256) void stats_finalize_kernel(const BnFinArgs a) 
         Q += ok ? (double)v[u].y + (double)v[u].x * (double)v[u].x * inv : 0.0;
       }
     }
-  __shared__ double2 red[4][64];
+  __shared__ double2 red[kFinLanes][64];
   __shared__ int flag;
   red[lane_r][threadIdx.x & 63] = make_double2(S, Q);
   __syncthreads();
   if (lane_r == 0 && c < a.C) {
     double2 t = red[0][threadIdx.x];
-    for (int i = 1; i < 4; ++i) { t.x += red[i][threadIdx.x].x; t.y += red[i][threadIdx.x].y; }
+    for (int i = 1; i < kFinLanes; ++i) { t.x += red[i][threadIdx.x].x; t.y += red[i][threadIdx.x].y; }
     store_wt(a.red + (size_t)g * a.C + c, t);
   }
   if (!ticket_last(a.cnt + blockIdx.x, a.G, &flag)) return;
@@ -375,31 +381,31 @@ struct BnBwdFinArgs {
 };
 
 // backward column sums + dgamma/dbeta/coefficients in one launch (same ticket hand-off)
-__global__ __launch_bounds__(256) void bwd_finalize_kernel(const BnBwdFinArgs a) {
+__global__ __launch_bounds__(64 * kFinLanes) void bwd_finalize_kernel(const BnBwdFinArgs a) {
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int lane_r = threadIdx.x >> 6;
   const int g = blockIdx.y;
   const int r0 = g * a.rpg, r1 = min(a.rows, r0 + a.rpg);
   double s = 0.0, q = 0.0;
   if (c < a.C)
-    for (int rb = r0 + lane_r; rb < r1; rb += 4 * kLoadBatch) {
+    for (int rb = r0 + lane_r; rb < r1; rb += kFinLanes * kLoadBatch) {
       float2 v[kLoadBatch];
 #pragma unroll
-      for (int u = 0; u < kLoadBatch; ++u) v[u] = a.part[(size_t)min(rb + 4 * u, r1 - 1) * a.C + c];
+      for (int u = 0; u < kLoadBatch; ++u) v[u] = a.part[(size_t)min(rb + kFinLanes * u, r1 - 1) * a.C + c];
 #pragma unroll
       for (int u = 0; u < kLoadBatch; ++u) {
-        const bool ok = rb + 4 * u < r1;
+        const bool ok = rb + kFinLanes * u < r1;
         s += ok ? (double)v[u].x : 0.0;
         q += ok ? (double)v[u].y : 0.0;
       }
     }
-  __shared__ double2 red[4][64];
+  __shared__ double2 red[kFinLanes][64];
   __shared__ int flag;
   red[lane_r][threadIdx.x & 63] = make_double2(s, q);
   __syncthreads();
   if (lane_r == 0 && c < a.C) {
     double2 t = red[0][threadIdx.x];
-    for (int i = 1; i < 4; ++i) { t.x += red[i][threadIdx.x].x; t.y += red[i][threadIdx.x].y; }
+    for (int i = 1; i < kFinLanes; ++i) { t.x += red[i][threadIdx.x].x; t.y += red[i][threadIdx.x].y; }
     store_wt(a.red + (size_t)g * a.C + c, t);
   }
   if (!ticket_last(a.cnt + blockIdx.x, a.G, &flag)) return;
@@ -715,7 +721,7 @@ int argus_bn_finalize(int C, int rows, int tile_rows, const float* part, int64_t
   a.red = reinterpret_cast<double2*>(reinterpret_cast<char*>(ws) + kBnCounterBytes);
   a.gamma = gamma; a.beta = beta; a.eps = eps; a.momentum = momentum; a.running_mean = rm; a.running_var = rv;
   a.nbt = nbt; a.mean_o = mean; a.invstd_o = invstd; a.scale_o = scale; a.shift_o = shift;
-  hipLaunchKernelGGL(stats_finalize_kernel, dim3((C + 63) / 64, a.G), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(stats_finalize_kernel, dim3((C + 63) / 64, a.G), dim3(64 * kFinLanes), 0, st, a);
   return check_launch("stats_finalize_kernel");
 }
 
@@ -810,7 +816,7 @@ int argus_bn_bwd_finalize(int C, int rows, const float* part, int64_t count, con
   a.cnt = reinterpret_cast<unsigned*>(ws);
   a.red = reinterpret_cast<double2*>(reinterpret_cast<char*>(ws) + kBnCounterBytes);
   a.gamma = gamma; a.mean = mean; a.invstd = invstd; a.dgamma = dgamma; a.dbeta = dbeta; a.ca = ca; a.cb = cb; a.cc = cc;
-  hipLaunchKernelGGL(bwd_finalize_kernel, dim3((C + 63) / 64, a.G), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(bwd_finalize_kernel, dim3((C + 63) / 64, a.G), dim3(64 * kFinLanes), 0, st, a);
   return check_launch("bwd_finalize_kernel");
 }
 
