@@ -1110,6 +1110,12 @@ static const Policy kDefaultPolicy = [] {
   p.v[kFwdBm128Rows] = 16 * 1024;
   p.v[kGldsMinRows] = 4 * 256;
   p.v[kFp8Passes] = 2;
+  // 38: a 1x1 dgrad with an apply prologue (dy = ca*dm + cb*y + cc) on the glds kernel after the
+  //     apply kernel materialises dy (0), rather than staging the apply in the register-staged kernel
+  //     (1): 1 saves the dy round trip but the register-staged kernel is slower at K >= 1024;
+  //     engine A/B 14.73-14.96 vs 14.76-14.88 ms (B=64), 51.5 vs 51.6 (B=256), 99.6 vs 100.2-100.6
+  //     (376x672 B=128): profiles/r04_ab_key38.txt
+  p.v[kDgradApStaged] = 0;
   return p;
 }();
 
@@ -1372,6 +1378,7 @@ static bool dgrad_stages_prologue(const argus_conv_desc& d, int dtype, IgParams&
     maxM = p.ph[i].M > maxM ? p.ph[i].M : maxM;
     maxK = p.ph[i].K > maxK ? p.ph[i].K : maxK;
   }
+  if ((*p.pol)[kDgradApStaged]) return true;  // the glds kernel is not used: no dy to materialise
   return !(dtype == ARGUS_BF16 && (conv3x3_halo_ok(p) || igemm_glds_ok(p, maxM, maxK)));
 }
 

@@ -39,7 +39,8 @@ enum TuneKey : int {
   kFwdBm128Rows = 35,   // fewest forward GEMM rows for 128-row tiles
   kGldsMinRows = 36,    // fewest GEMM rows (largest phase) for the glds kernel
   kFp8Passes = 37,      // ARGUS_FP8: which passes take MX-fp8 operands (1 fwd | 2 dgrad | 4 dgrad with apply)
-  kNumTuneKeys = 38
+  kDgradApStaged = 38,  // 1x1 dgrad with an apply prologue: register-staged (1) or apply kernel + glds (0)
+  kNumTuneKeys = 39
 };
 struct Policy {
   int v[kNumTuneKeys];
