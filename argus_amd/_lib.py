@@ -18,7 +18,7 @@ import torch  # noqa: F401  (must precede the CDLL, see module docstring)
 LIB_PATH = Path(os.environ.get("ARGUS_HIP_LIB", Path(__file__).resolve().parent / "libargus_hip.so"))
 
 F32, BF16, FP8 = 0, 1, 2
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 
 class Tuning(C.Structure):
@@ -96,6 +96,11 @@ SIGNATURES = {
     "argus_conv_wgrad_workspace_bytes": (_SZ, [_DESC, _I]),
     "argus_conv_wgrad": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     "argus_conv_wgrad_apply": (_I, [_DESC, _I, _P, _P, C.POINTER(BnBwdPrologue), _P, _P, _SZ, _P]),
+    "argus_conv_dgrad_wgrad_ok": (_I, [_DESC, _I]),
+    "argus_conv_dgrad_wgrad_workspace_bytes": (_SZ, [_DESC, _I]),
+    "argus_conv_dgrad_wgrad_bn_rows": (_I, [_DESC, _I]),
+    "argus_conv_dgrad_wgrad_bn": (_I, [_DESC, _I, _P, _P, _P, _P, C.POINTER(BnBwdEpilogue), C.POINTER(BnBwdPrologue),
+                                       _P, _P, _SZ, _P]),
     "argus_ktimer_enable": (_I, [C.c_char_p]),
     "argus_ktimer_enable_on": (_I, [C.c_char_p, _P]),
     "argus_ktimer_disable": (_I, []),

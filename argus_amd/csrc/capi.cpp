@@ -27,7 +27,7 @@ using namespace argus;
 
 extern "C" {
 
-int argus_abi_version(void) { return 11; }
+int argus_abi_version(void) { return 12; }
 
 const char* argus_last_error(void) { return g_last_error.c_str(); }
 
@@ -102,6 +102,26 @@ int argus_conv_wgrad_apply(const argus_conv_desc* d, int dtype, const void* x, c
                            const argus_bn_bwd_prologue* ap, float* dw, void* ws, size_t ws_bytes, argus_stream_t stream) {
   if (!d || !x || !dm || !ap || !dw || !ws) { set_error("conv_wgrad_apply: bad arguments"); return ARGUS_ERR_ARG; }
   return conv_wgrad_apply(*d, dtype, x, dm, *ap, dw, ws, ws_bytes, (hipStream_t)stream);
+}
+
+int argus_conv_dgrad_wgrad_ok(const argus_conv_desc* d, int dtype) {
+  return d && !conv_check_desc(*d) && conv_dgw_ok(*d, dtype) ? 1 : 0;
+}
+
+size_t argus_conv_dgrad_wgrad_workspace_bytes(const argus_conv_desc* d, int dtype) {
+  return d && !conv_check_desc(*d) ? conv_dgw_ws_bytes(*d, dtype) : 0;
+}
+
+int argus_conv_dgrad_wgrad_bn_rows(const argus_conv_desc* d, int dtype) {
+  return d && !conv_check_desc(*d) ? conv_dgw_rows(*d, dtype) : -1;
+}
+
+int argus_conv_dgrad_wgrad_bn(const argus_conv_desc* d, int dtype, const void* dm, const void* w_dgrad,
+                              const void* x, void* dx, const argus_bn_bwd_epilogue* bn,
+                              const argus_bn_bwd_prologue* pro, float* dw, void* workspace,
+                              size_t workspace_bytes, argus_stream_t stream) {
+  if (!d) { set_error("conv_dgrad_wgrad_bn: bad arguments"); return ARGUS_ERR_ARG; }
+  return conv_dgw(*d, dtype, dm, w_dgrad, x, dx, bn, pro, dw, workspace, workspace_bytes, (hipStream_t)stream);
 }
 
 size_t argus_conv_wgrad_workspace_bytes(const argus_conv_desc* d, int dtype) { return d ? conv_wgrad_ws(*d, dtype) : 0; }

@@ -997,6 +997,9 @@ __global__ __launch_bounds__(256) void weight_prep_one_f8_kernel(const WpEntry e
 // host launchers
 // ------------------------------------------------------------------------------------------------
 
+static int check_desc(const argus_conv_desc& d);
+int conv_check_desc(const argus_conv_desc& d) { return check_desc(d); }
+
 static int check_desc(const argus_conv_desc& d) {
   if (int e = check_tuning(d)) return e;
   if (d.n <= 0 || d.h <= 0 || d.w <= 0 || d.k <= 0 || d.r <= 0 || d.s <= 0 || d.stride <= 0) {

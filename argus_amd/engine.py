@@ -140,6 +140,10 @@ class ResNetEngine:
         # HIP priority of the side stream (torch convention: lower = higher priority; 0 = the main
         # stream's); set before the first backward
         self.side_priority = 0
+        # layer-1 conv3: data and weight gradient in one pass over dm3 / y3 on the main stream
+        # (argus_conv_dgrad_wgrad_bn) instead of the dgrad + the side stream's wgrad_apply, which read
+        # both 256-channel tensors again; set before the first forward
+        self.fuse_dgw = True
         # (the schedule switches above are attributes, not environment variables: tools/engine_ab.py
         # A/B-measures them; test_gpu_train.py runs the overlap / tail placements against each other)
 
@@ -244,6 +248,15 @@ class ResNetEngine:
         for cv in convs.values():  # BN-backward partials written by dgrad epilogues (rows x C_in)
             if not cv.desc.stem:
                 max_bwd = max(max_bwd, L.dll.argus_conv_dgrad_bn_rows(C.byref(cv.desc), self.cdt) * cv.desc.c)
+        # convs whose data and weight gradient run fused (argus_conv_dgrad_wgrad_bn)
+        self.dgw = {n for n, cv in convs.items() if self.fuse_dgw and n.endswith(".conv3") and not cv.desc.stem
+                    and L.dll.argus_conv_dgrad_wgrad_ok(C.byref(cv.desc), self.cdt)}
+        dgws = 16
+        for n in self.dgw:
+            d_ = C.byref(convs[n].desc)
+            max_bwd = max(max_bwd, L.dll.argus_conv_dgrad_wgrad_bn_rows(d_, self.cdt) * convs[n].desc.c)
+            dgws = max(dgws, L.dll.argus_conv_dgrad_wgrad_workspace_bytes(d_, self.cdt))
+        self.dgw_ws = torch.empty(dgws, dtype=torch.uint8, device=self.device)  # main stream only
         self.bwd_part = self._f(max_bwd * 2)
         self.bwd_part2 = self._f(max_bwd * 2)  # second branch (downsample BN) of a dual reduce
         ws = max(L.dll.argus_conv_wgrad_workspace_bytes(C.byref(cv.desc), dt) for cv in convs.values())
@@ -534,13 +547,22 @@ class ResNetEngine:
                     self._bn_apply_bwd(pf + ".bn3", px_o, b.cout, dh, a["y3"], dy3,
                                        (pf + ".downsample.1", a["yd"], dyd) if b.has_ds else None)
             # conv3 -> bn2
-            r2 = self._dgrad_bn(pf + ".conv3", dh if pro3 else dy3, dza, None, pf + ".bn2", a["y2"], 2, P=P, G=G,
-                                pro=pro3)
+            dgw = wg3_apply and self.fold_fin and pf + ".conv3" in self.dgw
+            if dgw:  # data + weight gradient in one pass (dW on the main stream)
+                r2 = self._dgrad_wgrad_bn(pf + ".conv3", dh, dza, pf + ".bn2", a["y2"], pf + ".bn3", a["y3"], a["a2"],
+                                          P, G)
+                if dy3 is not None:  # debug capture only: the fused kernel never stores dy3
+                    self._bn_apply_bwd(pf + ".bn3", px_o, b.cout, dh, a["y3"], dy3)
+            else:
+                r2 = self._dgrad_bn(pf + ".conv3", dh if pro3 else dy3, dza, None, pf + ".bn2", a["y2"], 2, P=P, G=G,
+                                    pro=pro3)
             if dy3 is not None:
                 cap("b_dy3", dy3, px_o * b.cout, (N, ho, wo, b.cout))
             cap("b_dz2", dza, px_o * b.width, (N, ho, wo, b.width))
             s2 = self.bn_state[pf + ".bn2"]
-            if wg3_apply:  # dh holds dm3 (read by the side stream until its event: dh is not reused)
+            if dgw:
+                pass
+            elif wg3_apply:  # dh holds dm3 (read by the side stream until its event: dh is not reused)
                 self._wgrad_apply(pf + ".conv3", a["a2"], dh, pf + ".bn3", a["y3"], G)
             elif a["a2"] is not None:
                 self._wgrad(pf + ".conv3", a["a2"], None, dy3, G)
@@ -682,6 +704,25 @@ class ResNetEngine:
         self._launch(cv, 1, lambda: self.L.conv_dgrad_bn(C.byref(cv.desc), self.cdt, ptr(dy), ptr(cv.wd), ptr(dm),
                                                           ptr(addend), C.byref(e), pp, stream()))
         return 0 if self.fold_fin else self.L.dll.argus_conv_dgrad_bn_rows(C.byref(cv.desc), self.cdt)
+
+    def _dgrad_wgrad_bn(self, conv, dm, dx, bn, y, pbn, py, x, P, G):
+        """Fused data + weight gradient of ``conv`` (argus_conv_dgrad_wgrad_bn): dy = the apply of BN
+        ``pbn`` (input ``py``) staged from ``dm``, dx = the masked input gradient of BN ``bn`` (input ``y``,
+        mask mode 2, finalize folded), dW from ``x``; returns 0 (nothing left to finalize)."""
+        cv = self.convs[conv]
+        st, cf, pc = self.bn_state[bn], self.bn_coef[bn], self.bn_coef[pbn]
+        e = BnBwdEpilogue()
+        e.workspace, e.gamma, e.dgamma, e.dbeta = ptr(self.bn_ws), ptr(P[bn + ".weight"]), ptr(G[bn + ".weight"]), \
+            ptr(G[bn + ".bias"])
+        e.ca, e.cb, e.cc = ptr(cf[0]), ptr(cf[1]), ptr(cf[2])
+        e.y, e.mean, e.invstd, e.mask_mode, e.scale, e.shift = ptr(y), ptr(st[0]), ptr(st[1]), 2, ptr(st[2]), ptr(st[3])
+        e.part = ptr(self.bwd_part)
+        pro = BnBwdPrologue(ptr(py), ptr(pc[0]), ptr(pc[1]), ptr(pc[2]), None)
+        self._guard(dx)
+        self._launch(cv, 1, lambda: self.L.conv_dgrad_wgrad_bn(
+            C.byref(cv.desc), self.cdt, ptr(dm), ptr(cv.wd), ptr(x), ptr(dx), C.byref(e), C.byref(pro),
+            ptr(G[conv + ".weight"]), ptr(self.dgw_ws), self.dgw_ws.numel(), stream()))
+        return 0
 
     def _prologue(self, pro):
         """argus_bn_bwd_prologue for ``pro`` = (bn name, y, dy_out): the dgrad stages dy = ca*dm + cb*y + cc

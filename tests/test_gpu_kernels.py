@@ -1308,3 +1308,70 @@ def _check_fp8_weight_layout(buf, w_fp32, cols):
     assert ((deq - wb).abs() <= wb.abs() * 2.0 ** -4 + scale * 2.0 ** -10).all()
     same = (vals == (wb / scale).float().to(torch.float8_e4m3fn).float()).double().mean().item()
     assert same > 0.999, same  # round-to-nearest-even ties may differ
+
+
+def test_fused_dgrad_wgrad_matches_separate_passes(cuda):
+    """argus_conv_dgrad_wgrad_bn (layer-1 conv3: one pass over dm3 / y3 for both gradients) against
+    argus_conv_dgrad_bn (apply prologue, mask-mode-2 epilogue) + argus_conv_wgrad_apply: dx bitwise
+    (same staged dy and the same MFMA k order), the folded bn2 finalize outputs and dW to fp32 / fp64
+    summation order (1e-5 relative), dW also against an fp64 torch weight gradient of the staged dy;
+    ragged row counts (P not a multiple of the 32-row tile, fewer tiles than the grid cap) and the
+    counters left at zero. Other shapes are refused."""
+    from argus_amd._lib import BnBwdEpilogue, BnBwdPrologue
+
+    torch.manual_seed(31)
+    L = lib()
+    cin, cout = 64, 256
+    bad, _ = _desc(2, 8, 8, 128, 256, 1, 1)
+    assert L.dll.argus_conv_dgrad_wgrad_ok(C.byref(bad), BF16) == 0
+    ws_bytes = L.dll.argus_bn_workspace_bytes(2048)
+    for n, h, w_ in [(2, 33, 33), (1, 5, 7), (8, 64, 64)]:
+        d, _ = _desc(n, h, w_, cin, cout, 1, 1)
+        assert L.dll.argus_conv_dgrad_wgrad_ok(C.byref(d), BF16) == 1
+        assert L.dll.argus_conv_dgrad_wgrad_ok(C.byref(d), F32) == 0
+        P = n * h * w_
+        wt_ohwi = torch.randn(cout, 1, 1, cin) * (2.0 / cin) ** 0.5
+        _, wt = _prep(d, "bf16", wt_ohwi.to(cuda), cuda)
+        dm = torch.randn(P, cout, device=cuda).to(torch.bfloat16)
+        y3 = torch.randn(P, cout, device=cuda).to(torch.bfloat16)
+        ca, cb, cc = (torch.randn(cout, device=cuda) * 0.3 for _ in range(3))
+        a2 = torch.relu(torch.randn(P, cin, device=cuda)).to(torch.bfloat16)
+        y2 = torch.randn(P, cin, device=cuda).to(torch.bfloat16)
+        mean, invstd = torch.randn(cin, device=cuda) * 0.1, torch.rand(cin, device=cuda) + 0.5
+        sc, sh = torch.randn(cin, device=cuda), torch.randn(cin, device=cuda)
+        g2 = torch.rand(cin, device=cuda) + 0.5
+        res = []
+        for fused in (False, True):
+            ws = torch.zeros(ws_bytes, dtype=torch.uint8, device=cuda)
+            rows = (L.dll.argus_conv_dgrad_wgrad_bn_rows if fused else L.dll.argus_conv_dgrad_bn_rows)(C.byref(d), BF16)
+            part = torch.empty(rows, cin, 2, device=cuda)
+            co = torch.zeros(5, cin, device=cuda)
+            e = BnBwdEpilogue()
+            e.y, e.mean, e.invstd, e.mask_mode, e.scale, e.shift, e.part = ptr(y2), ptr(mean), ptr(invstd), 2, \
+                ptr(sc), ptr(sh), ptr(part)
+            e.workspace, e.gamma, e.dgamma, e.dbeta = ptr(ws), ptr(g2), ptr(co[3]), ptr(co[4])
+            e.ca, e.cb, e.cc = ptr(co[0]), ptr(co[1]), ptr(co[2])
+            pro = BnBwdPrologue(ptr(y3), ptr(ca), ptr(cb), ptr(cc), None)
+            dx = torch.empty(P, cin, dtype=torch.bfloat16, device=cuda)
+            dw = torch.empty(cout, 1, 1, cin, device=cuda)
+            if fused:
+                wsw = torch.empty(L.dll.argus_conv_dgrad_wgrad_workspace_bytes(C.byref(d), BF16), dtype=torch.uint8,
+                                  device=cuda)
+                rc = L.dll.argus_conv_dgrad_wgrad_bn(C.byref(d), BF16, ptr(dm), ptr(wt), ptr(a2), ptr(dx), C.byref(e),
+                                                     C.byref(pro), ptr(dw), ptr(wsw), wsw.numel(), stream())
+                assert rc == 0, L.dll.argus_last_error()
+            else:
+                L.conv_dgrad_bn(C.byref(d), BF16, ptr(dm), ptr(wt), ptr(dx), None, C.byref(e), C.byref(pro), stream())
+                wsw = torch.empty(L.dll.argus_conv_wgrad_workspace_bytes(C.byref(d), BF16), dtype=torch.uint8,
+                                  device=cuda)
+                L.conv_wgrad_apply(C.byref(d), BF16, ptr(a2), ptr(dm), C.byref(pro), ptr(dw), ptr(wsw), wsw.numel(),
+                                   stream())
+            torch.cuda.synchronize()
+            assert int(ws[:16384].view(torch.int32).abs().sum()) == 0
+            res.append((dx.cpu(), dw.cpu(), co.cpu()))
+        (x0, w0, c0), (x1, w1, c1) = res
+        assert torch.equal(x0, x1), (n, h, w_)
+        assert _rel(c1, c0) < 1e-5 and _rel(w1, w0) < 1e-5, (n, h, w_, _rel(c1, c0), _rel(w1, w0))
+        dy = (ca.double() * dm.double() + (cb.double() * y3.double() + cc.double())).to(torch.bfloat16).double()
+        dw64 = (dy.T @ a2.double()).view(cout, 1, 1, cin)
+        assert _rel(w1, dw64.cpu()) < 1e-5, (n, h, w_)
