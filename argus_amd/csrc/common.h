@@ -25,7 +25,10 @@ namespace argus {
 // kLoadBatch into registers (addresses clamped to a valid element), then accumulate in the same fixed
 // order as before with selects (x + 0 = x), not branches: a branch per element lets the compiler sink
 // each load into its branch and the waits come back.
-constexpr int kLoadBatch = 8;
+#ifndef ARGUS_LOAD_BATCH
+#define ARGUS_LOAD_BATCH 8  // (a build with 1 restores one load per trip: the A/B baseline)
+#endif
+constexpr int kLoadBatch = ARGUS_LOAD_BATCH;
 
 constexpr int kWave = 64;
 
