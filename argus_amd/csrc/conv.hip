@@ -1119,6 +1119,7 @@ static const Policy kDefaultPolicy = [] {
   //     engine A/B 14.73-14.96 vs 14.76-14.88 ms (B=64), 51.5 vs 51.6 (B=256), 99.6 vs 100.2-100.6
   //     (376x672 B=128): profiles/r04_ab_key38.txt
   p.v[kDgradApStaged] = 0;
+  p.v[kGldsDgrad] = 1;
   return p;
 }();
 

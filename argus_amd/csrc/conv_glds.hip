@@ -323,7 +323,7 @@ static void launch_glds(const IgParams& p, int maxM, hipStream_t st) {
 // non-temporal epilogue stores (convbench B=64: fwd+dgrad 5.32 -> 5.20 ms). Key 9: fewest workgroups.
 bool igemm_glds_ok(const IgParams& p, int maxM, int maxK) {
   const int min_k = (*p.pol)[kGldsMinK];
-  if (min_k <= 0 || p.stem || p.pro_scale || p.ap.y || maxK < min_k || p.Cin % 64 || p.lda % 8 ||
+  if (min_k <= 0 || p.stem || p.pro_scale || p.ap.y || (!p.fwd && !(*p.pol)[kGldsDgrad]) || maxK < min_k || p.Cin % 64 || p.lda % 8 ||
       p.ldb % 8 || maxM < (*p.pol)[kGldsMinRows])
     return false;
   if (p.stats && p.stat_tile != 128 && p.stat_tile != 64) return false;

@@ -16,36 +16,39 @@ namespace argus {
 
 constexpr double kSmall = 1e-4;  // Taylor-branch threshold (matches oracle/se3.py)
 
-// value + gradient w.r.t. the 6 prediction inputs
-struct D6 {
+// value + its derivative along kND of the 6 prediction inputs: the loss kernel runs one input
+// direction per lane (6 lanes per sample, each with the value chain and one derivative: 2 doubles
+// per operation instead of 7 on one lane; the same arithmetic per direction, the same bits)
+constexpr int kND = 1;
+struct Dual {
   double v;
-  double d[6];
+  double d[kND];
 };
-ARGUS_DEV D6 cst(double x) { D6 r; r.v = x; for (int i = 0; i < 6; ++i) r.d[i] = 0.0; return r; }
-ARGUS_DEV D6 operator+(const D6& a, const D6& b) { D6 r; r.v = a.v + b.v; for (int i = 0; i < 6; ++i) r.d[i] = a.d[i] + b.d[i]; return r; }
-ARGUS_DEV D6 operator-(const D6& a, const D6& b) { D6 r; r.v = a.v - b.v; for (int i = 0; i < 6; ++i) r.d[i] = a.d[i] - b.d[i]; return r; }
-ARGUS_DEV D6 operator-(const D6& a) { D6 r; r.v = -a.v; for (int i = 0; i < 6; ++i) r.d[i] = -a.d[i]; return r; }
-ARGUS_DEV D6 operator*(const D6& a, const D6& b) { D6 r; r.v = a.v * b.v; for (int i = 0; i < 6; ++i) r.d[i] = a.d[i] * b.v + a.v * b.d[i]; return r; }
-ARGUS_DEV D6 operator*(double s, const D6& a) { D6 r; r.v = s * a.v; for (int i = 0; i < 6; ++i) r.d[i] = s * a.d[i]; return r; }
-ARGUS_DEV D6 operator/(const D6& a, const D6& b) {
-  D6 r; r.v = a.v / b.v; const double ib = 1.0 / b.v;
-  for (int i = 0; i < 6; ++i) r.d[i] = (a.d[i] - r.v * b.d[i]) * ib;
+ARGUS_DEV Dual cst(double x) { Dual r; r.v = x; for (int i = 0; i < kND; ++i) r.d[i] = 0.0; return r; }
+ARGUS_DEV Dual operator+(const Dual& a, const Dual& b) { Dual r; r.v = a.v + b.v; for (int i = 0; i < kND; ++i) r.d[i] = a.d[i] + b.d[i]; return r; }
+ARGUS_DEV Dual operator-(const Dual& a, const Dual& b) { Dual r; r.v = a.v - b.v; for (int i = 0; i < kND; ++i) r.d[i] = a.d[i] - b.d[i]; return r; }
+ARGUS_DEV Dual operator-(const Dual& a) { Dual r; r.v = -a.v; for (int i = 0; i < kND; ++i) r.d[i] = -a.d[i]; return r; }
+ARGUS_DEV Dual operator*(const Dual& a, const Dual& b) { Dual r; r.v = a.v * b.v; for (int i = 0; i < kND; ++i) r.d[i] = a.d[i] * b.v + a.v * b.d[i]; return r; }
+ARGUS_DEV Dual operator*(double s, const Dual& a) { Dual r; r.v = s * a.v; for (int i = 0; i < kND; ++i) r.d[i] = s * a.d[i]; return r; }
+ARGUS_DEV Dual operator/(const Dual& a, const Dual& b) {
+  Dual r; r.v = a.v / b.v; const double ib = 1.0 / b.v;
+  for (int i = 0; i < kND; ++i) r.d[i] = (a.d[i] - r.v * b.d[i]) * ib;
   return r;
 }
-ARGUS_DEV D6 fn(const D6& a, double f, double df) { D6 r; r.v = f; for (int i = 0; i < 6; ++i) r.d[i] = df * a.d[i]; return r; }
-ARGUS_DEV D6 dsqrt(const D6& a) { const double s = sqrt(a.v); return fn(a, s, s > 0.0 ? 0.5 / s : 0.0); }
-ARGUS_DEV D6 dsin(const D6& a) { return fn(a, sin(a.v), cos(a.v)); }
-ARGUS_DEV D6 dcos(const D6& a) { return fn(a, cos(a.v), -sin(a.v)); }
-ARGUS_DEV D6 datan(const D6& a) { return fn(a, atan(a.v), 1.0 / (1.0 + a.v * a.v)); }
+ARGUS_DEV Dual fn(const Dual& a, double f, double df) { Dual r; r.v = f; for (int i = 0; i < kND; ++i) r.d[i] = df * a.d[i]; return r; }
+ARGUS_DEV Dual dsqrt(const Dual& a) { const double s = sqrt(a.v); return fn(a, s, s > 0.0 ? 0.5 / s : 0.0); }
+ARGUS_DEV Dual dsin(const Dual& a) { return fn(a, sin(a.v), cos(a.v)); }
+ARGUS_DEV Dual dcos(const Dual& a) { return fn(a, cos(a.v), -sin(a.v)); }
+ARGUS_DEV Dual datan(const Dual& a) { return fn(a, atan(a.v), 1.0 / (1.0 + a.v * a.v)); }
 
-struct V3 { D6 x, y, z; };
+struct V3 { Dual x, y, z; };
 ARGUS_DEV V3 cross(const V3& a, const V3& b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
 ARGUS_DEV V3 add(const V3& a, const V3& b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
 ARGUS_DEV V3 sub(const V3& a, const V3& b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
-ARGUS_DEV V3 scale(const D6& s, const V3& a) { return {s * a.x, s * a.y, s * a.z}; }
-ARGUS_DEV D6 dot(const V3& a, const V3& b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+ARGUS_DEV V3 scale(const Dual& s, const V3& a) { return {s * a.x, s * a.y, s * a.z}; }
+ARGUS_DEV Dual dot(const V3& a, const V3& b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 
-struct Quat { V3 v; D6 w; };
+struct Quat { V3 v; Dual w; };
 ARGUS_DEV Quat qmul(const Quat& a, const Quat& b) {
   return {add(add(scale(a.w, b.v), scale(b.w, a.v)), cross(a.v, b.v)), a.w * b.w - dot(a.v, b.v)};
 }
@@ -56,9 +59,9 @@ ARGUS_DEV V3 qrot(const Quat& q, const V3& p) {
 
 // J_l(phi) x = x + c1 phi x x + c2 phi x (phi x x)
 ARGUS_DEV V3 jl_apply(const V3& phi, const V3& x, bool inverse) {
-  const D6 th2 = dot(phi, phi);
-  const D6 th = dsqrt(th2);
-  D6 c1, c2;
+  const Dual th2 = dot(phi, phi);
+  const Dual th = dsqrt(th2);
+  Dual c1, c2;
   if (!inverse) {
     if (th.v < kSmall) {
       c1 = cst(0.5) - (1.0 / 24) * th2 + (1.0 / 720) * (th2 * th2);
@@ -72,7 +75,7 @@ ARGUS_DEV V3 jl_apply(const V3& phi, const V3& x, bool inverse) {
     if (th.v < kSmall) {
       c2 = cst(1.0 / 12) + (1.0 / 720) * th2 + (1.0 / 30240) * (th2 * th2);
     } else {
-      const D6 half = 0.5 * th;
+      const Dual half = 0.5 * th;
       c2 = (cst(1.0) - half * dcos(half) / dsin(half)) / th2;
     }
   }
@@ -81,13 +84,13 @@ ARGUS_DEV V3 jl_apply(const V3& phi, const V3& x, bool inverse) {
   return add(add(x, scale(c1, k1)), scale(c2, k2));
 }
 
-ARGUS_DEV D6 se3_loss(const D6 (&xi)[6], const double (&T)[7]) {
+ARGUS_DEV Dual se3_loss(const Dual (&xi)[6], const double (&T)[7]) {
   // Exp(pred)
   const V3 rho = {xi[0], xi[1], xi[2]};
   const V3 phi = {xi[3], xi[4], xi[5]};
-  const D6 th2 = dot(phi, phi);
-  const D6 th = dsqrt(th2);
-  D6 imag, real;
+  const Dual th2 = dot(phi, phi);
+  const Dual th = dsqrt(th2);
+  Dual imag, real;
   if (th.v < kSmall) {
     imag = cst(0.5) - (1.0 / 48) * th2 + (1.0 / 3840) * (th2 * th2);
     real = cst(1.0) - (1.0 / 8) * th2 + (1.0 / 384) * (th2 * th2);
@@ -105,11 +108,11 @@ ARGUS_DEV D6 se3_loss(const D6 (&xi)[6], const double (&T)[7]) {
   const Quat qr = qmul(qp, qti);
   const V3 tr = add(tp, qrot(qp, tti));
   // Log
-  const D6 n2 = dot(qr.v, qr.v);
-  const D6 n = dsqrt(n2);
-  D6 w = qr.w;
+  const Dual n2 = dot(qr.v, qr.v);
+  const Dual n = dsqrt(n2);
+  Dual w = qr.w;
   if (w.v == 0.0) w.v = 1e-30;
-  D6 factor;
+  Dual factor;
   if (n.v < kSmall) {
     factor = cst(2.0) / w - (2.0 / 3.0) * n2 / (w * w * w);
   } else {
@@ -122,19 +125,17 @@ ARGUS_DEV D6 se3_loss(const D6 (&xi)[6], const double (&T)[7]) {
 
 __global__ void se3_loss_kernel(int B, const float* __restrict__ pred, const float* __restrict__ target,
                                 float* __restrict__ loss, float* __restrict__ dpred, float gscale) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = t / 6, dir = t - 6 * b;  // sample, input direction of this lane
   if (b >= B) return;
-  D6 xi[6];
-  for (int i = 0; i < 6; ++i) {
-    xi[i] = cst((double)pred[b * 6 + i]);
-    xi[i].d[i] = 1.0;
-  }
+  Dual xi[6];
+  for (int i = 0; i < 6; ++i) xi[i] = cst((double)pred[b * 6 + i]);
+  xi[dir].d[0] = 1.0;
   double T[7];
   for (int i = 0; i < 7; ++i) T[i] = (double)target[b * 7 + i];
-  const D6 L = se3_loss(xi, T);
-  loss[b] = (float)L.v;
-  if (dpred)
-    for (int i = 0; i < 6; ++i) dpred[b * 6 + i] = (float)(gscale * L.d[i]);
+  const Dual L = se3_loss(xi, T);
+  if (dir == 0) loss[b] = (float)L.v;
+  if (dpred) dpred[b * 6 + dir] = (float)(gscale * L.d[0]);
 }
 
 // se(3) -> SE(3) exponential map (pypose se3.Exp): out[b] = [t (3), q xyzw (4)], w >= 0 canonical
@@ -142,13 +143,13 @@ __global__ void se3_loss_kernel(int B, const float* __restrict__ pred, const flo
 __global__ void se3_exp_kernel(int B, const float* __restrict__ xi, float* __restrict__ out, int canon) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
-  D6 x[6];
+  Dual x[6];
   for (int i = 0; i < 6; ++i) x[i] = cst((double)xi[b * 6 + i]);
   const V3 rho = {x[0], x[1], x[2]};
   const V3 phi = {x[3], x[4], x[5]};
-  const D6 th2 = dot(phi, phi);
-  const D6 th = dsqrt(th2);
-  D6 imag, real;
+  const Dual th2 = dot(phi, phi);
+  const Dual th = dsqrt(th2);
+  Dual imag, real;
   if (th.v < kSmall) {
     imag = cst(0.5) - (1.0 / 48) * th2 + (1.0 / 3840) * (th2 * th2);
     real = cst(1.0) - (1.0 / 8) * th2 + (1.0 / 384) * (th2 * th2);
@@ -184,7 +185,7 @@ extern "C" int argus_se3_loss(int batch, const float* pred, const float* target,
     set_error("se3_loss: bad arguments");
     return ARGUS_ERR_ARG;
   }
-  hipLaunchKernelGGL(se3_loss_kernel, dim3((batch + 63) / 64), dim3(64), 0, (hipStream_t)stream, batch, pred, target,
+  hipLaunchKernelGGL(se3_loss_kernel, dim3((6 * batch + 255) / 256), dim3(256), 0, (hipStream_t)stream, batch, pred, target,
                      loss, dpred, grad_scale);
   return check_launch("se3_loss_kernel");
 }
