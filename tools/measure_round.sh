@@ -3,11 +3,11 @@
 # each fit one gpurun call:   bash tools/measure_round.sh TAG a|b
 #   a: bench lines for configs[1] (B=64) and the configs[2] per-rank point (B=256); B=64 kernel stats,
 #      FETCH/WRITE PMC traffic, MFMA/wave-state counters and the step timeline
-#   b: configs[3] (376x672, B=128) bench line + its kernel stats / PMC traffic / MFMA counters; the
-#      configs[4] per-rank batch (B=512) in fp8 and bf16
+#   b: configs[3] (376x672, B=128) bench line + its kernel stats / PMC traffic / MFMA counters
+#   c: configs[4]'s per-rank batch (B=512) in fp8 and bf16: PMC traffic + MFMA counters, bench lines
 set -e
 TAG=$1
-PART=${2:-a}
+PART=${2:-a}  # a | b | c
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/meas_$TAG
 mkdir -p $O
@@ -29,6 +29,21 @@ if [ "$PART" = a ]; then
   cp $O/pmc_mfma_summary.json profiles/${TAG}_pmc_mfma_summary.json
   timeout -k 10 240 python3 -u bench.py > $O/bench.json 2> $O/bench.err
   timeout -k 10 180 python3 -u bench.py --batch 256 --no-cpu-baseline > $O/bench_b256.json 2> $O/bench_b256.err
+elif [ "$PART" = c ]; then
+  # configs[4]'s per-rank batch (B=512): PMC traffic and MFMA counters for fp8 and bf16, then the lines
+  for DT in fp8 bf16; do
+    bash tools/profile_round.sh ${TAG}_b512_$DT --batch 512 --dtype $DT --steps 3 --warmup 1 --no-isolated
+    python3 tools/pmc_traffic.py gpurun_out/prof_${TAG}_b512_$DT/pmc_fetch gpurun_out/prof_${TAG}_b512_$DT/pmc_write \
+      $O/pmc_traffic_b512_$DT.json 512 256 256 $DT
+    WORKLOAD="512 256 256 $DT" bash tools/prof_pmc.sh ${TAG}_b512_$DT --batch 512 --dtype $DT
+    cp gpurun_out/pmc_${TAG}_b512_$DT/summary.json profiles/${TAG}_b512_${DT}_pmc_mfma_summary.json
+    cp gpurun_out/pmc_${TAG}_b512_$DT/summary.txt $O/b512_${DT}_pmc_mfma_summary.txt
+    cp $O/pmc_traffic_b512_$DT.json profiles/${TAG}_b512_${DT}_pmc_traffic.json
+  done
+  timeout -k 10 240 python3 -u bench.py --dtype fp8 --batch 512 --no-cpu-baseline --steps 5 --warmup 2 \
+    > $O/bench_b512_fp8.json 2> $O/bench_b512_fp8.err
+  timeout -k 10 240 python3 -u bench.py --batch 512 --no-cpu-baseline --steps 5 --warmup 2 \
+    > $O/bench_b512_bf16.json 2> $O/bench_b512_bf16.err
 else
   bash tools/profile_round.sh ${TAG}_376 --hw 376 672 --batch 128 --steps 5 --warmup 2
   python3 tools/pmc_traffic.py gpurun_out/prof_${TAG}_376/pmc_fetch gpurun_out/prof_${TAG}_376/pmc_write $O/pmc_traffic_376x672.json 128 376 672 bf16
@@ -39,9 +54,5 @@ else
   cp $O/376x672_pmc_mfma_summary.json profiles/${TAG}_376x672_pmc_mfma_summary.json
   timeout -k 10 240 python3 -u bench.py --hw 376 672 --batch 128 --no-cpu-baseline --kernels \
     > $O/bench_376x672.json 2> $O/bench_376x672_kernels.txt
-  timeout -k 10 240 python3 -u bench.py --dtype fp8 --batch 512 --no-cpu-baseline --steps 5 --warmup 2 \
-    > $O/bench_b512_fp8.json 2> $O/bench_b512_fp8.err
-  timeout -k 10 240 python3 -u bench.py --batch 512 --no-cpu-baseline --no-isolated --steps 5 --warmup 2 \
-    > $O/bench_b512_bf16.json 2> $O/bench_b512_bf16.err
 fi
 echo "measure $PART done"
