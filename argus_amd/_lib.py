@@ -99,8 +99,8 @@ SIGNATURES = {
     "argus_conv_dgrad_wgrad_ok": (_I, [_DESC, _I]),
     "argus_conv_dgrad_wgrad_workspace_bytes": (_SZ, [_DESC, _I]),
     "argus_conv_dgrad_wgrad_bn_rows": (_I, [_DESC, _I]),
-    "argus_conv_dgrad_wgrad_bn": (_I, [_DESC, _I, _P, _P, _P, _P, C.POINTER(BnBwdEpilogue), C.POINTER(BnBwdPrologue),
-                                       _P, _P, _SZ, _P]),
+    "argus_conv_dgrad_wgrad_bn": (_I, [_DESC, _I, _P, _P, _P, _P, _P, C.POINTER(BnBwdEpilogue),
+                                       C.POINTER(BnBwdPrologue), _P, _P, _SZ, _P]),
     "argus_ktimer_enable": (_I, [C.c_char_p]),
     "argus_ktimer_enable_on": (_I, [C.c_char_p, _P]),
     "argus_ktimer_disable": (_I, []),

@@ -117,11 +117,12 @@ int argus_conv_dgrad_wgrad_bn_rows(const argus_conv_desc* d, int dtype) {
 }
 
 int argus_conv_dgrad_wgrad_bn(const argus_conv_desc* d, int dtype, const void* dm, const void* w_dgrad,
-                              const void* x, void* dx, const argus_bn_bwd_epilogue* bn,
+                              const void* x, void* dx, const void* addend, const argus_bn_bwd_epilogue* bn,
                               const argus_bn_bwd_prologue* pro, float* dw, void* workspace,
                               size_t workspace_bytes, argus_stream_t stream) {
   if (!d) { set_error("conv_dgrad_wgrad_bn: bad arguments"); return ARGUS_ERR_ARG; }
-  return conv_dgw(*d, dtype, dm, w_dgrad, x, dx, bn, pro, dw, workspace, workspace_bytes, (hipStream_t)stream);
+  return conv_dgw(*d, dtype, dm, w_dgrad, x, dx, addend, bn, pro, dw, workspace, workspace_bytes,
+                  (hipStream_t)stream);
 }
 
 size_t argus_conv_wgrad_workspace_bytes(const argus_conv_desc* d, int dtype) { return d ? conv_wgrad_ws(*d, dtype) : 0; }

@@ -44,7 +44,8 @@ struct DgwParams {
   const float *ca, *cb, *cc;  // dy3 = ca*dm + cb*y + cc (bn3 backward coefficients)
   const bf16* wd;   // [64][256] dgrad weight (argus_conv_weight_prep w_dgrad)
   const bf16* x;    // [P][64] conv input (a2)
-  bf16* out;        // [P][64] masked bn2 input gradient
+  bf16* out;        // [P][64] masked bn2 input gradient (BNE) or the plain dx (+ addend)
+  const bf16* addend;  // !BNE: dx += addend (may alias out)
   float* part_w;    // [G][256][64] weight-gradient partials
   BnBwdEpi bb;      // bn2 (mode 2); partial rows = G
   BnFin fin;
@@ -86,6 +87,9 @@ struct DgwStage {
 
 }  // namespace
 
+// BNE: the dx epilogue is bn2's backward (mask mode 2, partial sums, optional folded finalize); else a
+// plain store of dx (+ addend: the first block's downsample, accumulated onto conv1's dgrad)
+template <bool BNE>
 __global__ __launch_bounds__(256, 2) void dgw1x1_kernel(const DgwParams p) {
   // dy3 tile (2 images of 128 channels), a2 tile, W (2 images): 56 KB, two workgroups per CU
   __shared__ __attribute__((aligned(16))) u32x4 lds[3 * kImg + 2 * kImgW];
@@ -184,7 +188,20 @@ __global__ __launch_bounds__(256, 2) void dgw1x1_kernel(const DgwParams p) {
       for (int r = 0; r < 4; ++r) Cs[(16 * rb + 4 * g + r) * LD + 32 * chh + 16 * ni + i16] = (bf16)dacc[ni][r];
     __syncthreads();
     const int m = t * kBr + tid / 8;
-    if (m < p.P) {  // BwdEpiAcc<bf16, 2>::step with the per-channel constants reloaded (L1)
+    if (!BNE && m < p.P) {  // plain: the bf16-rounded dx (+ addend), as igemm_kernel's epilogue
+      const size_t off = (size_t)m * kCi + xc * 8;
+      u32x4 v = *reinterpret_cast<const u32x4*>(Cs + (tid / 8) * LD + xc * 8);
+      if (p.addend) {
+        float f[8], o[8];
+        unpack(v, f);
+        unpack(ld16(p.addend + off), o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] += o[j];
+        v = pack(f);
+      }
+      st16_nt(p.out + off, v);
+    }
+    if (BNE && m < p.P) {  // BwdEpiAcc<bf16, 2>::step with the per-channel constants reloaded (L1)
       const size_t off = (size_t)m * kCi + xc * 8;
       float d[8], yv[8], mu[8], is[8], sc[8], sh[8];
       unpack(*reinterpret_cast<const u32x4*>(Cs + (tid / 8) * LD + xc * 8), d);
@@ -214,6 +231,7 @@ __global__ __launch_bounds__(256, 2) void dgw1x1_kernel(const DgwParams p) {
       for (int r = 0; r < 4; ++r) pw[(64 * wave + 16 * mi + 4 * g + r) * kCi + 16 * ni + i16] = wacc[mi][ni][r];
 
   // ---- bn2 partial row blockIdx.x (+ the folded finalize); scratch: the dy3 + a2 images (24 KB) ----
+  if constexpr (!BNE) return;
   BwdEpiAcc<bf16, 2> bwd;  // its fixed-order reduction of the per-thread sums (the constants are unused)
 #pragma unroll
   for (int j = 0; j < 8; ++j) { bwd.s[j] = esum[j]; bwd.t[j] = exs[j]; }
@@ -245,17 +263,18 @@ size_t conv_dgw_ws_bytes(const argus_conv_desc& d, int dtype) {
 int conv_dgw_rows(const argus_conv_desc& d, int dtype) { return conv_dgw_ok(d, dtype) ? dgw_grid(d) : -1; }
 
 int conv_dgw(const argus_conv_desc& d, int dtype, const void* dm, const void* wd, const void* x, void* dx,
-             const argus_bn_bwd_epilogue* bn, const argus_bn_bwd_prologue* pro, float* dw, void* ws, size_t ws_bytes,
-             hipStream_t st) {
+             const void* addend, const argus_bn_bwd_epilogue* bn, const argus_bn_bwd_prologue* pro, float* dw,
+             void* ws, size_t ws_bytes, hipStream_t st) {
   if (int e = conv_check_desc(d)) return e;
   if (!conv_dgw_ok(d, dtype)) {
     set_error("conv_dgrad_wgrad_bn: only bf16 1x1 stride-1 convs with 64 input and 256 output channels");
     return ARGUS_ERR_SHAPE;
   }
-  if (!dm || !wd || !x || !dx || !dw || !bn || !pro || !pro->y || !pro->ca || !pro->cb || !pro->cc || pro->dy_out ||
-      bn->mask_mode != 2 || !bn->y || !bn->mean || !bn->invstd || !bn->scale || !bn->shift || !bn->part || bn->y2 ||
-      bn->y == dx) {
-    set_error("conv_dgrad_wgrad_bn: bad arguments (apply prologue without dy_out, mask mode 2 epilogue)");
+  if (!dm || !wd || !x || !dx || !dw || !pro || !pro->y || !pro->ca || !pro->cb || !pro->cc || pro->dy_out ||
+      (bn && (addend || bn->mask_mode != 2 || !bn->y || !bn->mean || !bn->invstd || !bn->scale || !bn->shift ||
+              !bn->part || bn->y2 || bn->y == dx))) {
+    set_error("conv_dgrad_wgrad_bn: bad arguments (apply prologue without dy_out; a mask-mode-2 epilogue or none, "
+              "an addend only without it)");
     return ARGUS_ERR_ARG;
   }
   const int G = dgw_grid(d);
@@ -270,8 +289,16 @@ int conv_dgw(const argus_conv_desc& d, int dtype, const void* dm, const void* wd
   p.wd = reinterpret_cast<const bf16*>(wd);
   p.x = reinterpret_cast<const bf16*>(x);
   p.out = reinterpret_cast<bf16*>(dx);
+  p.addend = reinterpret_cast<const bf16*>(addend);
   p.part_w = reinterpret_cast<float*>(ws);
   p.P = d.n * d.ho * d.wo;
+  if (!bn) {
+    g_launch_work = 2.0 * 2.0 * p.P * kKo * kCi;
+    g_launch_bytes = 2.0 * ((double)p.P * (2 * kKo + (addend ? 3 : 2) * kCi)) + 4.0 * kKo * kCi;
+    timed_launch("argus::dgw1x1_kernel<false>", dgw1x1_kernel<false>, dim3(G), dim3(256), st, p);
+    if (int e = check_launch("dgw1x1_kernel")) return e;
+    return wgrad_reduce_launch(reinterpret_cast<const float*>(ws), G, kKo, kCi, 0, dw, st);
+  }
   BnBwdEpi& b = p.bb;
   b.y = bn->y; b.mean = bn->mean; b.invstd = bn->invstd; b.sc = bn->scale; b.sh = bn->shift;
   b.part = reinterpret_cast<float2*>(bn->part); b.mode = 2; b.prow = G;
@@ -293,7 +320,7 @@ int conv_dgw(const argus_conv_desc& d, int dtype, const void* dm, const void* wd
   // algorithmic work (ktimer): both GEMMs; bytes: dm, y, a2, y2 read, dx written, dW (fp32) written
   g_launch_work = 2.0 * 2.0 * p.P * kKo * kCi;
   g_launch_bytes = 2.0 * ((double)p.P * (2 * kKo + 3 * kCi)) + 4.0 * kKo * kCi;
-  timed_launch("argus::dgw1x1_kernel", dgw1x1_kernel, dim3(G), dim3(256), st, p);
+  timed_launch("argus::dgw1x1_kernel<true>", dgw1x1_kernel<true>, dim3(G), dim3(256), st, p);
   if (int e = check_launch("dgw1x1_kernel")) return e;
   return wgrad_reduce_launch(reinterpret_cast<const float*>(ws), G, kKo, kCi, 0, dw, st);
 }

@@ -66,8 +66,8 @@ bool conv_dgw_ok(const argus_conv_desc& d, int dtype);
 size_t conv_dgw_ws_bytes(const argus_conv_desc& d, int dtype);
 int conv_dgw_rows(const argus_conv_desc& d, int dtype);
 int conv_dgw(const argus_conv_desc& d, int dtype, const void* dm, const void* wd, const void* x, void* dx,
-             const argus_bn_bwd_epilogue* bn, const argus_bn_bwd_prologue* pro, float* dw, void* ws, size_t ws_bytes,
-             hipStream_t st);
+             const void* addend, const argus_bn_bwd_epilogue* bn, const argus_bn_bwd_prologue* pro, float* dw,
+             void* ws, size_t ws_bytes, hipStream_t st);
 int conv_dgrad_stages_prologue(const argus_conv_desc& d, int dtype);
 int conv_dgrad_bn(const argus_conv_desc& d, int dtype, const void* dy, const void* wt, void* dm,
                   const void* addend, const argus_bn_bwd_epilogue* bn, const argus_bn_bwd_prologue* pro,

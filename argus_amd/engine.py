@@ -249,8 +249,9 @@ class ResNetEngine:
             if not cv.desc.stem:
                 max_bwd = max(max_bwd, L.dll.argus_conv_dgrad_bn_rows(C.byref(cv.desc), self.cdt) * cv.desc.c)
         # convs whose data and weight gradient run fused (argus_conv_dgrad_wgrad_bn)
-        self.dgw = {n for n, cv in convs.items() if self.fuse_dgw and n.endswith(".conv3") and not cv.desc.stem
-                    and L.dll.argus_conv_dgrad_wgrad_ok(C.byref(cv.desc), self.cdt)}
+        # (layer-1 conv3s, and the first block's downsample: the same 64 -> 256 channel 1x1 shape)
+        self.dgw = {n for n, cv in convs.items() if self.fuse_dgw and n.endswith((".conv3", ".downsample.0"))
+                    and not cv.desc.stem and L.dll.argus_conv_dgrad_wgrad_ok(C.byref(cv.desc), self.cdt)}
         dgws = 16
         for n in self.dgw:
             d_ = C.byref(convs[n].desc)
@@ -507,6 +508,8 @@ class ResNetEngine:
             px_i = N * hi * wi
             dyd = self._next_dy() if b.has_ds else None
             dbg = self.debug
+            ds_dgw = (b.has_ds and idx == 0 and self.fuse_apply and rows3 is not None
+                      and pf + ".downsample.0" in self.dgw)
             # weight gradients that stage the BN-backward apply from dm themselves (dy never stored;
             # the debug capture keeps storing it for the stage checks)
             wg3_apply = (rows3 is not None and self.fuse_apply and self.wgrad_apply and a["a2"] is not None
@@ -540,7 +543,9 @@ class ResNetEngine:
                         self._bn_bwd_fin(P, G, pf + ".downsample.1", px_o, b.cout, self.bwd_part2, rows3)
                 if fuse:  # dy3 (and dyd) are staged by the conv3 (downsample) dgrad from dm3 = dh
                     pro3 = (pf + ".bn3", a["y3"], dy3)
-                    if b.has_ds and idx == 0:  # block 0's downsample dgrad is a plain dgrad: materialise dyd
+                    # block 0's downsample dgrad is a plain dgrad: materialise dyd, unless its data and
+                    # weight gradient run fused (staging dyd from dh; dyd then kept for the debug capture only)
+                    if b.has_ds and idx == 0 and (not ds_dgw or dbg is not None):
                         self._bn_apply_bwd(pf + ".downsample.1", px_o, b.cout, dh, a["yd"], dyd)
                 else:
                     pro3 = None
@@ -614,7 +619,10 @@ class ResNetEngine:
                                            second, P=P, G=G, pro=pro1)
             else:
                 self._dgrad(pf + ".conv1", dy1, dx)
-                if b.has_ds:
+                if ds_dgw:  # dx += the downsample dgrad, its dW from the same staged dyd tile
+                    self._dgrad_wgrad_bn(pf + ".downsample.0", dh, dx, None, None, pf + ".downsample.1", a["yd"],
+                                         h_in, P, G, addend=dx)
+                elif b.has_ds:
                     self._dgrad(pf + ".downsample.0", dyd, dx, addend=dx)
             if dy1 is not None:
                 cap("b_dy1", dy1, px_i * b.width, (N, hi, wi, b.width))
@@ -624,7 +632,7 @@ class ResNetEngine:
                 self._wgrad_apply(pf + ".conv1", h_in, dzb, pf + ".bn1", a["y1"], G)
             else:
                 self._wgrad(pf + ".conv1", h_in, None, dy1, G)
-            if b.has_ds:
+            if b.has_ds and not ds_dgw:
                 # (single process only: with on_ready a bucket holding this gradient could be reduced first)
                 if (idx == 0 and on_ready is None and self.tail_main and self.wgrad_overlap and self._stem_overlap
                         and self.fuse_apply):
@@ -705,23 +713,29 @@ class ResNetEngine:
                                                           ptr(addend), C.byref(e), pp, stream()))
         return 0 if self.fold_fin else self.L.dll.argus_conv_dgrad_bn_rows(C.byref(cv.desc), self.cdt)
 
-    def _dgrad_wgrad_bn(self, conv, dm, dx, bn, y, pbn, py, x, P, G):
+    def _dgrad_wgrad_bn(self, conv, dm, dx, bn, y, pbn, py, x, P, G, addend=None):
         """Fused data + weight gradient of ``conv`` (argus_conv_dgrad_wgrad_bn): dy = the apply of BN
         ``pbn`` (input ``py``) staged from ``dm``, dx = the masked input gradient of BN ``bn`` (input ``y``,
-        mask mode 2, finalize folded), dW from ``x``; returns 0 (nothing left to finalize)."""
+        mask mode 2, finalize folded) or, with ``bn`` None, the plain dx (+ ``addend``); dW from ``x``;
+        returns 0 (nothing left to finalize)."""
         cv = self.convs[conv]
-        st, cf, pc = self.bn_state[bn], self.bn_coef[bn], self.bn_coef[pbn]
-        e = BnBwdEpilogue()
-        e.workspace, e.gamma, e.dgamma, e.dbeta = ptr(self.bn_ws), ptr(P[bn + ".weight"]), ptr(G[bn + ".weight"]), \
-            ptr(G[bn + ".bias"])
-        e.ca, e.cb, e.cc = ptr(cf[0]), ptr(cf[1]), ptr(cf[2])
-        e.y, e.mean, e.invstd, e.mask_mode, e.scale, e.shift = ptr(y), ptr(st[0]), ptr(st[1]), 2, ptr(st[2]), ptr(st[3])
-        e.part = ptr(self.bwd_part)
+        pc = self.bn_coef[pbn]
+        e = None
+        if bn is not None:
+            st, cf = self.bn_state[bn], self.bn_coef[bn]
+            e = BnBwdEpilogue()
+            e.workspace, e.gamma, e.dgamma, e.dbeta = ptr(self.bn_ws), ptr(P[bn + ".weight"]), \
+                ptr(G[bn + ".weight"]), ptr(G[bn + ".bias"])
+            e.ca, e.cb, e.cc = ptr(cf[0]), ptr(cf[1]), ptr(cf[2])
+            e.y, e.mean, e.invstd, e.mask_mode, e.scale, e.shift = ptr(y), ptr(st[0]), ptr(st[1]), 2, ptr(st[2]), \
+                ptr(st[3])
+            e.part = ptr(self.bwd_part)
         pro = BnBwdPrologue(ptr(py), ptr(pc[0]), ptr(pc[1]), ptr(pc[2]), None)
         self._guard(dx)
         self._launch(cv, 1, lambda: self.L.conv_dgrad_wgrad_bn(
-            C.byref(cv.desc), self.cdt, ptr(dm), ptr(cv.wd), ptr(x), ptr(dx), C.byref(e), C.byref(pro),
-            ptr(G[conv + ".weight"]), ptr(self.dgw_ws), self.dgw_ws.numel(), stream()))
+            C.byref(cv.desc), self.cdt, ptr(dm), ptr(cv.wd), ptr(x), ptr(dx), ptr(addend),
+            C.byref(e) if e is not None else None, C.byref(pro), ptr(G[conv + ".weight"]), ptr(self.dgw_ws),
+            self.dgw_ws.numel(), stream()))
         return 0
 
     def _prologue(self, pro):

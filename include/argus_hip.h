@@ -205,17 +205,19 @@ int argus_conv_wgrad_apply(const argus_conv_desc* d, int dtype, const void* x, c
                            size_t workspace_bytes, argus_stream_t stream);
 /* Data and weight gradient of one 1x1 stride-1 conv in one pass over its output gradient (torch's
  * convolution backward with output_mask (grad_input, grad_weight) for Bottleneck.conv3 of ResNet-50
- * layer 1, reached from loss.backward() at argus/train.py:316; replaces argus_conv_dgrad_bn +
+ * layer 1 and of the first block's downsample, reached from loss.backward() at argus/train.py:316;
+ * replaces argus_conv_dgrad_bn (argus_conv_dgrad) +
  * argus_conv_wgrad_apply for that conv). `dm`, `pro` as in argus_conv_dgrad_bn with an apply
  * prologue (pro->dy_out must be NULL: dy is never stored); `bn` a mask-mode-2 BN-backward epilogue
- * (its partial rows: argus_conv_dgrad_wgrad_bn_rows; with bn->workspace the finalize is folded);
+ * (its partial rows: argus_conv_dgrad_wgrad_bn_rows; with bn->workspace the finalize is folded), or
+ * NULL for a plain dx, optionally dx += addend (may alias dx; the first block's downsample);
  * x = the conv input (for dw, fp32 OHWI). bf16 only, C = 64 input and K = 256 output channels
  * (argus_conv_dgrad_wgrad_ok); workspace: argus_conv_dgrad_wgrad_workspace_bytes. */
 int argus_conv_dgrad_wgrad_ok(const argus_conv_desc* d, int dtype);
 size_t argus_conv_dgrad_wgrad_workspace_bytes(const argus_conv_desc* d, int dtype);
 int argus_conv_dgrad_wgrad_bn_rows(const argus_conv_desc* d, int dtype);
 int argus_conv_dgrad_wgrad_bn(const argus_conv_desc* d, int dtype, const void* dm, const void* w_dgrad,
-                              const void* x, void* dx, const argus_bn_bwd_epilogue* bn,
+                              const void* x, void* dx, const void* addend, const argus_bn_bwd_epilogue* bn,
                               const argus_bn_bwd_prologue* pro, float* dw, void* workspace,
                               size_t workspace_bytes, argus_stream_t stream);
 
