@@ -577,6 +577,9 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(int n, int H, int W, i
     AV av[4];
     bool ok[4];
     unsigned want[4];
+    const size_t off = (size_t)pix * C + c0;
+    u32x4 yraw;
+    if constexpr (BNE) yraw = ld16(y + off);  // issued with the gathers below (one memory latency, not two)
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int oh = ohs[k >> 1], ow = ows[k & 1];
@@ -606,10 +609,9 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(int n, int H, int W, i
 #pragma unroll
       for (int j = 0; j < E; ++j) acc[j] += a[j] == want[k] ? gv[j] : 0.f;
     }
-    const size_t off = (size_t)pix * C + c0;
     if constexpr (BNE) {
       float yv[E];
-      unpack(ld16(y + off), yv);
+      unpack(yraw, yv);
       const u32x4 r = pack(acc);  // the dz value as stored by the plain kernel (rounded to T)
       unpack(r, acc);
 #pragma unroll
@@ -648,7 +650,13 @@ __global__ __launch_bounds__(256) void avgpool_fwd_kernel(int n, int hw, int C, 
   if (i >= (int64_t)n * C) return;
   const int img = (int)(i / C), c = (int)(i % C);
   float s = 0.f;
-  for (int p = 0; p < hw; ++p) s += to_f32(x[((int64_t)img * hw + p) * C + c]);
+  for (int pb = 0; pb < hw; pb += kLoadBatch) {  // kLoadBatch loads in flight (common.h), same order
+    float v[kLoadBatch];
+#pragma unroll
+    for (int u = 0; u < kLoadBatch; ++u) v[u] = to_f32(x[((int64_t)img * hw + min(pb + u, hw - 1)) * C + c]);
+#pragma unroll
+    for (int u = 0; u < kLoadBatch; ++u) s += pb + u < hw ? v[u] : 0.f;
+  }
   feat[i] = s / (float)hw;
 }
 

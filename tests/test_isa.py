@@ -123,6 +123,7 @@ REDUCTIONS = {
     "wgrad_reduce_kernel": "reduce.hip",
     "gemm_reduce_kernel": "head.hip",
     "colsum_kernel": "head.hip",
+    "avgpool_fwd_kernel": "bn.hip",
     # the folded BN-backward finalize's group merges (bnfin.h) inside a BN-epilogue dgrad
     "igemm_glds_kernelILi256ELi128ELi2E": "conv_glds.hip",
 }
