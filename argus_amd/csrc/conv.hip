@@ -1120,6 +1120,7 @@ static const Policy kDefaultPolicy = [] {
   //     (376x672 B=128): profiles/r04_ab_key38.txt
   p.v[kDgradApStaged] = 0;
   p.v[kGldsDgrad] = 1;
+  p.v[kHaloDgrad] = 1;
   return p;
 }();
 

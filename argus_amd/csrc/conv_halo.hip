@@ -372,7 +372,7 @@ static bool halo_geom(const IgParams& p, int& npos, int& tiles) {
 // variant on any shape: tests).
 int conv3x3_halo_ok(const IgParams& p) {
   const Policy& pol = *p.pol;
-  if (!pol[kHaloEnable] || p.stem || p.pro_scale || p.ap.y || p.nphase != 1 || p.ish != 1 || p.isw != 1 || p.osh != 1 ||
+  if (!pol[kHaloEnable] || (!p.fwd && !pol[kHaloDgrad]) || p.stem || p.pro_scale || p.ap.y || p.nphase != 1 || p.ish != 1 || p.isw != 1 || p.osh != 1 ||
       p.osw != 1)
     return 0;
   const IgPhase& ph = p.ph[0];

@@ -41,7 +41,8 @@ enum TuneKey : int {
   kFp8Passes = 37,      // ARGUS_FP8: which passes take MX-fp8 operands (1 fwd | 2 dgrad | 4 dgrad with apply)
   kDgradApStaged = 38,  // 1x1 dgrad with an apply prologue: register-staged (1) or apply kernel + glds (0)
   kGldsDgrad = 39,      // data gradients may run on the glds kernel (forwards: key 8 alone)
-  kNumTuneKeys = 40
+  kHaloDgrad = 40,      // 3x3 data gradients may run on the LDS-halo kernel (forwards: key 10 alone)
+  kNumTuneKeys = 41
 };
 struct Policy {
   int v[kNumTuneKeys];
