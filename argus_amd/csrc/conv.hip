@@ -812,11 +812,17 @@ __global__ __launch_bounds__(256) void images_to_nhwc4_kernel(const In* __restri
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
     const int64_t img = i / hw, pix = i - img * hw;
     const In* src = x + img * 3 * hw + pix;
-    T* dst = out + i * 4;
-    dst[0] = from_f32<T>(pixel_f32(src[0]));
-    dst[1] = from_f32<T>(pixel_f32(src[hw]));
-    dst[2] = from_f32<T>(pixel_f32(src[2 * hw]));
-    dst[3] = from_f32<T>(0.f);
+    if constexpr (sizeof(T) == 2) {  // the pixel's 4 bf16 as one 8-byte store
+      const T v[4] = {from_f32<T>(pixel_f32(src[0])), from_f32<T>(pixel_f32(src[hw])),
+                      from_f32<T>(pixel_f32(src[2 * hw])), from_f32<T>(0.f)};
+      *reinterpret_cast<uint2*>(out + i * 4) = __builtin_bit_cast(uint2, v);
+    } else {
+      T* dst = out + i * 4;
+      dst[0] = from_f32<T>(pixel_f32(src[0]));
+      dst[1] = from_f32<T>(pixel_f32(src[hw]));
+      dst[2] = from_f32<T>(pixel_f32(src[2 * hw]));
+      dst[3] = from_f32<T>(0.f);
+    }
   }
 }
 
