@@ -532,8 +532,11 @@ ARGUS_DEV int swz32(int row) { return (row & 3) | (((row >> 3) & 1) << 2); }
 // Two workgroups per CU; the 128x128 tile keeps a single staged k-step in registers (the 2-deep ring
 // would not fit two waves per SIMD without spilling; with it at one or two waves per SIMD, or as two
 // 256-thread sub-pipelines per workgroup, it measured slower: DESIGN.md §5).
+#ifndef ARGUS_WGRAD_OCC
+#define ARGUS_WGRAD_OCC 2  // workgroups per CU the register budget targets (a build with 3: A/B variant)
+#endif
 template <typename T, int BM, int BN, bool STEM, bool PRO, bool FAST, bool AP = false>
-__global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgParams p) {
+__global__ __launch_bounds__(256, ARGUS_WGRAD_OCC) void wgrad_kernel(const WgParams p) {
   constexpr int E = Chunk<T>::E;
   constexpr bool BF = (E == 8);
   constexpr int BKP = BF ? 64 : 32;               // pixels per k-step
