@@ -532,8 +532,13 @@ ARGUS_DEV int swz32(int row) { return (row & 3) | (((row >> 3) & 1) << 2); }
 // Two workgroups per CU; the 128x128 tile keeps a single staged k-step in registers (the 2-deep ring
 // would not fit two waves per SIMD without spilling; with it at one or two waves per SIMD, or as two
 // 256-thread sub-pipelines per workgroup, it measured slower: DESIGN.md §5).
+// Register budget of the weight gradient: launch bounds for 3 workgroups per CU. Its LDS (64 KB) still
+// admits 2 per CU, but the 128x128 apply-staging variant drops from 204 to 142 VGPRs (no spill), so
+// the main stream's 1x1 data gradients (128 VGPRs, 25 KB LDS) can share a CU with two of them instead
+// of waiting for them to retire: paired bench runs on one box 9068 / 9078 vs 9012 / 9014 img/s (B=64),
+// 376x672 and B=256 level (profiles/r04_pairs_lb1_occ3.txt, r04_pairs_occ3.txt).
 #ifndef ARGUS_WGRAD_OCC
-#define ARGUS_WGRAD_OCC 2  // workgroups per CU the register budget targets (a build with 3: A/B variant)
+#define ARGUS_WGRAD_OCC 3
 #endif
 template <typename T, int BM, int BN, bool STEM, bool PRO, bool FAST, bool AP = false>
 __global__ __launch_bounds__(256, ARGUS_WGRAD_OCC) void wgrad_kernel(const WgParams p) {
@@ -1115,7 +1120,10 @@ static const Policy kDefaultPolicy = [] {
   p.v[kWgHaloEnable] = 1;
   p.v[kWgHaloTarget] = 256;
   p.v[kHaloMinGrid] = 256;
-  p.v[kWgHaloMaxTiles] = 4;
+  // 14: the halo weight gradient for 3x3 convs of up to 64 (64 x 64) channel tiles, i.e. every layer
+  //     (round 4; 4 = layers 1-2 only before): engine A/B 13.86-14.05 vs 14.07-14.20 ms (B=64),
+  //     48.0 vs 48.5-48.9 ms (B=256), 93.6 vs 95.5-96.0 ms (376x672 B=128): profiles/r04_ab_key14.txt
+  p.v[kWgHaloMaxTiles] = 64;
   p.v[kStemLdsFwd] = 1;
   p.v[kWgradTarget3x3] = 512;
   p.v[kStemLdsWgrad] = 1;
@@ -1128,6 +1136,9 @@ static const Policy kDefaultPolicy = [] {
   //     engine A/B 14.73-14.96 vs 14.76-14.88 ms (B=64), 51.5 vs 51.6 (B=256), 99.6 vs 100.2-100.6
   //     (376x672 B=128): profiles/r04_ab_key38.txt
   p.v[kDgradApStaged] = 0;
+  // 39 / 40: data gradients may use the glds / LDS-halo kernels (0 = register-staged igemm): 39 = 0
+  //     14.02-14.05 vs 14.03-14.20 ms at B=64 but 96.6-96.9 vs 95.5-96.0 ms at 376x672; 40 = 0 within
+  //     the instance spread at both (profiles/r04_ab_coresidency.txt)
   p.v[kGldsDgrad] = 1;
   p.v[kHaloDgrad] = 1;
   return p;
