@@ -39,6 +39,10 @@ elif [ "$PART" = c ]; then
     cp gpurun_out/pmc_${TAG}_b512_$DT/summary.json profiles/${TAG}_b512_${DT}_pmc_mfma_summary.json
     cp gpurun_out/pmc_${TAG}_b512_$DT/summary.txt $O/b512_${DT}_pmc_mfma_summary.txt
     cp $O/pmc_traffic_b512_$DT.json profiles/${TAG}_b512_${DT}_pmc_traffic.json
+    python3 tools/profsum.py $(find gpurun_out/prof_${TAG}_b512_$DT/stats -name "*kernel_stats.csv" | head -1) 30 \
+      > $O/b512_${DT}_kernel_summary.txt
+    # keep the merge-back small: the B=512 traces and counter dumps are summarised above
+    find gpurun_out/prof_${TAG}_b512_$DT gpurun_out/pmc_${TAG}_b512_$DT -name "*.csv" -size +2M -delete
   done
   timeout -k 10 240 python3 -u bench.py --dtype fp8 --batch 512 --no-cpu-baseline --steps 5 --warmup 2 \
     > $O/bench_b512_fp8.json 2> $O/bench_b512_fp8.err
