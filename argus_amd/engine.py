@@ -249,14 +249,18 @@ class ResNetEngine:
             if not cv.desc.stem:
                 max_bwd = max(max_bwd, L.dll.argus_conv_dgrad_bn_rows(C.byref(cv.desc), self.cdt) * cv.desc.c)
         # convs whose data and weight gradient run fused (argus_conv_dgrad_wgrad_bn)
-        # (layer-1 conv3s, and the first block's downsample: the same 64 -> 256 channel 1x1 shape)
+        # (layer-1 conv3s, and the first block's downsample: the same 64 -> 256 channel 1x1 shape). It is a
+        # bf16 kernel: with compute_dtype fp8 it serves these convs too unless the fp8 pass policy (key 37)
+        # gives the 1x1 data gradients MX-fp8 operands (their weight copies are then fp8)
+        f8_1x1 = (self.tuning or {}).get(37, L.dll.argus_conv_policy_default(37)) & 4
+        self.dgw_dt = BF16 if self.cdt == FP8 and not f8_1x1 else self.cdt
         self.dgw = {n for n, cv in convs.items() if self.fuse_dgw and n.endswith((".conv3", ".downsample.0"))
-                    and not cv.desc.stem and L.dll.argus_conv_dgrad_wgrad_ok(C.byref(cv.desc), self.cdt)}
+                    and not cv.desc.stem and L.dll.argus_conv_dgrad_wgrad_ok(C.byref(cv.desc), self.dgw_dt)}
         dgws = 16
         for n in self.dgw:
             d_ = C.byref(convs[n].desc)
-            max_bwd = max(max_bwd, L.dll.argus_conv_dgrad_wgrad_bn_rows(d_, self.cdt) * convs[n].desc.c)
-            dgws = max(dgws, L.dll.argus_conv_dgrad_wgrad_workspace_bytes(d_, self.cdt))
+            max_bwd = max(max_bwd, L.dll.argus_conv_dgrad_wgrad_bn_rows(d_, self.dgw_dt) * convs[n].desc.c)
+            dgws = max(dgws, L.dll.argus_conv_dgrad_wgrad_workspace_bytes(d_, self.dgw_dt))
         self.dgw_ws = torch.empty(dgws, dtype=torch.uint8, device=self.device)  # main stream only
         self.bwd_part = self._f(max_bwd * 2)
         self.bwd_part2 = self._f(max_bwd * 2)  # second branch (downsample BN) of a dual reduce
@@ -733,7 +737,7 @@ class ResNetEngine:
         pro = BnBwdPrologue(ptr(py), ptr(pc[0]), ptr(pc[1]), ptr(pc[2]), None)
         self._guard(dx)
         self._launch(cv, 1, lambda: self.L.conv_dgrad_wgrad_bn(
-            C.byref(cv.desc), self.cdt, ptr(dm), ptr(cv.wd), ptr(x), ptr(dx), ptr(addend),
+            C.byref(cv.desc), self.dgw_dt, ptr(dm), ptr(cv.wd), ptr(x), ptr(dx), ptr(addend),
             C.byref(e) if e is not None else None, C.byref(pro), ptr(G[conv + ".weight"]), ptr(self.dgw_ws),
             self.dgw_ws.numel(), stream()))
         return 0
