@@ -1141,6 +1141,7 @@ static const Policy kDefaultPolicy = [] {
   //     the instance spread at both (profiles/r04_ab_coresidency.txt)
   p.v[kGldsDgrad] = 1;
   p.v[kHaloDgrad] = 1;
+  p.v[kGldsDgradStages] = 3;
   return p;
 }();
 

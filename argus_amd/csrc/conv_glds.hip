@@ -41,11 +41,13 @@ ARGUS_DEV void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int BM, int BN, int BW>
+// NSTAGE 3: k-steps kt+1 and kt+2 in flight during compute(kt) (144 KB LDS for 256 x 128); 2: kt+1
+// only, 96 KB, so a workgroup fits beside one side-stream weight-gradient workgroup (64 KB) on a CU
+template <int BM, int BN, int BW, int NSTAGE = 3>
 __global__ __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) void igemm_glds_kernel(const IgParams p) {
   constexpr int WM = BM / 64, WN = BN / 64, NW = WM * WN, NT = NW * 64;
   constexpr int STAGE = (BM + BN) * 128;      // bytes per pipeline stage (A image, then B image)
-  constexpr int NSTAGE = 3;
+  static_assert(NSTAGE == 2 || NSTAGE == 3, "glds ring depth");
   constexpr int LD = BN + 8;                   // epilogue C row stride (elements)
   constexpr int EPI = BM * LD * 2;
   constexpr int LDS0 = NSTAGE * STAGE > EPI ? NSTAGE * STAGE : EPI;
@@ -61,7 +63,9 @@ __global__ __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) void igemm_glds_kern
   const int mtiles = (ph.M + BM - 1) / BM;
   const int ntiles = p.N / BN;
   const int nwg = mtiles * ntiles;
-  __shared__ int fin_flag;
+  // the folded finalize's ticket flag: the last 16 bytes of the LDS array (bn_fin_arrive's scratch is its
+  // first NT * 32 bytes), so the 2-stage ring stays at exactly 96 KB
+  int& fin_flag = *reinterpret_cast<int*>(&lds[LDS_BYTES / 16 - 1]);
   if ((int)blockIdx.x >= nwg) {
     if constexpr (BW != 0) {
       const int e = blockIdx.x - nwg;
@@ -162,15 +166,24 @@ __global__ __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) void igemm_glds_kern
     }
   };
 
-  // ---- main loop: 3-stage ring, k-steps kt+1 and kt+2 in flight during compute(kt) ----
+  // ---- main loop: NSTAGE-deep ring ----
   const int nk = ph.K / 64;
   if (nk > 0) issue(0, 0);
-  if (nk > 1) issue(1, 1);
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) wait_vmcnt<GPS>(); else wait_vmcnt<0>();
-    raw_barrier();  // stage kt landed for every wave; every wave finished reading stage kt-1
-    if (kt + 2 < nk) issue(kt + 2, (kt + 2) % NSTAGE);
-    compute(kt % NSTAGE);
+  if constexpr (NSTAGE == 3) {  // k-steps kt+1 and kt+2 in flight during compute(kt)
+    if (nk > 1) issue(1, 1);
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) wait_vmcnt<GPS>(); else wait_vmcnt<0>();
+      raw_barrier();  // stage kt landed for every wave; every wave finished reading stage kt-1
+      if (kt + 2 < nk) issue(kt + 2, (kt + 2) % NSTAGE);
+      compute(kt % NSTAGE);
+    }
+  } else {  // k-step kt+1 in flight during compute(kt)
+    for (int kt = 0; kt < nk; ++kt) {
+      wait_vmcnt<0>();
+      raw_barrier();  // stage kt landed for every wave; every wave finished reading stage kt-1 (= kt+1's)
+      if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
+      compute(kt & 1);
+    }
   }
   wait_vmcnt<0>();
   __syncthreads();  // LDS is reused below
@@ -293,30 +306,37 @@ __global__ __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) void igemm_glds_kern
   }
 }
 
-template <int BM, int BN, int BW>
+template <int BM, int BN, int BW, int NS>
 static const char* glds_name() {
   static const std::string s = std::string("argus::igemm_glds_kernel<") + std::to_string(BM) + ", " +
-                               std::to_string(BN) + ", " + std::to_string(BW) + ">";
+                               std::to_string(BN) + ", " + std::to_string(BW) + ", " + std::to_string(NS) + ">";
   return s.c_str();
 }
 
-template <int BM, int BN, int BW>
+template <int BM, int BN, int BW, int NS>
 static void launch_glds1(const IgParams& p0, int maxM, hipStream_t st) {
   IgParams p = p0;
   plan_fin(p, BM);
   dim3 grid(cdiv(maxM, BM) * (p.N / BN), 1, p.nphase);
-  timed_launch(glds_name<BM, BN, BW>(), igemm_glds_kernel<BM, BN, BW>, grid, dim3((BM / 64) * (BN / 64) * 64), st,
-               p);
+  timed_launch(glds_name<BM, BN, BW, NS>(), igemm_glds_kernel<BM, BN, BW, NS>, grid,
+               dim3((BM / 64) * (BN / 64) * 64), st, p);
 }
 
+template <int BM, int BN, int NS>
+static void launch_glds_ns(const IgParams& p, int maxM, hipStream_t st) {
+  switch (bwd_variant(p.bb)) {
+    case 2: launch_glds1<BM, BN, 2, NS>(p, maxM, st); break;
+    case 3: launch_glds1<BM, BN, 3, NS>(p, maxM, st); break;
+    case 4: launch_glds1<BM, BN, 4, NS>(p, maxM, st); break;
+    default: launch_glds1<BM, BN, 0, NS>(p, maxM, st);
+  }
+}
+
+// policy key 41: ring depth of the data gradients (the forwards keep 3: no side stream beside them)
 template <int BM, int BN>
 static void launch_glds(const IgParams& p, int maxM, hipStream_t st) {
-  switch (bwd_variant(p.bb)) {
-    case 2: launch_glds1<BM, BN, 2>(p, maxM, st); break;
-    case 3: launch_glds1<BM, BN, 3>(p, maxM, st); break;
-    case 4: launch_glds1<BM, BN, 4>(p, maxM, st); break;
-    default: launch_glds1<BM, BN, 0>(p, maxM, st);
-  }
+  if (!p.fwd && (*p.pol)[kGldsDgradStages] == 2) launch_glds_ns<BM, BN, 2>(p, maxM, st);
+  else launch_glds_ns<BM, BN, 3>(p, maxM, st);
 }
 
 // policy key 8: smallest K (taps*C) served by the glds kernel (0 = off); 512 -> 1024 after the

@@ -42,7 +42,8 @@ enum TuneKey : int {
   kDgradApStaged = 38,  // 1x1 dgrad with an apply prologue: register-staged (1) or apply kernel + glds (0)
   kGldsDgrad = 39,      // data gradients may run on the glds kernel (forwards: key 8 alone)
   kHaloDgrad = 40,      // 3x3 data gradients may run on the LDS-halo kernel (forwards: key 10 alone)
-  kNumTuneKeys = 41
+  kGldsDgradStages = 41,  // LDS ring depth of the glds data gradients (3, or 2: 96 KB)
+  kNumTuneKeys = 42
 };
 struct Policy {
   int v[kNumTuneKeys];

@@ -1395,3 +1395,38 @@ def test_fused_dgrad_wgrad_matches_separate_passes(cuda):
         torch.cuda.synchronize()
         assert torch.equal(x_fused.cpu(), x_ref.cpu()), (n, h, w_)
         assert _rel(dw_f, dw_ref) < 1e-5, (n, h, w_)
+
+
+def test_glds_two_stage_ring_matches_three(cuda):
+    """The 96 KB two-stage glds ring (policy key 41 = 2, data gradients only) against the three-stage
+    ring: same k order, so dx and the BN-backward partials are bit-identical (plain and BN-epilogue
+    dgrads; 1x1 K = 1024 and a 3x3 K = 9 * 128 shape, the size thresholds lowered per call)."""
+    from argus_amd._lib import BnBwdEpilogue
+
+    torch.manual_seed(41)
+    L = lib()
+    for cin, cout, k, hin, n in [(256, 1024, 1, 12, 8), (128, 128, 3, 14, 8)]:
+        d0, _ = _desc(n, hin, hin, cin, cout, k, 1)
+        w = torch.randn(cout, k, k, cin) * (2.0 / (k * k * cin)) ** 0.5
+        _, wt = _prep(d0, "bf16", w.to(cuda), cuda)
+        dy = torch.randn(n, d0.ho, d0.wo, cout, device=cuda).to(torch.bfloat16)
+        yb = torch.randn(n, hin, hin, cin, device=cuda).to(torch.bfloat16)
+        mean, invstd = torch.randn(cin, device=cuda) * 0.1, torch.rand(cin, device=cuda) + 0.5
+        sc, sh = torch.randn(cin, device=cuda), torch.randn(cin, device=cuda)
+        outs = []
+        for stages in (3, 2):
+            d = d0.with_tuning({36: 1, 9: 1, 10: 0, 41: stages})  # glds for this small shape, no halo
+            assert L.dll.argus_conv_launch_info(C.byref(d), BF16, 1, None) > 0
+            rows = L.dll.argus_conv_dgrad_bn_rows(C.byref(d), BF16)
+            part = torch.zeros(rows, cin, 2, device=cuda)
+            e = BnBwdEpilogue()
+            e.y, e.mean, e.invstd, e.mask_mode, e.scale, e.shift, e.part = ptr(yb), ptr(mean), ptr(invstd), 2, \
+                ptr(sc), ptr(sh), ptr(part)
+            dm = torch.empty(n, hin, hin, cin, dtype=torch.bfloat16, device=cuda)
+            dx = torch.empty(n, hin, hin, cin, dtype=torch.bfloat16, device=cuda)
+            L.conv_dgrad_bn(C.byref(d), BF16, ptr(dy), ptr(wt), ptr(dm), None, C.byref(e), None, stream())
+            L.conv_dgrad(C.byref(d), BF16, ptr(dy), ptr(wt), ptr(dx), None, None, stream())
+            torch.cuda.synchronize()
+            outs.append((dm.cpu(), part.cpu(), dx.cpu()))
+        for a, b in zip(*outs):
+            assert torch.equal(a, b), (cin, cout, k)
