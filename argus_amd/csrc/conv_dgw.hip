@@ -83,6 +83,7 @@ ARGUS_DEV u32x4 dgw_frag_tr(const u32x4* img, int slot, int g, int i16) {
 struct DgwStage {
   u32x4 dm[4], y[4];  // rows tid/32 + 8i, channel chunk tid%32
   u32x4 x;            // row tid/8, channel chunk tid%8
+  u32x4 y2;           // BNE: the epilogue's BN input at the same (row, chunk) as x
 };
 
 }  // namespace
@@ -91,8 +92,10 @@ struct DgwStage {
 // plain store of dx (+ addend: the first block's downsample, accumulated onto conv1's dgrad)
 template <bool BNE>
 __global__ __launch_bounds__(256, 2) void dgw1x1_kernel(const DgwParams p) {
-  // dy3 tile (2 images of 128 channels), a2 tile, W (2 images): 56 KB, two workgroups per CU
+  // dy3 tile (2 images of 128 channels), a2 tile, W (2 images): 56 KB, two workgroups per CU; the
+  // per-channel constants (apply coefficients of dy3, bn2's mean / invstd / scale / shift): 4 KB
   __shared__ __attribute__((aligned(16))) u32x4 lds[3 * kImg + 2 * kImgW];
+  __shared__ __attribute__((aligned(16))) float cst[3 * kKo + 4 * kCi];
   u32x4* DY = lds;
   u32x4* XA = lds + 2 * kImg;
   u32x4* WD = lds + 3 * kImg;
@@ -107,6 +110,18 @@ __global__ __launch_bounds__(256, 2) void dgw1x1_kernel(const DgwParams p) {
     WD[(c >> 4) * kImgW + dgw_pos(row, c & 15)] = ld16(p.wd + row * kKo + c * 8);
   }
 
+  for (int i = tid; i < kKo; i += 256) {
+    cst[i] = p.ca[i];
+    cst[kKo + i] = p.cb[i];
+    cst[2 * kKo + i] = p.cc[i];
+  }
+  if (BNE && tid < kCi) {
+    float* b2 = cst + 3 * kKo;
+    b2[tid] = p.bb.mean[tid];
+    b2[kCi + tid] = p.bb.invstd[tid];
+    b2[2 * kCi + tid] = p.bb.sc[tid];
+    b2[3 * kCi + tid] = p.bb.sh[tid];
+  }
   const int ca_c = tid % 32;  // this thread's dy3 channel chunk (apply)
   const int xc = tid % 8;     // its a2 / dx channel chunk (staging, epilogue)
   float esum[8], exs[8];  // bn2 partial sums of this thread's channel chunk: sum dm, sum dm*xhat
@@ -120,7 +135,9 @@ __global__ __launch_bounds__(256, 2) void dgw1x1_kernel(const DgwParams p) {
       S.dm[i] = ld16(p.dm + (size_t)m * kKo + ca_c * 8);
       S.y[i] = ld16(p.y + (size_t)m * kKo + ca_c * 8);
     }
-    S.x = ld16(p.x + (size_t)min(t * kBr + tid / 8, p.P - 1) * kCi + xc * 8);
+    const size_t xo = (size_t)min(t * kBr + tid / 8, p.P - 1) * kCi + xc * 8;
+    S.x = ld16(p.x + xo);
+    if constexpr (BNE) S.y2 = ld16(reinterpret_cast<const bf16*>(p.bb.y) + xo);  // (the epilogue's, in flight)
   };
 
   f32x4 wacc[4][4];  // dW[ko = 64*wave + 16*mi + 4g + r][ci = 16*ni + i16]
@@ -135,11 +152,14 @@ __global__ __launch_bounds__(256, 2) void dgw1x1_kernel(const DgwParams p) {
   if (t < ntiles) load(t, S);
   for (; t < ntiles; t += gridDim.x) {
     // ---- stage dy3 = ca*dm + cb*y + cc (fp32, rounded to bf16; rows past P are zero) and a2 ----
+    if (t == (int)blockIdx.x) __syncthreads();  // the constants in LDS (first tile)
+    u32x4 y2cur;  // this tile's epilogue BN input (S is refilled with the next tile below)
+    if constexpr (BNE) y2cur = S.y2;
     {
-      float ca[8], cb[8], cc[8];  // reloaded per tile (L1-resident): registers go to the accumulators
-      BwdEpiAcc<bf16, 3>::ld(ca, p.ca + ca_c * 8);
-      BwdEpiAcc<bf16, 3>::ld(cb, p.cb + ca_c * 8);
-      BwdEpiAcc<bf16, 3>::ld(cc, p.cc + ca_c * 8);
+      float ca[8], cb[8], cc[8];  // from LDS: registers go to the accumulators
+      BwdEpiAcc<bf16, 3>::ld(ca, cst + ca_c * 8);
+      BwdEpiAcc<bf16, 3>::ld(cb, cst + kKo + ca_c * 8);
+      BwdEpiAcc<bf16, 3>::ld(cc, cst + 2 * kKo + ca_c * 8);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int row = tid / 32 + 8 * i;
@@ -201,15 +221,16 @@ __global__ __launch_bounds__(256, 2) void dgw1x1_kernel(const DgwParams p) {
       }
       st16_nt(p.out + off, v);
     }
-    if (BNE && m < p.P) {  // BwdEpiAcc<bf16, 2>::step with the per-channel constants reloaded (L1)
+    if (BNE && m < p.P) {  // BwdEpiAcc<bf16, 2>::step with the per-channel constants from LDS
       const size_t off = (size_t)m * kCi + xc * 8;
       float d[8], yv[8], mu[8], is[8], sc[8], sh[8];
       unpack(*reinterpret_cast<const u32x4*>(Cs + (tid / 8) * LD + xc * 8), d);
-      unpack(ld16(reinterpret_cast<const bf16*>(p.bb.y) + off), yv);
-      BwdEpiAcc<bf16, 3>::ld(mu, p.bb.mean + xc * 8);
-      BwdEpiAcc<bf16, 3>::ld(is, p.bb.invstd + xc * 8);
-      BwdEpiAcc<bf16, 3>::ld(sc, p.bb.sc + xc * 8);
-      BwdEpiAcc<bf16, 3>::ld(sh, p.bb.sh + xc * 8);
+      unpack(y2cur, yv);
+      const float* b2 = cst + 3 * kKo;
+      BwdEpiAcc<bf16, 3>::ld(mu, b2 + xc * 8);
+      BwdEpiAcc<bf16, 3>::ld(is, b2 + kCi + xc * 8);
+      BwdEpiAcc<bf16, 3>::ld(sc, b2 + 2 * kCi + xc * 8);
+      BwdEpiAcc<bf16, 3>::ld(sh, b2 + 3 * kCi + xc * 8);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         d[j] = fmaf(yv[j], sc[j], sh[j]) > 0.f ? d[j] : 0.f;
