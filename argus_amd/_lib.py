@@ -18,7 +18,7 @@ import torch  # noqa: F401  (must precede the CDLL, see module docstring)
 LIB_PATH = Path(os.environ.get("ARGUS_HIP_LIB", Path(__file__).resolve().parent / "libargus_hip.so"))
 
 F32, BF16, FP8 = 0, 1, 2
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 
 class Tuning(C.Structure):
@@ -119,6 +119,8 @@ SIGNATURES = {
     "argus_maxpool_bwd": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "argus_maxpool_bwd_bn_rows": (_I, [_I, _I, _I, _I, _I]),
     "argus_maxpool_bwd_bn": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "argus_maxpool_bwd_bn_fin": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                                      _P, _P, _P]),
     "argus_avgpool_fwd": (_I, [_I, _I, _I, _I, _P, _P, _P]),
     "argus_avgpool_bwd": (_I, [_I, _I, _I, _I, _P, _P, _P]),
     "argus_gemm_f32_workspace_bytes": (_SZ, [_I, _I, _I]),

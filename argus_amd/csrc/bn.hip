@@ -10,6 +10,7 @@
 // reduction (deterministic, run-to-run bitwise reproducible).
 #include "common.h"
 #include "internal.h"
+#include "bnfin.h"
 #include "ktimer.h"
 
 namespace argus {
@@ -545,13 +546,18 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(int n, int H, int W, i
 // dm = dz * (y0*scale+shift > 0) is stored instead of dz, and each block writes its column partials
 // {sum dm, sum dm*(y0-mean)*invstd} (a thread's channel chunk is fixed: the grid stride is a multiple
 // of the chunks per pixel) — one partial row per block, the input of argus_bn_bwd_finalize.
+// fin.mode: that finalize is folded in (bnfin.h, one producer tile per block, 64-channel column
+// tiles): the last blocks to finish merge the rows and write dgamma/dbeta/ca/cb/cc while the pass is
+// still resident. A separate finalize launch here is the first main-stream kernel after the pass and
+// waits for CUs behind the side stream's layer-1 weight gradients (54 us of 60 in profiles/r04c_timeline.txt).
 template <typename T, bool BNE>
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(int n, int H, int W, int C, int Ho, int Wo,
                                                           const T* __restrict__ dout, const uint8_t* __restrict__ amax,
                                                           T* __restrict__ dz, const T* __restrict__ y,
                                                           const float* __restrict__ sc, const float* __restrict__ sh,
                                                           const float* __restrict__ mean,
-                                                          const float* __restrict__ invstd, float2* __restrict__ part) {
+                                                          const float* __restrict__ invstd, float2* __restrict__ part,
+                                                          const BnFin fin) {
   constexpr int E = Chunk<T>::E;
   typedef typename AmaxVec<E>::type AV;
   const int CH = C / E;
@@ -637,7 +643,14 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(int n, int H, int W, i
       const float2* plane = red + (col % E) * lanes * CH + col / E;  // channel col = chunk * E + j
       float2 a = plane[0];
       for (int l = 1; l < lanes; ++l) { a.x += plane[l * CH].x; a.y += plane[l * CH].y; }
-      part[(size_t)blockIdx.x * C + col] = a;
+      if (fin.mode) store_part(part + (size_t)blockIdx.x * C + col, a);  // write-through for the merge
+      else part[(size_t)blockIdx.x * C + col] = a;
+    }
+    if (fin.mode) {
+      __shared__ int flag;
+      // red is free once fin_ticket's barrier has passed (>= 256 * 32 bytes: E >= 4)
+      for (int nt = 0; nt < C / 64; ++nt)
+        bn_fin_arrive<256, 64>(fin, blockIdx.x, nt, reinterpret_cast<double2*>(red), &flag);
     }
   }
 }
@@ -690,12 +703,20 @@ template <typename T, bool DU> static const char* bapp_name() {
   return s.c_str();
 }
 
-static int grid_for(int64_t work) {
+static int grid_for(int64_t work, int64_t cap = 8192) {
   int64_t b = (work + 255) / 256;
-  if (b > 8192) b = 8192;
+  if (b > cap) b = cap;
   if (b < 1) b = 1;
   return (int)b;
 }
+
+// maxpool backward with the stem BN reduction fused writes one partial row per block, which the serial
+// bwd_finalize at the end of the backward pass merges: 2048 blocks (8 per CU, 32 waves: a full CU) keep
+// the gather pass's occupancy and cut the merge to 2 load batches per lane (8192 rows took 4 + ~50 us).
+#ifndef ARGUS_MPB_BLOCKS
+#define ARGUS_MPB_BLOCKS 2048
+#endif
+constexpr int64_t kMaxpoolBwdBlocks = ARGUS_MPB_BLOCKS;
 
 }  // namespace argus
 
@@ -890,12 +911,20 @@ int argus_maxpool_bwd(int dtype, int n, int h, int w, int c, const void* dout, c
 
 int argus_maxpool_bwd_bn_rows(int dtype, int n, int h, int w, int c) {
   const int E = dtype == ARGUS_BF16 ? 8 : 4;
-  return c % E ? -1 : grid_for((int64_t)n * h * w * (c / E));
+  return c % E ? -1 : grid_for((int64_t)n * h * w * (c / E), kMaxpoolBwdBlocks);
 }
 
 int argus_maxpool_bwd_bn(int dtype, int n, int h, int w, int c, const void* dout, const uint8_t* amax, void* dm,
                          const void* y, const float* scale, const float* shift, const float* mean,
                          const float* invstd, float* part, argus_stream_t stream) {
+  return argus_maxpool_bwd_bn_fin(dtype, n, h, w, c, dout, amax, dm, y, scale, shift, mean, invstd, part, nullptr,
+                                  nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, stream);
+}
+
+int argus_maxpool_bwd_bn_fin(int dtype, int n, int h, int w, int c, const void* dout, const uint8_t* amax, void* dm,
+                             const void* y, const float* scale, const float* shift, const float* mean,
+                             const float* invstd, float* part, const float* gamma, float* dgamma, float* dbeta,
+                             float* ca, float* cb, float* cc, void* workspace, argus_stream_t stream) {
   const int E = dtype == ARGUS_BF16 ? 8 : 4;
   if (c % E || 256 % (c / E) || c > 256) { set_error("maxpool_bwd: bad channels"); return ARGUS_ERR_SHAPE; }
   if ((int64_t)n * h * w * c >= (1LL << 31)) { set_error("maxpool_bwd: tensor exceeds 2^31 elements"); return ARGUS_ERR_SHAPE; }
@@ -905,9 +934,25 @@ int argus_maxpool_bwd_bn(int dtype, int n, int h, int w, int c, const void* dout
   const int64_t work = (int64_t)n * h * w * (c / E);
   hipStream_t st = (hipStream_t)stream;
   float2* pt = reinterpret_cast<float2*>(part);
+  BnFin f{};
+  if (workspace) {  // the finalize folded in
+    if (!bne || !gamma || !ca || !cb || !cc || c % 64) {
+      set_error("maxpool_bwd_bn_fin: bad finalize arguments (needs y, gamma, ca/cb/cc, channels % 64 == 0)");
+      return ARGUS_ERR_ARG;
+    }
+    f.mode = 2; f.C = c; f.count = (long long)n * h * w;
+    bn_fin_plan(f, grid_for(work, kMaxpoolBwdBlocks), 1);
+    f.rows = f.T;
+    if ((size_t)(c / 64) * (f.ng + 1) * 4 > kBnCounterBytes) { set_error("maxpool_bwd_bn_fin: too many groups"); return ARGUS_ERR_ARG; }
+    f.cnt = reinterpret_cast<unsigned*>(workspace);
+    f.red = reinterpret_cast<double2*>(reinterpret_cast<char*>(workspace) + kBnCounterBytes);
+    f.part = pt;
+    f.gamma = gamma; f.bmean = mean; f.binvstd = invstd;
+    f.dgamma = dgamma; f.dbeta = dbeta; f.ca = ca; f.cb = cb; f.cc = cc;
+  }
 #define ARGUS_MPB(TT, B)                                                                                          \
-  hipLaunchKernelGGL((maxpool_bwd_kernel<TT, B>), dim3(grid_for(work)), dim3(256), 0, st, n, h, w, c, ho, wo,     \
-                     (const TT*)dout, amax, (TT*)dm, (const TT*)y, scale, shift, mean, invstd, pt)
+  hipLaunchKernelGGL((maxpool_bwd_kernel<TT, B>), dim3(grid_for(work, kMaxpoolBwdBlocks)), dim3(256), 0, st, n, h, w, c, ho, wo,     \
+                     (const TT*)dout, amax, (TT*)dm, (const TT*)y, scale, shift, mean, invstd, pt, f)
   if (dtype == ARGUS_BF16) {
     if (bne) ARGUS_MPB(bf16, true); else ARGUS_MPB(bf16, false);
   } else {

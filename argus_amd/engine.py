@@ -114,6 +114,8 @@ class ResNetEngine:
         # the separate bwd_finalize kernels. The forward statistics keep their own
         # finalize launch (folding it into the conv measured neutral).
         self.fold_fin = True
+        # ... and the stem BN's finalize into the maxpool backward pass (argus_maxpool_bwd_bn_fin)
+        self.fold_stem_fin = True
         self._side: torch.cuda.Stream | None = None
         self._pending: dict = {}  # buffer data_ptr -> (seq, event) of the last side-stream wgrad reading it
         self._last_side = None
@@ -660,10 +662,16 @@ class ResNetEngine:
             # maxpool backward + the stem BN's backward reduction in one pass (stores dm0), finalize, then
             # the stem weight gradient stages dy0 = ca*dm0 + cb*y0 + cc itself (dy0 is never written)
             st, cf = self.bn_state["resnet.bn1"], self.bn_coef["resnet.bn1"]
-            L.maxpool_bwd_bn(dt, N, H1, W1, 64, ptr(dh), ptr(self.amax), ptr(dz0), ptr(self.y0), ptr(st[2]),
-                             ptr(st[3]), ptr(st[0]), ptr(st[1]), ptr(self.bwd_part), s)
-            self._bn_bwd_fin(P, G, "resnet.bn1", N * H1 * W1, 64, self.bwd_part,
-                             L.dll.argus_maxpool_bwd_bn_rows(dt, N, H1, W1, 64))
+            if self.fold_fin and self.fold_stem_fin:  # the finalize folded into the pass's last workgroups
+                L.maxpool_bwd_bn_fin(dt, N, H1, W1, 64, ptr(dh), ptr(self.amax), ptr(dz0), ptr(self.y0),
+                                     ptr(st[2]), ptr(st[3]), ptr(st[0]), ptr(st[1]), ptr(self.bwd_part),
+                                     ptr(P["resnet.bn1.weight"]), ptr(G["resnet.bn1.weight"]),
+                                     ptr(G["resnet.bn1.bias"]), ptr(cf[0]), ptr(cf[1]), ptr(cf[2]), ptr(self.bn_ws), s)
+            else:
+                L.maxpool_bwd_bn(dt, N, H1, W1, 64, ptr(dh), ptr(self.amax), ptr(dz0), ptr(self.y0), ptr(st[2]),
+                                 ptr(st[3]), ptr(st[0]), ptr(st[1]), ptr(self.bwd_part), s)
+                self._bn_bwd_fin(P, G, "resnet.bn1", N * H1 * W1, 64, self.bwd_part,
+                                 L.dll.argus_maxpool_bwd_bn_rows(dt, N, H1, W1, 64))
             cv = self.convs["resnet.conv1"]
             ap = BnBwdPrologue(ptr(self.y0), ptr(cf[0]), ptr(cf[1]), ptr(cf[2]), None)
             fn = lambda: L.conv_wgrad_apply(C.byref(cv.desc), dt, ptr(self.x0), ptr(dz0), C.byref(ap),  # noqa: E731

@@ -305,6 +305,17 @@ int argus_maxpool_bwd_bn_rows(int dtype, int n, int h, int w, int c);
 int argus_maxpool_bwd_bn(int dtype, int n, int h, int w, int c, const void* dout, const uint8_t* argmax,
                          void* dm, const void* y, const float* scale, const float* shift,
                          const float* mean, const float* invstd, float* part, argus_stream_t stream);
+/* argus_maxpool_bwd_bn with argus_bn_bwd_finalize folded in (ABI 13; c % 64 == 0): the last workgroups
+ * of the pass merge `part` (write-through, deterministic fixed order) and write dgamma/dbeta (may be
+ * NULL) and ca/cb/cc exactly as argus_bn_bwd_finalize(c, rows, part, n*h*w, gamma, mean, invstd, ...)
+ * would; `workspace` is an argus_bn_workspace_bytes(c) BN workspace (zeroed once, not shared between
+ * concurrent streams). workspace == NULL: argus_maxpool_bwd_bn. Backward of the torchvision stem
+ * bn1 -> relu -> maxpool inside self.resnet(x) (models.py:43,84) under loss.backward() (train.py:316). */
+int argus_maxpool_bwd_bn_fin(int dtype, int n, int h, int w, int c, const void* dout, const uint8_t* argmax,
+                             void* dm, const void* y, const float* scale, const float* shift,
+                             const float* mean, const float* invstd, float* part, const float* gamma,
+                             float* dgamma, float* dbeta, float* ca, float* cb, float* cc, void* workspace,
+                             argus_stream_t stream);
 int argus_avgpool_fwd(int dtype, int n, int hw, int c, const void* x, float* feat,
                       argus_stream_t stream);
 int argus_avgpool_bwd(int dtype, int n, int hw, int c, const float* dfeat, void* dx,

@@ -1196,6 +1196,8 @@ def test_stem_backward_fusions(cuda, dt):
     assert torch.equal(dm.cpu(), (dz.double() * mask).to(TDT[dt]).cpu())
     a, b = part.double().sum(0).cpu(), part_ref.double().sum(0).cpu()
     assert ((a - b).abs() <= 1e-5 * b.abs().max()).all()
+    # the finalize folded into the pass (argus_maxpool_bwd_bn_fin) vs argus_bn_bwd_finalize on the same rows
+    _check_maxpool_fin(L, dt, cuda, n, H, W, dout, amax, y0, sc, sh, mean, invstd, dm, part)
     # stem weight gradient with the apply staged
     ca, cb, cc = (torch.randn(64, device=cuda) * 0.2 for _ in range(3))
     x0 = torch.randn(n, 2 * H, 2 * W, 4, device=cuda).to(TDT[dt])
@@ -1213,6 +1215,53 @@ def test_stem_backward_fusions(cuda, dt):
     L.conv_wgrad_apply(C.byref(d), DT[dt], ptr(x0), ptr(dm), C.byref(ap), ptr(dw), ptr(ws), ws.numel(), stream())
     torch.cuda.synchronize()
     assert torch.equal(dw.cpu(), dw_ref.cpu())
+
+
+def _check_maxpool_fin(L, dt, cuda, n, H, W, dout, amax, y0, sc, sh, mean, invstd, dm_ref, part_ref):
+    rows = L.dll.argus_maxpool_bwd_bn_rows(DT[dt], n, H, W, 64)
+    gamma = torch.rand(64, device=cuda) + 0.5
+    ws = torch.zeros(L.dll.argus_bn_workspace_bytes(64), dtype=torch.uint8, device=cuda)
+    ref = [torch.empty(64, device=cuda) for _ in range(5)]  # dgamma, dbeta, ca, cb, cc
+    L.bn_bwd_finalize(64, rows, ptr(part_ref), n * H * W, ptr(gamma), ptr(mean), ptr(invstd), *(ptr(t) for t in ref),
+                      ptr(ws), stream())
+    outs = []
+    for _ in range(2):  # deterministic, and the ticket counters are left zero for the next call
+        dm, part = torch.empty_like(dm_ref), torch.empty_like(part_ref)
+        o = [torch.full((64,), float("nan"), device=cuda) for _ in range(5)]
+        L.maxpool_bwd_bn_fin(DT[dt], n, H, W, 64, ptr(dout), ptr(amax), ptr(dm), ptr(y0), ptr(sc), ptr(sh), ptr(mean),
+                             ptr(invstd), ptr(part), ptr(gamma), *(ptr(t) for t in o), ptr(ws), stream())
+        torch.cuda.synchronize()
+        assert torch.equal(dm.cpu(), dm_ref.cpu()) and torch.equal(part.cpu(), part_ref.cpu())
+        outs.append(torch.stack(o).cpu())
+    assert torch.equal(outs[0], outs[1])
+    assert (ws[:16384] == 0).all()
+    r = torch.stack(ref).cpu()
+    # both merge the same fp32 rows in fp64 (different grouping), then round to fp32: within 2 ulp
+    assert torch.allclose(outs[0], r, rtol=2.5e-7, atol=1e-12), (outs[0] - r).abs().max()
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+def test_maxpool_bwd_folded_finalize_full_grid(cuda, dt):
+    """argus_maxpool_bwd_bn_fin at a size that caps the pass grid (2048 workgroups = partial rows):
+    dm and the partial rows identical to argus_maxpool_bwd_bn, the folded dgamma/dbeta/ca/cb/cc equal to
+    argus_bn_bwd_finalize's on those rows."""
+    torch.manual_seed(22)
+    L = lib()
+    n, H, W = 8, 112, 112
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    y0 = torch.randn(n, H, W, 64, device=cuda).to(TDT[dt])
+    sc, sh = torch.rand(64, device=cuda) + 0.5, torch.randn(64, device=cuda) * 0.3
+    mean, invstd = torch.randn(64, device=cuda) * 0.1, torch.rand(64, device=cuda) + 0.5
+    pooled = torch.empty(n, Ho, Wo, 64, device=cuda, dtype=TDT[dt])
+    amax = torch.empty(n, Ho, Wo, 64, device=cuda, dtype=torch.uint8)
+    L.maxpool_fwd(DT[dt], n, H, W, 64, ptr(y0), ptr(sc), ptr(sh), ptr(pooled), ptr(amax), stream())
+    dout = torch.randn(n, Ho, Wo, 64, device=cuda).to(TDT[dt])
+    rows = L.dll.argus_maxpool_bwd_bn_rows(DT[dt], n, H, W, 64)
+    assert rows == 2048
+    part, dm = torch.empty(rows, 64, 2, device=cuda), torch.empty_like(y0)
+    L.maxpool_bwd_bn(DT[dt], n, H, W, 64, ptr(dout), ptr(amax), ptr(dm), ptr(y0), ptr(sc), ptr(sh), ptr(mean),
+                     ptr(invstd), ptr(part), stream())
+    _check_maxpool_fin(L, dt, cuda, n, H, W, dout, amax, y0, sc, sh, mean, invstd, dm, part)
 
 
 FP8_CASES = [  # (cin, cout, k, stride, hin, n): reduction channels % 128 == 0 in each pass

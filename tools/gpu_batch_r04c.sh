@@ -1,0 +1,12 @@
+#!/bin/bash
+# dev (round 4, GPU box): stem BN finalize folded into the maxpool backward (argus_maxpool_bwd_bn_fin):
+# its parity tests + the engine parity tests, the kernel trace, then engine A/Bs of fold_stem_fin.
+O=gpurun_out/r04w
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/tests.txt 2>&1 || exit 1
+timeout -s KILL 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/tr -o run -- \
+  python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-val-oracle --no-isolated > $O/tr.json 2>$O/tr.err || exit 1
+python3 tools/profsum.py $O/tr/run_kernel_stats.csv 400 > $O/tr.sum 2>&1 || true
+timeout -k 10 500 python -u tools/engine_ab.py --batch 64 --cfg "" --cfg "fold_stem_fin=0" --cfg "" --cfg "fold_stem_fin=0" > $O/ab64.txt 2>&1 || exit 1
+timeout -k 10 500 python -u tools/engine_ab.py --batch 256 --steps 5 --cfg "" --cfg "fold_stem_fin=0" --cfg "" > $O/ab256.txt 2>&1 || exit 1
