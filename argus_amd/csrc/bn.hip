@@ -632,15 +632,20 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(int n, int H, int W, i
   }
   if constexpr (BNE) {
     // element planes red[j][lane row][chunk]: the 8-byte writes of consecutive threads (consecutive
-    // chunks) are contiguous, no bank conflicts (a [lane row][channel] layout put lanes 8 float2 apart:
-    // SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE 0.82 at 376 x 672); the lane rows are summed in order
-    __shared__ float2 red[256 * E];
+    // chunks) are contiguous (a [lane row][channel] layout put lanes 8 float2 apart: SQ_LDS_BANK_CONFLICT
+    // / SQ_LDS_IDX_ACTIVE 0.82 at 376 x 672); the lane rows are summed in order. The summing reads of
+    // one wave cover the E planes at the same row: planes kPlanePad float2 (64 bytes) apart beyond their
+    // 256 entries, so plane j starts 16 banks after plane j-1 (unpadded, 512 j + 2q put all E planes on
+    // the same banks: 0.70 in r04b_376x672_pmc_mfma_summary.txt)
+    constexpr int kPlanePad = 8;
+    constexpr int PS = 256 + kPlanePad;
+    __shared__ __attribute__((aligned(16))) float2 red[PS * E];  // 16-byte: reused as double2 (fin)
     const int lanes = 256 / CH, ln = threadIdx.x / CH;
 #pragma unroll
-    for (int j = 0; j < E; ++j) red[(j * lanes + ln) * CH + ch0] = make_float2(s[j], t[j]);
+    for (int j = 0; j < E; ++j) red[j * PS + ln * CH + ch0] = make_float2(s[j], t[j]);
     __syncthreads();
     for (int col = threadIdx.x; col < C; col += 256) {
-      const float2* plane = red + (col % E) * lanes * CH + col / E;  // channel col = chunk * E + j
+      const float2* plane = red + (col % E) * PS + col / E;  // channel col = chunk * E + j
       float2 a = plane[0];
       for (int l = 1; l < lanes; ++l) { a.x += plane[l * CH].x; a.y += plane[l * CH].y; }
       if (fin.mode) store_part(part + (size_t)blockIdx.x * C + col, a);  // write-through for the merge
