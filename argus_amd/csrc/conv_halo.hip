@@ -412,8 +412,9 @@ bool conv3x3_halo_launch(const IgParams& p, hipStream_t st) {
 // x[p + off(tap)][c]). A workgroup (8 waves, 2 x 4) owns 64
 // output channels x 9 taps x 64 input channels (a 64 x 576 tile; wave (wm, wn) holds rows 32wm..+31
 // and the 9 column blocks of 16 at 9wn..9wn+8) and reduces over a range of 128-pixel-slot tiles: a
-// TH x TW block of one image (TW divides W; 256 x 256 frames: whole rows, 376 x 672 frames: 3 x 42
-// blocks of the 168- and 84-wide layers, slots past TH*TW or below the image carry zero dy), or NI
+// TH x TW block of one image (TW divides W; 256 x 256 frames: 4 x 32 blocks of the 64-wide layer,
+// whole rows of the 32- and 16-wide ones; 376 x 672 frames: 3 x 42 blocks of the 168- and 84-wide
+// layers; slots past TH*TW or below the image carry zero dy; wg_halo_geom), or NI
 // whole images when H*W < 128. Per tile it glds-loads dy [128 slots][64 k] and the x halo
 // [(TH+2)*(TW+2) positions][64 c] once (7 uniform 1 KB pieces per wave, double-buffered
 // over tiles with a counted vmcnt); both MFMA operands are k(=pixel)-major, read with
@@ -446,11 +447,17 @@ ARGUS_DEV uint2 ds_tr_asm(uint32_t addr) {
   asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(addr) : "memory");
   return r;
 }
-// every LDS read issued so far has landed; the operands pass through the asm so no use moves above it
-ARGUS_DEV void lgkm_tie(u32x4 (&a)[2], u32x4 (&b)[9]) {
+// every LDS read issued so far has landed. The tie takes the asm reads' own uint2 results (not the
+// u32x4 fragments assembled from them): the compiler's waitcnt pass does not see inline-asm loads, so a
+// copy made before the wait (e.g. to pair two results into the 4-register tuple an MFMA operand needs)
+// would read registers whose data has not arrived. Tied here, no use or copy moves above the wait; the
+// fragments are assembled from the tied values afterwards.
+ARGUS_DEV void lgkm_tie(uint2 (&a)[2][2], uint2 (&b)[9][2]) {
   asm volatile("s_waitcnt lgkmcnt(0)"
-               : "+v"(a[0]), "+v"(a[1]), "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]), "+v"(b[4]), "+v"(b[5]),
-                 "+v"(b[6]), "+v"(b[7]), "+v"(b[8])
+               : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(a[1][0]), "+v"(a[1][1]), "+v"(b[0][0]), "+v"(b[0][1]),
+                 "+v"(b[1][0]), "+v"(b[1][1]), "+v"(b[2][0]), "+v"(b[2][1]), "+v"(b[3][0]), "+v"(b[3][1]),
+                 "+v"(b[4][0]), "+v"(b[4][1]), "+v"(b[5][0]), "+v"(b[5][1]), "+v"(b[6][0]), "+v"(b[6][1]),
+                 "+v"(b[7][0]), "+v"(b[7][1]), "+v"(b[8][0]), "+v"(b[8][1])
                :
                : "memory");
 }
@@ -568,11 +575,11 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(const WgHaloParam
       offb[s2][ni] = (unsigned)tr_off(h0 + toff, slot) | ((unsigned)tr_off(h1 + toff, slot) << 16);
     }
   }
-  auto frag = [&](uint32_t img, unsigned packed) {
-    const uint2 u0 = ds_tr_asm(img + (packed & 0xffffu));
-    const uint2 u1 = ds_tr_asm(img + (packed >> 16));
-    return u32x4{u0.x, u0.y, u1.x, u1.y};
+  auto frag = [&](uint32_t img, unsigned packed, uint2 (&u)[2]) {
+    u[0] = ds_tr_asm(img + (packed & 0xffffu));
+    u[1] = ds_tr_asm(img + (packed >> 16));
   };
+  auto join = [](const uint2 (&u)[2]) { return u32x4{u[0].x, u[0].y, u[1].x, u[1].y}; };
 
   // 3-stage ring: tile i lands in stage i % 3; tiles i+1 and i+2 stay in flight over tile i's MFMAs
   if (t0 < t1) issue(t0, 0);
@@ -594,12 +601,17 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(const WgHaloParam
     const uint32_t HXI = DYI + DYB;
 #pragma unroll
     for (int s2 = 0; s2 < 4; ++s2) {
+      uint2 ra[2][2], rb[9][2];
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) frag(DYI, offa[s2][mi], ra[mi]);
+#pragma unroll
+      for (int ni = 0; ni < 9; ++ni) frag(HXI, offb[s2][ni], rb[ni]);
+      lgkm_tie(ra, rb);
       u32x4 fa[2], fb[9];
 #pragma unroll
-      for (int mi = 0; mi < 2; ++mi) fa[mi] = frag(DYI, offa[s2][mi]);
+      for (int mi = 0; mi < 2; ++mi) fa[mi] = join(ra[mi]);
 #pragma unroll
-      for (int ni = 0; ni < 9; ++ni) fb[ni] = frag(HXI, offb[s2][ni]);
-      lgkm_tie(fa, fb);
+      for (int ni = 0; ni < 9; ++ni) fb[ni] = join(rb[ni]);
 #pragma unroll
       for (int ni = 0; ni < 9; ++ni)
 #pragma unroll
