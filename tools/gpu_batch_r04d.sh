@@ -1,4 +1,5 @@
 #!/bin/bash
+# (historical: the variant it measured was not kept and is no longer in the tree; result in DESIGN.md §5)
 # dev (round 4, GPU box): bn1 + ReLU applied in the 3x3 halo kernels' LDS (policy key 42, engine
 # lds_prologue): halo parity tests first, then the whole GPU suite, a kernel trace, engine A/Bs.
 O=gpurun_out/r04x

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (historical: the variant it measured was not kept and is no longer in the tree; result in DESIGN.md §5)
 # dev (round 4, GPU box): 32-pixel k-steps for the bf16 128x128 weight gradient (ARGUS_WG128_BKP32:
 # 32 KB LDS, three workgroups per CU): weight-gradient parity tests on the variant library, then paired
 # benches (default vs variant) in one instance.

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (historical: the variant it measured was not kept and is no longer in the tree; result in DESIGN.md §5)
 # dev (round 4, GPU box): elementwise-pass geometry (bn_apply / bn_bwd_apply ...): workgroup target
 # 512 (default) / 1024 / 2048 and 8 pixels in flight per thread, paired benches in one instance.
 O=gpurun_out/r04ew

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (historical: the variant it measured was not kept and is no longer in the tree; result in DESIGN.md §5)
 # dev (round 4, GPU box): XCD-contiguous pixel ranges in the max-pool forward / backward: stem tests,
 # kernel times and FETCH/WRITE traffic of both max-pool kernels (new vs previous library), paired benches.
 O=gpurun_out/r04mp
