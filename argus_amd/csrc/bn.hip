@@ -75,12 +75,12 @@ ARGUS_DEV double2 merge_groups(const double2* red, int G, int C, int c, double2 
   const int lane_r = threadIdx.x >> 6, cl = threadIdx.x & 63;
   double S = 0.0, Q = 0.0;
   if (c < C)
-    for (int gb = lane_r; gb < G; gb += kFinLanes * 4) {
-      double2 v[4];
+    for (int gb = lane_r; gb < G; gb += kFinLanes * kLoadBatch) {  // G <= 64: at most 2 batches
+      double2 v[kLoadBatch];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = red[(size_t)min(gb + kFinLanes * u, G - 1) * C + c];
+      for (int u = 0; u < kLoadBatch; ++u) v[u] = red[(size_t)min(gb + kFinLanes * u, G - 1) * C + c];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < kLoadBatch; ++u) {
         const bool ok = gb + kFinLanes * u < G;
         S += ok ? v[u].x : 0.0;
         Q += ok ? v[u].y : 0.0;
