@@ -29,8 +29,9 @@ Also reported:
                  itself says nothing about accuracy; val_vs_oracle is the same validation by the CPU
                  fp32 oracle with the same trained weights (rank 0, first 16 samples): the gap between
                  the two is the metric's error half (north_star: pose error within 1e-4 at fp32).
-Batch: 64 samples per rank on one GPU (configs[1]); 256 per rank when launched with N > 1 ranks
-(configs[2], cube_unity_data_medium-shaped); --batch overrides.
+Batch: 64 samples per rank (configs[1]) at every N, so the driver's N = 1, 2, 4, 8 lines form one
+weak-scaling series (per-GPU work fixed); --batch 256 gives configs[2]'s per-rank batch
+(cube_unity_data_medium-shaped), --batch overrides in general.
 """
 from __future__ import annotations
 
@@ -172,8 +173,8 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=None,
-                    help="samples (camera pairs) per rank (default 64 on one GPU = configs[1], 256 per rank "
-                         "for N > 1 = configs[2])")
+                    help="samples (camera pairs) per rank (default 64 = configs[1] at every N: weak scaling; "
+                         "256 = configs[2]'s per-rank batch)")
     ap.add_argument("--hw", type=int, nargs=2, default=(256, 256))
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp8"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -210,7 +211,7 @@ def main() -> None:
     from argus_amd.losses import geometric_loss_fn
 
     tuning = {int(k): int(v) for k, v in (kv.split("=") for kv in args.tune)}
-    B, (H, W) = (args.batch or (64 if world == 1 else 256)), args.hw
+    B, (H, W) = (args.batch or 64), args.hw
     torch.manual_seed(42)
     model = NCameraCNN(compute_dtype=args.dtype, kernel_tuning=tuning or None).to(dev)
     model.train()
