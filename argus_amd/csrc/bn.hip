@@ -111,21 +111,26 @@ __global__ __launch_bounds__(64 * kFinLanes) void stats_finalize_kernel(const Bn
   const int lane_r = threadIdx.x >> 6;
   const int g = blockIdx.y;
   const int r0 = g * a.rpg, r1 = min(a.rows, r0 + a.rpg);
-  // tile_rows < 0: every row is merged as a full row of |tile_rows| elements (ragged producers store
-  // {sum, M2 + sum^2 (1/n - 1/|tile_rows|)} for their n-element rows)
+  // tile_rows < 0 (ragged producers): row r holds n_r = counts[r] elements, the int32 counts following
+  // the float2[rows][C] partials
   const int tr = a.tile_rows < 0 ? -a.tile_rows : a.tile_rows;
   const double inv_full = 1.0 / (double)tr;
+  const int* counts = a.tile_rows < 0 ? reinterpret_cast<const int*>(a.part + (size_t)a.rows * a.C) : nullptr;
   double S = 0.0, Q = 0.0;
   if (c < a.C)
     for (int rb = r0 + lane_r; rb < r1; rb += kFinLanes * kLoadBatch) {
       float2 v[kLoadBatch];  // the batch's loads in flight together (clamped rows, masked below)
+      int nr[kLoadBatch];
 #pragma unroll
       for (int u = 0; u < kLoadBatch; ++u) v[u] = a.part[(size_t)min(rb + kFinLanes * u, r1 - 1) * a.C + c];
+#pragma unroll
+      for (int u = 0; u < kLoadBatch; ++u) nr[u] = counts ? counts[min(rb + kFinLanes * u, r1 - 1)] : tr;
 #pragma unroll
       for (int u = 0; u < kLoadBatch; ++u) {
         const int r = rb + kFinLanes * u;
         const int64_t left = a.count - (int64_t)r * tr;
-        const double inv = (a.tile_rows < 0 || left >= tr) ? inv_full : 1.0 / (double)left;
+        const double inv = counts ? (nr[u] > 0 ? 1.0 / (double)nr[u] : 0.0)
+                                  : (left >= tr ? inv_full : 1.0 / (double)left);
         const bool ok = r < r1;  // selects, not branches: a branch lets the compiler sink the loads
         S += ok ? (double)v[u].x : 0.0;
         Q += ok ? (double)v[u].y + (double)v[u].x * (double)v[u].x * inv : 0.0;

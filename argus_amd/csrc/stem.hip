@@ -14,9 +14,11 @@
 // halves: rows 0-3 and 4-7), the C tile staged through LDS and written as 16-byte non-temporal stores.
 // Served: bf16, any output size whose 8 x 32 tiling is >= 75 % useful. Ragged edge tiles (the 376 x 672
 // frame's 188 x 336 output: 4 spare rows, 16 spare columns) compute their spare pixels but neither
-// store them nor count them: such a half-tile's partial is {sum, M2 + sum^2 (1/n - 1/128)} over its n
-// valid pixels, i.e. sum x^2 - sum^2 / 128, which the finalize merges as a full 128-pixel row
-// (stat tile -128, argus_bn_finalize); full tiles' partials are unchanged.
+// store them nor count them: such a half-tile's partial is {sum, M2} over its n valid pixels (M2 about
+// their own mean, as a full tile's), and every half-tile also writes its pixel count n to the int32
+// row-count array that follows the partials (stat tile -128: argus_bn_finalize merges each row with
+// its own n in fp64; ADVICE r4: re-centring M2 to 128 pixels in fp32 lost the within-tile variance
+// when |mean| >> std).
 //
 // The weight gradient (stem_wgrad_kernel) uses the same tile: dW[oc][(r, s, c)] = sum over pixels of
 // dy[px][oc] * patch(2i + r, 2j + s)[c]. Both MFMA operands need 8 consecutive PIXELS per lane, which
@@ -49,6 +51,7 @@ struct StemParams {
   const bf16* w;   // w_fwd of the stem: [64][8][8][4] (r, s, c), padding zero
   bf16* y;         // (n, Ho, Wo, 64)
   float2* stats;   // {sum, M2} per 128 output pixels x 64 channels, or null
+  int* counts;     // ragged tilings: pixels per partial row (after the partials), else null
   int n, H, W, Ho, Wo;
 };
 
@@ -170,7 +173,7 @@ __global__ __launch_bounds__(256, 3) void stem_fwd_kernel(const StemParams p) {
       if (full) {
         const float d = (a0.x - a1.x) * (1.f / 64.f);
         o = make_float2(a0.x + a1.x, a0.y + a1.y + d * d * 32.f);
-      } else {  // Chan's merge over the valid counts, then re-centred to a 128-pixel row
+      } else {  // Chan's merge over the valid counts; the count goes to the row-count array
         const int na = min(max(vr - 4 * h, 0), 2) * vc, nb = min(max(vr - 4 * h - 2, 0), 2) * vc;
         const int n = na + nb;
         float m2 = a0.y + a1.y;
@@ -178,10 +181,13 @@ __global__ __launch_bounds__(256, 3) void stem_fwd_kernel(const StemParams p) {
           const float d = a0.x / (float)na - a1.x / (float)nb;
           m2 += d * d * ((float)na * (float)nb / (float)n);
         }
-        const float S = a0.x + a1.x;
-        o = n > 0 ? make_float2(S, m2 + S * S * (1.f / (float)n - 1.f / 128.f)) : make_float2(0.f, 0.f);
+        o = n > 0 ? make_float2(a0.x + a1.x, m2) : make_float2(0.f, 0.f);
       }
       store_part(p.stats + (tile_lin * 2 + h) * 64 + col, o);
+      if (p.counts && col == 0) {
+        const int n = full ? 128 : (min(max(vr - 4 * h, 0), 4) * vc);
+        p.counts[tile_lin * 2 + h] = n;
+      }
     }
     __syncthreads();
   }
@@ -404,7 +410,7 @@ bool stem_wgrad_launch(const argus_conv_desc& d, int dtype, const void* x, const
 bool stem_fwd_ok(const argus_conv_desc& d, int dtype) { return stem_shape_ok(d, dtype); }
 
 // The partial-row layout this kernel writes is argus_conv_fwd_stat_rows / _stat_tile: stem_stat_rows
-// rows of 128 pixels (-128 when ragged: every row merged as a full one)
+// rows of 128 pixels (-128 when ragged: int32 pixel counts per row follow the float2[rows][64] partials)
 bool stem_fwd_launch(const argus_conv_desc& d, int dtype, const void* x, const void* w, void* y, float* stats,
                      hipStream_t st) {
   if (!stem_fwd_ok(d, dtype)) return false;
@@ -413,6 +419,7 @@ bool stem_fwd_launch(const argus_conv_desc& d, int dtype, const void* x, const v
   p.w = reinterpret_cast<const bf16*>(w);
   p.y = reinterpret_cast<bf16*>(y);
   p.stats = reinterpret_cast<float2*>(stats);
+  p.counts = stats && stem_ragged(d) ? reinterpret_cast<int*>(p.stats + (size_t)stem_stat_rows(d) * 64) : nullptr;
   p.n = d.n; p.H = d.h; p.W = d.w; p.Ho = d.ho; p.Wo = d.wo;
   const int grid = d.n * stem_tpi(d.ho, d.wo);
   timed_launch("argus::stem_fwd_kernel", stem_fwd_kernel, dim3(grid), dim3(256), st, p);

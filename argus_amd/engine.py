@@ -146,6 +146,11 @@ class ResNetEngine:
         # (argus_conv_dgrad_wgrad_bn) instead of the dgrad + the side stream's wgrad_apply, which read
         # both 256-channel tensors again; set before the first forward
         self.fuse_dgw = True
+        # the 3x3 data gradients (compute-bound: ~500 FLOP/B) run alone: before each one the main stream
+        # waits for the weight gradients already issued on the side stream, whose workgroups would
+        # otherwise hold the CUs' LDS and registers beside it (the block's own deferred weight gradients
+        # are issued after it, at the block's end, as usual)
+        self.gate3x3 = False
         # (the schedule switches above are attributes, not environment variables: tools/engine_ab.py
         # A/B-measures them; test_gpu_train.py runs the overlap / tail placements against each other)
 
@@ -234,7 +239,8 @@ class ResNetEngine:
         self.bn_coef = {n: self._f(3, c) for n, c in chans.items()}
 
         max_stat = max(cv.stat_rows * cv.desc.k for cv in convs.values())
-        self.stat_part = self._f(max_stat * 2)
+        # + int32 row counts after the partials of a ragged producer (negative stat tile: the stem)
+        self.stat_part = self._f(max_stat * 2 + max(cv.stat_rows for cv in convs.values()))
         self.bn_ws = torch.zeros(L.dll.argus_bn_workspace_bytes(2048), dtype=torch.uint8, device=self.device)
         # the downsample branch's own statistics workspaces (it runs on the side stream in forward)
         ds_stat = max([cv.stat_rows * cv.desc.k for n, cv in convs.items() if ".downsample." in n] or [1])
@@ -590,6 +596,8 @@ class ResNetEngine:
             # conv2 -> bn1 (dm1 goes to a ring buffer when the side stream's conv1 wgrad reads it)
             if wg1_apply:
                 dzb = self._next_dy()
+            if self.gate3x3:
+                self._drain_side()
             r1 = self._dgrad_bn(pf + ".conv2", dza if pro2 else dy2, dzb, None, pf + ".bn1", a["y1"], 2, P=P, G=G,
                                 pro=pro2)
             cap("b_dy2", dy2, px_o * b.width, (N, ho, wo, b.width))
@@ -898,6 +906,14 @@ class ResNetEngine:
         self._side.wait_event(ev)
         with torch.cuda.stream(self._side):
             yield
+
+    def _drain_side(self) -> None:
+        """Main stream waits for the weight gradients issued on the side stream so far (the deferred ones
+        stay deferred): nothing of the side stream is resident during the next main-stream launch."""
+        if self._last_side is not None and self._waited_seq < self._side_seq:
+            torch.cuda.current_stream().wait_event(self._last_side)
+            self._pending.clear()
+            self._waited_seq = self._side_seq
 
     def _join(self) -> None:
         """Main stream waits for every weight gradient issued so far."""

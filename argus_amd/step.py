@@ -132,6 +132,9 @@ class FusedTrainer:
         self.bucketer = GradBucketer(self.flat.grad, self.flat.offset, group, bucket_mb) if self.distributed else None
         self._loss = None
         self._dpred = None
+        # when a list (bench.py): per step, the (start, end) events around the wait for the gradient
+        # all-reduce after the backward's own work - the collective tail the overlap did not hide
+        self.tail_events: list | None = None
 
     def step(self, images: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
         """One optimisation step on a device-resident batch; returns the per-sample losses (B,)."""
@@ -152,7 +155,14 @@ class FusedTrainer:
         if self.bucketer is not None:
             self.bucketer.start()
             eng.backward(self._dpred, P, self.flat.G, on_ready=self.bucketer.ready)
+            t0 = t1 = None
+            if self.tail_events is not None:  # main stream: end of its backward work -> collectives done
+                t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                t0.record()
             self.bucketer.finish()
+            if t1 is not None:
+                t1.record()
+                self.tail_events.append((t0, t1))
         else:
             eng.backward(self._dpred, P, self.flat.G)
         self.step_count += 1

@@ -95,7 +95,9 @@ int argus_conv_weight_prep_batch(int dtype, int count, const void* device_table,
  * (the producer's BatchNorm+ReLU applied while staging; zero padding stays zero), else x.
  * If stat_part != NULL, per-(row-tile, channel) {sum, M2} of y (fp32 accumulators, before
  * rounding; M2 about the tile mean) are written: float2[argus_conv_fwd_stat_rows(d)][k], each row
- * tile covering argus_conv_fwd_stat_tile(d) output pixels (the last one possibly fewer). */
+ * tile covering argus_conv_fwd_stat_tile(d) output pixels (the last one possibly fewer); a negative
+ * stat tile (ragged tiling) also writes int32 pixel counts[rows] after them, so stat_part must then
+ * hold 2*rows*k floats + rows ints. */
 int argus_conv_fwd(const argus_conv_desc* d, int dtype, const void* x, const void* w_fwd, void* y,
                    const float* pro_scale, const float* pro_shift, float* stat_part,
                    argus_stream_t stream);
@@ -247,7 +249,8 @@ size_t argus_bn_workspace_bytes(int channels);
 /* From tile partials float2[rows][C] = {sum, M2 (sum of squared deviations from the tile mean)},
  * tile t holding min(tile_rows, count - t*tile_rows) elements per channel (as argus_conv_fwd
  * writes them; tile_rows < 0, as argus_conv_fwd_stat_tile reports for a producer with ragged tiles:
- * every row is merged as |tile_rows| elements, its M2 stored as sum x^2 - sum^2/|tile_rows|): merged
+ * row r holds counts[r] <= |tile_rows| elements, the int32 counts[rows] stored right after the
+ * float2[rows][C] partials, i.e. at (const int*)(part + 2*rows*C)): merged
  * in fp64 (Chan), gives mean, invstd, the fused apply coefficients
  * scale = gamma*invstd, shift = beta - mean*scale; updates running stats (momentum, unbiased
  * variance) and num_batches_tracked when those pointers are non-NULL. */

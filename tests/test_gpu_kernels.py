@@ -59,11 +59,14 @@ def _q(t, dt):  # round to the compute dtype (reference inputs)
     return t.to(TDT[dt]).to(torch.float64)
 
 
-def _merge_stats(part, tile, count):
+def _merge_stats(part, tile, count, counts=None):
     """Chan-merge per-tile {sum, M2} partials (rows, C, 2) -> per-channel (mean, biased var). tile < 0
-    (argus_conv_fwd_stat_tile of a ragged producer): every row is merged as |tile| elements."""
+    (argus_conv_fwd_stat_tile of a ragged producer): row r holds counts[r] elements (the int32 array
+    the producer writes after the partials)."""
     if tile < 0:
-        n = torch.full((part.shape[0],), float(-tile), dtype=torch.float64)
+        assert counts is not None and counts.shape[0] == part.shape[0]
+        assert int(counts.sum()) == count and int(counts.max()) <= -tile and int(counts.min()) >= 0
+        n = counts.to(torch.float64).clamp_min(1.0)
     else:
         n = torch.tensor([min(tile, count - t * tile) for t in range(part.shape[0])], dtype=torch.float64)
     mean_t = part[..., 0] / n[:, None]
@@ -213,20 +216,67 @@ def test_stem_lds_patch_kernel(cuda):
             tile = L.dll.argus_conv_fwd_stat_tile(C.byref(dk), BF16)
             assert tile == (-128 if served and key19 and (d.ho % 8 or d.wo % 32) else 128), (n, H, W, key19, tile)
             y = torch.empty(n, d.ho, d.wo, 64, dtype=torch.bfloat16, device=cuda)
-            stats = torch.full((rows, 64, 2), float("nan"), device=cuda)
+            buf = torch.full((rows * 128 + rows,), float("nan"), device=cuda)  # partials (+ counts if ragged)
+            stats = buf[:rows * 128].view(rows, 64, 2)
             with KernelTimer() as t:
-                L.conv_fwd(C.byref(dk), BF16, ptr(x4), ptr(wf), ptr(y), None, None, ptr(stats), stream())
+                L.conv_fwd(C.byref(dk), BF16, ptr(x4), ptr(wf), ptr(y), None, None, ptr(buf), stream())
             names = list(t.summary())
             assert ("argus::stem_fwd_kernel" in names) == (served and key19 == 1), (n, H, W, key19, names)
             assert _rel(y.permute(0, 3, 1, 2), ref) < TOL["bf16"], ("stem fwd", n, H, W, key19)
             assert torch.isfinite(stats).all()
-            mean, var = _merge_stats(stats.double().cpu(), tile, M)
+            counts = buf[rows * 128:].view(torch.int32).cpu() if tile < 0 else None
+            mean, var = _merge_stats(stats.double().cpu(), tile, M, counts)
             yr = ref.permute(0, 2, 3, 1).reshape(-1, 64)
+            vr = yr.var(0, unbiased=False)
             assert (mean - yr.mean(0)).abs().max() < 2e-2 * yr.std(0).max(), ("stats mean", n, H, W, key19)
-            assert _rel(var, yr.var(0, unbiased=False)) < 2e-2, ("stats var", n, H, W, key19)
+            assert _rel(var, vr) < 2e-2, ("stats var", n, H, W, key19, _rel(var, vr))
+            # the library's finalize (fp64 merge) on the same partials: mean / invstd of the host merge
+            g1, b0 = torch.ones(64, device=cuda), torch.zeros(64, device=cuda)
+            mo, io = torch.empty(64, device=cuda), torch.empty(64, device=cuda)
+            ws = torch.zeros(L.dll.argus_bn_workspace_bytes(64), dtype=torch.uint8, device=cuda)
+            L.bn_finalize(64, rows, tile, ptr(buf), M, ptr(g1), ptr(b0), C.c_float(0.0), C.c_float(0.1), None, None,
+                          None, ptr(mo), ptr(io), None, None, ptr(ws), stream())
+            assert (mo.double().cpu() - mean).abs().max() < 1e-6 * (1 + mean.abs().max()), ("finalize mean", n, H, W)
+            assert _rel(io.double().cpu() ** -2, var) < 1e-4, ("finalize var", n, H, W, key19)
             outs.append((y.float(), mean, var))
         assert _rel(outs[0][0], outs[1][0]) < 1e-2
         assert _rel(outs[0][2], outs[1][2]) < 1e-4 and (outs[0][1] - outs[1][1]).abs().max() < 1e-4
+
+
+def test_bn_finalize_row_counts_large_mean(cuda):
+    """argus_bn_finalize with a ragged producer's layout (stat tile -128: int32 row counts after the
+    partials, as stem_fwd_kernel writes them) on rows whose mean is 1e4 standard deviations off zero:
+    every row keeps its own {sum, M2 about the row mean}, so the fp64 merge recovers the variance to
+    fp32 input rounding (re-centring each ragged row to 128 elements in fp32 lost it)."""
+    L = lib()
+    g = torch.Generator().manual_seed(5)
+    rows, c = 300, 64
+    counts = torch.randint(1, 129, (rows,), generator=g, dtype=torch.int32)
+    counts[::7] = 128
+    counts[5] = 0  # an empty half-tile (the bottom half of a 4-row ragged tile)
+    mean_c = 1e4 * (1 + torch.rand(c, generator=g, dtype=torch.float64))
+    xs = [mean_c + torch.randn(int(k), c, generator=g, dtype=torch.float64) for k in counts]
+    part = torch.zeros(rows, c, 2, dtype=torch.float64)
+    for r, x in enumerate(xs):
+        if x.shape[0]:
+            part[r, :, 0] = x.sum(0)
+            part[r, :, 1] = ((x - x.mean(0)) ** 2).sum(0)
+    allx = torch.cat(xs)
+    M = allx.shape[0]
+    buf = torch.cat([part.float().flatten(), counts.view(torch.float32)]).to(cuda)
+    g1, b0 = torch.ones(c, device=cuda), torch.zeros(c, device=cuda)
+    mo, io = torch.empty(c, device=cuda), torch.empty(c, device=cuda)
+    ws = torch.zeros(L.dll.argus_bn_workspace_bytes(c), dtype=torch.uint8, device=cuda)
+    L.bn_finalize(c, rows, -128, ptr(buf), M, ptr(g1), ptr(b0), C.c_float(0.0), C.c_float(0.1), None, None, None,
+                  ptr(mo), ptr(io), None, None, ptr(ws), stream())
+    var = allx.var(0, unbiased=False)
+    got = io.double().cpu() ** -2
+    print("max rel var error", _rel(got, var))
+    assert _rel(got, var) < 1e-3
+    assert ((mo.double().cpu() - allx.mean(0)).abs() / allx.std(0)).max() < 1e-2
+    # the host merge used by the stem test agrees
+    hm, hv = _merge_stats(part.float().double(), -128, M, counts)
+    assert _rel(hv, var) < 1e-3
 
 
 def test_stem_wgrad_lds_patch_kernel(cuda):

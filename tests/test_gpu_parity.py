@@ -294,6 +294,48 @@ def test_bf16_b64_steps_bit_reproducible(cuda):
     assert torch.equal(l0, l1) and torch.equal(p0, p1) and torch.equal(v0, v1)
 
 
+@pytest.mark.parametrize("dtype,factor", [("bf16", 2.0), ("fp8", 4.0)])
+def test_lowp_eval_predictions_at_trained_point(cuda, dtype, factor):
+    """Eval-mode predictions of TRAINED weights (running BN statistics moved off their init values,
+    as in argus/train.py:327-348's validation after training) on the reduced-precision path, against
+    the CPU fp32 oracle carrying the same weights and buffers.
+
+    Stated bar: max |pred diff| and max |per-sample loss diff| no more than ``factor`` x the distance of
+    the reference's own reduced-precision mode (autocast, train.py:334-337; bf16 on the CPU) from
+    fp32 on the same weights and samples: 2x for bf16 (the pattern of the bf16 gradient bar above), 4x
+    for fp8 (its re-stated bars, test_fp8_forward_and_fused_step). The trained point: 10 fused steps
+    at lr 1e-3 on fresh B=8 batches of 256x256."""
+    from argus_amd.step import FusedTrainer
+
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    B = 8
+    m = _product(cuda, dtype)
+    tr = FusedTrainer(m, lr=1e-3, max_grad_norm=1.0)
+    for i in range(10):
+        tr.step(mg.synthetic_images(B, 256, 256, seed=300 + i).to(cuda), mg.synthetic_targets(B, seed=400 + i).to(cuda))
+    m.eval()
+    xv, Tv = mg.synthetic_images(B, 256, 256, seed=500), mg.synthetic_targets(B, seed=501)
+    with torch.no_grad():
+        ours = m(xv.to(cuda)).float().cpu()
+    ref = build_reference_model(42)
+    ref.load_state_dict({k: v.detach().float().cpu() for k, v in m.state_dict().items()})
+    ref.eval()
+    with torch.no_grad():
+        p32 = ref(xv)
+        with torch.autocast("cpu", dtype=torch.bfloat16):
+            p16 = ref(xv).float()
+    l32, l16, lo = (se3.geometric_loss(p.double(), Tv.double()) for p in (p32, p16, ours))
+    d_pred, r_pred = (ours - p32).abs().max().item(), (p16 - p32).abs().max().item()
+    d_loss, r_loss = (lo - l32).abs().max().item(), (l16 - l32).abs().max().item()
+    # the trained point is not the init: BN running statistics and weights moved
+    rv = dict(m.named_buffers())["resnet.layer4.2.bn3.running_var"]
+    assert not torch.allclose(rv.cpu(), torch.ones_like(rv.cpu()))
+    print(f"{dtype} eval at the trained point: pred {d_pred:.3e} (reference bf16 autocast {r_pred:.3e}), "
+          f"per-sample loss {d_loss:.3e} ({r_loss:.3e})")
+    assert d_pred <= factor * r_pred, (d_pred, r_pred)
+    assert d_loss <= factor * r_loss, (d_loss, r_loss)
+
+
 # ------------------------------------------------------------------------------------------------ fp8
 def test_fp8_forward_and_fused_step(cuda):
     """compute_dtype="fp8" (BASELINE configs[4]: OCP MX-fp8 conv fwd / dgrad operands, bf16

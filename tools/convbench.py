@@ -42,7 +42,7 @@ def main():
         dy = torch.randn(d.n, d.ho, d.wo, d.k, device=dev).to(tdt)
         dx = torch.empty(d.n, d.h, d.w, d.c, device=dev, dtype=tdt)
         dw = torch.empty(d.k * d.r * d.s * d.c, device=dev)
-        st = torch.empty(cv.stat_rows * d.k * 2, device=dev)
+        st = torch.empty(cv.stat_rows * d.k * 2 + cv.stat_rows, device=dev)  # + ragged row counts
         ws = torch.empty(L.dll.argus_conv_wgrad_workspace_bytes(C.byref(d), dt), dtype=torch.uint8, device=dev)
         wf = cv.wf.normal_() if tdt == torch.float32 else cv.wf.copy_(torch.randn_like(cv.wf, dtype=torch.float32))
         wd = cv.wd if cv.wd is not None else None

@@ -3,8 +3,10 @@ interleaved (A B A B ...) on one box so drift between them cancels.
 
     python tools/engine_ab.py --batch 64 --cfg "" --cfg "side_priority=-1" --cfg "tune:6=256" [--rounds 3]
 
-Model instances differ by about 1 % on their own (allocation placement): repeat a configuration
-(e.g. defaults first and last) to see that spread.
+Each configuration is rebuilt (same seed) for every round and freed before the next, so only one
+model is resident at a time; the peak device memory of each configuration is printed. Model
+instances differ by about 1 % on their own (allocation placement): repeat a configuration (e.g.
+defaults first and last) to see that spread.
 """
 import argparse
 import sys
@@ -30,8 +32,8 @@ def main():
 
     dev = torch.device("cuda", 0)
     images, targets = synthetic_batch(a.batch, *a.hw, 1000, dev)
-    runs = []
-    for cfg in a.cfg or [""]:
+
+    def parse(cfg):
         tune, attrs = {}, {}
         for kv in filter(None, cfg.split(",")):
             k, v = kv.split("=")
@@ -39,6 +41,15 @@ def main():
                 tune[int(k[5:])] = int(v)
             else:
                 attrs[k] = v
+        return tune, attrs
+
+    def run(cfg):
+        """One configuration: build (seeded), 3 warm-up steps, the timed steps, then free everything
+        before the next configuration (only one model is resident at a time; r04 kept them all and
+        ran out of memory at 376x672 B=128). Returns (ms/step, peak device GiB of this configuration)."""
+        tune, attrs = parse(cfg)
+        torch.cuda.empty_cache()
+        torch.cuda.reset_peak_memory_stats(dev)
         torch.manual_seed(42)
         m = NCameraCNN(compute_dtype=a.dtype, kernel_tuning=tune or None).to(dev).train()
         eng = m._engine(dev)
@@ -48,19 +59,28 @@ def main():
         tr = FusedTrainer(m, lr=1e-4, max_grad_norm=1.0)
         for _ in range(3):
             tr.step(images, targets)
-        runs.append((cfg, tr, []))
-    for _ in range(a.rounds):
-        for cfg, tr, res in runs:
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(a.steps):
-                tr.step(images, targets)
-            torch.cuda.synchronize()
-            res.append(1e3 * (time.perf_counter() - t0) / a.steps)
-    for cfg, _, res in runs:
-        print(f"{cfg or 'defaults':40s} ms/step " + " ".join(f"{r:7.3f}" for r in res) +
-              f"   img/s best {2 * a.batch / min(res) * 1e3:8.1f}", flush=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            tr.step(images, targets)
+        torch.cuda.synchronize()
+        ms = 1e3 * (time.perf_counter() - t0) / a.steps
+        peak = torch.cuda.max_memory_allocated(dev) / 2**30
+        del tr, eng, m
+        return ms, peak
 
+    cfgs = a.cfg or [""]
+    res = {c: [] for c in cfgs}
+    peaks = {c: 0.0 for c in cfgs}
+    for _ in range(a.rounds):  # interleaved A B A B ... so drift between configurations cancels
+        for c in cfgs:
+            ms, pk = run(c)
+            res[c].append(ms)
+            peaks[c] = max(peaks[c], pk)
+    for c in cfgs:
+        r = res[c]
+        print(f"{c or 'defaults':40s} ms/step " + " ".join(f"{x:7.3f}" for x in r) +
+              f"   img/s best {2 * a.batch / min(r) * 1e3:8.1f}   peak {peaks[c]:.2f} GiB", flush=True)
 
 if __name__ == "__main__":
     main()
