@@ -85,6 +85,7 @@ SIGNATURES = {
                                           C.POINTER(_P), _P, _SZ, C.POINTER(_I)]),
     "argus_conv_weight_prep_batch": (_I, [_I, _I, _P, _I, _P]),
     "argus_conv_fwd": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "argus_conv_fwd_bn_out": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "argus_conv_fwd_stat_rows": (_I, [_DESC, _I]),
     "argus_conv_fwd_stat_tile": (_I, [_DESC, _I]),
     "argus_conv_policy_default": (_I, [_I]),

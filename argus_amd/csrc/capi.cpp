@@ -62,13 +62,23 @@ int argus_conv_weight_prep_batch(int dtype, int count, const void* device_table,
 
 int argus_conv_fwd(const argus_conv_desc* d, int dtype, const void* x, const void* w, void* y, const float* sc,
                    const float* sh, float* stats, argus_stream_t stream) {
-  if (!d || !x || !w || !y || (sc == nullptr) != (sh == nullptr)) {
+  if (!d || !x || !w || (!y && !stats) || (sc == nullptr) != (sh == nullptr)) {
     set_error("conv_fwd: bad arguments");
     return ARGUS_ERR_ARG;
   }
   return conv_fwd(*d, dtype, x, w, y, sc, sh, stats, (hipStream_t)stream);
 }
 
+int argus_conv_fwd_bn_out(const argus_conv_desc* d, int dtype, const void* x, const void* w_fwd, const float* scale,
+                          const float* shift, const void* res, const float* res_scale, const float* res_shift, void* out,
+                          uint8_t* mask_bits, void* y, argus_stream_t stream) {
+  if (!d) {
+    set_error("conv_fwd_bn_out: bad arguments");
+    return ARGUS_ERR_ARG;
+  }
+  return conv_fwd_bn_out(*d, dtype, x, w_fwd, scale, shift, res, res_scale, res_shift, out, mask_bits, y,
+                         (hipStream_t)stream);
+}
 int argus_conv_fwd_stat_rows(const argus_conv_desc* d, int dtype) { return d ? conv_fwd_stat_rows(*d, dtype) : 0; }
 
 int argus_conv_policy_default(int key) { return policy_default(key); }

@@ -85,6 +85,8 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
   constexpr int BW = BWX & 7;                   // BN-backward epilogue variant
   constexpr bool AP = (BWX & kApplyBit) != 0;   // BN-backward apply prologue
   constexpr bool F8 = (BWX & kFp8Bit) != 0;     // MX-fp8 operands (bf16 activations, fp8 weights)
+  constexpr bool OUT = (BWX & kOutBit) != 0;    // forward: bn3 + residual + ReLU epilogue (BnOutEpi)
+  static_assert(!OUT || (BW == 0 && !AP && !F8 && !STEM && !PRO), "block-output epilogue: plain forward");
   static_assert(!F8 || (sizeof(T) == 2 && !STEM && !PRO), "fp8: bf16 tensors, no BN+ReLU prologue");
   constexpr int E = Chunk<T>::E;
   constexpr int EF = F8 ? 2 * E : E;  // elements one thread stages per row per k-step
@@ -446,6 +448,9 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
     }
     __syncthreads();
   }
+  if constexpr (BW == 0 && !OUT) {
+    if (!p.c) return;  // statistics-only forward (argus_conv_fwd with y == NULL)
+  }
 
   // ---- epilogue: stage the C tile in LDS, then 16-byte coalesced (+accumulating) stores ----
   constexpr int LD = epi_ld<T, BN>();
@@ -460,6 +465,20 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
   const bool c_ident = p.osh == 1 && p.osw == 1 && ph.oh0 == 0 && ph.ow0 == 0 && ph.Hq == p.Ho && ph.Wq == p.Wo;
   BwdEpiAcc<T, BW> bwd;
   if constexpr (BW != 0) bwd.init(p.bb, nt * BN + (tid % CPR) * E);
+  // block-output epilogue: this thread's chunk coefficients (its chunk column is fixed)
+  float oa[OUT ? E : 1], ob[OUT ? E : 1], ra[OUT ? E : 1], rb[OUT ? E : 1];
+  if constexpr (OUT) {
+    const int ch = nt * BN + (tid % CPR) * E;
+    BwdEpiAcc<T, 3>::ld(oa, p.oe.sc + ch);
+    BwdEpiAcc<T, 3>::ld(ob, p.oe.sh + ch);
+    if (p.oe.rsc) {
+      BwdEpiAcc<T, 3>::ld(ra, p.oe.rsc + ch);
+      BwdEpiAcc<T, 3>::ld(rb, p.oe.rsh + ch);
+    } else {
+#pragma unroll
+      for (int j = 0; j < E; ++j) { ra[j] = 1.f; rb[j] = 0.f; }
+    }
+  }
 #pragma unroll
   for (int q = 0; q < EPASS; ++q) {
     if (EPASS == 1 || wm == q) {
@@ -497,14 +516,30 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
           const int oh = qh * p.osh + ph.oh0, ow = qw * p.osw + ph.ow0;
           off[u] = (((size_t)nimg * p.Ho + oh) * p.Wo + ow) * p.ldc + nt * BN + c * E;
         }
-        if (ok[u]) epi_load<T, BW>(p, off[u], in[u]);
+        if constexpr (OUT) {
+          if (ok[u]) in[u].add = ld16(reinterpret_cast<const T*>(p.oe.res) + off[u]);
+        } else if (ok[u]) {
+          epi_load<T, BW>(p, off[u], in[u]);
+        }
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (!ok[u]) continue;
         const int rr = tid / CPR + RPP * (i0 + u);
         const u32x4 v = *reinterpret_cast<const u32x4*>(Cs + rr * LD + c * E);
-        st16_nt(Cg + off[u], epi_apply<T, BW>(p, v, in[u], bwd));
+        if constexpr (OUT) {  // argus_bn_apply's arithmetic on the stored (rounded) y, bit for bit
+          if (Cg) st16_nt(Cg + off[u], v);
+          float f[E], r[E];
+          unpack(v, f);
+          unpack(in[u].add, r);
+#pragma unroll
+          for (int j = 0; j < E; ++j) f[j] = fmaxf(fmaf(f[j], oa[j], ob[j]) + fmaf(r[j], ra[j], rb[j]), 0.f);
+          const u32x4 o = pack(f);
+          st16(reinterpret_cast<T*>(p.oe.out) + off[u], o);
+          p.oe.bits[off[u] / E] = chunk_positive_bits<T>(o);
+        } else {
+          st16_nt(Cg + off[u], epi_apply<T, BW>(p, v, in[u], bwd));
+        }
       }
     }
     if (EPASS > 1) __syncthreads();
@@ -1196,8 +1231,17 @@ static int run_ig(const IgParams& p, hipStream_t st, int bm, int bn) {
       else dispatch_ig_bwd1<T, 2, kFp8Bit>(p, maxM, bm, bn, st);
       return check_launch("igemm_kernel");
     }
-    if (conv3x3_halo_launch(p, st)) return check_launch("conv3x3_halo_kernel");
-    if (igemm_glds_launch(p, maxM, maxK, st)) return check_launch("igemm_glds_kernel");
+    // the statistics-only forward and the block-output epilogue exist on the register-staged kernel only
+    if (p.c || !p.fwd) {
+      if (!p.oe.out && conv3x3_halo_launch(p, st)) return check_launch("conv3x3_halo_kernel");
+      if (!p.oe.out && igemm_glds_launch(p, maxM, maxK, st)) return check_launch("igemm_glds_kernel");
+    }
+  }
+  if (p.oe.out) {
+    if (p.stem || p.pro_scale || p.bb.mode || p.ap.y) { set_error("conv_fwd_bn_out: plain forward only"); return ARGUS_ERR_ARG; }
+    if (smallk) dispatch_ig<T, false, 4, kOutBit>(p, maxM, bm, bn, st);
+    else dispatch_ig<T, false, 2, kOutBit>(p, maxM, bm, bn, st);
+    return check_launch("igemm_kernel");
   }
   if (p.stem) {
     if (p.N != 64 || bm != 128) { set_error("igemm: stem expects 64 output channels"); return ARGUS_ERR_SHAPE; }
@@ -1293,6 +1337,11 @@ int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, 
                         (double)d.n * d.ho * d.wo * d.k) +
                    (stats ? 8.0 * conv_fwd_stat_rows(d, dtype) * d.k : 0.0);
   if (d.stem && sc) { set_error("conv_fwd: stem has no prologue"); return ARGUS_ERR_ARG; }
+  if (!y && (!stats || d.stem || f8 || dtype != ARGUS_BF16)) {
+    set_error("conv_fwd: y may be NULL only for a bf16 non-stem forward with statistics");
+    return ARGUS_ERR_ARG;
+  }
+  if (!y) g_launch_bytes -= 2.0 * d.n * d.ho * d.wo * d.k;  // nothing stored
   const Policy pol = policy_of(d);
   if (f8 && sc) {
     int f8f, f8d;
@@ -1309,6 +1358,31 @@ int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, 
   p.stat_tile = bm;
   p.f8 = f8;
   return dtype == ARGUS_BF16 ? run_ig<bf16>(p, st, bm, bn) : run_ig<float>(p, st, bm, bn);
+}
+
+int conv_fwd_bn_out(const argus_conv_desc& d, int dtype, const void* x, const void* w, const float* sc,
+                    const float* sh, const void* res, const float* rsc, const float* rsh, void* out, uint8_t* bits,
+                    void* y, hipStream_t st) {
+  if (int e = check_desc(d)) return e;
+  if (dtype != ARGUS_BF16 || d.stem || d.r != 1 || d.s != 1 || d.stride != 1 || d.pad != 0 || d.k % 64) {
+    set_error("conv_fwd_bn_out: bf16 1x1 stride-1 convs only");
+    return ARGUS_ERR_ARG;
+  }
+  if (!x || !w || !sc || !sh || !res || !out || !bits || (rsc == nullptr) != (rsh == nullptr)) {
+    set_error("conv_fwd_bn_out: null operand");
+    return ARGUS_ERR_ARG;
+  }
+  const double px = (double)d.n * d.ho * d.wo;
+  g_launch_work = 2.0 * px * d.k * d.c;
+  g_launch_bytes = 2.0 * (px * d.c + (double)d.k * d.c + px * d.k * (y ? 3 : 2)) + px * d.k / 8;
+  const Policy pol = policy_of(d);
+  IgParams p;
+  fwd_params(d, pol, p);
+  p.a = x; p.b = w; p.c = y;
+  p.oe.sc = sc; p.oe.sh = sh; p.oe.res = res; p.oe.rsc = rsc; p.oe.rsh = rsh; p.oe.out = out; p.oe.bits = bits;
+  const int bm = fwd_bm(d, pol), bn = pick_bn(pol, 0, d.k);
+  p.stat_tile = bm;
+  return run_ig<bf16>(p, st, bm, bn);
 }
 
 static void dgrad_params(const argus_conv_desc& d, const Policy& pol, const void* dy, const void* wt, void* dx,

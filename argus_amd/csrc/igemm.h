@@ -46,6 +46,18 @@ struct BnApplyPro {
   void* out;
 };
 
+// Forward epilogue of the bottleneck tail (argus_conv_fwd_bn_out): out = relu(y*sc + sh + res*rsc + rsh)
+// (rsc null: + res) with its ReLU mask bits, from the conv's own output tile (y need not be stored)
+struct BnOutEpi {
+  const float* sc;
+  const float* sh;
+  const void* res;
+  const float* rsc;
+  const float* rsh;
+  void* out;
+  uint8_t* bits;
+};
+
 struct IgParams {
   const void* a;
   const void* b;
@@ -62,6 +74,7 @@ struct IgParams {
   BnBwdEpi bb;    // dgrad only
   BnFin fin;      // BN finalize folded into this launch (fin.mode != 0)
   BnApplyPro ap;  // dgrad only: the A operand is dm (ap.y != nullptr)
+  BnOutEpi oe;    // forward only (kOutBit): the block output from the C tile
   int f8;         // ARGUS_FP8: MX-fp8 operands where the shape allows (host dispatch only)
   int fwd;        // host: forward params (1) or data gradient (0) - the fp8 pass policy (key 37)
   int ksz;        // host: filter size of the conv (1 or 3; the fp8 pass policy)
@@ -75,6 +88,8 @@ constexpr int kApplyBit = 16;
 // bit 5: MX-fp8 operands (OCP e4m3 + one E8M0 scale per 32 K-elements of a row, quantized while
 // staging from the bf16 tensors; v_mfma_scale_f32_16x16x128_f8f6f4)
 constexpr int kFp8Bit = 32;
+// bit 6: forward epilogue BnOutEpi (the bottleneck's bn3 + residual + ReLU applied to the C tile)
+constexpr int kOutBit = 64;
 
 struct WgParams {
   const void* x;

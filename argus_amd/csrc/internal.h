@@ -12,6 +12,9 @@ namespace argus {
 void set_error(const std::string& msg);
 int check_launch(const char* what);
 
+int conv_fwd_bn_out(const argus_conv_desc& d, int dtype, const void* x, const void* w, const float* sc,
+                    const float* sh, const void* res, const float* rsc, const float* rsh, void* out, uint8_t* bits,
+                    void* y, hipStream_t st);
 int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, void* y,
              const float* sc, const float* sh, float* stats, hipStream_t st);
 int conv_fwd_stat_rows(const argus_conv_desc& d, int dtype);

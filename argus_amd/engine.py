@@ -151,6 +151,10 @@ class ResNetEngine:
         # otherwise hold the CUs' LDS and registers beside it (the block's own deferred weight gradients
         # are issued after it, at the block's end, as usual)
         self.gate3x3 = False
+        # the bottleneck tail on the bf16 schedule: conv3's forward only reduces bn3's statistics (nothing
+        # stored), then one pass recomputes its C tile and applies bn3 + the residual + ReLU there
+        # (argus_conv_fwd_bn_out): the bn_apply pass no longer reads y3 back (bit-identical outputs)
+        self.fuse_out = True
         # (the schedule switches above are attributes, not environment variables: tools/engine_ab.py
         # A/B-measures them; test_gpu_train.py runs the overlap / tail placements against each other)
 
@@ -334,13 +338,26 @@ class ResNetEngine:
             sc, sh = self.bn_state[pro][2], self.bn_state[pro][3]
         part = self.stat_part if part is None else part
         ws = self.bn_ws if ws is None else ws
-        self._launch(cv, 0, lambda: self.L.conv_fwd(C.byref(cv.desc), self.cdt, ptr(x), ptr(cv.wf), ptr(y), ptr(sc),
+        if y is None and not training:  # eval: the fused tail needs no statistics pass
+            self._bn_eval(P, Bf, bn)
+            return
+        cdt = BF16 if y is None else self.cdt  # the statistics-only forward is the bf16 kernel
+        self._launch(cv, 0, lambda: self.L.conv_fwd(C.byref(cv.desc), cdt, ptr(x), ptr(cv.wf), ptr(y), ptr(sc),
                                                      ptr(sh), ptr(part) if training else None, stream()))
         if training:
             count = cv.desc.n * cv.desc.ho * cv.desc.wo
             self._bn_train(P, Bf, bn, cv.stat_rows, cv.stat_tile, count, part, ws)
         else:
             self._bn_eval(P, Bf, bn)
+
+    def _fused_tail(self) -> bool:
+        """The bottleneck tail runs as argus_conv_fwd(stats only) + argus_conv_fwd_bn_out: the bf16
+        schedule (materialised a2), with conv3's forward not on MX-fp8 operands (policy key 37 bit 1)."""
+        if not (self.fuse_out and self.materialize):
+            return False
+        if self.cdt == FP8:
+            return not ((self.tuning or {}).get(37, self.L.dll.argus_conv_policy_default(37)) & 1)
+        return True
 
     def _act(self, bn, y, out, px, ch):
         """out = relu(y*scale + shift) with the finalized coefficients of BN layer ``bn``."""
@@ -407,11 +424,12 @@ class ResNetEngine:
                                                               a["yd"], None, training, self.stat_part_ds,
                                                               self.bn_ws_ds))
             self._conv_bn(P, Bf, pf + ".conv1", pf + ".bn1", h, a["y1"], None, training)
+            tail = self._fused_tail()
             if self.materialize:
                 self._act(pf + ".bn1", a["y1"], a["a1"], N * a["hw_in"][0] * a["hw_in"][1], b.width)
                 self._conv_bn(P, Bf, pf + ".conv2", pf + ".bn2", a["a1"], a["y2"], None, training)
                 self._act(pf + ".bn2", a["y2"], a["a2"], N * a["hw"][0] * a["hw"][1], b.width)
-                self._conv_bn(P, Bf, pf + ".conv3", pf + ".bn3", a["a2"], a["y3"], None, training)
+                self._conv_bn(P, Bf, pf + ".conv3", pf + ".bn3", a["a2"], None if tail else a["y3"], None, training)
             else:
                 self._conv_bn(P, Bf, pf + ".conv2", pf + ".bn2", a["y1"], a["y2"], pf + ".bn1", training)
                 self._conv_bn(P, Bf, pf + ".conv3", pf + ".bn3", a["y2"], a["y3"], pf + ".bn2", training)
@@ -423,10 +441,16 @@ class ResNetEngine:
                 else:
                     torch.cuda.current_stream().wait_event(ds_done)
                 sd = self.bn_state[pf + ".downsample.1"]
-                L.bn_apply(dt, px, b.cout, ptr(a["y3"]), ptr(s3[2]), ptr(s3[3]), ptr(a["yd"]), ptr(sd[2]),
-                           ptr(sd[3]), 1, ptr(a["out"]), ptr(a["bits"]), s)
+                res, rsc, rsh = a["yd"], sd[2], sd[3]
             else:
-                L.bn_apply(dt, px, b.cout, ptr(a["y3"]), ptr(s3[2]), ptr(s3[3]), ptr(h), None, None, 1,
+                res, rsc, rsh = h, None, None
+            if tail:  # conv3's C tile recomputed: y3 (kept for the backward), out and its mask in one pass
+                cv3 = self.convs[pf + ".conv3"]
+                self._launch(cv3, 0, lambda: L.conv_fwd_bn_out(
+                    C.byref(cv3.desc), BF16, ptr(a["a2"]), ptr(cv3.wf), ptr(s3[2]), ptr(s3[3]), ptr(res), ptr(rsc),
+                    ptr(rsh), ptr(a["out"]), ptr(a["bits"]), ptr(a["y3"]), s))
+            else:
+                L.bn_apply(dt, px, b.cout, ptr(a["y3"]), ptr(s3[2]), ptr(s3[3]), ptr(res), ptr(rsc), ptr(rsh), 1,
                            ptr(a["out"]), ptr(a["bits"]), s)
             h = a["out"]
             if self.debug is not None:

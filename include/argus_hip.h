@@ -101,6 +101,18 @@ int argus_conv_weight_prep_batch(int dtype, int count, const void* device_table,
 int argus_conv_fwd(const argus_conv_desc* d, int dtype, const void* x, const void* w_fwd, void* y,
                    const float* pro_scale, const float* pro_shift, float* stat_part,
                    argus_stream_t stream);
+/* y == NULL (bf16, not the stem, stat_part given): statistics only, nothing stored (ABI 14; the
+ * bottleneck's conv3 before argus_conv_fwd_bn_out). */
+/* Bottleneck tail in one forward pass (ABI 14; replaces conv3 + bn3 + the residual add + ReLU of
+ * torchvision's Bottleneck.forward, argus/models.py:43 -> torchvision resnet.py, in train mode after
+ * argus_bn_finalize of bn3, or eval mode with argus_bn_eval_coeffs): the 1x1 stride-1 conv's C tile t
+ * (rounded to bf16, as argus_conv_fwd stores it) gives out = relu(t*scale + shift + res'), res' = res *
+ * res_scale + res_shift when res_scale != NULL (the downsample BN) else res, with argus_bn_apply's
+ * mask bits (one byte per 16-byte chunk). Bit-identical to argus_conv_fwd + argus_bn_apply. y: optional
+ * store of t (NULL: not stored). bf16 only; every tensor NHWC. */
+int argus_conv_fwd_bn_out(const argus_conv_desc* d, int dtype, const void* x, const void* w_fwd,
+                          const float* scale, const float* shift, const void* res, const float* res_scale,
+                          const float* res_shift, void* out, uint8_t* mask_bits, void* y, argus_stream_t stream);
 int argus_conv_fwd_stat_rows(const argus_conv_desc* d, int dtype);
 int argus_conv_fwd_stat_tile(const argus_conv_desc* d, int dtype);
 /* dx = dgrad(dy, w_dgrad) [+ addend]: when addend != NULL (same NHWC layout as dx; may be dx itself

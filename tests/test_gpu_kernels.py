@@ -1529,3 +1529,53 @@ def test_glds_two_stage_ring_matches_three(cuda):
             outs.append((dm.cpu(), part.cpu(), dx.cpu()))
         for a, b in zip(*outs):
             assert torch.equal(a, b), (cin, cout, k)
+
+
+@pytest.mark.parametrize("cin,cout,hw,ds", [(64, 256, 24, False), (64, 256, 24, True), (128, 512, 12, True),
+                                            (512, 2048, 5, False), (256, 1024, 7, True)])
+def test_conv_fwd_bn_out_matches_conv_and_apply(cuda, cin, cout, hw, ds):
+    """argus_conv_fwd_bn_out (the bottleneck tail: conv3's C tile -> bn3 + residual (+ the downsample
+    BN) + ReLU, mask bits) and the statistics-only forward (argus_conv_fwd with y = NULL) against
+    argus_conv_fwd + argus_bn_apply: every output bit-identical (y, out, mask bits, BN partials);
+    ragged row tiles (hw = 5, 7) included."""
+    torch.manual_seed(77)
+    L = lib()
+    n = 3
+    d, _ = _desc(n, hw, hw, cin, cout, 1, 1)
+    x = torch.relu(torch.randn(n, hw, hw, cin, device=cuda)).to(torch.bfloat16)
+    w = (torch.randn(cout, 1, 1, cin) * (2.0 / cin) ** 0.5).to(cuda)
+    wf, _ = _prep(d, "bf16", w, cuda)
+    rows = L.dll.argus_conv_fwd_stat_rows(C.byref(d), BF16)
+    st_ref = torch.full((rows * cout * 2,), float("nan"), device=cuda)
+    st_new = torch.full((rows * cout * 2,), float("nan"), device=cuda)
+    y_ref = torch.empty(n, hw, hw, cout, dtype=torch.bfloat16, device=cuda)
+    L.conv_fwd(C.byref(d), BF16, ptr(x), ptr(wf), ptr(y_ref), None, None, ptr(st_ref), stream())
+    L.conv_fwd(C.byref(d), BF16, ptr(x), ptr(wf), None, None, None, ptr(st_new), stream())
+    assert torch.equal(st_ref, st_new)
+    sc, sh = torch.rand(cout, device=cuda) + 0.5, torch.randn(cout, device=cuda)
+    res = torch.randn(n, hw, hw, cout, device=cuda).to(torch.bfloat16)
+    rsc = rsh = None
+    if ds:
+        rsc, rsh = torch.rand(cout, device=cuda) + 0.5, torch.randn(cout, device=cuda)
+    px = n * hw * hw
+    o_ref = torch.empty_like(y_ref)
+    b_ref = torch.zeros(px * cout // 8, dtype=torch.uint8, device=cuda)
+    L.bn_apply(BF16, px, cout, ptr(y_ref), ptr(sc), ptr(sh), ptr(res), ptr(rsc), ptr(rsh), 1, ptr(o_ref), ptr(b_ref),
+               stream())
+    for store_y in (True, False):
+        y = torch.zeros_like(y_ref)
+        o = torch.empty_like(y_ref)
+        b = torch.full_like(b_ref, 0x5A)
+        L.conv_fwd_bn_out(C.byref(d), BF16, ptr(x), ptr(wf), ptr(sc), ptr(sh), ptr(res), ptr(rsc), ptr(rsh), ptr(o),
+                          ptr(b), ptr(y) if store_y else None, stream())
+        torch.cuda.synchronize()
+        assert torch.equal(o.view(torch.int16), o_ref.view(torch.int16)), (cin, cout, hw, ds, store_y)
+        assert torch.equal(b, b_ref)
+        if store_y:
+            assert torch.equal(y.view(torch.int16), y_ref.view(torch.int16))
+        else:
+            assert not y.any()
+    # and against torch: relu(conv * sc + sh + res')
+    ref = torch.einsum("nhwc,kc->nhwk", x.double(), wf.double()).to(torch.bfloat16).double() * sc.double() + sh.double()
+    r = res.double() if rsc is None else res.double() * rsc.double() + rsh.double()
+    assert _rel(o_ref, torch.relu(ref + r)) < TOL["bf16"]

@@ -141,7 +141,11 @@ def test_side_stream_overlap_is_bit_identical(cuda):
     """The weight-gradient / downsample side stream (engine.wgrad_overlap) and the first block's
     downsample weight gradient moved to the main stream's tail (engine.tail_main) only reorder
     independent launches: three bf16 training steps with and without them must give bitwise-identical parameters,
-    Adam moments, BN running statistics and losses (a missed event would show up as a race here)."""
+    Adam moments, BN running statistics and losses (a missed event would show up as a race here).
+    The same holds for the other schedule switches that do not change arithmetic: the fused bottleneck
+    tail (engine.fuse_out: conv3's statistics-only forward + argus_conv_fwd_bn_out instead of conv3 +
+    bn_apply) and the 3x3 data gradients run alone (engine.gate3x3); eval-mode predictions after the
+    steps too."""
     from argus_amd.models import NCameraCNN
     from argus_amd.step import FusedTrainer
     from oracle import se3
@@ -150,21 +154,26 @@ def test_side_stream_overlap_is_bit_identical(cuda):
     x = (torch.randint(0, 256, (8, 6, 128, 128), generator=g, dtype=torch.uint8).float() / 255.0).to(cuda)
     T = se3.random_targets(8, generator=g).float().to(cuda)
     runs = []
-    # (side stream, first block's downsample weight gradient on the main stream's tail)
-    for overlap, tail in ((True, True), (True, False), (False, True)):
+    # (side stream, first block's downsample weight gradient on the main stream's tail, ...)
+    for attrs in ({}, {"tail_main": False}, {"wgrad_overlap": False}, {"fuse_out": False}, {"gate3x3": True}):
         torch.manual_seed(42)
         model = NCameraCNN(compute_dtype="bf16").to(cuda).train()
         tr = FusedTrainer(model, lr=1e-3, max_grad_norm=1.0)
         eng = model._engine(cuda)
-        eng.wgrad_overlap, eng.tail_main = overlap, tail
+        for k, v in attrs.items():
+            setattr(eng, k, v)
         losses = [tr.step(x, T).clone() for _ in range(3)]
+        model.eval()
+        with torch.no_grad():
+            pe = model(x).clone()
         torch.cuda.synchronize()
         runs.append((torch.stack(losses).cpu(), tr.flat.param.cpu(), tr.exp_avg_sq.cpu(),
-                     {k: v.cpu() for k, v in model.state_dict().items()}))
-    (l1, p1, v1, s1) = runs[0]
-    for l0, p0, v0, s0 in runs[1:]:
-        assert torch.equal(l1, l0) and torch.equal(p1, p0) and torch.equal(v1, v0)
-        assert all(torch.equal(s1[k], s0[k]) for k in s1)
+                     {k: v.cpu() for k, v in model.state_dict().items()}, pe.cpu(), attrs))
+    (l1, p1, v1, s1, e1, _) = runs[0]
+    for l0, p0, v0, s0, e0, attrs in runs[1:]:
+        assert torch.equal(l1, l0) and torch.equal(p1, p0) and torch.equal(v1, v0), attrs
+        assert all(torch.equal(s1[k], s0[k]) for k in s1), attrs
+        assert torch.equal(e1, e0), attrs
 
 
 def test_rotation_angle_error_matches_oracle(cuda):

@@ -70,17 +70,16 @@ def main():
         return ms, peak
 
     cfgs = a.cfg or [""]
-    res = {c: [] for c in cfgs}
-    peaks = {c: 0.0 for c in cfgs}
+    res = [[] for _ in cfgs]
+    peaks = [0.0 for _ in cfgs]
     for _ in range(a.rounds):  # interleaved A B A B ... so drift between configurations cancels
-        for c in cfgs:
+        for i, c in enumerate(cfgs):
             ms, pk = run(c)
-            res[c].append(ms)
-            peaks[c] = max(peaks[c], pk)
-    for c in cfgs:
-        r = res[c]
+            res[i].append(ms)
+            peaks[i] = max(peaks[i], pk)
+    for c, r, pk in zip(cfgs, res, peaks):
         print(f"{c or 'defaults':40s} ms/step " + " ".join(f"{x:7.3f}" for x in r) +
-              f"   img/s best {2 * a.batch / min(r) * 1e3:8.1f}   peak {peaks[c]:.2f} GiB", flush=True)
+              f"   img/s best {2 * a.batch / min(r) * 1e3:8.1f}   peak {pk:.2f} GiB", flush=True)
 
 if __name__ == "__main__":
     main()
