@@ -18,7 +18,7 @@ import torch  # noqa: F401  (must precede the CDLL, see module docstring)
 LIB_PATH = Path(os.environ.get("ARGUS_HIP_LIB", Path(__file__).resolve().parent / "libargus_hip.so"))
 
 F32, BF16, FP8 = 0, 1, 2
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 
 class Tuning(C.Structure):
@@ -56,7 +56,8 @@ class BnBwdEpilogue(C.Structure):
                 ("part2", C.c_void_p), ("workspace", C.c_void_p), ("gamma", C.c_void_p), ("dgamma", C.c_void_p),
                 ("dbeta", C.c_void_p), ("ca", C.c_void_p), ("cb", C.c_void_p), ("cc", C.c_void_p),
                 ("gamma2", C.c_void_p), ("dgamma2", C.c_void_p), ("dbeta2", C.c_void_p), ("ca2", C.c_void_p),
-                ("cb2", C.c_void_p), ("cc2", C.c_void_p)]
+                ("cb2", C.c_void_p), ("cc2", C.c_void_p), ("y_x", C.c_void_p), ("y_w", C.c_void_p),
+                ("y_k", C.c_int32), ("reserved2", C.c_int32)]
 
 
 class BnBwdPrologue(C.Structure):

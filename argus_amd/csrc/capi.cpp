@@ -27,7 +27,7 @@ using namespace argus;
 
 extern "C" {
 
-int argus_abi_version(void) { return 14; }
+int argus_abi_version(void) { return 15; }
 
 const char* argus_last_error(void) { return g_last_error.c_str(); }
 

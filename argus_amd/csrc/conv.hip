@@ -87,6 +87,8 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
   constexpr bool F8 = (BWX & kFp8Bit) != 0;     // MX-fp8 operands (bf16 activations, fp8 weights)
   constexpr bool OUT = (BWX & kOutBit) != 0;    // forward: bn3 + residual + ReLU epilogue (BnOutEpi)
   static_assert(!OUT || (BW == 0 && !AP && !F8 && !STEM && !PRO), "block-output epilogue: plain forward");
+  constexpr bool YREC = (BWX & kYrecBit) != 0;  // BN-backward epilogue: y recomputed (BnBwdEpi::yx)
+  static_assert(!YREC || ((BW == 3 || BW == 4) && !F8 && !STEM && !PRO && sizeof(T) == 2), "y recompute: bf16 dgrad");
   static_assert(!F8 || (sizeof(T) == 2 && !STEM && !PRO), "fp8: bf16 tensors, no BN+ReLU prologue");
   constexpr int E = Chunk<T>::E;
   constexpr int EF = F8 ? 2 * E : E;  // elements one thread stages per row per k-step
@@ -99,8 +101,11 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
   __shared__ uint8_t lds_sc[1][F8 ? BM + BN : 1][4];  // fp8: E8M0 scale of (row, 32-element block)
   constexpr int HALF_C = (BM / 2) * (BN + 16 / (int)sizeof(T)) * (int)sizeof(T);  // epilogue pass of BM/2 rows
   constexpr int RED_B = (256 / (BN * (int)sizeof(T) / 16)) * BN * 8;            // BN-backward column sums
+  // y recompute: the full C tile and the recomputed y tile side by side (BM x (BN + 8) bf16 each)
+  constexpr int YREC_B = YREC ? 2 * BM * (BN + 8) * 2 : 0;
   constexpr int LDS0 = NBUF * (BM + BN) * 128 > HALF_C ? NBUF * (BM + BN) * 128 : HALF_C;
-  constexpr int LDS_BYTES = LDS0 > RED_B ? LDS0 : RED_B;
+  constexpr int LDS1 = LDS0 > RED_B ? LDS0 : RED_B;
+  constexpr int LDS_BYTES = LDS1 > YREC_B ? LDS1 : YREC_B;
   __shared__ __attribute__((aligned(16))) u32x4 lds[LDS_BYTES / 16];
   __shared__ __attribute__((aligned(16))) float pro_lds[(PRO && !STEM) ? 2 * kProLds : 4];
 
@@ -457,12 +462,64 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
   constexpr int EPASS = (BM * LD * (int)sizeof(T) > LDS_BYTES) ? 2 : 1;
   constexpr int ROWS = BM / EPASS;
   static_assert(ROWS * LD * (int)sizeof(T) <= LDS_BYTES, "epilogue C tile exceeds the LDS array");
+  static_assert(!YREC || (EPASS == 1 && 2 * BM * LD * (int)sizeof(T) <= LDS_BYTES), "y recompute: C + y tiles");
   constexpr int CPR = BN * (int)sizeof(T) / 16;  // 16-byte chunks per row
   constexpr int RPP = 256 / CPR;                  // rows per store pass
   T* Cs = reinterpret_cast<T*>(lds);
+  T* Ys = Cs + BM * LD;  // YREC: the recomputed y tile
   T* __restrict__ Cg = reinterpret_cast<T*>(p.c);
   // output pixel = GEMM row (forward, stride-1 dgrad): no division per stored row
   const bool c_ident = p.osh == 1 && p.osw == 1 && ph.oh0 == 0 && ph.ow0 == 0 && ph.Hq == p.Ho && ph.Wq == p.Wo;
+  if constexpr (YREC) {
+    // y = conv1x1(yx, yw) of this tile's rows and columns, accumulated exactly as the forward GEMM does
+    // (k-steps of 64 in order, two 32-k MFMAs each, operands as the forward's LDS fragments), so the
+    // bf16-rounded result equals the y the forward would have stored, bit for bit. Runs while no other
+    // epilogue state is live (acc is still held; one B fragment at a time keeps the register budget).
+    const T* __restrict__ X2 = reinterpret_cast<const T*>(p.bb.yx);
+    const T* __restrict__ W2 = reinterpret_cast<const T*>(p.bb.yw);
+    const int K2 = p.bb.yk;
+    int xo[MI];
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi) {
+      const int m = mt * BM + wm * (BM / 2) + mi * 16 + i16;
+      const int mm = m < ph.M ? m : 0;
+      int px = mm;
+      if (!c_ident) {
+        const int nimg = mm / HWq, rem = mm - nimg * HWq;
+        const int qh = rem / ph.Wq, qw = rem - qh * ph.Wq;
+        px = (nimg * p.Ho + qh * p.osh + ph.oh0) * p.Wo + qw * p.osw + ph.ow0;
+      }
+      xo[mi] = px * K2;
+    }
+    const T* wrow = W2 + (size_t)(nt * BN + wn * (BN / 2) + i16) * K2;
+    f32x4 acc2[MI][NI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < K2; k0 += 64) {
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int kk = k0 + (4 * s2 + g) * 8;
+        u32x4 fa[MI];
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi) fa[mi] = ld16(X2 + xo[mi] + kk);
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) {
+          const u32x4 fb = ld16(wrow + (size_t)ni * 16 * K2 + kk);
+#pragma unroll
+          for (int mi = 0; mi < MI; ++mi) Mma<T>::run(acc2[mi][ni], fa[mi], fb);
+        }
+      }
+    }
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          Ys[(wm * (BM / 2) + mi * 16 + g * 4 + r) * LD + wn * (BN / 2) + ni * 16 + i16] = from_f32<T>(acc2[mi][ni][r]);
+  }
   BwdEpiAcc<T, BW> bwd;
   if constexpr (BW != 0) bwd.init(p.bb, nt * BN + (tid % CPR) * E);
   // block-output epilogue: this thread's chunk coefficients (its chunk column is fixed)
@@ -518,6 +575,11 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
         }
         if constexpr (OUT) {
           if (ok[u]) in[u].add = ld16(reinterpret_cast<const T*>(p.oe.res) + off[u]);
+        } else if constexpr (YREC) {
+          if (ok[u]) {
+            epi_load<T, BW, false>(p, off[u], in[u]);
+            in[u].y = *reinterpret_cast<const u32x4*>(Ys + rr * LD + c * E);
+          }
         } else if (ok[u]) {
           epi_load<T, BW>(p, off[u], in[u]);
         }
@@ -1109,6 +1171,13 @@ static void dispatch_ig(const IgParams& p, int maxM, int bm, int bn, hipStream_t
 // BN-backward epilogue (+ apply prologue) variants (dgrad only: no stem, no BN+ReLU prologue)
 template <typename T, int OCC, int APB>
 static void dispatch_ig_bwd1(const IgParams& p, int maxM, int bm, int bn, hipStream_t st) {
+  if constexpr (sizeof(T) == 2 && !(APB & kFp8Bit)) {
+    if (p.bb.yx) {  // y recomputed in the epilogue (block-output BN: mask bits, + the downsample branch)
+      if (bwd_variant(p.bb) == 4) dispatch_ig<T, false, OCC, 4 | APB | kYrecBit>(p, maxM, bm, bn, st);
+      else dispatch_ig<T, false, OCC, 3 | APB | kYrecBit>(p, maxM, bm, bn, st);
+      return;
+    }
+  }
   switch (bwd_variant(p.bb)) {
     case 2: dispatch_ig<T, false, OCC, 2 | APB>(p, maxM, bm, bn, st); break;
     case 3: dispatch_ig<T, false, OCC, 3 | APB>(p, maxM, bm, bn, st); break;
@@ -1177,6 +1246,9 @@ static const Policy kDefaultPolicy = [] {
   p.v[kGldsDgrad] = 1;
   p.v[kHaloDgrad] = 1;
   p.v[kGldsDgradStages] = 3;
+  // 42: the small-K dgrads with a BN-backward epilogue or an apply prologue built for 4 workgroups per CU
+  //     (128 VGPRs: the 64 x 128 apply + mask-bits variants spill 6 registers) or 3 (168 VGPRs)
+  p.v[kBwdSmallKOcc] = 4;
   return p;
 }();
 
@@ -1226,15 +1298,15 @@ static int run_ig(const IgParams& p, hipStream_t st, int bm, int bn) {
   }
   const bool smallk = maxK <= (*p.pol)[kSmallKMax];
   if constexpr (sizeof(T) == 2) {
-    if (f8_ok(p)) {  // single-buffered (the staged bf16 pair per chunk doubles the staging registers)
+    if (f8_ok(p) && !p.bb.yx) {  // single-buffered (the staged bf16 pair per chunk doubles the staging registers)
       if (p.ap.y) dispatch_ig_bwd1<T, 2, kFp8Bit | kApplyBit>(p, maxM, bm, bn, st);
       else dispatch_ig_bwd1<T, 2, kFp8Bit>(p, maxM, bm, bn, st);
       return check_launch("igemm_kernel");
     }
     // the statistics-only forward and the block-output epilogue exist on the register-staged kernel only
-    if (p.c || !p.fwd) {
-      if (!p.oe.out && conv3x3_halo_launch(p, st)) return check_launch("conv3x3_halo_kernel");
-      if (!p.oe.out && igemm_glds_launch(p, maxM, maxK, st)) return check_launch("igemm_glds_kernel");
+    if ((p.c || !p.fwd) && !p.oe.out && !p.bb.yx) {
+      if (conv3x3_halo_launch(p, st)) return check_launch("conv3x3_halo_kernel");
+      if (igemm_glds_launch(p, maxM, maxK, st)) return check_launch("igemm_glds_kernel");
     }
   }
   if (p.oe.out) {
@@ -1250,7 +1322,8 @@ static int run_ig(const IgParams& p, hipStream_t st, int bm, int bn) {
     if (smallk) dispatch_ig<T, true, 4>(p, maxM, bm, bn, st);
     else dispatch_ig<T, true, 2>(p, maxM, bm, bn, st);
   } else if (p.bb.mode || p.ap.y) {
-    if (smallk) dispatch_ig_bwd<T, 4>(p, maxM, bm, bn, st);
+    if (smallk && (*p.pol)[kBwdSmallKOcc] == 3) dispatch_ig_bwd<T, 3>(p, maxM, bm, bn, st);
+    else if (smallk) dispatch_ig_bwd<T, 4>(p, maxM, bm, bn, st);
     else dispatch_ig_bwd<T, 2>(p, maxM, bm, bn, st);
   } else {
     if (smallk) dispatch_ig<T, false, 4>(p, maxM, bm, bn, st);
@@ -1425,7 +1498,7 @@ static int dgrad_prow(const IgParams& p, int dtype) {
     maxM = p.ph[i].M > maxM ? p.ph[i].M : maxM;
     maxK = p.ph[i].K > maxK ? p.ph[i].K : maxK;
   }
-  if (dtype == ARGUS_BF16 && !f8_ok(p)) {
+  if (dtype == ARGUS_BF16 && !f8_ok(p) && !p.bb.yx) {
     if (conv3x3_halo_ok(p)) return conv3x3_halo_tiles(p);
     if (igemm_glds_ok(p, maxM, maxK)) return cdiv(maxM, 256);
   }
@@ -1501,9 +1574,14 @@ int conv_dgrad_bn(const argus_conv_desc& d, int dtype, const void* dy, const voi
   static const argus_bn_bwd_epilogue no_epilogue = {};
   const bool epi = bn != nullptr;
   if (!epi) bn = &no_epilogue;
-  if (epi && (!bn->y || !bn->mean || !bn->invstd || !bn->part || (bn->mask_mode != 2 && bn->mask_mode != 3)) ||
+  const bool yrec = epi && bn->y_x;
+  if (yrec && (dtype != ARGUS_BF16 || bn->y || !bn->y_w || bn->mask_mode != 3 || bn->y_k <= 0 || bn->y_k % 64)) {
+    set_error("conv_dgrad_bn: y recompute needs bf16, mask mode 3, y == NULL, y_w and y_k % 64 == 0");
+    return ARGUS_ERR_ARG;
+  }
+  if ((epi && ((!bn->y && !yrec) || !bn->mean || !bn->invstd || !bn->part || (bn->mask_mode != 2 && bn->mask_mode != 3))) ||
       (bn->mask_mode == 2 && (!bn->scale || !bn->shift || bn->y2)) || (bn->mask_mode == 3 && !bn->mask_bits) ||
-      (bn->y2 && (!bn->mean2 || !bn->invstd2 || !bn->part2)) || bn->y == dm) {
+      (bn->y2 && (!bn->mean2 || !bn->invstd2 || !bn->part2)) || (bn->y && bn->y == dm)) {
     set_error("conv_dgrad_bn: bad BN-backward epilogue arguments");
     return ARGUS_ERR_ARG;
   }
@@ -1514,7 +1592,8 @@ int conv_dgrad_bn(const argus_conv_desc& d, int dtype, const void* dy, const voi
   const Policy pol = policy_of(d);
   IgParams p;
   dgrad_params(d, pol, dy, wt, dm, addend, nullptr, p);
-  p.f8 = f8;
+  p.f8 = f8 && !yrec;
+  if (yrec) { p.bb.yx = bn->y_x; p.bb.yw = bn->y_w; p.bb.yk = bn->y_k; }
   if (pro) {
     // the register-staged kernel stages dy = ca*dm + cb*y + cc itself; the halo / glds kernels (LDS
     // DMA, no staging transform) get it materialised by the apply kernel first
@@ -1533,6 +1612,10 @@ int conv_dgrad_bn(const argus_conv_desc& d, int dtype, const void* dy, const voi
     }
   }
   dgrad_work(d, dtype, addend != nullptr, bn->mask_mode == 3, epi, bn->y2 != nullptr);
+  if (yrec) {  // y not read: its producing conv's input instead (+ the recompute flops)
+    g_launch_bytes -= 2.0 * (double)d.n * d.h * d.w * (d.c - bn->y_k);
+    g_launch_work += 2.0 * d.n * d.h * d.w * d.c * bn->y_k;
+  }
   if (p.ap.y)  // y in (+ dy out)
     g_launch_bytes += (dtype == ARGUS_BF16 ? 2.0 : 4.0) * (p.ap.out ? 2.0 : 1.0) * d.n * d.ho * d.wo * d.k;
   BnBwdEpi& b = p.bb;

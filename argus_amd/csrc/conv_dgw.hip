@@ -90,7 +90,10 @@ struct DgwStage {
 
 // BNE: the dx epilogue is bn2's backward (mask mode 2, partial sums, optional folded finalize); else a
 // plain store of dx (+ addend: the first block's downsample, accumulated onto conv1's dgrad)
-template <bool BNE>
+// YR: y (bn3's input, = this conv's own forward output conv(x, W)) is not read but recomputed from the
+// staged a2 tile and W (the transposed dgrad images), with the forward GEMM's accumulation order, so the
+// bf16 values equal what argus_conv_fwd would have stored (y need not exist: argus_conv_fwd_bn_out)
+template <bool BNE, bool YR>
 __global__ __launch_bounds__(256, 2) void dgw1x1_kernel(const DgwParams p) {
   // dy3 tile (2 images of 128 channels), a2 tile, W (2 images): 56 KB, two workgroups per CU; the
   // per-channel constants (apply coefficients of dy3, bn2's mean / invstd / scale / shift): 4 KB
@@ -133,7 +136,7 @@ __global__ __launch_bounds__(256, 2) void dgw1x1_kernel(const DgwParams p) {
     for (int i = 0; i < 4; ++i) {
       const int m = min(t * kBr + tid / 32 + 8 * i, p.P - 1);  // clamped; rows >= P are zeroed at staging
       S.dm[i] = ld16(p.dm + (size_t)m * kKo + ca_c * 8);
-      S.y[i] = ld16(p.y + (size_t)m * kKo + ca_c * 8);
+      if constexpr (!YR) S.y[i] = ld16(p.y + (size_t)m * kKo + ca_c * 8);
     }
     const size_t xo = (size_t)min(t * kBr + tid / 8, p.P - 1) * kCi + xc * 8;
     S.x = ld16(p.x + xo);
@@ -155,6 +158,44 @@ __global__ __launch_bounds__(256, 2) void dgw1x1_kernel(const DgwParams p) {
     if (t == (int)blockIdx.x) __syncthreads();  // the constants in LDS (first tile)
     u32x4 y2cur;  // this tile's epilogue BN input (S is refilled with the next tile below)
     if constexpr (BNE) y2cur = S.y2;
+    if constexpr (YR) {
+      // y[32 x 256] = a2[32 x 64] . W^T: wave w computes channels 64w .. 64w+63 (A from the a2 image, B by
+      // transposed reads of the W images: k = input channel j = image row), then writes its bf16 values
+      // into the dy3 images, where the apply below reads them as it would have read y
+      XA[dgw_pos(tid / 8, xc)] = sel(t * kBr + tid / 8 < p.P, S.x);
+      __syncthreads();
+      f32x4 yacc[2][4];
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) yacc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const u32x4* wimg = WD + (wave >> 1) * kImgW;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        u32x4 fa[2], fb[4];
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi) fa[mi] = dgw_frag(XA, 16 * mi + i16, 4 * s2 + g);
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) fb[ni] = dgw_frag_tr(wimg + 32 * s2 * 16, (wave & 1) * 4 + ni, g, i16);
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni) Mma<bf16>::run(yacc[mi][ni], fa[mi], fb[ni]);
+      }
+      bf16* dyh = reinterpret_cast<bf16*>(DY);
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+          const int ch = 64 * wave + 16 * ni + i16;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = 16 * mi + 4 * g + r;
+            dyh[((ch >> 7) * kImg + dgw_pos(row, (ch & 127) >> 3)) * 8 + (ch & 7)] = (bf16)yacc[mi][ni][r];
+          }
+        }
+      __syncthreads();
+    }
     {
       float ca[8], cb[8], cc[8];  // from LDS: registers go to the accumulators
       BwdEpiAcc<bf16, 3>::ld(ca, cst + ca_c * 8);
@@ -165,12 +206,13 @@ __global__ __launch_bounds__(256, 2) void dgw1x1_kernel(const DgwParams p) {
         const int row = tid / 32 + 8 * i;
         float d[8], yv[8];
         unpack(S.dm[i], d);
-        unpack(S.y[i], yv);
+        if constexpr (YR) unpack(DY[(ca_c >> 4) * kImg + dgw_pos(row, ca_c & 15)], yv);  // recomputed above
+        else unpack(S.y[i], yv);
 #pragma unroll
         for (int j = 0; j < 8; ++j) d[j] = fmaf(ca[j], d[j], fmaf(cb[j], yv[j], cc[j]));
         DY[(ca_c >> 4) * kImg + dgw_pos(row, ca_c & 15)] = sel(t * kBr + row < p.P, pack(d));
       }
-      XA[dgw_pos(tid / 8, xc)] = sel(t * kBr + tid / 8 < p.P, S.x);
+      if constexpr (!YR) XA[dgw_pos(tid / 8, xc)] = sel(t * kBr + tid / 8 < p.P, S.x);
     }
     __syncthreads();
     if (t + (int)gridDim.x < ntiles) load(t + gridDim.x, S);  // next tile in flight during the MFMAs
@@ -291,7 +333,7 @@ int conv_dgw(const argus_conv_desc& d, int dtype, const void* dm, const void* wd
     set_error("conv_dgrad_wgrad_bn: only bf16 1x1 stride-1 convs with 64 input and 256 output channels");
     return ARGUS_ERR_SHAPE;
   }
-  if (!dm || !wd || !x || !dx || !dw || !pro || !pro->y || !pro->ca || !pro->cb || !pro->cc || pro->dy_out ||
+  if (!dm || !wd || !x || !dx || !dw || !pro || !pro->ca || !pro->cb || !pro->cc || pro->dy_out ||
       (bn && (addend || bn->mask_mode != 2 || !bn->y || !bn->mean || !bn->invstd || !bn->scale || !bn->shift ||
               !bn->part || bn->y2 || bn->y == dx))) {
     set_error("conv_dgrad_wgrad_bn: bad arguments (apply prologue without dy_out; a mask-mode-2 epilogue or none, "
@@ -313,10 +355,12 @@ int conv_dgw(const argus_conv_desc& d, int dtype, const void* dm, const void* wd
   p.addend = reinterpret_cast<const bf16*>(addend);
   p.part_w = reinterpret_cast<float*>(ws);
   p.P = d.n * d.ho * d.wo;
+  const bool yr = p.y == nullptr;  // y recomputed from x and W (pro->y NULL)
   if (!bn) {
-    g_launch_work = 2.0 * 2.0 * p.P * kKo * kCi;
-    g_launch_bytes = 2.0 * ((double)p.P * (2 * kKo + (addend ? 3 : 2) * kCi)) + 4.0 * kKo * kCi;
-    timed_launch("argus::dgw1x1_kernel<false>", dgw1x1_kernel<false>, dim3(G), dim3(256), st, p);
+    g_launch_work = (yr ? 3.0 : 2.0) * 2.0 * p.P * kKo * kCi;
+    g_launch_bytes = 2.0 * ((double)p.P * ((yr ? 1 : 2) * kKo + (addend ? 3 : 2) * kCi)) + 4.0 * kKo * kCi;
+    if (yr) timed_launch("argus::dgw1x1_kernel<false, true>", dgw1x1_kernel<false, true>, dim3(G), dim3(256), st, p);
+    else timed_launch("argus::dgw1x1_kernel<false>", dgw1x1_kernel<false, false>, dim3(G), dim3(256), st, p);
     if (int e = check_launch("dgw1x1_kernel")) return e;
     return wgrad_reduce_launch(reinterpret_cast<const float*>(ws), G, kKo, kCi, 0, dw, st);
   }
@@ -339,9 +383,10 @@ int conv_dgw(const argus_conv_desc& d, int dtype, const void* dm, const void* wd
     f.rows = f.T;
   }
   // algorithmic work (ktimer): both GEMMs; bytes: dm, y, a2, y2 read, dx written, dW (fp32) written
-  g_launch_work = 2.0 * 2.0 * p.P * kKo * kCi;
-  g_launch_bytes = 2.0 * ((double)p.P * (2 * kKo + 3 * kCi)) + 4.0 * kKo * kCi;
-  timed_launch("argus::dgw1x1_kernel<true>", dgw1x1_kernel<true>, dim3(G), dim3(256), st, p);
+  g_launch_work = (yr ? 3.0 : 2.0) * 2.0 * p.P * kKo * kCi;
+  g_launch_bytes = 2.0 * ((double)p.P * ((yr ? 1 : 2) * kKo + 3 * kCi)) + 4.0 * kKo * kCi;
+  if (yr) timed_launch("argus::dgw1x1_kernel<true, true>", dgw1x1_kernel<true, true>, dim3(G), dim3(256), st, p);
+  else timed_launch("argus::dgw1x1_kernel<true>", dgw1x1_kernel<true, false>, dim3(G), dim3(256), st, p);
   if (int e = check_launch("dgw1x1_kernel")) return e;
   return wgrad_reduce_launch(reinterpret_cast<const float*>(ws), G, kKo, kCi, 0, dw, st);
 }

@@ -32,6 +32,9 @@ struct BnBwdEpi {
   float2* part2;
   int mode;               // 0 = off, 2, 3
   int prow;               // partial rows per dgrad phase
+  const void* yx;         // kYrecBit: y = conv1x1(yx, yw) recomputed in the epilogue (yk input channels)
+  const void* yw;
+  int yk;
 };
 
 // BN-backward apply folded into the A-operand staging of a dgrad (argus_bn_bwd_prologue): the A
@@ -90,6 +93,8 @@ constexpr int kApplyBit = 16;
 constexpr int kFp8Bit = 32;
 // bit 6: forward epilogue BnOutEpi (the bottleneck's bn3 + residual + ReLU applied to the C tile)
 constexpr int kOutBit = 64;
+// bit 7: the BN-backward epilogue's y recomputed from its producing 1x1 conv (BnBwdEpi::yx / yw)
+constexpr int kYrecBit = 128;
 
 struct WgParams {
   const void* x;
@@ -232,7 +237,7 @@ struct EpiIn {
   unsigned amask, bits;
 };
 
-template <typename T, int BW>
+template <typename T, int BW, bool LOADY = true>
 ARGUS_DEV void epi_load(const IgParams& p, size_t off, EpiIn& in) {
   constexpr int E = Chunk<T>::E;
   if (p.addend) {
@@ -240,7 +245,7 @@ ARGUS_DEV void epi_load(const IgParams& p, size_t off, EpiIn& in) {
     in.amask = p.addend_mask ? p.addend_mask[off / E] : 0xffu;
   }
   if constexpr (BW != 0) {
-    in.y = ld16(reinterpret_cast<const T*>(p.bb.y) + off);
+    if constexpr (LOADY) in.y = ld16(reinterpret_cast<const T*>(p.bb.y) + off);
     if constexpr (!BwdMode<BW>::RECOMPUTE) in.bits = p.bb.bits[off / E];
     if constexpr (BwdMode<BW>::DUAL) in.y2 = ld16(reinterpret_cast<const T*>(p.bb.y2) + off);
   }

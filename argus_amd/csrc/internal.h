@@ -46,7 +46,8 @@ enum TuneKey : int {
   kGldsDgrad = 39,      // data gradients may run on the glds kernel (forwards: key 8 alone)
   kHaloDgrad = 40,      // 3x3 data gradients may run on the LDS-halo kernel (forwards: key 10 alone)
   kGldsDgradStages = 41,  // LDS ring depth of the glds data gradients (3, or 2: 96 KB)
-  kNumTuneKeys = 42
+  kBwdSmallKOcc = 42,     // workgroups per CU the small-K BN-epilogue / apply-prologue dgrads are built for (4 or 3)
+  kNumTuneKeys = 43
 };
 struct Policy {
   int v[kNumTuneKeys];

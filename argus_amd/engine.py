@@ -155,6 +155,17 @@ class ResNetEngine:
         # stored), then one pass recomputes its C tile and applies bn3 + the residual + ReLU there
         # (argus_conv_fwd_bn_out): the bn_apply pass no longer reads y3 back (bit-identical outputs)
         self.fuse_out = True
+        # the block-output BN's backward reduction (in the epilogue of the next block's conv1 / downsample
+        # data gradient) recomputes bn3's input y3 from a2 and conv3's bf16 weights instead of reading it
+        # (argus_bn_bwd_epilogue.y_x; bit-identical): the 4w-channel y3 read becomes a w-channel a2 read.
+        # Measured slower (round 5, profiles/r05c_*): the recompute GEMM in the epilogue is load-latency
+        # bound, the producing dgrads took 244 / 237 us instead of 191 us (B=64; step 14.75 vs 14.06 ms)
+        self.yrec_epi = False
+        # ... and where every other reader of y3 recomputes it too (layer 1: the fused conv3 data + weight
+        # gradient, argus_conv_dgrad_wgrad_bn with pro->y NULL), y3 is never stored: the forward's fused
+        # tail writes only the block output (the debug capture keeps storing it for the stage checks);
+        # needs yrec_epi (saves ~0.1 ms at B=64 on its own: not enough to pay for it)
+        self.y3_free = False
         # (the schedule switches above are attributes, not environment variables: tools/engine_ab.py
         # A/B-measures them; test_gpu_train.py runs the overlap / tail placements against each other)
 
@@ -259,7 +270,9 @@ class ResNetEngine:
                       L.dll.argus_maxpool_bwd_bn_rows(dt, N, H1, W1, 64) * 64)
         for cv in convs.values():  # BN-backward partials written by dgrad epilogues (rows x C_in)
             if not cv.desc.stem:
-                max_bwd = max(max_bwd, L.dll.argus_conv_dgrad_bn_rows(C.byref(cv.desc), self.cdt) * cv.desc.c)
+                d_ = cv.desc
+                max_bwd = max(max_bwd, L.dll.argus_conv_dgrad_bn_rows(C.byref(d_), self.cdt) * d_.c,
+                              (4 - (-(d_.n * d_.h * d_.w) // 64)) * d_.c)  # y-recompute epilogues: 64-row tiles per phase
         # convs whose data and weight gradient run fused (argus_conv_dgrad_wgrad_bn)
         # (layer-1 conv3s, and the first block's downsample: the same 64 -> 256 channel 1x1 shape). It is a
         # bf16 kernel: with compute_dtype fp8 it serves these convs too unless the fp8 pass policy (key 37)
@@ -414,7 +427,7 @@ class ResNetEngine:
         H1, W1 = self.stem_hw
         L.maxpool_fwd(dt, N, H1, W1, 64, ptr(self.y0), ptr(st[2]), ptr(st[3]), ptr(self.p0), ptr(self.amax), s)
         h = self.p0
-        for b, a in zip(self.blocks, self.act):
+        for bi, (b, a) in enumerate(zip(self.blocks, self.act)):
             pf = b.prefix
             ds_done = None
             if b.has_ds and self.wgrad_overlap:
@@ -444,11 +457,12 @@ class ResNetEngine:
                 res, rsc, rsh = a["yd"], sd[2], sd[3]
             else:
                 res, rsc, rsh = h, None, None
-            if tail:  # conv3's C tile recomputed: y3 (kept for the backward), out and its mask in one pass
+            if tail:  # conv3's C tile recomputed: out, its mask (and y3 where the backward reads it) in one pass
                 cv3 = self.convs[pf + ".conv3"]
+                y3 = a["y3"] if training and not self._y3_free(bi) else None
                 self._launch(cv3, 0, lambda: L.conv_fwd_bn_out(
                     C.byref(cv3.desc), BF16, ptr(a["a2"]), ptr(cv3.wf), ptr(s3[2]), ptr(s3[3]), ptr(res), ptr(rsc),
-                    ptr(rsh), ptr(a["out"]), ptr(a["bits"]), ptr(a["y3"]), s))
+                    ptr(rsh), ptr(a["out"]), ptr(a["bits"]), ptr(y3), s))
             else:
                 L.bn_apply(dt, px, b.cout, ptr(a["y3"]), ptr(s3[2]), ptr(s3[3]), ptr(res), ptr(rsc), ptr(rsh), 1,
                            ptr(a["out"]), ptr(a["bits"]), s)
@@ -589,9 +603,9 @@ class ResNetEngine:
                                        (pf + ".downsample.1", a["yd"], dyd) if b.has_ds else None)
             # conv3 -> bn2
             dgw = wg3_apply and self.fold_fin and pf + ".conv3" in self.dgw
-            if dgw:  # data + weight gradient in one pass (dW on the main stream)
-                r2 = self._dgrad_wgrad_bn(pf + ".conv3", dh, dza, pf + ".bn2", a["y2"], pf + ".bn3", a["y3"], a["a2"],
-                                          P, G)
+            if dgw:  # data + weight gradient in one pass (dW on the main stream; y3 recomputed when not stored)
+                r2 = self._dgrad_wgrad_bn(pf + ".conv3", dh, dza, pf + ".bn2", a["y2"], pf + ".bn3",
+                                          None if self._y3_free(idx) else a["y3"], a["a2"], P, G)
                 if dy3 is not None:  # debug capture only: the fused kernel never stores dy3
                     self._bn_apply_bwd(pf + ".bn3", px_o, b.cout, dh, a["y3"], dy3)
             else:
@@ -647,14 +661,16 @@ class ResNetEngine:
             if idx > 0:
                 pb, pa = self.blocks[idx - 1], self.act[idx - 1]
                 second = (pb.prefix + ".downsample.1", pa["yd"]) if pb.has_ds else None
+                yrec = self._yrec(pb, pa)
+                y3p = None if yrec else pa["y3"]
                 if b.has_ds:
                     self._dgrad_plain_or_pro(pf + ".conv1", c1_in, dx, pro1)
                     rows3 = self._dgrad_bn(pf + ".downsample.0", dh if fuse else dyd, dx, dx, pb.prefix + ".bn3",
-                                           pa["y3"], 3, pa["bits"], second, P=P, G=G,
-                                           pro=(pf + ".downsample.1", a["yd"], dyd) if fuse else None)
+                                           y3p, 3, pa["bits"], second, P=P, G=G,
+                                           pro=(pf + ".downsample.1", a["yd"], dyd) if fuse else None, yrec=yrec)
                 else:
-                    rows3 = self._dgrad_bn(pf + ".conv1", c1_in, dx, dh, pb.prefix + ".bn3", pa["y3"], 3, pa["bits"],
-                                           second, P=P, G=G, pro=pro1)
+                    rows3 = self._dgrad_bn(pf + ".conv1", c1_in, dx, dh, pb.prefix + ".bn3", y3p, 3, pa["bits"],
+                                           second, P=P, G=G, pro=pro1, yrec=yrec)
             else:
                 self._dgrad(pf + ".conv1", dy1, dx)
                 if ds_dgw:  # dx += the downsample dgrad, its dW from the same staged dyd tile
@@ -724,7 +740,28 @@ class ResNetEngine:
         if on_ready is not None:
             on_ready("resnet.conv1.weight", self._comm)
 
-    def _dgrad_bn(self, conv, dy, dm, addend, bn, y, mode, bits=None, second=None, P=None, G=None, pro=None):
+    def _y3_free(self, idx: int) -> bool:
+        """Block ``idx``'s bn3 input y3 is never stored: its forward tail is fused, the next block's
+        BN-backward epilogue recomputes it, and its conv3 backward is the fused data + weight gradient,
+        which recomputes it as well (train mode; the last block's bn3 backward reads y3)."""
+        b = self.blocks[idx]
+        c3 = b.prefix + ".conv3"
+        return (self.y3_free and self._fused_tail() and self.debug is None and idx < len(self.blocks) - 1
+                and self.fuse_apply and self.wgrad_apply and self.fold_fin and c3 in self.dgw
+                and self.stages_pro[c3] and self._yrec(b, self.act[idx]) is not None)
+
+    def _yrec(self, blk, act):
+        """(a2, conv3's bf16 w_fwd, width) when block ``blk``'s y3 is recomputed rather than read by the
+        BN-backward epilogue that reduces its bn3 (bf16 schedule; not where the 1x1 data gradients take
+        MX-fp8 weights, policy key 37 bit 4), else None."""
+        if not (self.yrec_epi and self.materialize and act["a2"] is not None):
+            return None
+        if self.cdt == FP8 and (self.tuning or {}).get(37, self.L.dll.argus_conv_policy_default(37)) & 4:
+            return None
+        return act["a2"], self.convs[blk.prefix + ".conv3"].wf, blk.width
+
+    def _dgrad_bn(self, conv, dy, dm, addend, bn, y, mode, bits=None, second=None, P=None, G=None, pro=None,
+                  yrec=None):
         """dgrad of ``conv`` whose output feeds BN ``bn`` (input ``y``) backward: stores the masked dm
         and writes bwd_part (+ bwd_part2 for ``second`` = (bn name, y) of a downsample BN); returns the
         partial row count. With ``fold_fin`` the BN-backward finalize (dgamma, dbeta, ca/cb/cc) runs in
@@ -743,6 +780,8 @@ class ResNetEngine:
                     ptr(G[second[0] + ".bias"])
                 e.ca2, e.cb2, e.cc2 = ptr(cf2[0]), ptr(cf2[1]), ptr(cf2[2])
         e.y, e.mean, e.invstd, e.mask_mode = ptr(y), ptr(st[0]), ptr(st[1]), mode
+        if yrec is not None:  # y recomputed in the epilogue: conv1x1(a2, w_fwd of conv3)
+            e.y_x, e.y_w, e.y_k = ptr(yrec[0]), ptr(yrec[1]), yrec[2]
         if mode == 2:
             e.scale, e.shift = ptr(st[2]), ptr(st[3])
         else:

@@ -158,6 +158,15 @@ typedef struct {
   float* ca2;
   float* cb2;
   float* cc2;
+  /* Optional (ABI 15): with y_x != NULL the main branch's y is not read but recomputed in the kernel as
+   * the 1x1 stride-1 convolution of y_x (NHWC, y_k channels, the same pixel grid as dm) with y_w (the
+   * bf16 w_fwd copy of that conv, [C][y_k], argus_conv_weight_prep): bit-identical to the y that
+   * argus_conv_fwd would have stored, so y itself need not exist (argus_conv_fwd_bn_out with y = NULL).
+   * bf16, mask_mode 3, y_k a multiple of 64; y must then be NULL. */
+  const void* y_x;
+  const void* y_w;
+  int32_t y_k;
+  int32_t reserved2;
 } argus_bn_bwd_epilogue;
 /* Optional BN-backward apply folded into the dgrad's operand staging: with `pro` != NULL the `dy`
  * argument of argus_conv_dgrad_bn holds dm (the masked gradient of a BN output) and the dgrad consumes
@@ -197,8 +206,10 @@ int argus_conv_dgrad_bn(const argus_conv_desc* d, int dtype, const void* dy, con
  * (1) or on the register-staged weight-gradient kernel (0), key 35 the fewest GEMM rows (output
  * pixels) for which the forward uses 128-row tiles (fewer: 64), key 36 the fewest GEMM rows for the
  * glds kernel, key 37 which ARGUS_FP8 passes take MX-fp8 operands (bits: 1 forward, 2 data gradient of
- * a 3x3 conv, 4 data gradient of a 1x1 conv; argus_conv_weight_prep follows the same key). (Keys scaled with the batch keep a smaller batch's kernel selection that of the larger
- * one: tests/test_gpu_parity.py stage-checks the benched configurations' kernels that way.) */
+ * a 3x3 conv, 4 data gradient of a 1x1 conv; argus_conv_weight_prep follows the same key), key 42 the
+ * workgroups per CU (4 or 3) the small-K BN-epilogue / apply-prologue data gradients are built for.
+ * (Keys scaled with the batch keep a smaller batch's kernel selection that of the larger one:
+ * tests/test_gpu_parity.py stage-checks the benched configurations' kernels that way.) */
 int argus_conv_policy_default(int key);
 /* Which tile a pass launches and its algorithmic work: pass 0 fwd, 1 dgrad, 2 wgrad. Returns a
  * tag (kind*10^7 + dtype*10^6 + tile_m*1000 + tile_n; kind 1 igemm, 2 wgrad) and writes

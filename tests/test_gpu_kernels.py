@@ -1579,3 +1579,122 @@ def test_conv_fwd_bn_out_matches_conv_and_apply(cuda, cin, cout, hw, ds):
     ref = torch.einsum("nhwc,kc->nhwk", x.double(), wf.double()).to(torch.bfloat16).double() * sc.double() + sh.double()
     r = res.double() if rsc is None else res.double() * rsc.double() + rsh.double()
     assert _rel(o_ref, torch.relu(ref + r)) < TOL["bf16"]
+
+
+@pytest.mark.parametrize("w3,cout,hin,k1,s,dual,with_pro", [(64, 256, 12, 64, 1, False, True), (64, 256, 10, 128, 2, True, True),
+                                                            (128, 512, 6, 128, 1, True, False), (128, 512, 8, 256, 2, False, True)])
+def test_dgrad_bn_epilogue_y_recompute_bit_identical(cuda, w3, cout, hin, k1, s, dual, with_pro):
+    """argus_bn_bwd_epilogue.y_x: the block-output BN's input y (= conv3(a2), a 1x1 conv with w3 input
+    channels) recomputed inside the BN-backward epilogue of the next data gradient (a 1x1 conv from `cout`
+    to k1 channels, stride s: the next block's conv1 or its strided downsample, strided phases with
+    no taps included) instead of being read: dm, the partials (+ the downsample branch) and the folded
+    finalize's outputs bit-identical to the same dgrad reading the y that argus_conv_fwd stored."""
+    from argus_amd._lib import BnBwdEpilogue, BnBwdPrologue
+
+    torch.manual_seed(91)
+    L = lib()
+    n = 3
+    # conv3 of block b: a2 (w3 channels) -> y3 (cout), as the forward stores it
+    d3, _ = _desc(n, hin, hin, w3, cout, 1, 1)
+    a2 = torch.relu(torch.randn(n, hin, hin, w3, device=cuda)).to(torch.bfloat16)
+    wf3, _ = _prep(d3, "bf16", (torch.randn(cout, 1, 1, w3) * (2.0 / w3) ** 0.5).to(cuda), cuda)
+    y3 = torch.empty(n, hin, hin, cout, dtype=torch.bfloat16, device=cuda)
+    rows3 = L.dll.argus_conv_fwd_stat_rows(C.byref(d3), BF16)
+    st3 = torch.empty(rows3 * cout * 2, device=cuda)
+    L.conv_fwd(C.byref(d3), BF16, ptr(a2), ptr(wf3), ptr(y3), None, None, ptr(st3), stream())
+    # the data gradient of block b+1's 1x1 conv (cout -> k1, stride s) whose output feeds bn3's backward
+    d, _ = _desc(n, hin, hin, cout, k1, 1, s)
+    _, wt = _prep(d, "bf16", (torch.randn(k1, 1, 1, cout) * (2.0 / cout) ** 0.5).to(cuda), cuda)
+    dm_in = torch.randn(n, d.ho, d.wo, k1, device=cuda).to(torch.bfloat16)
+    ycoef = torch.randn(n, d.ho, d.wo, k1, device=cuda).to(torch.bfloat16)
+    ca, cb, cc = (torch.randn(k1, device=cuda) * 0.5 for _ in range(3))
+    yd = torch.randn(n, hin, hin, cout, device=cuda).to(torch.bfloat16)
+    mean, invstd = torch.randn(cout, device=cuda) * 0.1, torch.rand(cout, device=cuda) + 0.5
+    mean2, invstd2 = torch.randn(cout, device=cuda) * 0.1, torch.rand(cout, device=cuda) + 0.5
+    gamma, gamma2 = torch.rand(cout, device=cuda) + 0.5, torch.rand(cout, device=cuda) + 0.5
+    bits = torch.randint(0, 256, (n * hin * hin * cout // 8,), dtype=torch.uint8, device=cuda)
+    add = torch.randn(n, hin, hin, cout, device=cuda).to(torch.bfloat16)
+    rows = L.dll.argus_conv_dgrad_bn_rows(C.byref(d), BF16) + 8
+    outs = []
+    for rec in (False, True):
+        dm = add.clone()
+        part = torch.zeros(rows, cout, 2, device=cuda)
+        part2 = torch.zeros(rows, cout, 2, device=cuda)
+        ws = torch.zeros(L.dll.argus_bn_workspace_bytes(cout), dtype=torch.uint8, device=cuda)
+        fin = [torch.full((cout,), float("nan"), device=cuda) for _ in range(10)]
+        e = BnBwdEpilogue()
+        e.mean, e.invstd, e.mask_mode, e.mask_bits, e.part = ptr(mean), ptr(invstd), 3, ptr(bits), ptr(part)
+        e.workspace, e.gamma, e.dgamma, e.dbeta, e.ca, e.cb, e.cc = ptr(ws), ptr(gamma), *(ptr(t) for t in fin[:5])
+        if dual:
+            e.y2, e.mean2, e.invstd2, e.part2 = ptr(yd), ptr(mean2), ptr(invstd2), ptr(part2)
+            e.gamma2, e.dgamma2, e.dbeta2, e.ca2, e.cb2, e.cc2 = ptr(gamma2), *(ptr(t) for t in fin[5:])
+        if rec:
+            e.y_x, e.y_w, e.y_k = ptr(a2), ptr(wf3), w3
+        else:
+            e.y = ptr(y3)
+        pro = BnBwdPrologue(ptr(ycoef), ptr(ca), ptr(cb), ptr(cc), None) if with_pro else None
+        L.conv_dgrad_bn(C.byref(d), BF16, ptr(dm_in), ptr(wt), ptr(dm), ptr(dm), C.byref(e),
+                        C.byref(pro) if pro is not None else None, stream())
+        torch.cuda.synchronize()
+        outs.append((dm.clone(), part.clone(), part2.clone(), [t.clone() for t in fin]))
+    (a, p_, q, f), (b, r_, t_, h) = outs
+    assert torch.equal(a.view(torch.int16), b.view(torch.int16))
+    assert torch.equal(p_, r_) and torch.equal(q, t_)
+    assert all(torch.equal(x, z) or (torch.isnan(x).all() and torch.isnan(z).all()) for x, z in zip(f, h))
+    assert torch.isfinite(f[0]).all()
+
+
+def test_fused_dgrad_wgrad_y_recompute_bit_identical(cuda):
+    """argus_conv_dgrad_wgrad_bn with pro->y == NULL: bn3's input y3 = conv3(a2) recomputed inside the fused
+    layer-1 conv3 data + weight gradient (from the staged a2 tile and the W images) instead of read:
+    dx, dW and the folded bn2 finalize bit-identical to the same kernel reading the y3 argus_conv_fwd
+    stored; with and without the BN epilogue; ragged row counts."""
+    from argus_amd._lib import BnBwdEpilogue, BnBwdPrologue
+
+    torch.manual_seed(32)
+    L = lib()
+    cin, cout = 64, 256
+    for n, h, w_ in [(2, 33, 33), (1, 5, 7), (4, 64, 64)]:
+        d, _ = _desc(n, h, w_, cin, cout, 1, 1)
+        P = n * h * w_
+        wt_ohwi = (torch.randn(cout, 1, 1, cin) * (2.0 / cin) ** 0.5).to(cuda)
+        wf, wt = _prep(d, "bf16", wt_ohwi, cuda)
+        a2 = torch.relu(torch.randn(P, cin, device=cuda)).to(torch.bfloat16)
+        y3 = torch.empty(P, cout, dtype=torch.bfloat16, device=cuda)
+        st = torch.empty(L.dll.argus_conv_fwd_stat_rows(C.byref(d), BF16) * cout * 2, device=cuda)
+        L.conv_fwd(C.byref(d), BF16, ptr(a2), ptr(wf), ptr(y3), None, None, ptr(st), stream())
+        dm = torch.randn(P, cout, device=cuda).to(torch.bfloat16)
+        ca, cb, cc = (torch.randn(cout, device=cuda) * 0.3 for _ in range(3))
+        y2 = torch.randn(P, cin, device=cuda).to(torch.bfloat16)
+        mean, invstd = torch.randn(cin, device=cuda) * 0.1, torch.rand(cin, device=cuda) + 0.5
+        sc, sh = torch.randn(cin, device=cuda), torch.randn(cin, device=cuda)
+        g2 = torch.rand(cin, device=cuda) + 0.5
+        base = torch.randn(P, cin, device=cuda).to(torch.bfloat16)
+        for with_bn in (True, False):
+            res = []
+            for rec in (False, True):
+                ws = torch.zeros(L.dll.argus_bn_workspace_bytes(2048), dtype=torch.uint8, device=cuda)
+                rows = L.dll.argus_conv_dgrad_wgrad_bn_rows(C.byref(d), BF16)
+                part = torch.empty(rows, cin, 2, device=cuda)
+                co = torch.zeros(5, cin, device=cuda)
+                e = BnBwdEpilogue()
+                e.y, e.mean, e.invstd, e.mask_mode, e.scale, e.shift, e.part = ptr(y2), ptr(mean), ptr(invstd), 2, \
+                    ptr(sc), ptr(sh), ptr(part)
+                e.workspace, e.gamma, e.dgamma, e.dbeta = ptr(ws), ptr(g2), ptr(co[3]), ptr(co[4])
+                e.ca, e.cb, e.cc = ptr(co[0]), ptr(co[1]), ptr(co[2])
+                pro = BnBwdPrologue(None if rec else ptr(y3), ptr(ca), ptr(cb), ptr(cc), None)
+                dx = base.clone()
+                dw = torch.empty(cout, 1, 1, cin, device=cuda)
+                wsw = torch.empty(L.dll.argus_conv_dgrad_wgrad_workspace_bytes(C.byref(d), BF16), dtype=torch.uint8,
+                                  device=cuda)
+                rc = L.dll.argus_conv_dgrad_wgrad_bn(C.byref(d), BF16, ptr(dm), ptr(wt), ptr(a2), ptr(dx),
+                                                     None if with_bn else ptr(dx), C.byref(e) if with_bn else None,
+                                                     C.byref(pro), ptr(dw), ptr(wsw), wsw.numel(), stream())
+                assert rc == 0, L.dll.argus_last_error()
+                torch.cuda.synchronize()
+                res.append((dx.view(torch.int16).cpu(), dw.cpu(), co.cpu(), part.cpu()))
+            (x0, w0, c0, p0), (x1, w1, c1, p1) = res
+            assert torch.equal(x0, x1), (n, h, w_, with_bn)
+            assert torch.equal(w0, w1), (n, h, w_, with_bn)
+            if with_bn:
+                assert torch.equal(c0, c1) and torch.equal(p0, p1), (n, h, w_)

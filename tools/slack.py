@@ -50,6 +50,8 @@ def main():
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--pmc", default=None)
+    ap.add_argument("--cfg", default="", help="engine attributes attr=value[,attr=value] (as tools/engine_ab.py)")
+    ap.add_argument("--streams", default="main,all", help="which tables: main, all")
     a = ap.parse_args()
     from argus_amd.models import NCameraCNN
     from argus_amd.profiling import KernelTimer
@@ -63,19 +65,27 @@ def main():
     images, targets = synthetic_batch(a.batch, *a.hw, 1000, dev)
     torch.manual_seed(42)
     m = NCameraCNN(compute_dtype=a.dtype).to(dev).train()
+    eng = m._engine(dev)
+    for kv in filter(None, a.cfg.split(",")):
+        k, v = kv.split("=")
+        cur = getattr(eng, k)
+        setattr(eng, k, v == "1" if isinstance(cur, bool) else type(cur)(int(v)))
     tr = FusedTrainer(m, lr=1e-4, max_grad_norm=1.0)
     for _ in range(3):
         tr.step(images, targets)
     torch.cuda.synchronize()
     main_stream = torch.cuda.current_stream().cuda_stream
+    want = a.streams.split(",")
     for label, st in (("main stream", main_stream), ("all streams", None)):
+        if label.split()[0] not in want:
+            continue
         t = KernelTimer(stream=st)
         t.start()
         for _ in range(a.steps):
             tr.step(images, targets)
         s = t.summary()
         t.stop()
-        print(f"== {label}: B={a.batch} {a.hw[0]}x{a.hw[1]} {a.dtype}, per step (mean of {a.steps})")
+        print(f"== {label}: B={a.batch} {a.hw[0]}x{a.hw[1]} {a.dtype} [{a.cfg or 'defaults'}], per step (mean of {a.steps})")
         print(table(s, a.steps, a.dtype, pmc), flush=True)
 
 
