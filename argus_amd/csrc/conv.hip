@@ -1249,6 +1249,9 @@ static const Policy kDefaultPolicy = [] {
   // 42: the small-K dgrads with a BN-backward epilogue or an apply prologue built for 4 workgroups per CU
   //     (128 VGPRs: the 64 x 128 apply + mask-bits variants spill 6 registers) or 3 (168 VGPRs)
   p.v[kBwdSmallKOcc] = 4;
+  // 43: the bottleneck conv1 data gradients (1x1, apply prologue, mask-bits BN epilogue with the folded
+  //     finalize) on the persistent kernel of conv_p1x1.hip (1) or the register-staged igemm (0)
+  p.v[kP1x1Dgrad] = 1;
   return p;
 }();
 
@@ -1590,6 +1593,14 @@ int conv_dgrad_bn(const argus_conv_desc& d, int dtype, const void* dy, const voi
     return ARGUS_ERR_ARG;
   }
   const Policy pol = policy_of(d);
+  // the persistent conv1 data gradient (conv_p1x1.hip): the same dm bits, fewer partial rows
+  if (pol[kP1x1Dgrad] && epi && !yrec && bn->mask_mode == 3 && pro && !pro->dy_out && p1x1_ok(d, dtype) &&
+      !(f8 && (pol[kFp8Passes] & 4)) && bn->workspace && bn->gamma && bn->ca && bn->cb && bn->cc &&
+      (!bn->y2 || (bn->gamma2 && bn->ca2 && bn->cb2 && bn->cc2))) {
+    dgrad_work(d, dtype, addend != nullptr, true, true, bn->y2 != nullptr);
+    g_launch_bytes += 2.0 * d.n * d.ho * d.wo * d.k;  // the apply's y
+    return p1x1_launch(d, dy, wt, dm, addend, bn, pro, st);
+  }
   IgParams p;
   dgrad_params(d, pol, dy, wt, dm, addend, nullptr, p);
   p.f8 = f8 && !yrec;

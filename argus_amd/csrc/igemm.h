@@ -303,6 +303,12 @@ int wgrad_reduce_launch(const float* part, int splits, int M, int N, int stem, f
 // served by it (then conv.hip's kernel runs). _ok: the same choice without launching.
 bool igemm_glds_ok(const IgParams& p, int maxM, int maxK);
 bool igemm_glds_launch(const IgParams& p, int maxM, int maxK, hipStream_t st);
+// persistent 1x1 stride-1 dgrad with an apply prologue and a mask-bits BN-backward epilogue (the
+// bottleneck conv1 data gradients, conv_p1x1.hip): shape check, BN partial rows, launch
+bool p1x1_ok(const argus_conv_desc& d, int dtype);
+int p1x1_rows(const argus_conv_desc& d);
+int p1x1_launch(const argus_conv_desc& d, const void* dm, const void* wd, void* out, const void* addend,
+                const argus_bn_bwd_epilogue* bn, const argus_bn_bwd_prologue* pro, hipStream_t st);
 // 3x3 stride-1 forward / dgrad with an LDS-resident halo tile (conv_halo.hip); false = not served.
 // _ok returns the column tile it would launch (128 / 64) or 0.
 int conv3x3_halo_ok(const IgParams& p);

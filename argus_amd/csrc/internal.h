@@ -47,7 +47,8 @@ enum TuneKey : int {
   kHaloDgrad = 40,      // 3x3 data gradients may run on the LDS-halo kernel (forwards: key 10 alone)
   kGldsDgradStages = 41,  // LDS ring depth of the glds data gradients (3, or 2: 96 KB)
   kBwdSmallKOcc = 42,     // workgroups per CU the small-K BN-epilogue / apply-prologue dgrads are built for (4 or 3)
-  kNumTuneKeys = 43
+  kP1x1Dgrad = 43,        // the persistent 1x1 dgrad (apply prologue + mask-bits BN epilogue) for conv1 (1 on)
+  kNumTuneKeys = 44
 };
 struct Policy {
   int v[kNumTuneKeys];

@@ -650,7 +650,10 @@ class ResNetEngine:
             dy1 = None if wg1_apply and dbg is None else self._next_dy()
             pro1 = None
             if fuse and idx > 0:
-                pro1 = (pf + ".bn1", a["y1"], dy1)
+                # where the weight gradient stages the same apply (wg1_apply), the dgrad stores no dy1: the
+                # debug capture materialises it with the apply pass below instead, so the stage checks run
+                # the benched kernels (the persistent conv1 dgrad takes no dy_out)
+                pro1 = (pf + ".bn1", a["y1"], None if wg1_apply else dy1)
             else:
                 self._bn_apply_bwd(pf + ".bn1", px_i, b.width, dzb, a["y1"], dy1)
             # the block-input gradient goes to a fresh ring buffer (dm3 / dm1 may still be read by the
@@ -679,6 +682,8 @@ class ResNetEngine:
                 elif b.has_ds:
                     self._dgrad(pf + ".downsample.0", dyd, dx, addend=dx)
             if dy1 is not None:
+                if pro1 is not None and pro1[2] is None:  # debug capture only (see pro1)
+                    self._bn_apply_bwd(pf + ".bn1", px_i, b.width, dzb, a["y1"], dy1)
                 cap("b_dy1", dy1, px_i * b.width, (N, hi, wi, b.width))
             if b.has_ds:
                 cap("b_dyd", dyd, px_o * b.cout, (N, ho, wo, b.cout))

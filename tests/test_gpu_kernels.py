@@ -1698,3 +1698,64 @@ def test_fused_dgrad_wgrad_y_recompute_bit_identical(cuda):
             assert torch.equal(w0, w1), (n, h, w_, with_bn)
             if with_bn:
                 assert torch.equal(c0, c1) and torch.equal(p0, p1), (n, h, w_)
+
+
+@pytest.mark.parametrize("n4w,w,hw,dual", [(256, 64, 12, False), (256, 64, 9, True), (512, 128, 8, True),
+                                           (1024, 256, 5, False), (1024, 256, 7, True)])
+def test_persistent_conv1_dgrad_matches_igemm(cuda, n4w, w, hw, dual):
+    """The persistent 1x1 data gradient (conv_p1x1.hip, policy key 43: a bottleneck conv1's dgrad with the
+    BN-backward apply prologue and the previous block's output-BN backward epilogue, mask bits, optional
+    downsample branch, folded finalize) against the register-staged igemm_kernel it replaces (key 43 = 0):
+    dm bit-identical (same apply, same MFMA order, same bf16 rounding, addend, mask); the finalize outputs
+    (dgamma, dbeta, ca, cb, cc of both branches) to fp32 summation order (their partial rows group
+    differently); ragged row counts (hw = 5, 7, 9)."""
+    from argus_amd._lib import BnBwdEpilogue, BnBwdPrologue
+    from argus_amd.profiling import KernelTimer
+
+    torch.manual_seed(93)
+    L = lib()
+    n = 5
+    d, _ = _desc(n, hw, hw, n4w, w, 1, 1)  # conv1: 4w -> w; its dgrad: w -> 4w channels
+    _, wt = _prep(d, "bf16", (torch.randn(w, 1, 1, n4w) * (2.0 / n4w) ** 0.5).to(cuda), cuda)
+    P = n * hw * hw
+    dm1 = torch.randn(P, w, device=cuda).to(torch.bfloat16)
+    y1 = torch.randn(P, w, device=cuda).to(torch.bfloat16)
+    ca, cb, cc = (torch.randn(w, device=cuda) * 0.5 for _ in range(3))
+    dh = torch.randn(P, n4w, device=cuda).to(torch.bfloat16)
+    y3 = torch.randn(P, n4w, device=cuda).to(torch.bfloat16)
+    yd = torch.randn(P, n4w, device=cuda).to(torch.bfloat16)
+    bits = torch.randint(0, 256, (P * n4w // 8,), dtype=torch.uint8, device=cuda)
+    mean, invstd = torch.randn(n4w, device=cuda) * 0.1, torch.rand(n4w, device=cuda) + 0.5
+    mean2, invstd2 = torch.randn(n4w, device=cuda) * 0.1, torch.rand(n4w, device=cuda) + 0.5
+    gamma, gamma2 = torch.rand(n4w, device=cuda) + 0.5, torch.rand(n4w, device=cuda) + 0.5
+    rows = L.dll.argus_conv_dgrad_bn_rows(C.byref(d), BF16)
+    outs = []
+    for key in (0, 1):
+        dk = d.with_tuning({43: key})
+        out = torch.empty(P, n4w, dtype=torch.bfloat16, device=cuda)
+        part = torch.zeros(rows, n4w, 2, device=cuda)
+        part2 = torch.zeros(rows, n4w, 2, device=cuda)
+        ws = torch.zeros(L.dll.argus_bn_workspace_bytes(n4w), dtype=torch.uint8, device=cuda)
+        fin = [torch.full((n4w,), float("nan"), device=cuda) for _ in range(10)]
+        e = BnBwdEpilogue()
+        e.y, e.mean, e.invstd, e.mask_mode, e.mask_bits, e.part = ptr(y3), ptr(mean), ptr(invstd), 3, ptr(bits), \
+            ptr(part)
+        e.workspace, e.gamma, e.dgamma, e.dbeta, e.ca, e.cb, e.cc = ptr(ws), ptr(gamma), *(ptr(t) for t in fin[:5])
+        if dual:
+            e.y2, e.mean2, e.invstd2, e.part2 = ptr(yd), ptr(mean2), ptr(invstd2), ptr(part2)
+            e.gamma2, e.dgamma2, e.dbeta2, e.ca2, e.cb2, e.cc2 = ptr(gamma2), *(ptr(t) for t in fin[5:])
+        pro = BnBwdPrologue(ptr(y1), ptr(ca), ptr(cb), ptr(cc), None)
+        with KernelTimer() as kt:
+            L.conv_dgrad_bn(C.byref(dk), BF16, ptr(dm1), ptr(wt), ptr(out), ptr(dh), C.byref(e), C.byref(pro), stream())
+        torch.cuda.synchronize()
+        names = list(kt.summary())
+        assert any(nm.startswith("argus::p1x1_dgrad_kernel") for nm in names) == bool(key), names
+        assert int(ws[:16384].view(torch.int32).abs().sum()) == 0  # finalize counters left at zero
+        outs.append((out.view(torch.int16).clone(), [t.clone() for t in fin]))
+    (o0, f0), (o1, f1) = outs
+    assert torch.equal(o0, o1), (n4w, w, hw, dual)
+    for i, (a, b) in enumerate(zip(f0, f1)):
+        if not dual and i >= 5:
+            continue
+        assert torch.isfinite(b).all(), i
+        assert _rel(b, a) < 1e-5, (i, _rel(b, a))

@@ -167,7 +167,7 @@ def _conv_kernels(fn):
 
     with KernelTimer() as kt:
         fn()
-    return {n for n in kt.summary() if "igemm" in n or "conv3x3" in n or "wgrad" in n or "stem" in n}
+    return {n for n in kt.summary() if any(k in n for k in ("igemm", "conv3x3", "wgrad", "stem", "p1x1", "dgw"))}
 
 
 # (id, the benched configuration (B, H, W, dtype), the small batch its stages are re-derived at,
