@@ -18,7 +18,7 @@ import torch  # noqa: F401  (must precede the CDLL, see module docstring)
 LIB_PATH = Path(os.environ.get("ARGUS_HIP_LIB", Path(__file__).resolve().parent / "libargus_hip.so"))
 
 F32, BF16, FP8 = 0, 1, 2
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 
 class Tuning(C.Structure):
@@ -87,6 +87,9 @@ SIGNATURES = {
     "argus_conv_weight_prep_batch": (_I, [_I, _I, _P, _I, _P]),
     "argus_conv_fwd": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P, _P]),
     "argus_conv_fwd_bn_out": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "argus_conv_x8_ok": (_I, [_DESC, _I]),
+    "argus_conv_fwd_x8": (_I, [_DESC, _P, _P, _P, _P, _P]),
+    "argus_conv_dgrad_bn_x8": (_I, [_DESC, _P, _P, _P, C.POINTER(BnBwdEpilogue), _P]),
     "argus_conv_fwd_stat_rows": (_I, [_DESC, _I]),
     "argus_conv_fwd_stat_tile": (_I, [_DESC, _I]),
     "argus_conv_policy_default": (_I, [_I]),
@@ -113,10 +116,12 @@ SIGNATURES = {
     "argus_bn_finalize": (_I, [_I, _I, _I, _P, _I64, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "argus_bn_eval_coeffs": (_I, [_I, _P, _P, _P, _P, _F, _P, _P, _P]),
     "argus_bn_apply": (_I, [_I, _I64, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P]),
+    "argus_bn_apply_x8": (_I, [_I64, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P]),
     "argus_bn_bwd_rows": (_I, [_I64, _I]),
     "argus_bn_bwd_reduce": (_I, [_I, _I64, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "argus_bn_bwd_finalize": (_I, [_I, _I, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "argus_bn_bwd_apply": (_I, [_I, _I64, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "argus_bn_bwd_apply_x8": (_I, [_I64, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "argus_maxpool_fwd": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
     "argus_maxpool_bwd": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "argus_maxpool_bwd_bn_rows": (_I, [_I, _I, _I, _I, _I]),

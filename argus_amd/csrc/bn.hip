@@ -210,12 +210,23 @@ static EwGeom ew_geom(int C, int E, int64_t pixels, int target_blocks) {
 // flight (the memory-level parallelism an HBM stream needs at 4-8 waves per SIMD).
 constexpr int kEwU = 4;
 
+// MX-fp8 copy of a stored bf16 chunk (element offset off of a [P][C] tensor): 8 e4m3 bytes at out8 + off
+// and, by the first of the 4 lanes of each 32-channel block (chunk cc % 4 == 0), its E8M0 scale at
+// out8 + P*C + off / 32 (the x8 layout: argus_conv_fwd_x8)
+ARGUS_DEV void st_x8(uint8_t* out8, int64_t pc, int64_t off, u32x4 o, int cc) {
+  int e;
+  const uint2 q = mx_fp8_quant8(o, e);
+  *reinterpret_cast<uint2*>(out8 + off) = q;
+  if ((cc & 3) == 0) out8[pc + off / 32] = (uint8_t)(127 + e);
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void bn_apply_kernel(int64_t pixels, int C, int CC, int PL, int64_t ppb,
                                                        const T* __restrict__ y, const float* __restrict__ sc,
                                                        const float* __restrict__ sh, const T* __restrict__ res,
                                                        const float* __restrict__ rsc, const float* __restrict__ rsh,
-                                                       int relu, T* __restrict__ out, uint8_t* __restrict__ mask_out) {
+                                                       int relu, T* __restrict__ out, uint8_t* __restrict__ mask_out,
+                                                       uint8_t* __restrict__ out8) {
   constexpr int E = Chunk<T>::E;
   const int cc = threadIdx.x % CC, pl = threadIdx.x / CC;
   const int c0 = (blockIdx.x * CC + cc) * E;
@@ -255,6 +266,9 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(int64_t pixels, int C, in
       const u32x4 o = pack(f);
       st16(out + off, o);
       if (mask_out) mask_out[off / E] = chunk_positive_bits<T>(o);
+      if constexpr (E == 8) {
+        if (out8) st_x8(out8, pixels * C, off, o, cc);
+      }
     }
   }
 }
@@ -438,7 +452,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(int64_t pixels, int C
                                                            const float* __restrict__ cc_, T* __restrict__ dy,
                                                            T* __restrict__ dm_out, const T* __restrict__ y2,
                                                            const float* __restrict__ ca2, const float* __restrict__ cb2,
-                                                           const float* __restrict__ cc2, T* __restrict__ dy2) {
+                                                           const float* __restrict__ cc2, T* __restrict__ dy2,
+                                                           uint8_t* __restrict__ dy8) {
   constexpr int E = Chunk<T>::E;
   const int cc = threadIdx.x % CC, pl = threadIdx.x / CC;
   const int c0 = (blockIdx.x * CC + cc) * E;
@@ -479,7 +494,11 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(int64_t pixels, int C
       float o[E];
 #pragma unroll
       for (int j = 0; j < E; ++j) o[j] = fmaf(A[j], d[j], fmaf(Bc[j], yv[j], Cc[j]));
-      st16(dy + off, pack(o));
+      const u32x4 ov = pack(o);
+      st16(dy + off, ov);
+      if constexpr (E == 8) {
+        if (dy8) st_x8(dy8, pixels * C, off, ov, cc);
+      }
       if constexpr (DUAL) {
         float y2v[E];
         unpack(y2r[u], y2v);
@@ -788,10 +807,32 @@ int argus_bn_apply(int dtype, int64_t pixels, int C, const void* y, const float*
   g_launch_bytes = (16.0 / E) * pc * (2.0 + (res ? 1.0 : 0.0)) + (mask_out ? pc / E : 0.0);
   if (dtype == ARGUS_BF16)
     timed_launch(apply_name<bf16>(), bn_apply_kernel<bf16>, grid, dim3(256), st, pixels, C, g.CC, g.PL,
-                 g.ppb, (const bf16*)y, scale, shift, (const bf16*)res, rsc, rsh, relu, (bf16*)out, mask_out);
+                 g.ppb, (const bf16*)y, scale, shift, (const bf16*)res, rsc, rsh, relu, (bf16*)out, mask_out,
+                 (uint8_t*)nullptr);
   else
     timed_launch(apply_name<float>(), bn_apply_kernel<float>, grid, dim3(256), st, pixels, C, g.CC,
-                 g.PL, g.ppb, (const float*)y, scale, shift, (const float*)res, rsc, rsh, relu, (float*)out, mask_out);
+                 g.PL, g.ppb, (const float*)y, scale, shift, (const float*)res, rsc, rsh, relu, (float*)out, mask_out,
+                 (uint8_t*)nullptr);
+  return check_launch("bn_apply_kernel");
+}
+
+int argus_bn_apply_x8(int64_t pixels, int C, const void* y, const float* scale, const float* shift, const void* res,
+                      const float* rsc, const float* rsh, int relu, void* out, uint8_t* mask_out, void* out8,
+                      argus_stream_t stream) {
+  if (C % 32 || pixels <= 0 || !y || !scale || !shift || !out || !out8 || ((rsc == nullptr) != (rsh == nullptr)) ||
+      (rsc && !res)) {
+    set_error("bn_apply_x8: bad arguments (bf16, C a multiple of 32, out8 required)");
+    return ARGUS_ERR_ARG;
+  }
+  const EwGeom g = ew_geom(C, 8, pixels, kEwTarget);
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid(g.cgroups, g.rows);
+  const double pc = (double)pixels * C;
+  g_launch_work = 0.0;  // algorithmic bytes: y, residual, out, mask bits, the fp8 copy and its scales
+  g_launch_bytes = 2.0 * pc * (2.0 + (res ? 1.0 : 0.0)) + (mask_out ? pc / 8 : 0.0) + pc * (1.0 + 1.0 / 32);
+  timed_launch("argus::bn_apply_kernel<__bf16, x8>", bn_apply_kernel<bf16>, grid, dim3(256), st, pixels, C, g.CC,
+               g.PL, g.ppb, (const bf16*)y, scale, shift, (const bf16*)res, rsc, rsh, relu, (bf16*)out, mask_out,
+               (uint8_t*)out8);
   return check_launch("bn_apply_kernel");
 }
 
@@ -886,13 +927,33 @@ int argus_bn_bwd_apply(int dtype, int64_t pixels, int C, const void* dz, int mod
   timed_launch(bapp_name<TT, DU>(), bn_bwd_apply_kernel<TT, DU>, grid, dim3(256), st,     \
                pixels, C, g.CC, g.PL, g.ppb, (const TT*)dz, mode, mode == 1 ? (const TT*)mask : (const TT*)nullptr,  \
                mb, (const TT*)y, scale, shift, ca, cb, cc, (TT*)dy, (TT*)dm_out, (const TT*)y2, ca2, cb2, cc2,      \
-               (TT*)dy2)
+               (TT*)dy2, (uint8_t*)nullptr)
   if (dtype == ARGUS_BF16) {
     if (dual) ARGUS_BWD_APPLY(bf16, true); else ARGUS_BWD_APPLY(bf16, false);
   } else {
     if (dual) ARGUS_BWD_APPLY(float, true); else ARGUS_BWD_APPLY(float, false);
   }
 #undef ARGUS_BWD_APPLY
+  return check_launch("bn_bwd_apply_kernel");
+}
+
+int argus_bn_bwd_apply_x8(int64_t pixels, int C, const void* dm, const void* y, const float* ca, const float* cb,
+                          const float* cc, void* dy, void* dy8, argus_stream_t stream) {
+  if (C % 32 || pixels <= 0 || !dm || !y || !ca || !cb || !cc || !dy || !dy8) {
+    set_error("bn_bwd_apply_x8: bad arguments (bf16, C a multiple of 32, dy8 required)");
+    return ARGUS_ERR_ARG;
+  }
+  const EwGeom g = ew_geom(C, 8, pixels, kEwTarget);
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid(g.cgroups, g.rows);
+  const double pc = (double)pixels * C;
+  g_launch_work = 0.0;  // algorithmic bytes: dm, y, dy, the fp8 copy and its scales
+  g_launch_bytes = 2.0 * pc * 3.0 + pc * (1.0 + 1.0 / 32);
+  timed_launch("argus::bn_bwd_apply_kernel<__bf16, false, x8>", bn_bwd_apply_kernel<bf16, false>, grid, dim3(256), st,
+               pixels, C, g.CC, g.PL, g.ppb, (const bf16*)dm, 0, (const bf16*)nullptr, (const uint8_t*)nullptr,
+               (const bf16*)y, (const float*)nullptr, (const float*)nullptr, ca, cb, cc, (bf16*)dy, (bf16*)nullptr,
+               (const bf16*)nullptr, (const float*)nullptr, (const float*)nullptr, (const float*)nullptr,
+               (bf16*)nullptr, (uint8_t*)dy8);
   return check_launch("bn_bwd_apply_kernel");
 }
 

@@ -27,7 +27,7 @@ using namespace argus;
 
 extern "C" {
 
-int argus_abi_version(void) { return 15; }
+int argus_abi_version(void) { return 16; }
 
 const char* argus_last_error(void) { return g_last_error.c_str(); }
 
@@ -106,6 +106,20 @@ int argus_conv_dgrad_bn(const argus_conv_desc* d, int dtype, const void* dy, con
                         argus_stream_t stream) {
   if (!d || !dy || !wt || !dm) { set_error("conv_dgrad_bn: bad arguments"); return ARGUS_ERR_ARG; }
   return conv_dgrad_bn(*d, dtype, dy, wt, dm, addend, bn, pro, (hipStream_t)stream);
+}
+
+int argus_conv_x8_ok(const argus_conv_desc* d, int pass) { return d ? conv_x8_ok(*d, pass) : 0; }
+
+int argus_conv_fwd_x8(const argus_conv_desc* d, const void* x8, const void* w, void* y, float* stats,
+                      argus_stream_t stream) {
+  if (!d) { set_error("conv_fwd_x8: bad arguments"); return ARGUS_ERR_ARG; }
+  return conv_fwd_x8(*d, x8, w, y, stats, (hipStream_t)stream);
+}
+
+int argus_conv_dgrad_bn_x8(const argus_conv_desc* d, const void* dy8, const void* wt, void* dm,
+                           const argus_bn_bwd_epilogue* bn, argus_stream_t stream) {
+  if (!d || !dy8 || !wt || !dm) { set_error("conv_dgrad_bn_x8: bad arguments"); return ARGUS_ERR_ARG; }
+  return conv_dgrad_bn_x8(*d, dy8, wt, dm, bn, (hipStream_t)stream);
 }
 
 int argus_conv_wgrad_apply(const argus_conv_desc* d, int dtype, const void* x, const void* dm,

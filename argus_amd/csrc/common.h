@@ -139,6 +139,36 @@ ARGUS_DEV u32x4 mx_fp8_quant(u32x4 lo, u32x4 hi, int& e) {
   return u32x4{o[0], o[1], o[2], o[3]};
 }
 
+// The same quantization for 8 bf16 (one chunk; a 32-element block spans the 4 lanes l & ~3 .. l | 3,
+// which must all be active): the block amax over the 4 lanes, then 8 e4m3 bytes. Used by the
+// elementwise passes that store an MX-fp8 copy of their output (argus_bn_apply_x8 / _bwd_apply_x8):
+// the bytes and the exponent equal what mx_fp8_quant gives for the same 32 values.
+ARGUS_DEV uint2 mx_fp8_quant8(u32x4 v, int& e) {
+  const unsigned w[4] = {v.x, v.y, v.z, v.w};
+  u16x2v m = __builtin_bit_cast(u16x2v, w[0] & 0x7fff7fffu);
+#pragma unroll
+  for (int j = 1; j < 4; ++j) m = __builtin_elementwise_max(m, __builtin_bit_cast(u16x2v, w[j] & 0x7fff7fffu));
+  unsigned mb = m.x > m.y ? m.x : m.y;
+  unsigned mo = (unsigned)__shfl_xor((int)mb, 1, 64);
+  mb = mb > mo ? mb : mo;
+  mo = (unsigned)__shfl_xor((int)mb, 2, 64);
+  mb = mb > mo ? mb : mo;
+  const int E = (int)(mb >> 7), f = (int)(mb & 127u);
+  int ex = E == 0 ? 0 : E - 135 + (f >= 96 ? 1 : 0);
+  ex = ex < -126 ? -126 : (ex > 127 ? 127 : ex);
+  e = ex;
+  const float sc = __int_as_float((127 + ex) << 23);
+  unsigned o[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    s16x2v r = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16((s16x2v){0, 0}, __builtin_bit_cast(bf16x2v, w[2 * q]), sc,
+                                                          false);
+    r = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(r, __builtin_bit_cast(bf16x2v, w[2 * q + 1]), sc, true);
+    o[q] = __builtin_bit_cast(unsigned, r);
+  }
+  return uint2{o[0], o[1]};
+}
+
 // ReLU mask of a stored chunk: bit j set <=> element j > 0 (one byte per 16-byte chunk).
 template <typename T>
 ARGUS_DEV uint8_t chunk_positive_bits(u32x4 v) {

@@ -988,13 +988,18 @@ ARGUS_HOST_DEV inline int wp_blocks(int K, int R, int S, int C, int stem) {
 // moves that work out of every forward / dgrad launch.
 // policy key 37 bit of a pass: 1 forward, 2 data gradient of a 3x3 conv, 4 data gradient of a 1x1 conv
 // (with or without the apply prologue: one weight copy serves both)
+// Bit 8: the forward of 3x3 stride-1 convs only (the convs argus_conv_fwd_x8 serves from an MX-fp8
+// stored input; the other forwards stay bf16)
 static int fp8_pass_bits(int fwd, int ksz) { return fwd ? 1 : (ksz == 1 ? 4 : 2); }
+static bool fp8_pass(int passes, int fwd, int ksz, int stride) {
+  return (passes & fp8_pass_bits(fwd, ksz)) || (fwd && ksz == 3 && stride == 1 && (passes & 8));
+}
 
 // the passes of conv d that take fp8 operands under its policy: their weight copies get the fp8 layout
 static void wp_f8_layouts(const argus_conv_desc& d, int& f8f, int& f8d) {
   const int passes = policy_of(d)[kFp8Passes];
-  f8f = !d.stem && d.c % 128 == 0 && (passes & fp8_pass_bits(1, d.r));
-  f8d = !d.stem && d.k % 128 == 0 && (passes & fp8_pass_bits(0, d.r));
+  f8f = !d.stem && d.c % 128 == 0 && fp8_pass(passes, 1, d.r, d.stride);
+  f8d = !d.stem && d.k % 128 == 0 && fp8_pass(passes, 0, d.r, d.stride);
 }
 
 // 16 fp32 weights of one row -> bf16 (as the bf16 copy) -> 16 e4m3 + the 32-element block's scale
@@ -1286,7 +1291,7 @@ Policy policy_of(const argus_conv_desc& d) {
 // with ARGUS_FP8: wp_f8_fwd / wp_f8_dgrad pick the same convs).
 static bool f8_ok(const IgParams& p) {
   if (!p.f8 || p.stem || p.pro_scale || p.Cin % 128) return false;
-  if (!(fp8_pass_bits(p.fwd, p.ksz) & (*p.pol)[kFp8Passes])) return false;
+  if (!fp8_pass((*p.pol)[kFp8Passes], p.fwd, p.ksz, p.fwd ? p.ish : 0)) return false;
   for (int i = 0; i < p.nphase; ++i)
     if (p.ph[i].K % 128) return false;
   return true;
@@ -1301,6 +1306,11 @@ static int run_ig(const IgParams& p, hipStream_t st, int bm, int bn) {
   }
   const bool smallk = maxK <= (*p.pol)[kSmallKMax];
   if constexpr (sizeof(T) == 2) {
+    if (p.x8) {  // MX-fp8 stored operands: the F8 halo kernel only (argus_conv_fwd_x8 checked the shape)
+      if (conv3x3_halo_launch(p, st)) return check_launch("conv3x3_halo_kernel");
+      set_error("conv x8: not a halo-eligible conv");
+      return ARGUS_ERR_SHAPE;
+    }
     if (f8_ok(p) && !p.bb.yx) {  // single-buffered (the staged bf16 pair per chunk doubles the staging registers)
       if (p.ap.y) dispatch_ig_bwd1<T, 2, kFp8Bit | kApplyBit>(p, maxM, bm, bn, st);
       else dispatch_ig_bwd1<T, 2, kFp8Bit>(p, maxM, bm, bn, st);
@@ -1501,6 +1511,7 @@ static int dgrad_prow(const IgParams& p, int dtype) {
     maxM = p.ph[i].M > maxM ? p.ph[i].M : maxM;
     maxK = p.ph[i].K > maxK ? p.ph[i].K : maxK;
   }
+  if (p.x8) return conv3x3_halo_tiles(p);
   if (dtype == ARGUS_BF16 && !f8_ok(p) && !p.bb.yx) {
     if (conv3x3_halo_ok(p)) return conv3x3_halo_tiles(p);
     if (igemm_glds_ok(p, maxM, maxK)) return cdiv(maxM, 256);
@@ -1567,9 +1578,9 @@ int conv_dgrad_stages_prologue(const argus_conv_desc& d, int dtype) {
   return dgrad_stages_prologue(d, p.f8 ? ARGUS_BF16 : dtype, p) ? 1 : 0;
 }
 
-int conv_dgrad_bn(const argus_conv_desc& d, int dtype, const void* dy, const void* wt, void* dm,
-                  const void* addend, const argus_bn_bwd_epilogue* bn, const argus_bn_bwd_prologue* pro,
-                  hipStream_t st) {
+static int dgrad_bn_impl(const argus_conv_desc& d, int dtype, const void* dy, const void* wt, void* dm,
+                         const void* addend, const argus_bn_bwd_epilogue* bn, const argus_bn_bwd_prologue* pro,
+                         bool x8, hipStream_t st) {
   if (int e = check_desc(d)) return e;
   const bool f8 = dtype == ARGUS_FP8;
   if (f8) dtype = ARGUS_BF16;
@@ -1593,8 +1604,12 @@ int conv_dgrad_bn(const argus_conv_desc& d, int dtype, const void* dy, const voi
     return ARGUS_ERR_ARG;
   }
   const Policy pol = policy_of(d);
+  if (x8 && (pro || yrec || addend || (epi && bn->mask_mode != 2))) {
+    set_error("conv_dgrad_bn_x8: no apply prologue, addend or y recompute; BN epilogue mask mode 2 only");
+    return ARGUS_ERR_ARG;
+  }
   // the persistent conv1 data gradient (conv_p1x1.hip): the same dm bits, fewer partial rows
-  if (pol[kP1x1Dgrad] && epi && !yrec && bn->mask_mode == 3 && pro && !pro->dy_out && p1x1_ok(d, dtype) &&
+  if (!x8 && pol[kP1x1Dgrad] && epi && !yrec && bn->mask_mode == 3 && pro && !pro->dy_out && p1x1_ok(d, dtype) &&
       !(f8 && (pol[kFp8Passes] & 4)) && bn->workspace && bn->gamma && bn->ca && bn->cb && bn->cc &&
       (!bn->y2 || (bn->gamma2 && bn->ca2 && bn->cb2 && bn->cc2))) {
     dgrad_work(d, dtype, addend != nullptr, true, true, bn->y2 != nullptr);
@@ -1604,6 +1619,18 @@ int conv_dgrad_bn(const argus_conv_desc& d, int dtype, const void* dy, const voi
   IgParams p;
   dgrad_params(d, pol, dy, wt, dm, addend, nullptr, p);
   p.f8 = f8 && !yrec;
+  if (x8) {
+    int f8f, f8d;
+    wp_f8_layouts(d, f8f, f8d);
+    p.x8 = 1;
+    p.bb.mode = epi ? 2 : 0;  // (the shape check below sees the epilogue variant)
+    if (!f8d || !conv3x3_halo_x8_ok(p)) {
+      set_error("conv_dgrad_bn_x8: not served (3x3 stride-1 halo shapes, K % 128, MX-fp8 dgrad weights: "
+                "policy key 37 bit 2)");
+      return ARGUS_ERR_ARG;
+    }
+    p.bb.mode = 0;
+  }
   if (yrec) { p.bb.yx = bn->y_x; p.bb.yw = bn->y_w; p.bb.yk = bn->y_k; }
   if (pro) {
     // the register-staged kernel stages dy = ca*dm + cb*y + cc itself; the halo / glds kernels (LDS
@@ -1623,6 +1650,8 @@ int conv_dgrad_bn(const argus_conv_desc& d, int dtype, const void* dy, const voi
     }
   }
   dgrad_work(d, dtype, addend != nullptr, bn->mask_mode == 3, epi, bn->y2 != nullptr);
+  if (x8)  // dy and the weights as e4m3 + E8M0 scales
+    g_launch_bytes -= (double)d.n * d.ho * d.wo * d.k * (2.0 - 33.0 / 32) + (double)d.k * 9 * d.c * (2.0 - 33.0 / 32);
   if (yrec) {  // y not read: its producing conv's input instead (+ the recompute flops)
     g_launch_bytes -= 2.0 * (double)d.n * d.h * d.w * (d.c - bn->y_k);
     g_launch_work += 2.0 * d.n * d.h * d.w * d.c * bn->y_k;
@@ -1653,6 +1682,63 @@ int conv_dgrad_bn(const argus_conv_desc& d, int dtype, const void* dy, const voi
   }
   const int bm = dgrad_bm(pol), bn_ = pick_bn(pol, 1, d.c);
   return dtype == ARGUS_BF16 ? run_ig<bf16>(p, st, bm, bn_) : run_ig<float>(p, st, bm, bn_);
+}
+
+int conv_dgrad_bn(const argus_conv_desc& d, int dtype, const void* dy, const void* wt, void* dm,
+                  const void* addend, const argus_bn_bwd_epilogue* bn, const argus_bn_bwd_prologue* pro,
+                  hipStream_t st) {
+  return dgrad_bn_impl(d, dtype, dy, wt, dm, addend, bn, pro, false, st);
+}
+
+int conv_dgrad_bn_x8(const argus_conv_desc& d, const void* dy8, const void* wt, void* dm, const argus_bn_bwd_epilogue* bn,
+                     hipStream_t st) {
+  return dgrad_bn_impl(d, ARGUS_FP8, dy8, wt, dm, nullptr, bn, nullptr, true, st);
+}
+
+// MX-fp8 stored-operand forward (argus_conv_fwd_x8): the input as e4m3 [P][C] + E8M0 [P][C/32] (the
+// x8 copy argus_bn_apply_x8 writes beside the bf16 activation), the forward weights in the fp8 layout
+// (policy key 37 bit 8 or 1), bf16 y and the BN statistics partials as argus_conv_fwd
+int conv_fwd_x8(const argus_conv_desc& d, const void* x8, const void* w, void* y, float* stats, hipStream_t st) {
+  if (int e = check_desc(d)) return e;
+  if (!x8 || !w || !y) { set_error("conv_fwd_x8: bad arguments"); return ARGUS_ERR_ARG; }
+  const Policy pol = policy_of(d);
+  int f8f, f8d;
+  wp_f8_layouts(d, f8f, f8d);
+  IgParams p;
+  fwd_params(d, pol, p);
+  p.a = x8; p.b = w; p.c = y;
+  p.stats = reinterpret_cast<float2*>(stats);
+  p.stat_tile = fwd_bm(d, pol);
+  p.f8 = 1;
+  p.x8 = 1;
+  if (d.stem || !f8f || !conv3x3_halo_x8_ok(p)) {
+    set_error("conv_fwd_x8: not served (3x3 stride-1 halo shapes, C % 128, MX-fp8 forward weights: policy key 37 "
+              "bit 8)");
+    return ARGUS_ERR_ARG;
+  }
+  const double px = (double)d.n * d.ho * d.wo;
+  g_launch_work = 2.0 * px * d.k * 9 * d.c;
+  g_launch_bytes = 33.0 / 32 * ((double)d.n * d.h * d.w * d.c + (double)d.k * 9 * d.c) + 2.0 * px * d.k +
+                   (stats ? 8.0 * conv_fwd_stat_rows(d, ARGUS_FP8) * d.k : 0.0);
+  return run_ig<bf16>(p, st, p.stat_tile, 128);
+}
+
+// 1 when argus_conv_fwd_x8 (pass 0) / argus_conv_dgrad_bn_x8 (pass 1) serves conv d under its policy
+int conv_x8_ok(const argus_conv_desc& d, int pass) {
+  if (check_desc(d) || d.stem) return 0;
+  const Policy pol = policy_of(d);
+  int f8f, f8d;
+  wp_f8_layouts(d, f8f, f8d);
+  IgParams p;
+  if (pass == 0) {
+    fwd_params(d, pol, p);
+    if (!f8f) return 0;
+  } else {
+    dgrad_params(d, pol, nullptr, nullptr, nullptr, nullptr, nullptr, p);
+    if (!f8d) return 0;
+  }
+  p.x8 = 1;
+  return conv3x3_halo_x8_ok(p) ? 1 : 0;
 }
 
 struct WgPlan {

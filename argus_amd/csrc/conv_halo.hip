@@ -48,22 +48,38 @@ constexpr int kHaloPos1 = 416;  // single-buffer variant: 2 x (416 x 128 B + 3 x
 
 // HB = halo image buffers: 2 (double-buffered over 64-channel chunks) or 1 (Cin = 64: a single chunk,
 // nothing to prefetch; the 64-column tile then fits two workgroups per CU in LDS)
-template <int BN, int BW, int HB>
+// F8 (round 5): the A operand (the conv input / the data gradient's dy) and the weights are stored in the
+// OCP MX-fp8 x8 layout (e4m3 bytes [pixel][C] followed by one E8M0 scale per 32 channels [pixel][C/32],
+// written by argus_bn_apply_x8 / argus_bn_bwd_apply_x8 and argus_conv_weight_prep): a 128-channel chunk
+// is 128 bytes per halo position (the bf16 chunk's LDS footprint), its E8M0 scales 4 bytes per position
+// in their own LDS image, and each tap runs v_mfma_scale_f32_16x16x128_f8f6f4 (K = 128) per 16 x 16 tile:
+// twice the bf16 MFMA rate and half its LDS fragment reads per channel. Two weight stages instead of
+// three (the scale images take the third one's LDS), so the weight tile of tap j+1 loads under tap j.
+template <int BN, int BW, int HB, bool F8 = false>
 __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_halo_kernel(const IgParams p) {
   constexpr int WN = BN / 64, NW = 4 * WN, NT = NW * 64;
   constexpr int HPOS = HB == 1 ? kHaloPos1 : kHaloPos;  // halo positions per image buffer
   constexpr int HALO = HPOS * 128;              // bytes per halo image
   constexpr int BST = BN * 128;                 // bytes per weight stage
-  constexpr int NBS = 3;
+  constexpr int NBS = F8 ? 2 : 3;
+  constexpr int CH = F8 ? 128 : 64;             // channels per chunk (128 bytes per halo position either way)
+  constexpr int ES = F8 ? 1 : 2;                // bytes per element
+  constexpr int HSI = F8 ? (HPOS + 64 * NW - 1) / (64 * NW) : 0;  // halo scale DMAs per wave per chunk
+  // F8: E8M0 scales of one halo image (4 per position; padded to whole DMAs, so every wave issues the
+  // same number and the counted waits hold) and of one weight stage (4 per row)
+  constexpr int HSB = F8 ? HSI * NW * 256 : 0;
+  constexpr int BSB = F8 ? BN * 4 : 0;
+  constexpr int HS_OFF = HB * HALO + NBS * BST, BS_OFF = HS_OFF + HB * HSB;
   constexpr int LD = BN + 8;
   constexpr int EPI = 256 * LD * 2;
-  constexpr int MAIN = HB * HALO + NBS * BST;
+  constexpr int MAIN = HB * HALO + NBS * BST + HB * HSB + NBS * BSB;
   constexpr int LDS0 = MAIN > EPI ? MAIN : EPI;
   constexpr int RED_B = (NT / (BN / 8)) * BN * 8;  // BN-backward column sums
   constexpr int LDS_BYTES = LDS0 > RED_B ? LDS0 : RED_B;
   constexpr int HG = HPOS / (8 * NW);           // halo glds per wave per chunk
   constexpr int BG = BN * 8 / NT;               // weight glds per wave per tap
   static_assert(HG * 8 * NW == HPOS && BG * NT == BN * 8, "halo / tile partition");
+  static_assert(!F8 || (BN / NW == 16 && LDS_BYTES <= 163840 && BW != 3 && BW != 4), "fp8 halo: 16 weight rows per wave");
   __shared__ __attribute__((aligned(1024))) u32x4 lds[LDS_BYTES / 16];
 
   const IgPhase& ph = p.ph[0];
@@ -75,8 +91,8 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_h
   const int mt = bid / ntiles, nt = bid - mt * ntiles;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave - wm * WN;
-  const bf16* __restrict__ X = reinterpret_cast<const bf16*>(p.a);
-  const bf16* __restrict__ Wt = reinterpret_cast<const bf16*>(p.b);
+  const char* __restrict__ X = reinterpret_cast<const char*>(p.a);
+  const char* __restrict__ Wt = reinterpret_cast<const char*>(p.b);
   const uint32_t lds0 = (uint32_t)(uintptr_t)lds;
 
   // tile geometry: NI images x R rows x W columns of output = input (stride 1): 256 consecutive pixels
@@ -99,30 +115,63 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_h
     const int hr = rem / HWD, hc = rem - hr * HWD;
     const int ih = r0 + hr - 1, iw = hc - 1;
     h_ok[i] = q < npos && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
-    h_off[i] = h_ok[i] ? (((img0 + ii) * H + ih) * W + iw) * p.lda + ((lane & 7) ^ swz8(q)) * 8 : 0;
+    h_off[i] = h_ok[i] ? (((img0 + ii) * H + ih) * W + iw) * p.lda * ES + ((lane & 7) ^ swz8(q)) * 16 : 0;
   }
-  const bf16* b_src[BG];
+  const char* b_src[BG];
 #pragma unroll
   for (int i = 0; i < BG; ++i) {
     const int row = 8 * (i * NW + wave) + (lane >> 3);
-    b_src[i] = Wt + (size_t)(nt * BN + row) * p.ldb + ((lane & 7) ^ swz8(row)) * 8;
+    b_src[i] = Wt + (size_t)(nt * BN + row) * p.ldb * ES + ((lane & 7) ^ swz8(row)) * 16;
   }
   const void* zero = (const void*)halo_zero_page;
-  const int nch = p.Cin / 64;
+  const int nch = p.Cin / CH;
   const int nk = 9 * nch;
+  // F8: the scale DMAs (4 bytes a lane): halo position qs = 64*(j*NW + wave) + lane; weight row
+  // 16*wave + lane (lanes < 16)
+  const uint8_t* XS = reinterpret_cast<const uint8_t*>(p.a) + (size_t)ph.M * p.Cin;
+  const uint8_t* WS = reinterpret_cast<const uint8_t*>(p.b) + (size_t)p.N * p.ldb;
+  int hs_off[F8 ? HSI : 1];
+  bool hs_ok[F8 ? HSI : 1];
+  if constexpr (F8) {
+#pragma unroll
+    for (int j = 0; j < HSI; ++j) {
+      const int q = 64 * (j * NW + wave) + lane;
+      const int ii = q / IMGP, rem = q - ii * IMGP;
+      const int hr = rem / HWD, hc = rem - hr * HWD;
+      const int ih = r0 + hr - 1, iw = hc - 1;
+      hs_ok[j] = q < npos && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+      hs_off[j] = hs_ok[j] ? (((img0 + ii) * H + ih) * W + iw) * (p.Cin / 32) : 0;
+    }
+  }
+  const uint8_t* ws_row = WS + (size_t)(nt * BN + 16 * wave + (lane & 15)) * (p.ldb / 32);
 
   auto issue_halo = [&](int cc) {
     const uint32_t base = lds0 + (HB == 2 ? (cc & 1) * HALO : 0) + wave * 1024;
-    const int ci0 = cc * 64;
+    const int ci0 = cc * CH * ES;
 #pragma unroll
     for (int i = 0; i < HG; ++i) gl16(h_ok[i] ? (const void*)(X + h_off[i] + ci0) : zero, base + i * NW * 1024);
+    if constexpr (F8) {
+      const uint32_t sb = lds0 + HS_OFF + (HB == 2 ? (cc & 1) * HSB : 0);
+#pragma unroll
+      for (int j = 0; j < HSI; ++j)
+        __builtin_amdgcn_global_load_lds(hs_ok[j] ? (const void*)(XS + hs_off[j] + cc * 4) : zero,
+                                         (__attribute__((address_space(3))) void*)(uintptr_t)(sb + (j * NW + wave) * 256),
+                                         4, 0, 0);
+    }
   };
   auto issue_b = [&](int kt) {
     const int cc = kt / 9, t = kt - cc * 9;
-    const int off = ph.boff[t] + cc * 64;
+    const int off = (ph.boff[t] + cc * CH) * ES;
     const uint32_t base = lds0 + HB * HALO + (kt % NBS) * BST + wave * 1024;
 #pragma unroll
     for (int i = 0; i < BG; ++i) gl16(b_src[i] + off, base + i * NW * 1024);
+    if constexpr (F8) {  // this wave's 16 weight rows: 4 scale bytes each (lanes >= 16 masked)
+      if (lane < 16)
+        __builtin_amdgcn_global_load_lds((const void*)(ws_row + off / 32),
+                                         (__attribute__((address_space(3))) void*)(uintptr_t)(
+                                             lds0 + BS_OFF + (kt % NBS) * BSB + wave * 64),
+                                         4, 0, 0);
+    }
   };
 
   // per-thread fragment rows: halo position of output pixel m at tap (0,0)
@@ -147,6 +196,33 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_h
     const int toff = (ph.dh[t] + 1) * HWD + (ph.dw[t] + 1);
     const char* Hl = reinterpret_cast<const char*>(lds) + (HB == 2 ? (cc & 1) * HALO : 0);
     const char* Bl = reinterpret_cast<const char*>(lds) + HB * HALO + (kt % NBS) * BST;
+    if constexpr (F8) {
+      // lane (i16, g): K bytes [16g, 16g+16) and [64+16g, 64+16g+16) of the 128-channel chunk = 16-byte
+      // chunks g and g + 4; the scale operand: the E8M0 scale of (row i16, 32-channel block g)
+      const uint8_t* Hs = reinterpret_cast<const uint8_t*>(lds) + HS_OFF + (HB == 2 ? (cc & 1) * HSB : 0);
+      const uint8_t* Bs = reinterpret_cast<const uint8_t*>(lds) + BS_OFF + (kt % NBS) * BSB;
+      v8i fb[4];
+      int sb[4];
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const int row = wn * 64 + ni * 16 + i16;
+        fb[ni] = cat8(*reinterpret_cast<const u32x4*>(Bl + row * 128 + ((g ^ swz8(row)) << 4)),
+                      *reinterpret_cast<const u32x4*>(Bl + row * 128 + (((g + 4) ^ swz8(row)) << 4)));
+        sb[ni] = Bs[row * 4 + g];
+      }
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        const int q = hb[mi] + toff;
+        const v8i fa = cat8(*reinterpret_cast<const u32x4*>(Hl + q * 128 + ((g ^ swz8(q)) << 4)),
+                            *reinterpret_cast<const u32x4*>(Hl + q * 128 + (((g + 4) ^ swz8(q)) << 4)));
+        const int sa = Hs[q * 4 + g];
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fa, fb[ni], acc[mi][ni], 0, 0, 0, sa, 0,
+                                                                          sb[ni]);
+      }
+      return;
+    }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       u32x4 fa[4], fb[4];
@@ -175,10 +251,27 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_h
   // issue (an addend adds more: the wait below then only waits longer).
   constexpr int CPR_ = BN / 8, NITP = 256 / (NT / CPR_);
   // (BW 2 only, the 3x3 dgrads of the step: the mask-bit variants would spill the extra registers)
-  constexpr bool PRE = BW == 2;
+  constexpr bool PRE = BW == 2 && !F8;
   constexpr int NLD = PRE ? NITP : 0;
   EpiIn pre[PRE ? NITP : 1];
   const int kpre = p.epi_pre ? nk - 9 : -2;
+  if constexpr (F8) {
+    // two weight stages: issue order H(0) B(0) | per step j, after its barrier: [B(j+1)] [H(chunk(j)+1) if
+    // tap(j)==0]; a step waits for everything up to its B(j), the next chunk's halo may stay in flight
+    constexpr int HGS = HG + HSI;
+    issue_halo(0);
+    issue_b(0);
+    for (int kt = 0; kt < nk; ++kt) {
+      const int t = kt % 9, cc = kt / 9;
+      const bool halo_after = kt >= 1 && ((kt - 1) % 9 == 0) && ((kt - 1) / 9 + 1 < nch);
+      if (halo_after) waitvm<HGS>();
+      else waitvm<0>();
+      sbar();
+      if (kt + 1 < nk) issue_b(kt + 1);
+      if (t == 0 && cc + 1 < nch) issue_halo(cc + 1);
+      compute(kt);
+    }
+  } else {
   issue_halo(0);
   issue_b(0);
   if (nk > 1) issue_b(1);
@@ -210,6 +303,7 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_h
     if (t == 0 && cc + 1 < nch) issue_halo(cc + 1);
     if (kt + 2 < nk) issue_b(kt + 2);
     compute(kt);
+  }
   }
   waitvm<0>();
   __syncthreads();
@@ -303,28 +397,34 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_h
   }
 }
 
-template <int BN, int BW, int HB>
+template <int BN, int BW, int HB, bool F8>
 static const char* halo_name() {
   static const std::string s = std::string("argus::conv3x3_halo_kernel<") + std::to_string(BN) + ", " +
-                               std::to_string(BW) + ", " + std::to_string(HB) + ">";
+                               std::to_string(BW) + ", " + std::to_string(HB) + (F8 ? ", true>" : ">");
   return s.c_str();
 }
 
 // The BN-backward epilogue operands of the halo dgrad are prefetched under its last channel chunk on
 // the single-buffer 64-column variant (layer 1: 172 -> 163 us); on the 128-column one it measured
 // 83 -> 100 us (the step within noise), so that variant loads them after the loop.
-template <int BN, int BW, int HB>
+template <int BN, int BW, int HB, bool F8 = false>
 static void launch_halo2(const IgParams& p0, hipStream_t st) {
   IgParams p = p0;
   p.epi_pre = HB == 1;
   plan_fin(p, 256);
   dim3 grid(conv3x3_halo_tiles(p) * (p.N / BN));
-  timed_launch(halo_name<BN, BW, HB>(), conv3x3_halo_kernel<BN, BW, HB>, grid, dim3(4 * (BN / 64) * 64),
+  timed_launch(halo_name<BN, BW, HB, F8>(), conv3x3_halo_kernel<BN, BW, HB, F8>, grid, dim3(4 * (BN / 64) * 64),
                st, p);
 }
 
 template <int BN, int BW>
 static void launch_halo1(const IgParams& p, hipStream_t st) {
+  if constexpr (BW == 0 || BW == 2) {
+    if (p.x8) {  // conv3x3_halo_x8_ok: 128-channel chunks, two halo buffers
+      launch_halo2<BN, BW, 2, true>(p, st);
+      return;
+    }
+  }
   if constexpr (BN == 64) {
     const int HWi = p.H * p.W;
     const int npos = HWi >= 256 ? (256 / p.W + 2) * (p.W + 2) : (256 / HWi) * (p.H + 2) * (p.W + 2);
@@ -398,8 +498,18 @@ int conv3x3_halo_tiles(const IgParams& p) {
   return halo_geom(p, npos, tiles) ? tiles : 0;
 }
 
-bool conv3x3_halo_launch(const IgParams& p, hipStream_t st) {
+// the MX-fp8 stored-operand variant (argus_conv_fwd_x8 / argus_conv_dgrad_bn_x8): the halo shapes with
+// 128-channel chunks (Cin % 128), the plain forward or the BN-backward epilogue of mask mode 2, and
+// tightly packed x8 rows (lda == Cin; the scales follow the M x Cin bytes)
+int conv3x3_halo_x8_ok(const IgParams& p) {
   const int bn = conv3x3_halo_ok(p);
+  if (!bn || p.Cin % 128 || p.lda != p.Cin || p.ldb % 128 || p.addend || p.addend_mask) return 0;
+  const int bw = bwd_variant(p.bb);
+  return bw == 0 || bw == 2 ? bn : 0;
+}
+
+bool conv3x3_halo_launch(const IgParams& p, hipStream_t st) {
+  const int bn = p.x8 ? conv3x3_halo_x8_ok(p) : conv3x3_halo_ok(p);
   if (!bn) return false;
   if (bn == 128) launch_halo<128>(p, st);
   else launch_halo<64>(p, st);

@@ -82,6 +82,7 @@ struct IgParams {
   int fwd;        // host: forward params (1) or data gradient (0) - the fp8 pass policy (key 37)
   int ksz;        // host: filter size of the conv (1 or 3; the fp8 pass policy)
   int epi_pre;    // halo dgrad: prefetch the BN-backward epilogue operands under the last chunk
+  int x8;         // A and B stored as MX-fp8 (e4m3 rows + E8M0 scales): the F8 halo kernel (conv_halo.hip)
   const Policy* pol;  // host only (kernel selection of this call; never read on the device)
 };
 
@@ -315,6 +316,7 @@ int conv3x3_halo_ok(const IgParams& p);
 // workgroup row tiles of the halo fwd/dgrad for these params (BN-backward partial rows of its dgrad)
 int conv3x3_halo_tiles(const IgParams& p);
 bool conv3x3_halo_launch(const IgParams& p, hipStream_t st);
+int conv3x3_halo_x8_ok(const IgParams& p);
 // 3x3 stride-1 weight gradient with an LDS-resident halo tile (conv_halo.hip): plan / launch of the
 // split partials (fp32 [splits][K][9C]); false = not served
 bool wgrad3x3_halo_plan(const argus_conv_desc& d, int dtype, int* splits, int* tiles_per_split);

@@ -18,6 +18,10 @@ int conv_fwd_bn_out(const argus_conv_desc& d, int dtype, const void* x, const vo
 int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, void* y,
              const float* sc, const float* sh, float* stats, hipStream_t st);
 int conv_fwd_stat_rows(const argus_conv_desc& d, int dtype);
+int conv_fwd_x8(const argus_conv_desc& d, const void* x8, const void* w, void* y, float* stats, hipStream_t st);
+int conv_dgrad_bn_x8(const argus_conv_desc& d, const void* dy8, const void* wt, void* dm, const argus_bn_bwd_epilogue* bn,
+                     hipStream_t st);
+int conv_x8_ok(const argus_conv_desc& d, int pass);
 // BN workspace layout (bn.hip): [0, kBnCounterBytes) ticket counters, then double2 group results
 constexpr size_t kBnCounterBytes = 16384;
 int conv_fwd_stat_tile(const argus_conv_desc& d, int dtype);
@@ -41,7 +45,7 @@ enum TuneKey : int {
   kStemLdsWgrad = 34,   // bf16 stem weight gradient on the LDS-patch kernel
   kFwdBm128Rows = 35,   // fewest forward GEMM rows for 128-row tiles
   kGldsMinRows = 36,    // fewest GEMM rows (largest phase) for the glds kernel
-  kFp8Passes = 37,      // ARGUS_FP8: which passes take MX-fp8 operands (1 fwd | 2 dgrad | 4 dgrad with apply)
+  kFp8Passes = 37,      // ARGUS_FP8: which passes take MX-fp8 operands (1 fwd | 2 3x3 dgrad | 4 1x1 dgrad | 8 3x3 s1 fwd)
   kDgradApStaged = 38,  // 1x1 dgrad with an apply prologue: register-staged (1) or apply kernel + glds (0)
   kGldsDgrad = 39,      // data gradients may run on the glds kernel (forwards: key 8 alone)
   kHaloDgrad = 40,      // 3x3 data gradients may run on the LDS-halo kernel (forwards: key 10 alone)

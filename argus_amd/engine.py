@@ -166,6 +166,13 @@ class ResNetEngine:
         # tail writes only the block output (the debug capture keeps storing it for the stage checks);
         # needs yrec_epi (saves ~0.1 ms at B=64 on its own: not enough to pay for it)
         self.y3_free = False
+        # fp8: the 3x3 stride-1 convs whose forward (policy key 37 bit 8) / data gradient (bit 2) take
+        # MX-fp8 operands read them as stored MX-fp8 copies (argus_conv_fwd_x8 / argus_conv_dgrad_bn_x8):
+        # bn1's apply and bn2's backward apply write the e4m3 + E8M0 copy beside their bf16 output (the
+        # weight gradient still reads the bf16 one), and the LDS-halo kernel's F8 variant runs the conv at
+        # the fp8 MFMA rate; False: the register-staged fp8 kernel quantizes while staging (set before
+        # the first forward)
+        self.x8 = True
         # (the schedule switches above are attributes, not environment variables: tools/engine_ab.py
         # A/B-measures them; test_gpu_train.py runs the overlap / tail placements against each other)
 
@@ -235,6 +242,22 @@ class ResNetEngine:
         self.act = act
         self.final_hw = (h, w)
         self.convs = convs
+        # x8 passes of the 3x3 convs (fwd, dgrad) and one scratch buffer for their MX-fp8 operand (written
+        # and read back-to-back on the main stream)
+        self.x8_conv = {}
+        x8_bytes = 16
+        for b in self.blocks:
+            n = b.prefix + ".conv2"
+            d_ = convs[n].desc
+            on = self.x8 and self.cdt == FP8 and self.materialize
+            f = on and bool(L.dll.argus_conv_x8_ok(C.byref(d_), 0))
+            g = on and bool(L.dll.argus_conv_x8_ok(C.byref(d_), 1))
+            self.x8_conv[n] = (f, g)
+            if f:
+                x8_bytes = max(x8_bytes, d_.n * d_.h * d_.w * d_.c * 33 // 32)
+            if g:
+                x8_bytes = max(x8_bytes, d_.n * d_.ho * d_.wo * d_.k * 33 // 32)
+        self.x8buf = torch.empty(x8_bytes, dtype=torch.uint8, device=self.device)
 
         # BN state: rows of [mean, invstd, scale, shift] and backward coefficients [ca, cb, cc]
         self.bn_names = ["resnet.bn1"]
@@ -344,7 +367,9 @@ class ResNetEngine:
                               ptr(Bf[name + ".running_mean"]), ptr(Bf[name + ".running_var"]),
                               C.c_float(Bf.get(name + ".eps", 1e-5)), ptr(st[2]), ptr(st[3]), stream())
 
-    def _conv_bn(self, P, Bf, conv, bn, x, y, pro, training, part=None, ws=None):
+    def _conv_bn(self, P, Bf, conv, bn, x, y, pro, training, part=None, ws=None, x8=None):
+        """conv (+ BN statistics and finalize when training); ``x8``: the input's MX-fp8 copy
+        (argus_conv_fwd_x8 instead of argus_conv_fwd)."""
         cv = self.convs[conv]
         sc = sh = None
         if pro is not None:
@@ -355,8 +380,12 @@ class ResNetEngine:
             self._bn_eval(P, Bf, bn)
             return
         cdt = BF16 if y is None else self.cdt  # the statistics-only forward is the bf16 kernel
-        self._launch(cv, 0, lambda: self.L.conv_fwd(C.byref(cv.desc), cdt, ptr(x), ptr(cv.wf), ptr(y), ptr(sc),
-                                                     ptr(sh), ptr(part) if training else None, stream()))
+        if x8 is not None:
+            self._launch(cv, 0, lambda: self.L.conv_fwd_x8(C.byref(cv.desc), ptr(x8), ptr(cv.wf), ptr(y),
+                                                            ptr(part) if training else None, stream()))
+        else:
+            self._launch(cv, 0, lambda: self.L.conv_fwd(C.byref(cv.desc), cdt, ptr(x), ptr(cv.wf), ptr(y), ptr(sc),
+                                                         ptr(sh), ptr(part) if training else None, stream()))
         if training:
             count = cv.desc.n * cv.desc.ho * cv.desc.wo
             self._bn_train(P, Bf, bn, cv.stat_rows, cv.stat_tile, count, part, ws)
@@ -372,9 +401,14 @@ class ResNetEngine:
             return not ((self.tuning or {}).get(37, self.L.dll.argus_conv_policy_default(37)) & 1)
         return True
 
-    def _act(self, bn, y, out, px, ch):
-        """out = relu(y*scale + shift) with the finalized coefficients of BN layer ``bn``."""
+    def _act(self, bn, y, out, px, ch, out8=None):
+        """out = relu(y*scale + shift) with the finalized coefficients of BN layer ``bn`` (+ its MX-fp8
+        copy in ``out8``)."""
         st = self.bn_state[bn]
+        if out8 is not None:
+            self.L.bn_apply_x8(px, ch, ptr(y), ptr(st[2]), ptr(st[3]), None, None, None, 1, ptr(out), None, ptr(out8),
+                               stream())
+            return
         self.L.bn_apply(self.dt, px, ch, ptr(y), ptr(st[2]), ptr(st[3]), None, None, None, 1, ptr(out), None, stream())
 
     def prepare_weights(self, P) -> None:
@@ -439,8 +473,11 @@ class ResNetEngine:
             self._conv_bn(P, Bf, pf + ".conv1", pf + ".bn1", h, a["y1"], None, training)
             tail = self._fused_tail()
             if self.materialize:
-                self._act(pf + ".bn1", a["y1"], a["a1"], N * a["hw_in"][0] * a["hw_in"][1], b.width)
-                self._conv_bn(P, Bf, pf + ".conv2", pf + ".bn2", a["a1"], a["y2"], None, training)
+                x8f = self.x8_conv[pf + ".conv2"][0]
+                self._act(pf + ".bn1", a["y1"], a["a1"], N * a["hw_in"][0] * a["hw_in"][1], b.width,
+                          self.x8buf if x8f else None)
+                self._conv_bn(P, Bf, pf + ".conv2", pf + ".bn2", a["a1"], a["y2"], None, training,
+                              x8=self.x8buf if x8f else None)
                 self._act(pf + ".bn2", a["y2"], a["a2"], N * a["hw"][0] * a["hw"][1], b.width)
                 self._conv_bn(P, Bf, pf + ".conv3", pf + ".bn3", a["a2"], None if tail else a["y3"], None, training)
             else:
@@ -626,18 +663,19 @@ class ResNetEngine:
             if r2:
                 self._bn_bwd_fin(P, G, pf + ".bn2", px_o, b.width, self.bwd_part, r2)
             dy2 = self._next_dy()
-            if fuse:
+            x8d = self.x8_conv[pf + ".conv2"][1]
+            if fuse and not x8d:
                 pro2 = (pf + ".bn2", a["y2"], dy2)
             else:
                 pro2 = None
-                self._bn_apply_bwd(pf + ".bn2", px_o, b.width, dza, a["y2"], dy2)
+                self._bn_apply_bwd(pf + ".bn2", px_o, b.width, dza, a["y2"], dy2, dy8=self.x8buf if x8d else None)
             # conv2 -> bn1 (dm1 goes to a ring buffer when the side stream's conv1 wgrad reads it)
             if wg1_apply:
                 dzb = self._next_dy()
             if self.gate3x3:
                 self._drain_side()
             r1 = self._dgrad_bn(pf + ".conv2", dza if pro2 else dy2, dzb, None, pf + ".bn1", a["y1"], 2, P=P, G=G,
-                                pro=pro2)
+                                pro=pro2, x8=self.x8buf if x8d else None)
             cap("b_dy2", dy2, px_o * b.width, (N, ho, wo, b.width))
             cap("b_dz1", dzb, px_i * b.width, (N, hi, wi, b.width))
             s1 = self.bn_state[pf + ".bn1"]
@@ -766,7 +804,7 @@ class ResNetEngine:
         return act["a2"], self.convs[blk.prefix + ".conv3"].wf, blk.width
 
     def _dgrad_bn(self, conv, dy, dm, addend, bn, y, mode, bits=None, second=None, P=None, G=None, pro=None,
-                  yrec=None):
+                  yrec=None, x8=None):
         """dgrad of ``conv`` whose output feeds BN ``bn`` (input ``y``) backward: stores the masked dm
         and writes bwd_part (+ bwd_part2 for ``second`` = (bn name, y) of a downsample BN); returns the
         partial row count. With ``fold_fin`` the BN-backward finalize (dgamma, dbeta, ca/cb/cc) runs in
@@ -797,8 +835,12 @@ class ResNetEngine:
             e.y2, e.mean2, e.invstd2, e.part2 = ptr(second[1]), ptr(st2[0]), ptr(st2[1]), ptr(self.bwd_part2)
         pp = self._prologue(pro)
         self._guard(dm)
-        self._launch(cv, 1, lambda: self.L.conv_dgrad_bn(C.byref(cv.desc), self.cdt, ptr(dy), ptr(cv.wd), ptr(dm),
-                                                          ptr(addend), C.byref(e), pp, stream()))
+        if x8 is not None:  # dy read as its MX-fp8 copy (argus_conv_dgrad_bn_x8; no addend / prologue)
+            self._launch(cv, 1, lambda: self.L.conv_dgrad_bn_x8(C.byref(cv.desc), ptr(x8), ptr(cv.wd), ptr(dm),
+                                                                 C.byref(e), stream()))
+        else:
+            self._launch(cv, 1, lambda: self.L.conv_dgrad_bn(C.byref(cv.desc), self.cdt, ptr(dy), ptr(cv.wd),
+                                                              ptr(dm), ptr(addend), C.byref(e), pp, stream()))
         return 0 if self.fold_fin else self.L.dll.argus_conv_dgrad_bn_rows(C.byref(cv.desc), self.cdt)
 
     def _dgrad_wgrad_bn(self, conv, dm, dx, bn, y, pbn, py, x, P, G, addend=None):
@@ -848,10 +890,15 @@ class ResNetEngine:
         self._launch(cv, 1, lambda: self.L.conv_dgrad_bn(C.byref(cv.desc), self.cdt, ptr(dy), ptr(cv.wd), ptr(dx),
                                                           None, None, pp, stream()))
 
-    def _bn_apply_bwd(self, name, px, ch, dm, y, dy_out, second=None):
-        """dy = ca*dm + cb*y + cc from an already-masked dm (+ the downsample BN's dy2 from the same dm)."""
+    def _bn_apply_bwd(self, name, px, ch, dm, y, dy_out, second=None, dy8=None):
+        """dy = ca*dm + cb*y + cc from an already-masked dm (+ the downsample BN's dy2 from the same dm, or
+        dy's MX-fp8 copy in ``dy8``)."""
         cf = self.bn_coef[name]
         self._guard(dy_out)
+        if dy8 is not None:
+            self.L.bn_bwd_apply_x8(px, ch, ptr(dm), ptr(y), ptr(cf[0]), ptr(cf[1]), ptr(cf[2]), ptr(dy_out), ptr(dy8),
+                                   stream())
+            return
         y2 = ca2 = cb2 = cc2 = dy2 = None
         if second is not None:
             cf2 = self.bn_coef[second[0]]

@@ -190,6 +190,23 @@ int argus_conv_dgrad_stages_prologue(const argus_conv_desc* d, int dtype);
 int argus_conv_dgrad_bn(const argus_conv_desc* d, int dtype, const void* dy, const void* w_dgrad,
                         void* dm, const void* addend, const argus_bn_bwd_epilogue* bn,
                         const argus_bn_bwd_prologue* pro, argus_stream_t stream);
+/* MX-fp8 stored operands (ABI 16; ARGUS_FP8 networks, the 3x3 stride-1 convs of Bottleneck.conv2 in
+ * torchvision's ResNet-50 layers 2-4, argus/models.py:43). An "x8" tensor is the MX-fp8 copy of a bf16
+ * NHWC tensor [P][C]: P*C e4m3 bytes (OCP, the value / 2^e rounded to nearest even) followed by P*C/32
+ * E8M0 scale bytes (127 + e, one per 32 consecutive channels of a pixel), e chosen as ARGUS_FP8's
+ * staging quantizer chooses it; argus_bn_apply_x8 / argus_bn_bwd_apply_x8 write it beside their bf16
+ * output. argus_conv_fwd_x8 is argus_conv_fwd(ARGUS_FP8) without a prologue, its input read as the x8
+ * copy x8 (bit-identical to quantizing the bf16 input while staging); argus_conv_dgrad_bn_x8 is
+ * argus_conv_dgrad_bn(ARGUS_FP8) with dy read as x8 (bn NULL, or mask mode 2; no addend / prologue /
+ * y recompute). Both need the fp8 weight copies of argus_conv_weight_prep(ARGUS_FP8): policy key 37
+ * bit 8 (forward of 3x3 stride-1 convs) and bit 2 (3x3 data gradients). argus_conv_x8_ok(d, pass)
+ * is 1 when pass 0 (forward) / 1 (data gradient) of d is served (C resp. K % 128 == 0, the LDS-halo
+ * shapes, the policy bits). */
+int argus_conv_x8_ok(const argus_conv_desc* d, int pass);
+int argus_conv_fwd_x8(const argus_conv_desc* d, const void* x8, const void* w_fwd, void* y, float* stat_part,
+                      argus_stream_t stream);
+int argus_conv_dgrad_bn_x8(const argus_conv_desc* d, const void* dy8, const void* w_dgrad, void* dm,
+                           const argus_bn_bwd_epilogue* bn, argus_stream_t stream);
 /* Kernel-selection policy: the library's immutable default of a key (-1 for an unknown key); a conv
  * descriptor may override keys for its own call (argus_conv_desc.tuning; an unknown key there makes
  * the call fail with ARGUS_ERR_ARG). Every default is the measured best.
@@ -206,7 +223,8 @@ int argus_conv_dgrad_bn(const argus_conv_desc* d, int dtype, const void* dy, con
  * (1) or on the register-staged weight-gradient kernel (0), key 35 the fewest GEMM rows (output
  * pixels) for which the forward uses 128-row tiles (fewer: 64), key 36 the fewest GEMM rows for the
  * glds kernel, key 37 which ARGUS_FP8 passes take MX-fp8 operands (bits: 1 forward, 2 data gradient of
- * a 3x3 conv, 4 data gradient of a 1x1 conv; argus_conv_weight_prep follows the same key), key 42 the
+ * a 3x3 conv, 4 data gradient of a 1x1 conv, 8 forward of a 3x3 stride-1 conv;
+ * argus_conv_weight_prep follows the same key), key 42 the
  * workgroups per CU (4 or 3) the small-K BN-epilogue / apply-prologue data gradients are built for.
  * (Keys scaled with the batch keep a smaller batch's kernel selection that of the larger one:
  * tests/test_gpu_parity.py stage-checks the benched configurations' kernels that way.) */
@@ -293,6 +311,11 @@ int argus_bn_apply(int dtype, int64_t pixels, int channels, const void* y, const
                    const float* shift, const void* res, const float* res_scale,
                    const float* res_shift, int relu, void* out, uint8_t* mask_out,
                    argus_stream_t stream);
+/* argus_bn_apply (bf16, channels % 32 == 0) that also writes the x8 copy of out to out8 (ABI 16;
+ * argus_conv_fwd_x8). */
+int argus_bn_apply_x8(int64_t pixels, int channels, const void* y, const float* scale, const float* shift,
+                      const void* res, const float* res_scale, const float* res_shift, int relu, void* out,
+                      uint8_t* mask_out, void* out8, argus_stream_t stream);
 /* Backward. mask_mode: 0 none; 1 relu mask from the tensor `mask` (>0, e.g. a block output);
  * 2 relu mask recomputed from y as (y*scale+shift > 0); 3 relu mask from the bits `mask` written
  * by argus_bn_apply. dm = dz*mask.
@@ -317,6 +340,10 @@ int argus_bn_bwd_apply(int dtype, int64_t pixels, int channels, const void* dz, 
                        const float* ca, const float* cb, const float* cc, void* dy, void* dm_out,
                        const void* y2, const float* ca2, const float* cb2, const float* cc2, void* dy2,
                        argus_stream_t stream);
+/* dy = ca*dm + cb*y + cc from an already-masked dm (mask mode 0, bf16, channels % 32 == 0), plus the
+ * x8 copy of dy in dy8 (ABI 16; argus_conv_dgrad_bn_x8). */
+int argus_bn_bwd_apply_x8(int64_t pixels, int channels, const void* dm, const void* y, const float* ca,
+                          const float* cb, const float* cc, void* dy, void* dy8, argus_stream_t stream);
 
 /* ---- pooling (MaxPool2d(3,2,1) fused with the stem's BN+ReLU; AdaptiveAvgPool2d(1)) ----------- */
 int argus_maxpool_fwd(int dtype, int n, int h, int w, int c, const void* y, const float* scale,

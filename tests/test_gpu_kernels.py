@@ -1409,6 +1409,132 @@ def _check_fp8_weight_layout(buf, w_fp32, cols):
     assert same > 0.999, same  # round-to-nearest-even ties may differ
 
 
+def _deq_x8(buf, rows, cols):
+    """MX-fp8 'x8' tensor (e4m3 [rows][cols] then E8M0 [rows][cols / 32]) -> fp64 values, and the raw
+    e4m3 values / exponents."""
+    raw = buf.view(torch.uint8).reshape(-1)[: rows * cols + rows * cols // 32].cpu()
+    vals = raw[: rows * cols].view(torch.float8_e4m3fn).double().reshape(rows, cols)
+    e = raw[rows * cols:].to(torch.int32).reshape(rows, cols // 32) - 127
+    scale = torch.pow(2.0, e.double()).repeat_interleave(32, dim=1)
+    return vals * scale, vals, scale
+
+
+def _check_x8_quant(buf, t_bf16):
+    """x8 copy written by argus_bn_apply_x8 / argus_bn_bwd_apply_x8 of the bf16 tensor t: the tightest
+    E8M0 block scale (amax * 2^-e in [224, 448)) and the e4m3 values torch's float8_e4m3fn rounding of
+    t / 2^e gives (round-to-nearest-even ties may differ)."""
+    P, Cc = t_bf16.numel() // t_bf16.shape[-1], t_bf16.shape[-1]
+    deq, vals, scale = _deq_x8(buf, P, Cc)
+    tb = t_bf16.reshape(P, Cc).double().cpu()
+    amax = tb.abs().reshape(P, Cc // 32, 32).amax(-1).repeat_interleave(32, dim=1)
+    assert (amax / scale < 448).all() and ((amax / scale >= 224) | (amax == 0)).all()
+    same = (vals == (tb / scale).float().to(torch.float8_e4m3fn).float().double()).double().mean().item()
+    assert same > 0.999, same
+    assert ((deq - tb).abs() <= tb.abs() * 2.0 ** -4 + scale * 2.0 ** -9).all()
+    return deq
+
+
+X8_CASES = [  # (n, h, w, c, k): whole-image tiles (H*W < 256), row tiles, a 64-column forward (key 13 = 1:
+    # the halo kernel at these small grids)
+    (8, 8, 8, 128, 128), (2, 16, 16, 256, 128), (4, 32, 32, 128, 256), (2, 16, 16, 512, 512), (2, 16, 16, 128, 64),
+]
+
+
+def test_conv_x8_halo_fwd_dgrad(cuda):
+    """MX-fp8 stored operands (ABI 16): argus_bn_apply_x8 / argus_bn_bwd_apply_x8 write the bf16 output
+    bit-identical to argus_bn_apply / argus_bn_bwd_apply plus its x8 copy (checked against torch's e4m3
+    rounding under the tightest E8M0 scale); argus_conv_fwd_x8 / argus_conv_dgrad_bn_x8 (the LDS-halo
+    kernel's F8 variant) against the fp64 conv of the dequantized operands (tolerance: fp32 accumulation
+    + the bf16 output rounding, 2^-8 of the output's max magnitude), against the register-staged
+    ARGUS_FP8 kernel that quantizes the same bf16 tensors while staging (same bytes, another fp32
+    summation order: 2^-7), the forward BN partials and the dgrad's folded BN-backward finalize."""
+    from argus_amd._lib import BnBwdEpilogue
+    from argus_amd.profiling import KernelTimer
+
+    torch.manual_seed(23)
+    L = lib()
+    extra = {13: 1}
+    for n, h, w, c, k in X8_CASES:
+        d, _ = _desc(n, h, w, c, k, 3, 1)
+        d = d.with_tuning({37: 10, **extra})  # bit 8: fp8 forward weights of the 3x3 stride-1 convs
+        P = n * h * w
+        assert L.dll.argus_conv_x8_ok(C.byref(d), 0) == 1
+        assert L.dll.argus_conv_x8_ok(C.byref(d), 1) == (1 if k % 128 == 0 else 0)
+        assert L.dll.argus_conv_x8_ok(C.byref(d.with_tuning({37: 2, **extra})), 0) == 0  # no fp8 forward weights
+        w_ = torch.randn(k, 3, 3, c) * (2.0 / (9 * c)) ** 0.5
+        wf, wd = _prep(d, "fp8", w_.to(cuda), cuda)
+        wfd = _deq_x8(wf, k, 9 * c)[0].reshape(k, 3, 3, c).permute(0, 3, 1, 2)
+        # forward: a = relu(y*scale+shift) with its x8 copy
+        yin = torch.randn(n, h, w, c, device=cuda).to(torch.bfloat16)
+        sc, sh = torch.rand(c, device=cuda) + 0.5, torch.randn(c, device=cuda) * 0.3
+        a = torch.empty_like(yin)
+        a_ref = torch.empty_like(yin)
+        a8 = torch.empty(P * c * 33 // 32, dtype=torch.uint8, device=cuda)
+        L.bn_apply_x8(P, c, ptr(yin), ptr(sc), ptr(sh), None, None, None, 1, ptr(a), None, ptr(a8), stream())
+        L.bn_apply(BF16, P, c, ptr(yin), ptr(sc), ptr(sh), None, None, None, 1, ptr(a_ref), None, stream())
+        assert torch.equal(a, a_ref)
+        ad = _check_x8_quant(a8, a).reshape(n, h, w, c).permute(0, 3, 1, 2)
+        rows = L.dll.argus_conv_fwd_stat_rows(C.byref(d), FP8)
+        stats = torch.empty(rows, k, 2, device=cuda)
+        y = torch.empty(n, h, w, k, dtype=torch.bfloat16, device=cuda)
+        with KernelTimer("argus::conv3x3_halo_kernel") as t:
+            L.conv_fwd_x8(C.byref(d), ptr(a8), ptr(wf), ptr(y), ptr(stats), stream())
+        assert any(nm.endswith(", true>") for nm in t.summary()), list(t.summary())
+        ref = F.conv2d(ad, wfd, padding=1)
+        e = _rel(y.permute(0, 3, 1, 2), ref)
+        assert e < 2.0 ** -8, ("x8 fwd", n, h, w, c, k, e)
+        y_st = torch.empty_like(y)
+        L.conv_fwd(C.byref(d), FP8, ptr(a), ptr(wf), ptr(y_st), None, None, None, stream())
+        assert _rel(y, y_st) < 2.0 ** -7
+        assert _rel(stats.double().sum(0)[:, 0].cpu(), ref.sum((0, 2, 3))) < 1e-3  # the partials sum y
+        if k % 128:
+            continue
+        # data gradient: dy = ca*dm + cb*y2 + cc with its x8 copy, then the mask-mode-2 BN epilogue
+        dmz = torch.randn(n, h, w, k, device=cuda).to(torch.bfloat16)
+        y2 = torch.randn(n, h, w, k, device=cuda).to(torch.bfloat16)
+        ca, cb, cc = (torch.randn(k, device=cuda) * 0.3 for _ in range(3))
+        dy, dy_ref = torch.empty_like(dmz), torch.empty_like(dmz)
+        dy8 = torch.empty(P * k * 33 // 32, dtype=torch.uint8, device=cuda)
+        L.bn_bwd_apply_x8(P, k, ptr(dmz), ptr(y2), ptr(ca), ptr(cb), ptr(cc), ptr(dy), ptr(dy8), stream())
+        L.bn_bwd_apply(BF16, P, k, ptr(dmz), 0, None, ptr(y2), None, None, ptr(ca), ptr(cb), ptr(cc), ptr(dy_ref),
+                       None, None, None, None, None, None, stream())
+        assert torch.equal(dy, dy_ref)
+        dyd = _check_x8_quant(dy8, dy).reshape(n, h, w, k).permute(0, 3, 1, 2)
+        wdd = _deq_x8(wd, c, 9 * k)[0].reshape(c, 3, 3, k)  # [c][tap][k]: w_dgrad = the forward weights transposed
+        wdd = wdd.permute(3, 0, 1, 2)  # [k][c][r][s] as conv2d weights of the forward conv
+        ybn = torch.randn(n, h, w, c, device=cuda).to(torch.bfloat16)
+        mean, invstd = torch.randn(c, device=cuda) * 0.1, torch.rand(c, device=cuda) + 0.5
+        gamma = torch.rand(c, device=cuda) + 0.5
+        ws = torch.zeros(L.dll.argus_bn_workspace_bytes(2048), dtype=torch.uint8, device=cuda)
+        outs = {}
+        for name in ("x8", "staged"):
+            brows = L.dll.argus_conv_dgrad_bn_rows(C.byref(d), FP8)
+            part = torch.zeros(brows, c, 2, device=cuda)
+            coef = torch.zeros(5, c, device=cuda)
+            e_ = BnBwdEpilogue()
+            e_.y, e_.mean, e_.invstd, e_.mask_mode, e_.scale, e_.shift, e_.part = ptr(ybn), ptr(mean), ptr(invstd), 2, \
+                ptr(sc), ptr(sh), ptr(part)
+            e_.workspace, e_.gamma, e_.dgamma, e_.dbeta = ptr(ws), ptr(gamma), ptr(coef[0]), ptr(coef[1])
+            e_.ca, e_.cb, e_.cc = ptr(coef[2]), ptr(coef[3]), ptr(coef[4])
+            dm = torch.empty(n, h, w, c, device=cuda, dtype=torch.bfloat16)
+            if name == "x8":
+                with KernelTimer("argus::conv3x3_halo_kernel") as t:
+                    L.conv_dgrad_bn_x8(C.byref(d), ptr(dy8), ptr(wd), ptr(dm), C.byref(e_), stream())
+                assert any(nm.endswith(", 2, 2, true>") for nm in t.summary()), list(t.summary())
+            else:
+                L.conv_dgrad_bn(C.byref(d), FP8, ptr(dy), ptr(wd), ptr(dm), None, C.byref(e_), None, stream())
+            outs[name] = (dm, coef)
+        refd = torch.nn.grad.conv2d_input((n, c, h, w), wdd, dyd, padding=1)
+        mask = ((ybn.double() * sc.double() + sh.double()) > 0).cpu().permute(0, 3, 1, 2)
+        dm = outs["x8"][0]
+        e = _rel(dm.permute(0, 3, 1, 2), refd * mask)
+        assert e < 2.0 ** -8, ("x8 dgrad", n, h, w, c, k, e)
+        assert _rel(dm, outs["staged"][0]) < 2.0 ** -7
+        for i in range(5):  # dgamma, dbeta, ca, cb, cc of the folded finalize
+            assert _rel(outs["x8"][1][i], outs["staged"][1][i]) < 1e-2, i
+        assert int(ws[:16384].count_nonzero()) == 0  # ticket counters left at zero
+
+
 def test_fused_dgrad_wgrad_matches_separate_passes(cuda):
     """argus_conv_dgrad_wgrad_bn (layer-1 conv3: one pass over dm3 / y3 for both gradients) against
     argus_conv_dgrad_bn (apply prologue, mask-mode-2 epilogue) + argus_conv_wgrad_apply: dx bitwise

@@ -50,7 +50,8 @@ def main():
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--pmc", default=None)
-    ap.add_argument("--cfg", default="", help="engine attributes attr=value[,attr=value] (as tools/engine_ab.py)")
+    ap.add_argument("--cfg", default="", help="engine attributes attr=value and tune:key=value policy overrides, "
+                    "comma-separated (as tools/engine_ab.py)")
     ap.add_argument("--streams", default="main,all", help="which tables: main, all")
     a = ap.parse_args()
     from argus_amd.models import NCameraCNN
@@ -64,10 +65,16 @@ def main():
     dev = torch.device("cuda", 0)
     images, targets = synthetic_batch(a.batch, *a.hw, 1000, dev)
     torch.manual_seed(42)
-    m = NCameraCNN(compute_dtype=a.dtype).to(dev).train()
-    eng = m._engine(dev)
+    tune, attrs = {}, {}
     for kv in filter(None, a.cfg.split(",")):
         k, v = kv.split("=")
+        if k.startswith("tune:"):  # a kernel-selection policy override (argus_conv_policy_default key)
+            tune[int(k[5:])] = int(v)
+        else:
+            attrs[k] = v
+    m = NCameraCNN(compute_dtype=a.dtype, kernel_tuning=tune or None).to(dev).train()
+    eng = m._engine(dev)
+    for k, v in attrs.items():
         cur = getattr(eng, k)
         setattr(eng, k, v == "1" if isinstance(cur, bool) else type(cur)(int(v)))
     tr = FusedTrainer(m, lr=1e-4, max_grad_norm=1.0)
