@@ -1238,7 +1238,11 @@ static const Policy kDefaultPolicy = [] {
   p.v[kStemLdsWgrad] = 1;
   p.v[kFwdBm128Rows] = 16 * 1024;
   p.v[kGldsMinRows] = 4 * 256;
-  p.v[kFp8Passes] = 2;
+  // 37: the 3x3 data gradients (2) and the 3x3 stride-1 forwards (8) on MX-fp8 operands; where the
+  //     engine stores their inputs as MX-fp8 copies (argus_conv_fwd_x8 / _dgrad_bn_x8) they run on the
+  //     halo kernel's F8 variant (B=512: forward 3x3 3.49 -> 2.32 ms/step, the step 90.8 -> 90.1 ms
+  //     median of 3, profiles/r05l_*)
+  p.v[kFp8Passes] = 10;
   // 38: a 1x1 dgrad with an apply prologue (dy = ca*dm + cb*y + cc) on the glds kernel after the
   //     apply kernel materialises dy (0), rather than staging the apply in the register-staged kernel
   //     (1): 1 saves the dy round trip but the register-staged kernel is slower at K >= 1024;

@@ -45,6 +45,9 @@ ARGUS_DEV void sbar() {
 
 constexpr int kHaloPos = 448;  // halo positions per image buffer (max (rows+2)*(W+2) over the shapes served)
 constexpr int kHaloPos1 = 416;  // single-buffer variant: 2 x (416 x 128 B + 3 x 8 KB weight stages) fit one CU
+// F8 variant: 400 positions per halo image (the fp8 shapes: 340 / 324 / 400 at W = 32 / 16x16 / 8x8),
+// so two images, their scales and three weight stages fit one CU
+constexpr int kHaloPosF8 = 400;
 
 // HB = halo image buffers: 2 (double-buffered over 64-channel chunks) or 1 (Cin = 64: a single chunk,
 // nothing to prefetch; the 64-column tile then fits two workgroups per CU in LDS)
@@ -53,15 +56,17 @@ constexpr int kHaloPos1 = 416;  // single-buffer variant: 2 x (416 x 128 B + 3 x
 // written by argus_bn_apply_x8 / argus_bn_bwd_apply_x8 and argus_conv_weight_prep): a 128-channel chunk
 // is 128 bytes per halo position (the bf16 chunk's LDS footprint), its E8M0 scales 4 bytes per position
 // in their own LDS image, and each tap runs v_mfma_scale_f32_16x16x128_f8f6f4 (K = 128) per 16 x 16 tile:
-// twice the bf16 MFMA rate and half its LDS fragment reads per channel. Two weight stages instead of
-// three (the scale images take the third one's LDS), so the weight tile of tap j+1 loads under tap j.
+// twice the bf16 MFMA rate and half its LDS fragment reads per channel. The images hold 400 positions
+// (not 448: the fp8 shapes need no more), which leaves room for the scale images and three weight
+// stages; a wave whose last halo DMA would cover positions past 400 sends it to a 1 KB dummy slot (every
+// wave issues the same DMAs, so the counted waits hold).
 template <int BN, int BW, int HB, bool F8 = false>
 __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_halo_kernel(const IgParams p) {
   constexpr int WN = BN / 64, NW = 4 * WN, NT = NW * 64;
-  constexpr int HPOS = HB == 1 ? kHaloPos1 : kHaloPos;  // halo positions per image buffer
+  constexpr int HPOS = F8 ? kHaloPosF8 : (HB == 1 ? kHaloPos1 : kHaloPos);  // halo positions per image buffer
   constexpr int HALO = HPOS * 128;              // bytes per halo image
   constexpr int BST = BN * 128;                 // bytes per weight stage
-  constexpr int NBS = F8 ? 2 : 3;
+  constexpr int NBS = 3;
   constexpr int CH = F8 ? 128 : 64;             // channels per chunk (128 bytes per halo position either way)
   constexpr int ES = F8 ? 1 : 2;                // bytes per element
   constexpr int HSI = F8 ? (HPOS + 64 * NW - 1) / (64 * NW) : 0;  // halo scale DMAs per wave per chunk
@@ -70,15 +75,17 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_h
   constexpr int HSB = F8 ? HSI * NW * 256 : 0;
   constexpr int BSB = F8 ? BN * 4 : 0;
   constexpr int HS_OFF = HB * HALO + NBS * BST, BS_OFF = HS_OFF + HB * HSB;
+  constexpr int DUMMY = BS_OFF + NBS * BSB;  // F8: 1 KB sink of the halo DMAs past HPOS
   constexpr int LD = BN + 8;
   constexpr int EPI = 256 * LD * 2;
-  constexpr int MAIN = HB * HALO + NBS * BST + HB * HSB + NBS * BSB;
+  constexpr int MAIN = HB * HALO + NBS * BST + HB * HSB + NBS * BSB + (F8 ? 1024 : 0);
   constexpr int LDS0 = MAIN > EPI ? MAIN : EPI;
   constexpr int RED_B = (NT / (BN / 8)) * BN * 8;  // BN-backward column sums
   constexpr int LDS_BYTES = LDS0 > RED_B ? LDS0 : RED_B;
-  constexpr int HG = HPOS / (8 * NW);           // halo glds per wave per chunk
+  constexpr int HG = (HPOS + 8 * NW - 1) / (8 * NW);  // halo glds per wave per chunk
   constexpr int BG = BN * 8 / NT;               // weight glds per wave per tap
-  static_assert(HG * 8 * NW == HPOS && BG * NT == BN * 8, "halo / tile partition");
+  static_assert((F8 || HG * 8 * NW == HPOS) && HPOS % 8 == 0 && BG * NT == BN * 8, "halo / tile partition");
+  constexpr int HGC = HG + HSI, BGC = BG + (F8 ? 1 : 0);  // DMAs per wave: one chunk's halo, one tap's weights
   static_assert(!F8 || (BN / NW == 16 && LDS_BYTES <= 163840 && BW != 3 && BW != 4), "fp8 halo: 16 weight rows per wave");
   __shared__ __attribute__((aligned(1024))) u32x4 lds[LDS_BYTES / 16];
 
@@ -149,7 +156,9 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_h
     const uint32_t base = lds0 + (HB == 2 ? (cc & 1) * HALO : 0) + wave * 1024;
     const int ci0 = cc * CH * ES;
 #pragma unroll
-    for (int i = 0; i < HG; ++i) gl16(h_ok[i] ? (const void*)(X + h_off[i] + ci0) : zero, base + i * NW * 1024);
+    for (int i = 0; i < HG; ++i)
+      gl16(h_ok[i] ? (const void*)(X + h_off[i] + ci0) : zero,
+           (!F8 || 8 * (i * NW + wave) < HPOS) ? base + i * NW * 1024 : lds0 + DUMMY);
     if constexpr (F8) {
       const uint32_t sb = lds0 + HS_OFF + (HB == 2 ? (cc & 1) * HSB : 0);
 #pragma unroll
@@ -255,23 +264,6 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_h
   constexpr int NLD = PRE ? NITP : 0;
   EpiIn pre[PRE ? NITP : 1];
   const int kpre = p.epi_pre ? nk - 9 : -2;
-  if constexpr (F8) {
-    // two weight stages: issue order H(0) B(0) | per step j, after its barrier: [B(j+1)] [H(chunk(j)+1) if
-    // tap(j)==0]; a step waits for everything up to its B(j), the next chunk's halo may stay in flight
-    constexpr int HGS = HG + HSI;
-    issue_halo(0);
-    issue_b(0);
-    for (int kt = 0; kt < nk; ++kt) {
-      const int t = kt % 9, cc = kt / 9;
-      const bool halo_after = kt >= 1 && ((kt - 1) % 9 == 0) && ((kt - 1) / 9 + 1 < nch);
-      if (halo_after) waitvm<HGS>();
-      else waitvm<0>();
-      sbar();
-      if (kt + 1 < nk) issue_b(kt + 1);
-      if (t == 0 && cc + 1 < nch) issue_halo(cc + 1);
-      compute(kt);
-    }
-  } else {
   issue_halo(0);
   issue_b(0);
   if (nk > 1) issue_b(1);
@@ -285,9 +277,9 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_h
     }
     const bool b_after = kt + 1 < nk;
     const bool after_pre = PRE && kt == kpre + 1;  // the prefetch went out after B(kt)
-    if (halo_after && b_after) waitvm<HG + BG>();
-    else if (halo_after) waitvm<HG>();
-    else if (b_after) { if (after_pre) waitvm<BG + NLD>(); else waitvm<BG>(); }
+    if (halo_after && b_after) waitvm<HGC + BGC>();
+    else if (halo_after) waitvm<HGC>();
+    else if (b_after) { if (after_pre) waitvm<BGC + NLD>(); else waitvm<BGC>(); }
     else waitvm<0>();
     sbar();
     if constexpr (PRE) {
@@ -303,7 +295,6 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_h
     if (t == 0 && cc + 1 < nch) issue_halo(cc + 1);
     if (kt + 2 < nk) issue_b(kt + 2);
     compute(kt);
-  }
   }
   waitvm<0>();
   __syncthreads();
@@ -503,7 +494,10 @@ int conv3x3_halo_tiles(const IgParams& p) {
 // tightly packed x8 rows (lda == Cin; the scales follow the M x Cin bytes)
 int conv3x3_halo_x8_ok(const IgParams& p) {
   const int bn = conv3x3_halo_ok(p);
-  if (!bn || p.Cin % 128 || p.lda != p.Cin || p.ldb % 128 || p.addend || p.addend_mask) return 0;
+  int npos, tiles;
+  if (!bn || !halo_geom(p, npos, tiles) || npos > kHaloPosF8 || p.Cin % 128 || p.lda != p.Cin || p.ldb % 128 ||
+      p.addend || p.addend_mask)
+    return 0;
   const int bw = bwd_variant(p.bb);
   return bw == 0 || bw == 2 ? bn : 0;
 }

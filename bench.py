@@ -407,9 +407,11 @@ def main() -> None:
                     f"the CPU fp32 oracle with the same weights",
         }
 
-    # the dominant kernel's own MFMA roof: MX-fp8 igemm variants (template flag 32) run at the dense
-    # fp8 rate; in an "fp8" run the weight gradients and the 64-channel convs stay bf16
-    f8_kernel = dom.startswith("argus::igemm_kernel<") and int(dom.rstrip(">").split(",")[-1]) >= 32
+    # the dominant kernel's own MFMA roof: MX-fp8 igemm variants (template flag 32) and the fp8 halo
+    # kernel (its last template argument true) run at the dense fp8 rate; in an "fp8" run the weight
+    # gradients and the 64-channel convs stay bf16
+    f8_kernel = ((dom.startswith("argus::igemm_kernel<") and int(dom.rstrip(">").split(",")[-1]) >= 32) or
+                 (dom.startswith("argus::conv3x3_halo_kernel<") and dom.endswith(", true>")))
     peak_flops = (FP8_DENSE_PEAK_TFLOPS if f8_kernel else
                   BF16_DENSE_PEAK_TFLOPS if args.dtype in ("bf16", "fp8") else F32_MFMA_PEAK_TFLOPS)
     tflops = ks["flops_per_launch"] / (ks["avg_us"] * 1e-6) / 1e12
@@ -441,9 +443,11 @@ def main() -> None:
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": args.dtype,
-        "dtype_detail": ("OCP MX-fp8 (e4m3 + E8M0 scale per 32 K-elements) operands for the conv forward and "
-                         "data-gradient GEMMs with >= 128 reduction channels; bf16 tensors, BN, weight gradients "
-                         "and the 64-channel convs; fp32 accumulation, statistics, head, optimizer"
+        "dtype_detail": ("OCP MX-fp8 (e4m3 + E8M0 scale per 32 K-elements) operands for the 3x3 conv forward "
+                         "(stride 1) and data-gradient GEMMs with >= 128 reduction channels (policy key 37); the "
+                         "stride-1 ones read MX-fp8 copies of their inputs that the BN apply passes store beside "
+                         "the bf16 tensors; bf16 tensors, BN, 1x1 convs, weight gradients and the 64-channel "
+                         "convs; fp32 accumulation, statistics, head, optimizer"
                          if args.dtype == "fp8" else None),
         "data": "synthetic (uint8-uniform images, Exp(N(0,0.5^2)) SE(3) targets, seeded random-init weights)",
         "config": {

@@ -223,7 +223,7 @@ int argus_conv_dgrad_bn_x8(const argus_conv_desc* d, const void* dy8, const void
  * (1) or on the register-staged weight-gradient kernel (0), key 35 the fewest GEMM rows (output
  * pixels) for which the forward uses 128-row tiles (fewer: 64), key 36 the fewest GEMM rows for the
  * glds kernel, key 37 which ARGUS_FP8 passes take MX-fp8 operands (bits: 1 forward, 2 data gradient of
- * a 3x3 conv, 4 data gradient of a 1x1 conv, 8 forward of a 3x3 stride-1 conv;
+ * a 3x3 conv, 4 data gradient of a 1x1 conv, 8 forward of a 3x3 stride-1 conv; default 10;
  * argus_conv_weight_prep follows the same key), key 42 the
  * workgroups per CU (4 or 3) the small-K BN-epilogue / apply-prologue data gradients are built for.
  * (Keys scaled with the batch keep a smaller batch's kernel selection that of the larger one:

@@ -49,10 +49,19 @@ def test_bad_arguments_are_reported():
     # kernel-selection policy: immutable defaults, per-call overrides on the descriptor only
     assert L.dll.argus_conv_policy_default(99) == -1 and L.dll.argus_conv_policy_default(20) == -1
     assert L.dll.argus_conv_policy_default(35) == 16384 and L.dll.argus_conv_policy_default(7) == 1024
-    assert L.dll.argus_conv_policy_default(37) in (0, 1, 2, 3, 4, 5, 6, 7)
+    assert 0 <= L.dll.argus_conv_policy_default(37) <= 15
     forced = good.with_tuning({1: 128, 4: 64})  # dgrad row / column tiles
     assert L.dll.argus_conv_launch_info(C.byref(forced), 1, 1, None) % 1000000 == 128 * 1000 + 64
     assert L.dll.argus_conv_launch_info(C.byref(good), 1, 1, None) % 1000000 == 64 * 1000 + 64
+    # the MX-fp8 stored-operand convs (argus_conv_x8_ok, host-only): 3x3 stride-1 halo shapes whose
+    # reduction channels are multiples of 128, under the fp8 pass bits (key 37: 8 forward, 2 dgrad)
+    x8 = ConvDesc(8, 16, 16, 256, 256, 3, 3, 1, 1, 16, 16, 0)
+    assert [L.dll.argus_conv_x8_ok(C.byref(x8.with_tuning({13: 1})), ps) for ps in (0, 1)] == [1, 1]
+    assert [L.dll.argus_conv_x8_ok(C.byref(x8.with_tuning({13: 1, 37: 2})), ps) for ps in (0, 1)] == [0, 1]
+    assert [L.dll.argus_conv_x8_ok(C.byref(x8.with_tuning({13: 1, 37: 8})), ps) for ps in (0, 1)] == [1, 0]
+    s2 = ConvDesc(8, 16, 16, 256, 256, 3, 3, 2, 1, 8, 8, 0).with_tuning({13: 1})
+    c64 = ConvDesc(8, 16, 16, 64, 64, 3, 3, 1, 1, 16, 16, 0).with_tuning({13: 1})
+    assert [L.dll.argus_conv_x8_ok(C.byref(d_), ps) for d_ in (s2, c64) for ps in (0, 1)] == [0, 0, 0, 0]
     unknown = good.with_tuning({30: 1})  # removed key (the 64-channel halo variant is a constant)
     with pytest.raises(ArgusHipError, match="unknown tuning key 30"):
         L.conv_fwd(C.byref(unknown), 1, 16, 16, 16, None, None, None, None)

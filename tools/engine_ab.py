@@ -25,7 +25,8 @@ def main():
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--cfg", action="append", default=[], help="attr=value[,attr=value] (\"\" = defaults)")
+    ap.add_argument("--cfg", action="append", default=[],
+                    help="attr=value[,attr=value] (\"\" = defaults; tune:key=value a policy override, dtype=bf16|fp8)")
     a = ap.parse_args()
     from argus_amd.models import NCameraCNN
     from argus_amd.step import FusedTrainer
@@ -48,10 +49,11 @@ def main():
         before the next configuration (only one model is resident at a time; r04 kept them all and
         ran out of memory at 376x672 B=128). Returns (ms/step, peak device GiB of this configuration)."""
         tune, attrs = parse(cfg)
+        dtype = attrs.pop("dtype", a.dtype)  # a per-configuration compute dtype (e.g. fp8 vs bf16)
         torch.cuda.empty_cache()
         torch.cuda.reset_peak_memory_stats(dev)
         torch.manual_seed(42)
-        m = NCameraCNN(compute_dtype=a.dtype, kernel_tuning=tune or None).to(dev).train()
+        m = NCameraCNN(compute_dtype=dtype, kernel_tuning=tune or None).to(dev).train()
         eng = m._engine(dev)
         for k, v in attrs.items():
             cur = getattr(eng, k)
