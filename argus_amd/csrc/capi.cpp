@@ -69,6 +69,15 @@ int argus_conv_fwd(const argus_conv_desc* d, int dtype, const void* x, const voi
   return conv_fwd(*d, dtype, x, w, y, sc, sh, stats, (hipStream_t)stream);
 }
 
+int argus_conv_fwd_apply_out(const argus_conv_desc* d, int dtype, const void* x, const void* w, void* y,
+                             const float* sc, const float* sh, float* stats, void* x_out, argus_stream_t stream) {
+  if (!d || !x || !w || (!y && !stats) || !sc || !sh || !x_out) {
+    set_error("conv_fwd_apply_out: bad arguments");
+    return ARGUS_ERR_ARG;
+  }
+  return conv_fwd(*d, dtype, x, w, y, sc, sh, stats, (hipStream_t)stream, x_out);
+}
+
 int argus_conv_fwd_bn_out(const argus_conv_desc* d, int dtype, const void* x, const void* w_fwd, const float* scale,
                           const float* shift, const void* res, const float* res_scale, const float* res_shift, void* out,
                           uint8_t* mask_bits, void* y, argus_stream_t stream) {

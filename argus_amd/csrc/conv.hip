@@ -261,7 +261,7 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
         }
       }
       S.ch = ch;
-      if constexpr (AP) S.tap0 = dh == 0 && dw == 0 && blockIdx.z == 0 && nt == 0;
+      if constexpr (AP || PRO) S.tap0 = dh == 0 && dw == 0 && blockIdx.z == 0 && nt == 0;
     }
   };
 
@@ -272,7 +272,11 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
       if (pro_in_lds) pc.load_lds(pro_lds, S.ch);
       else pc.load(p.pro_scale, p.pro_shift, S.ch);
 #pragma unroll
-      for (int i = 0; i < AR; ++i) S.a[i] = sel(S.ok[i], pc.apply(S.a[i]));
+      for (int i = 0; i < AR; ++i) {
+        S.a[i] = sel(S.ok[i], pc.apply(S.a[i]));
+        // the applied input stored once (column tile 0; 1x1 stride-1 convs only: argus_conv_fwd_apply_out)
+        if (p.pro_out && S.tap0 && S.ok[i]) st16(reinterpret_cast<T*>(p.pro_out) + a_off[i] + S.ch, S.a[i]);
+      }
     }
     if constexpr (AP) {  // dy = ca*dm + cb*y + cc; zero outside the image (dgrad's zero padding of dy)
 #pragma unroll
@@ -1321,7 +1325,7 @@ static int run_ig(const IgParams& p, hipStream_t st, int bm, int bn) {
       return check_launch("igemm_kernel");
     }
     // the statistics-only forward and the block-output epilogue exist on the register-staged kernel only
-    if ((p.c || !p.fwd) && !p.oe.out && !p.bb.yx) {
+    if ((p.c || !p.fwd) && !p.oe.out && !p.bb.yx && !p.pro_out) {
       if (conv3x3_halo_launch(p, st)) return check_launch("conv3x3_halo_kernel");
       if (igemm_glds_launch(p, maxM, maxK, st)) return check_launch("igemm_glds_kernel");
     }
@@ -1417,8 +1421,13 @@ static void fwd_params(const argus_conv_desc& d, const Policy& pol, IgParams& p)
 }
 
 int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, void* y,
-             const float* sc, const float* sh, float* stats, hipStream_t st) {
+             const float* sc, const float* sh, float* stats, hipStream_t st, void* pro_out) {
   if (int e = check_desc(d)) return e;
+  if (pro_out && (!sc || d.stem || d.r != 1 || d.s != 1 || d.stride != 1 || d.pad != 0 || pro_out == x ||
+                  dtype == ARGUS_FP8)) {
+    set_error("conv_fwd_apply_out: a BN+ReLU prologue on a 1x1 stride-1 bf16/fp32 conv, x_out != x");
+    return ARGUS_ERR_ARG;
+  }
   const bool f8 = dtype == ARGUS_FP8;  // bf16 tensors, MX-fp8 GEMM operands where the shape allows
   if (f8) dtype = ARGUS_BF16;
   g_launch_work = 2.0 * d.n * d.ho * d.wo * d.k * d.r * d.s * d.c;  // algorithmic flops / bytes (ktimer)
@@ -1432,6 +1441,7 @@ int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, 
     return ARGUS_ERR_ARG;
   }
   if (!y) g_launch_bytes -= 2.0 * d.n * d.ho * d.wo * d.k;  // nothing stored
+  if (pro_out) g_launch_bytes += (dtype == ARGUS_BF16 ? 2.0 : 4.0) * d.n * d.h * d.w * d.c;  // x' stored
   const Policy pol = policy_of(d);
   if (f8 && sc) {
     int f8f, f8d;
@@ -1442,7 +1452,7 @@ int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, 
     return check_launch("stem_fwd_kernel");
   IgParams p;
   fwd_params(d, pol, p);
-  p.a = x; p.b = w; p.c = y; p.pro_scale = sc; p.pro_shift = sh;
+  p.a = x; p.b = w; p.c = y; p.pro_scale = sc; p.pro_shift = sh; p.pro_out = pro_out;
   p.stats = reinterpret_cast<float2*>(stats);
   const int bm = fwd_bm(d, pol), bn = d.stem ? 64 : pick_bn(pol, 0, d.k);
   p.stat_tile = bm;

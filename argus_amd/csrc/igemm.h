@@ -67,6 +67,7 @@ struct IgParams {
   void* c;
   const float* pro_scale;
   const float* pro_shift;
+  void* pro_out;  // forward with a prologue: the staged relu(x*scale+shift) stored here (1x1 stride 1)
   float2* stats;
   const void* addend;          // C += addend (same layout as C; may alias C), masked by addend_mask
   const uint8_t* addend_mask;  // one byte per 16-byte chunk, bit j <-> element j (bn_apply mask)

@@ -173,6 +173,13 @@ class ResNetEngine:
         # the fp8 MFMA rate; False: the register-staged fp8 kernel quantizes while staging (set before
         # the first forward)
         self.x8 = True
+        # training forward with the fused tail: conv3's statistics pass applies bn2 to y2 while staging its
+        # operand and stores a2 itself (argus_conv_fwd_apply_out, bit-identical to the bn_apply pass it
+        # replaces: one pass over y2 and one launch fewer per block). Measured slower (round 5, B=64
+        # interleaved x3: 14.06-14.09 vs 13.99-14.02 ms, profiles/r05o_ab_a2_in_stats.txt): the register-
+        # staged statistics pass applies bn2 once per column tile and its stores lengthen the short,
+        # latency-bound workgroups more than the apply pass costs
+        self.a2_in_stats = False
         # (the schedule switches above are attributes, not environment variables: tools/engine_ab.py
         # A/B-measures them; test_gpu_train.py runs the overlap / tail placements against each other)
 
@@ -367,9 +374,10 @@ class ResNetEngine:
                               ptr(Bf[name + ".running_mean"]), ptr(Bf[name + ".running_var"]),
                               C.c_float(Bf.get(name + ".eps", 1e-5)), ptr(st[2]), ptr(st[3]), stream())
 
-    def _conv_bn(self, P, Bf, conv, bn, x, y, pro, training, part=None, ws=None, x8=None):
+    def _conv_bn(self, P, Bf, conv, bn, x, y, pro, training, part=None, ws=None, x8=None, x_out=None):
         """conv (+ BN statistics and finalize when training); ``x8``: the input's MX-fp8 copy
-        (argus_conv_fwd_x8 instead of argus_conv_fwd)."""
+        (argus_conv_fwd_x8 instead of argus_conv_fwd); ``x_out``: where the prologue's applied input is
+        stored (argus_conv_fwd_apply_out)."""
         cv = self.convs[conv]
         sc = sh = None
         if pro is not None:
@@ -380,7 +388,11 @@ class ResNetEngine:
             self._bn_eval(P, Bf, bn)
             return
         cdt = BF16 if y is None else self.cdt  # the statistics-only forward is the bf16 kernel
-        if x8 is not None:
+        if x_out is not None:
+            self._launch(cv, 0, lambda: self.L.conv_fwd_apply_out(C.byref(cv.desc), cdt, ptr(x), ptr(cv.wf), ptr(y),
+                                                                   ptr(sc), ptr(sh), ptr(part) if training else None,
+                                                                   ptr(x_out), stream()))
+        elif x8 is not None:
             self._launch(cv, 0, lambda: self.L.conv_fwd_x8(C.byref(cv.desc), ptr(x8), ptr(cv.wf), ptr(y),
                                                             ptr(part) if training else None, stream()))
         else:
@@ -478,8 +490,13 @@ class ResNetEngine:
                           self.x8buf if x8f else None)
                 self._conv_bn(P, Bf, pf + ".conv2", pf + ".bn2", a["a1"], a["y2"], None, training,
                               x8=self.x8buf if x8f else None)
-                self._act(pf + ".bn2", a["y2"], a["a2"], N * a["hw"][0] * a["hw"][1], b.width)
-                self._conv_bn(P, Bf, pf + ".conv3", pf + ".bn3", a["a2"], None if tail else a["y3"], None, training)
+                if tail and training and self.a2_in_stats:
+                    self._conv_bn(P, Bf, pf + ".conv3", pf + ".bn3", a["y2"], None, pf + ".bn2", training,
+                                  x_out=a["a2"])
+                else:
+                    self._act(pf + ".bn2", a["y2"], a["a2"], N * a["hw"][0] * a["hw"][1], b.width)
+                    self._conv_bn(P, Bf, pf + ".conv3", pf + ".bn3", a["a2"], None if tail else a["y3"], None,
+                                  training)
             else:
                 self._conv_bn(P, Bf, pf + ".conv2", pf + ".bn2", a["y1"], a["y2"], pf + ".bn1", training)
                 self._conv_bn(P, Bf, pf + ".conv3", pf + ".bn3", a["y2"], a["y3"], pf + ".bn2", training)

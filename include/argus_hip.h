@@ -103,6 +103,14 @@ int argus_conv_fwd(const argus_conv_desc* d, int dtype, const void* x, const voi
                    argus_stream_t stream);
 /* y == NULL (bf16, not the stem, stat_part given): statistics only, nothing stored (ABI 14; the
  * bottleneck's conv3 before argus_conv_fwd_bn_out). */
+/* argus_conv_fwd with its BN+ReLU prologue (pro_scale / pro_shift required) that also stores the
+ * staged input x' = relu(x*pro_scale+pro_shift) to x_out, bit-identical to argus_bn_apply(relu = 1)
+ * of x (ABI 16; 1x1 stride-1 convs, bf16 or fp32): the bottleneck's conv3 statistics pass applies bn2
+ * to y2 while staging it and writes a2 (the operand of the fused tail and of conv3's weight gradient),
+ * replacing the separate bn2 apply pass of torchvision's Bottleneck.forward (argus/models.py:43). */
+int argus_conv_fwd_apply_out(const argus_conv_desc* d, int dtype, const void* x, const void* w_fwd, void* y,
+                             const float* pro_scale, const float* pro_shift, float* stat_part, void* x_out,
+                             argus_stream_t stream);
 /* Bottleneck tail in one forward pass (ABI 14; replaces conv3 + bn3 + the residual add + ReLU of
  * torchvision's Bottleneck.forward, argus/models.py:43 -> torchvision resnet.py, in train mode after
  * argus_bn_finalize of bn3, or eval mode with argus_bn_eval_coeffs): the 1x1 stride-1 conv's C tile t

@@ -1535,6 +1535,44 @@ def test_conv_x8_halo_fwd_dgrad(cuda):
         assert int(ws[:16384].count_nonzero()) == 0  # ticket counters left at zero
 
 
+def test_conv_fwd_apply_out_matches_apply_then_conv(cuda):
+    """argus_conv_fwd_apply_out (ABI 16): a 1x1 stride-1 forward whose BN+ReLU prologue also stores the
+    applied input: x_out bit-identical to argus_bn_apply(relu) of x, and y / the BN statistics partials
+    bit-identical to argus_conv_fwd on that stored x' (the same bf16 operands in the same k order), with
+    y stored and statistics-only (y NULL); ragged M; refused for 3x3 / strided convs and x_out == x."""
+    from argus_amd._lib import ArgusHipError
+
+    torch.manual_seed(29)
+    L = lib()
+    for n, h, w, c, k in [(2, 16, 16, 64, 256), (3, 7, 9, 128, 512), (1, 32, 32, 256, 64)]:
+        d, _ = _desc(n, h, w, c, k, 1, 1)
+        P = n * h * w
+        x = torch.randn(n, h, w, c, device=cuda).to(torch.bfloat16)
+        sc, sh = torch.rand(c, device=cuda) + 0.5, torch.randn(c, device=cuda) * 0.5
+        wf, _ = _prep(d, "bf16", (torch.randn(k, 1, 1, c) * c ** -0.5).to(cuda), cuda)
+        rows = L.dll.argus_conv_fwd_stat_rows(C.byref(d), BF16)
+        a_ref = torch.empty_like(x)
+        L.bn_apply(BF16, P, c, ptr(x), ptr(sc), ptr(sh), None, None, None, 1, ptr(a_ref), None, stream())
+        for store_y in (True, False):
+            a = torch.full_like(x, float("nan"))
+            y = torch.empty(n, h, w, k, device=cuda, dtype=torch.bfloat16) if store_y else None
+            st = torch.empty(rows, k, 2, device=cuda)
+            L.conv_fwd_apply_out(C.byref(d), BF16, ptr(x), ptr(wf), ptr(y), ptr(sc), ptr(sh), ptr(st), ptr(a),
+                                 stream())
+            assert torch.equal(a, a_ref), (n, h, w, c, k)
+            y_ref = torch.empty(n, h, w, k, device=cuda, dtype=torch.bfloat16) if store_y else None
+            st_ref = torch.empty_like(st)
+            L.conv_fwd(C.byref(d), BF16, ptr(a_ref), ptr(wf), ptr(y_ref), None, None, ptr(st_ref), stream())
+            assert torch.equal(st, st_ref), (n, h, w, c, k, store_y)
+            if store_y:
+                assert torch.equal(y, y_ref)
+    d3, _ = _desc(2, 8, 8, 64, 64, 3, 1)
+    with pytest.raises(ArgusHipError, match="apply_out"):
+        L.conv_fwd_apply_out(C.byref(d3), BF16, ptr(x), ptr(wf), None, ptr(sc), ptr(sh), ptr(st), ptr(a), stream())
+    with pytest.raises(ArgusHipError, match="apply_out"):
+        L.conv_fwd_apply_out(C.byref(d), BF16, ptr(x), ptr(wf), None, ptr(sc), ptr(sh), ptr(st), ptr(x), stream())
+
+
 def test_fused_dgrad_wgrad_matches_separate_passes(cuda):
     """argus_conv_dgrad_wgrad_bn (layer-1 conv3: one pass over dm3 / y3 for both gradients) against
     argus_conv_dgrad_bn (apply prologue, mask-mode-2 epilogue) + argus_conv_wgrad_apply: dx bitwise

@@ -146,7 +146,8 @@ def test_side_stream_overlap_is_bit_identical(cuda):
     tail (engine.fuse_out: conv3's statistics-only forward + argus_conv_fwd_bn_out instead of conv3 +
     bn_apply), the 3x3 data gradients run alone (engine.gate3x3) and bn3's input recomputed from a2 in
     the BN-backward epilogue rather than read (engine.yrec_epi) or never stored at all for the layer-1
-    blocks (engine.y3_free: the fused conv3 data + weight gradient recomputes it too); eval-mode
+    blocks (engine.y3_free: the fused conv3 data + weight gradient recomputes it too), bn2's apply
+    inside conv3's statistics pass (engine.a2_in_stats off: the separate bn_apply pass); eval-mode
     predictions after the steps too."""
     from argus_amd.models import NCameraCNN
     from argus_amd.step import FusedTrainer
@@ -158,7 +159,7 @@ def test_side_stream_overlap_is_bit_identical(cuda):
     runs = []
     # (side stream, first block's downsample weight gradient on the main stream's tail, ...)
     for attrs in ({}, {"tail_main": False}, {"wgrad_overlap": False}, {"fuse_out": False}, {"gate3x3": True},
-                  {"yrec_epi": True}, {"yrec_epi": True, "y3_free": True}):
+                  {"yrec_epi": True}, {"yrec_epi": True, "y3_free": True}, {"a2_in_stats": False}):
         torch.manual_seed(42)
         model = NCameraCNN(compute_dtype="bf16").to(cuda).train()
         tr = FusedTrainer(model, lr=1e-3, max_grad_norm=1.0)
