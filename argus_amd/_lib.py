@@ -88,6 +88,8 @@ SIGNATURES = {
     "argus_conv_fwd": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P, _P]),
     "argus_conv_fwd_bn_out": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "argus_conv_x8_ok": (_I, [_DESC, _I]),
+    "argus_conv_fwd_stats_only_rows": (_I, [_DESC, _I]),
+    "argus_conv_fwd_stats_only_tile": (_I, [_DESC, _I]),
     "argus_conv_fwd_apply_out": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "argus_conv_fwd_x8": (_I, [_DESC, _P, _P, _P, _P, _P]),
     "argus_conv_dgrad_bn_x8": (_I, [_DESC, _P, _P, _P, C.POINTER(BnBwdEpilogue), _P]),

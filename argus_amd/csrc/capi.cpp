@@ -89,6 +89,12 @@ int argus_conv_fwd_bn_out(const argus_conv_desc* d, int dtype, const void* x, co
                          (hipStream_t)stream);
 }
 int argus_conv_fwd_stat_rows(const argus_conv_desc* d, int dtype) { return d ? conv_fwd_stat_rows(*d, dtype) : 0; }
+int argus_conv_fwd_stats_only_rows(const argus_conv_desc* d, int dtype) {
+  return d ? conv_fwd_stats_only_rows(*d, dtype) : 0;
+}
+int argus_conv_fwd_stats_only_tile(const argus_conv_desc* d, int dtype) {
+  return d ? conv_fwd_stats_only_tile(*d, dtype) : 0;
+}
 
 int argus_conv_policy_default(int key) { return policy_default(key); }
 

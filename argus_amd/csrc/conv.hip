@@ -1262,6 +1262,11 @@ static const Policy kDefaultPolicy = [] {
   // 42: the small-K dgrads with a BN-backward epilogue or an apply prologue built for 4 workgroups per CU
   //     (128 VGPRs: the 64 x 128 apply + mask-bits variants spill 6 registers) or 3 (168 VGPRs)
   p.v[kBwdSmallKOcc] = 4;
+  // 44: statistics-only 1x1 forwards (the bottleneck conv3 before argus_conv_fwd_bn_out) on the
+  //     persistent kernel of conv_p1x1.hip (1) or the register-staged igemm (0): layer 1 44.5-47.7 ->
+  //     32.2 us, layers 2-4 31-33 -> 26-29 us per launch (B=64, profiles/r05q_timeline/); the step
+  //     within drift (13.921 vs 13.924 ms under the profiler, r05p_ab_key44.txt)
+  p.v[kP1x1FwdStats] = 1;
   // 43: the bottleneck conv1 data gradients (1x1, apply prologue, mask-bits BN epilogue with the folded
   //     finalize) on the persistent kernel of conv_p1x1.hip (1) or the register-staged igemm (0)
   p.v[kP1x1Dgrad] = 1;
@@ -1373,6 +1378,18 @@ static bool stem_lds_fwd(const argus_conv_desc& d, int dtype, const Policy& pol)
   return d.stem && pol[kStemLdsFwd] && stem_fwd_ok(d, dtype == ARGUS_FP8 ? ARGUS_BF16 : dtype);
 }
 
+int conv_fwd_stats_only_rows(const argus_conv_desc& d, int dtype) {
+  if (check_desc(d)) return 0;
+  if (p1x1_fwd_stats_ok(d, dtype, policy_of(d)[kP1x1FwdStats])) return p1x1_fwd_stats_rows(d);
+  return conv_fwd_stat_rows(d, dtype);
+}
+
+int conv_fwd_stats_only_tile(const argus_conv_desc& d, int dtype) {
+  if (check_desc(d)) return 0;
+  if (p1x1_fwd_stats_ok(d, dtype, policy_of(d)[kP1x1FwdStats])) return -p1x1_fwd_stats_tile(d);
+  return conv_fwd_stat_tile(d, dtype);
+}
+
 int conv_fwd_stat_rows(const argus_conv_desc& d, int dtype) {
   if (check_desc(d)) return 0;
   const Policy pol = policy_of(d);
@@ -1450,6 +1467,8 @@ int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, 
   }
   if (stem_lds_fwd(d, dtype, pol) && stem_fwd_launch(d, dtype, x, w, y, stats, st))  // stem.hip (bf16)
     return check_launch("stem_fwd_kernel");
+  if (!y && !sc && p1x1_fwd_stats_ok(d, dtype, pol[kP1x1FwdStats]))  // statistics only: conv_p1x1.hip
+    return p1x1_fwd_stats_launch(d, x, w, stats, st);
   IgParams p;
   fwd_params(d, pol, p);
   p.a = x; p.b = w; p.c = y; p.pro_scale = sc; p.pro_shift = sh; p.pro_out = pro_out;

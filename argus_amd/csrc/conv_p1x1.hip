@@ -261,4 +261,238 @@ int p1x1_launch(const argus_conv_desc& d, const void* dm, const void* wd, void* 
   return check_launch("p1x1_dgrad_kernel");
 }
 
+// ================================================================================================
+// Persistent statistics-only 1x1 forward (the bottleneck conv3 before argus_conv_fwd_bn_out): per-channel
+// {sum, M2} of y = x w^T over all pixels, y never stored.
+//
+// Why: on the register-staged igemm (128 x 128 tiles, one or two K-steps) this pass is latency-bound:
+// at B=64 the layer-1 launch is 8,192 workgroups that each stage a weight tile, run one K-step and
+// write a partial row, 45 us for a 67 MB read (profiles/r05n_*). Here a workgroup keeps a column block
+// of the weights [BNC][K] in LDS for the launch, walks its share of the 64-row tiles with the next
+// two tiles' rows in flight in registers, and accumulates per-lane moments of its column values about a
+// per-lane shift (no per-tile reductions); the lanes and row halves are Chan-merged once at the end:
+// one partial row and one pixel count per row split. Products are igemm_kernel's (the same bf16
+// operands, the same MFMA K order); only the moment grouping differs.
+// ================================================================================================
+struct P1FParams {
+  const bf16* x;   // [P][K]
+  const bf16* w;   // [N][K] w_fwd of the 1x1 conv
+  float2* part;    // [G][N] {sum, M2}
+  int* counts;     // [G] pixels per partial row (after the partials)
+  int P, N, G, NB, tiles;
+};
+
+template <int K, int BNC>
+__global__ __launch_bounds__(256) void p1x1_fwd_stats_kernel(const P1FParams p) {
+  constexpr int KC = K / 8;           // 16-byte chunks per row
+  constexpr int ARP = 256 / KC;       // A rows per staging pass
+  constexpr int APS = kP1BM / ARP;    // A passes
+  constexpr int NI = BNC / 32;        // 16-column blocks per wave (waves 2 x 2: 32 rows x BNC/2 columns)
+  constexpr int DEPTH = K <= 256 ? 2 : 1;  // tiles of A rows in flight in registers
+  constexpr int W_B = BNC * K * 2, A_B = kP1BM * K * 2;
+  static_assert(A_B >= 2 * BNC * 16, "reduction scratch");
+  __shared__ __attribute__((aligned(16))) u32x4 lds[(W_B + A_B) / 16];
+  u32x4* Wl = lds;
+  u32x4* Al = lds + W_B / 16;
+
+  const int total = p.G * p.NB;
+  const int wid = xcd_remap(blockIdx.x, total);
+  const int nb = wid % p.NB, g0 = wid / p.NB;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int g = lane >> 4, i16 = lane & 15;
+
+#pragma unroll
+  for (int i = 0; i < BNC * KC / 256; ++i) {
+    const int idx = tid + 256 * i, r = idx / KC, c = idx - r * KC;
+    Wl[p1_pos<KC>(r, c)] = ld16(p.w + (size_t)(nb * BNC + r) * K + c * 8);
+  }
+  const int ac = tid % KC, ar0 = tid / KC;
+  auto load_a = [&](int t, u32x4 (&A)[APS]) {
+#pragma unroll
+    for (int i = 0; i < APS; ++i) {
+      const int m = min(t * kP1BM + ar0 + ARP * i, p.P - 1);
+      A[i] = ld16(p.x + (size_t)m * K + ac * 8);
+    }
+  };
+  // per-lane moments of its column values (rows 4g + r of its 16-row groups), about a per-lane shift
+  // (the lane's first value of the column: sums of differences, no cancellation at large means)
+  float shf[NI], ls[NI], lq[NI];
+  int ln = 0;
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni) { shf[ni] = 0.f; ls[ni] = 0.f; lq[ni] = 0.f; }
+
+  auto tile = [&](int t, u32x4 (&A)[APS], int tnext) {
+#pragma unroll
+    for (int i = 0; i < APS; ++i) {
+      const int r = ar0 + ARP * i;
+      Al[p1_pos<KC>(r, ac)] = A[i];
+    }
+    if (tnext < p.tiles) load_a(tnext, A);  // DEPTH tiles ahead, under this tile's MFMAs
+    __syncthreads();  // the A tile (and, first time round, the weight block)
+    f32x4 acc[2][NI];
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < K / 32; ++kk) {  // igemm_kernel's order: 64-k steps, chunks 4*s2 + g
+      const int ch = 4 * kk + g;
+      u32x4 fa[2], fb[NI];
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) fa[mi] = Al[p1_pos<KC>(32 * wm + 16 * mi + i16, ch)];
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) fb[ni] = Wl[p1_pos<KC>((BNC / 2) * wn + 16 * ni + i16, ch)];
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) Mma<bf16>::run(acc[mi][ni], fa[mi], fb[ni]);
+    }
+    __syncthreads();  // every wave is done with the A tile before the next one is staged
+    const int row0 = t * kP1BM + 32 * wm + 4 * g;
+    if (row0 + 19 < p.P) {  // all 8 of this lane's rows (row0 + 16 mi + r) valid
+      if (ln == 0) {
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) shf[ni] = acc[0][ni][0];
+      }
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float d = acc[mi][ni][r] - shf[ni];
+            ls[ni] += d;
+            lq[ni] = fmaf(d, d, lq[ni]);
+          }
+      ln += 8;
+    } else {  // the ragged last tile
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (row0 + 16 * mi + r >= p.P) continue;
+          if (ln == 0) {
+#pragma unroll
+            for (int ni = 0; ni < NI; ++ni) shf[ni] = acc[mi][ni][r];
+          }
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni) {
+            const float d = acc[mi][ni][r] - shf[ni];
+            ls[ni] += d;
+            lq[ni] = fmaf(d, d, lq[ni]);
+          }
+          ++ln;
+        }
+    }
+  };
+
+  u32x4 A0[APS], A1[DEPTH == 2 ? APS : 1];
+  int t = g0;
+  if (t < p.tiles) load_a(t, A0);
+  if constexpr (DEPTH == 2) {
+    if (t + p.G < p.tiles) load_a(t + p.G, A1);
+    for (; t < p.tiles; t += 2 * p.G) {
+      tile(t, A0, t + 2 * p.G);
+      if (t + p.G < p.tiles) tile(t + p.G, A1, t + 3 * p.G);
+    }
+  } else {
+    for (; t < p.tiles; t += p.G) tile(t, A0, t + p.G);
+  }
+
+  // lane moments -> {n, mean, M2}, Chan-merged over the 4 lanes of a column (g) and the two row
+  // halves (wm, through LDS): one {sum, M2} row and pixel count per row split
+  float* red = reinterpret_cast<float*>(Al);  // [wm][BNC] {n, mean, m2}
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni) {
+    float n = (float)ln;
+    float mean = ln ? shf[ni] + ls[ni] / n : 0.f;
+    float m2 = ln ? fmaxf(lq[ni] - ls[ni] * ls[ni] / n, 0.f) : 0.f;
+#pragma unroll
+    for (int x = 16; x <= 32; x *= 2) {
+      const float no = __shfl_xor(n, x, 64), mo = __shfl_xor(mean, x, 64), qo = __shfl_xor(m2, x, 64);
+      const float nn = n + no;
+      if (nn > 0.f) {
+        const float d = mo - mean;
+        m2 = m2 + qo + d * d * (n * no / nn);
+        mean = mean + d * (no / nn);
+      }
+      n = nn;
+    }
+    if (g == 0) {
+      const int col = (BNC / 2) * wn + 16 * ni + i16;
+      red[(wm * BNC + col) * 3 + 0] = n;
+      red[(wm * BNC + col) * 3 + 1] = mean;
+      red[(wm * BNC + col) * 3 + 2] = m2;
+    }
+  }
+  __syncthreads();
+  if (tid < BNC) {
+    const float na = red[tid * 3], ma = red[tid * 3 + 1], qa = red[tid * 3 + 2];
+    const float nb_ = red[(BNC + tid) * 3], mb = red[(BNC + tid) * 3 + 1], qb = red[(BNC + tid) * 3 + 2];
+    const float n = na + nb_;
+    float sum = 0.f, m2 = 0.f;
+    if (n > 0.f) {
+      const float d = mb - ma;
+      sum = na * ma + nb_ * mb;
+      m2 = qa + qb + d * d * (na * nb_ / n);
+    }
+    store_part(p.part + (size_t)g0 * p.N + nb * BNC + tid, make_float2(sum, m2));
+    if (nb == 0 && tid == 0) p.counts[g0] = (int)n;
+  }
+}
+
+static bool p1f_shape(const argus_conv_desc& d, int dtype) {
+  return dtype == ARGUS_BF16 && !d.stem && d.r == 1 && d.s == 1 && d.stride == 1 && d.pad == 0 &&
+         (d.c == 64 || d.c == 128 || d.c == 256 || d.c == 512) && d.k % (d.c == 512 ? 64 : 128) == 0 &&
+         d.h == d.ho && d.w == d.wo && (long)d.n * d.h * d.w > 0;
+}
+
+static int p1f_bnc(const argus_conv_desc& d) { return d.c == 512 ? 64 : 128; }
+
+// workgroups per CU the LDS admits (W block + A tile), at most 4 (registers: 90-104 VGPRs at K <= 128)
+static int p1f_occ(const argus_conv_desc& d) {
+  const int bytes = p1f_bnc(d) * d.c * 2 + kP1BM * d.c * 2;
+  const int o = 160 * 1024 / bytes;
+  return o < 1 ? 1 : (o > 4 ? 4 : o);
+}
+
+bool p1x1_fwd_stats_ok(const argus_conv_desc& d, int dtype, int enabled) { return enabled && p1f_shape(d, dtype); }
+
+int p1x1_fwd_stats_rows(const argus_conv_desc& d) {
+  const int tiles = (int)(((long)d.n * d.h * d.w + kP1BM - 1) / kP1BM);
+  const int nb = d.k / p1f_bnc(d);
+  int G = p1f_occ(d) * 256 / nb;
+  if (G < 1) G = 1;
+  return G < tiles ? G : tiles;
+}
+
+// the most pixels one partial row holds (argus_conv_fwd_stat_tile reports it negated: ragged rows)
+int p1x1_fwd_stats_tile(const argus_conv_desc& d) {
+  const int tiles = (int)(((long)d.n * d.h * d.w + kP1BM - 1) / kP1BM);
+  const int G = p1x1_fwd_stats_rows(d);
+  return ((tiles + G - 1) / G) * kP1BM;
+}
+
+int p1x1_fwd_stats_launch(const argus_conv_desc& d, const void* x, const void* w, float* stats, hipStream_t st) {
+  P1FParams p{};
+  p.x = reinterpret_cast<const bf16*>(x);
+  p.w = reinterpret_cast<const bf16*>(w);
+  p.P = d.n * d.h * d.w;
+  p.N = d.k;
+  p.NB = d.k / p1f_bnc(d);
+  p.tiles = (p.P + kP1BM - 1) / kP1BM;
+  p.G = p1x1_fwd_stats_rows(d);
+  p.part = reinterpret_cast<float2*>(stats);
+  p.counts = reinterpret_cast<int*>(stats + (size_t)2 * p.G * p.N);
+  const dim3 grid(p.G * p.NB);
+  switch (d.c) {
+    case 64: timed_launch("argus::p1x1_fwd_stats_kernel<64, 128>", p1x1_fwd_stats_kernel<64, 128>, grid, dim3(256), st, p); break;
+    case 128: timed_launch("argus::p1x1_fwd_stats_kernel<128, 128>", p1x1_fwd_stats_kernel<128, 128>, grid, dim3(256), st, p); break;
+    case 256: timed_launch("argus::p1x1_fwd_stats_kernel<256, 128>", p1x1_fwd_stats_kernel<256, 128>, grid, dim3(256), st, p); break;
+    default: timed_launch("argus::p1x1_fwd_stats_kernel<512, 64>", p1x1_fwd_stats_kernel<512, 64>, grid, dim3(256), st, p);
+  }
+  return check_launch("p1x1_fwd_stats_kernel");
+}
+
 }  // namespace argus

@@ -308,6 +308,10 @@ bool igemm_glds_launch(const IgParams& p, int maxM, int maxK, hipStream_t st);
 // persistent 1x1 stride-1 dgrad with an apply prologue and a mask-bits BN-backward epilogue (the
 // bottleneck conv1 data gradients, conv_p1x1.hip): shape check, BN partial rows, launch
 bool p1x1_ok(const argus_conv_desc& d, int dtype);
+bool p1x1_fwd_stats_ok(const argus_conv_desc& d, int dtype, int enabled);
+int p1x1_fwd_stats_rows(const argus_conv_desc& d);
+int p1x1_fwd_stats_tile(const argus_conv_desc& d);
+int p1x1_fwd_stats_launch(const argus_conv_desc& d, const void* x, const void* w, float* stats, hipStream_t st);
 int p1x1_rows(const argus_conv_desc& d);
 int p1x1_launch(const argus_conv_desc& d, const void* dm, const void* wd, void* out, const void* addend,
                 const argus_bn_bwd_epilogue* bn, const argus_bn_bwd_prologue* pro, hipStream_t st);

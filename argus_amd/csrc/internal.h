@@ -25,6 +25,9 @@ int conv_x8_ok(const argus_conv_desc& d, int pass);
 // BN workspace layout (bn.hip): [0, kBnCounterBytes) ticket counters, then double2 group results
 constexpr size_t kBnCounterBytes = 16384;
 int conv_fwd_stat_tile(const argus_conv_desc& d, int dtype);
+// the partial-row layout of a statistics-only forward (argus_conv_fwd with y == NULL)
+int conv_fwd_stats_only_rows(const argus_conv_desc& d, int dtype);
+int conv_fwd_stats_only_tile(const argus_conv_desc& d, int dtype);
 
 // Kernel-selection policy (argus_conv_policy_default): the immutable library table overlaid with one
 // call's overrides (argus_conv_desc.tuning). Host-only; built per call, never stored.
@@ -52,7 +55,8 @@ enum TuneKey : int {
   kGldsDgradStages = 41,  // LDS ring depth of the glds data gradients (3, or 2: 96 KB)
   kBwdSmallKOcc = 42,     // workgroups per CU the small-K BN-epilogue / apply-prologue dgrads are built for (4 or 3)
   kP1x1Dgrad = 43,        // the persistent 1x1 dgrad (apply prologue + mask-bits BN epilogue) for conv1 (1 on)
-  kNumTuneKeys = 44
+  kP1x1FwdStats = 44,     // statistics-only 1x1 forwards on the persistent kernel (conv_p1x1.hip; 1 on)
+  kNumTuneKeys = 45
 };
 struct Policy {
   int v[kNumTuneKeys];

@@ -63,6 +63,8 @@ class _Conv:
     stat_tile: int
     tags: tuple  # kernel instantiation per pass (fwd, dgrad, wgrad)
     flops: int  # algorithmic flops of one pass
+    so_rows: int  # BN partial rows / tile of a statistics-only forward (y not stored: the fused tail)
+    so_tile: int
 
 
 class ResNetEngine:
@@ -213,7 +215,9 @@ class ResNetEngine:
             tile = L.dll.argus_conv_fwd_stat_tile(C.byref(d), dt)
             fl = C.c_int64(0)
             tags = tuple(L.dll.argus_conv_launch_info(C.byref(d), dt, ps, C.byref(fl)) for ps in range(3))
-            convs[name] = _Conv(name, d, wf, wd, rows, tile, tags, fl.value)
+            so = (L.dll.argus_conv_fwd_stats_only_rows(C.byref(d), BF16),
+                  L.dll.argus_conv_fwd_stats_only_tile(C.byref(d), BF16))
+            convs[name] = _Conv(name, d, wf, wd, rows, tile, tags, fl.value, *so)
             return d.ho, d.wo
 
         H1, W1 = add("resnet.conv1", N, H, W, 3, 64, 7, 2, 3, stem=True)
@@ -283,9 +287,10 @@ class ResNetEngine:
         self.bn_state = {n: self._f(4, c) for n, c in chans.items()}
         self.bn_coef = {n: self._f(3, c) for n, c in chans.items()}
 
-        max_stat = max(cv.stat_rows * cv.desc.k for cv in convs.values())
-        # + int32 row counts after the partials of a ragged producer (negative stat tile: the stem)
-        self.stat_part = self._f(max_stat * 2 + max(cv.stat_rows for cv in convs.values()))
+        max_stat = max(max(cv.stat_rows, cv.so_rows) * cv.desc.k for cv in convs.values())
+        # + int32 row counts after the partials of a ragged producer (negative stat tile: the stem, the
+        # persistent statistics-only forward)
+        self.stat_part = self._f(max_stat * 2 + max(max(cv.stat_rows, cv.so_rows) for cv in convs.values()))
         self.bn_ws = torch.zeros(L.dll.argus_bn_workspace_bytes(2048), dtype=torch.uint8, device=self.device)
         # the downsample branch's own statistics workspaces (it runs on the side stream in forward)
         ds_stat = max([cv.stat_rows * cv.desc.k for n, cv in convs.items() if ".downsample." in n] or [1])
@@ -400,7 +405,10 @@ class ResNetEngine:
                                                          ptr(sh), ptr(part) if training else None, stream()))
         if training:
             count = cv.desc.n * cv.desc.ho * cv.desc.wo
-            self._bn_train(P, Bf, bn, cv.stat_rows, cv.stat_tile, count, part, ws)
+            if y is None and sc is None and x_out is None:  # the statistics-only forward's partial layout
+                self._bn_train(P, Bf, bn, cv.so_rows, cv.so_tile, count, part, ws)
+            else:
+                self._bn_train(P, Bf, bn, cv.stat_rows, cv.stat_tile, count, part, ws)
         else:
             self._bn_eval(P, Bf, bn)
 

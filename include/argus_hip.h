@@ -123,6 +123,12 @@ int argus_conv_fwd_bn_out(const argus_conv_desc* d, int dtype, const void* x, co
                           const float* res_shift, void* out, uint8_t* mask_bits, void* y, argus_stream_t stream);
 int argus_conv_fwd_stat_rows(const argus_conv_desc* d, int dtype);
 int argus_conv_fwd_stat_tile(const argus_conv_desc* d, int dtype);
+/* The partial layout (rows, tile as above) of a statistics-only argus_conv_fwd (y == NULL, no
+ * prologue; ABI 16): bf16 1x1 stride-1 convs with 64..512 input channels run on a persistent kernel
+ * (policy key 44) that writes one {sum, M2} row per row split and the int32 pixel counts after them
+ * (negative tile: ragged rows); other convs as argus_conv_fwd_stat_rows / _stat_tile. */
+int argus_conv_fwd_stats_only_rows(const argus_conv_desc* d, int dtype);
+int argus_conv_fwd_stats_only_tile(const argus_conv_desc* d, int dtype);
 /* dx = dgrad(dy, w_dgrad) [+ addend]: when addend != NULL (same NHWC layout as dx; may be dx itself
  * for in-place accumulation) it is added, element-wise masked by addend_mask when that is non-NULL
  * (the bn_apply ReLU mask: the residual path of a bottleneck, dx += relu'(out) * dout). */
@@ -233,7 +239,9 @@ int argus_conv_dgrad_bn_x8(const argus_conv_desc* d, const void* dy8, const void
  * glds kernel, key 37 which ARGUS_FP8 passes take MX-fp8 operands (bits: 1 forward, 2 data gradient of
  * a 3x3 conv, 4 data gradient of a 1x1 conv, 8 forward of a 3x3 stride-1 conv; default 10;
  * argus_conv_weight_prep follows the same key), key 42 the
- * workgroups per CU (4 or 3) the small-K BN-epilogue / apply-prologue data gradients are built for.
+ * workgroups per CU (4 or 3) the small-K BN-epilogue / apply-prologue data gradients are built for,
+ * key 43 the bottleneck conv1 data gradients on the persistent kernel (1) or the igemm (0), key 44 the
+ * statistics-only 1x1 forwards on the persistent kernel (1) or the igemm (0).
  * (Keys scaled with the batch keep a smaller batch's kernel selection that of the larger one:
  * tests/test_gpu_parity.py stage-checks the benched configurations' kernels that way.) */
 int argus_conv_policy_default(int key);

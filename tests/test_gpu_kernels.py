@@ -1535,6 +1535,45 @@ def test_conv_x8_halo_fwd_dgrad(cuda):
         assert int(ws[:16384].count_nonzero()) == 0  # ticket counters left at zero
 
 
+def test_stats_only_forward_persistent_kernel(cuda):
+    """Statistics-only 1x1 forward (argus_conv_fwd, y == NULL) on the persistent kernel (policy key 44):
+    one {sum, M2} row per row split plus int32 pixel counts (argus_conv_fwd_stats_only_rows / _tile,
+    negative tile), merged mean / biased variance within 1e-5 of the fp64 moments of x w^T on the same
+    bf16 operands and within 2e-6 of the register-staged igemm's partials (key 44 = 0: the same
+    products, another merge grouping); every input width 64..512, ragged pixel counts, more row splits
+    than some workgroups get tiles."""
+    from argus_amd.profiling import KernelTimer
+
+    torch.manual_seed(37)
+    L = lib()
+    for n, h, w, c, k in [(4, 16, 16, 64, 256), (3, 7, 9, 128, 512), (2, 8, 8, 256, 1024), (2, 5, 5, 512, 2048),
+                          (64, 64, 64, 64, 256)]:
+        d, _ = _desc(n, h, w, c, k, 1, 1)
+        P = n * h * w
+        rows = L.dll.argus_conv_fwd_stats_only_rows(C.byref(d), BF16)
+        tile = L.dll.argus_conv_fwd_stats_only_tile(C.byref(d), BF16)
+        assert tile < 0 and rows * -tile >= P
+        x = torch.randn(n, h, w, c, device=cuda).to(torch.bfloat16)
+        wf, _ = _prep(d, "bf16", (torch.randn(k, 1, 1, c) * c ** -0.5).to(cuda), cuda)
+        st = torch.full((rows * k * 2 + rows,), float("nan"), device=cuda)
+        with KernelTimer("argus::p1x1_fwd_stats_kernel") as t:
+            L.conv_fwd(C.byref(d), BF16, ptr(x), ptr(wf), None, None, None, ptr(st), stream())
+        assert len(t.summary()) == 1, list(t.summary())
+        part = st[: rows * k * 2].reshape(rows, k, 2).double().cpu()
+        counts = st[rows * k * 2:].view(torch.int32).cpu()
+        mean, var = _merge_stats(part, tile, P, counts)
+        y = x.reshape(P, c).double().cpu() @ wf.double().cpu().reshape(k, c).t()
+        assert _rel(mean, y.mean(0)) < 1e-5 and _rel(var, y.var(0, unbiased=False)) < 1e-5, (n, h, w, c, k)
+        d0 = d.with_tuning({44: 0})
+        r0, t0 = (L.dll.argus_conv_fwd_stats_only_rows(C.byref(d0), BF16),
+                  L.dll.argus_conv_fwd_stats_only_tile(C.byref(d0), BF16))
+        assert (r0, t0) == (L.dll.argus_conv_fwd_stat_rows(C.byref(d0), BF16), L.dll.argus_conv_fwd_stat_tile(C.byref(d0), BF16))
+        st0 = torch.empty(r0, k, 2, device=cuda)
+        L.conv_fwd(C.byref(d0), BF16, ptr(x), ptr(wf), None, None, None, ptr(st0), stream())
+        m0, v0 = _merge_stats(st0.double().cpu(), t0, P)
+        assert _rel(mean, m0) < 2e-6 and _rel(var, v0) < 2e-6, (n, h, w, c, k)
+
+
 def test_conv_fwd_apply_out_matches_apply_then_conv(cuda):
     """argus_conv_fwd_apply_out (ABI 16): a 1x1 stride-1 forward whose BN+ReLU prologue also stores the
     applied input: x_out bit-identical to argus_bn_apply(relu) of x, and y / the BN statistics partials

@@ -157,15 +157,21 @@ def test_side_stream_overlap_is_bit_identical(cuda):
     x = (torch.randint(0, 256, (8, 6, 128, 128), generator=g, dtype=torch.uint8).float() / 255.0).to(cuda)
     T = se3.random_targets(8, generator=g).float().to(cuda)
     runs = []
-    # (side stream, first block's downsample weight gradient on the main stream's tail, ...)
-    for attrs in ({}, {"tail_main": False}, {"wgrad_overlap": False}, {"fuse_out": False}, {"gate3x3": True},
-                  {"yrec_epi": True}, {"yrec_epi": True, "y3_free": True}, {"a2_in_stats": False}):
+    # (side stream, first block's downsample weight gradient on the main stream's tail, ...). The fused
+    # tail's statistics-only conv3 pass runs on the persistent kernel (policy key 44), whose partial sums
+    # group differently from the stored-y forward's: fuse_out is compared under key 44 = 0 (a second
+    # baseline, itself checked against the default only through the kernel tests' tolerances).
+    cases = ({}, {"tail_main": False}, {"wgrad_overlap": False}, {"gate3x3": True}, {"yrec_epi": True},
+             {"yrec_epi": True, "y3_free": True}, {"a2_in_stats": False}, {"_tune": {44: 0}},
+             {"_tune": {44: 0}, "fuse_out": False})
+    for attrs in cases:
         torch.manual_seed(42)
-        model = NCameraCNN(compute_dtype="bf16").to(cuda).train()
+        model = NCameraCNN(compute_dtype="bf16", kernel_tuning=attrs.get("_tune")).to(cuda).train()
         tr = FusedTrainer(model, lr=1e-3, max_grad_norm=1.0)
         eng = model._engine(cuda)
         for k, v in attrs.items():
-            setattr(eng, k, v)
+            if k != "_tune":
+                setattr(eng, k, v)
         losses = [tr.step(x, T).clone() for _ in range(3)]
         model.eval()
         with torch.no_grad():
@@ -173,11 +179,12 @@ def test_side_stream_overlap_is_bit_identical(cuda):
         torch.cuda.synchronize()
         runs.append((torch.stack(losses).cpu(), tr.flat.param.cpu(), tr.exp_avg_sq.cpu(),
                      {k: v.cpu() for k, v in model.state_dict().items()}, pe.cpu(), attrs))
-    (l1, p1, v1, s1, e1, _) = runs[0]
-    for l0, p0, v0, s0, e0, attrs in runs[1:]:
-        assert torch.equal(l1, l0) and torch.equal(p1, p0) and torch.equal(v1, v0), attrs
-        assert all(torch.equal(s1[k], s0[k]) for k in s1), attrs
-        assert torch.equal(e1, e0), attrs
+    for base, others in ((runs[0], runs[1:-2]), (runs[-2], runs[-1:])):
+        (l1, p1, v1, s1, e1, _) = base
+        for l0, p0, v0, s0, e0, attrs in others:
+            assert torch.equal(l1, l0) and torch.equal(p1, p0) and torch.equal(v1, v0), attrs
+            assert all(torch.equal(s1[k], s0[k]) for k in s1), attrs
+            assert torch.equal(e1, e0), attrs
 
 
 def test_rotation_angle_error_matches_oracle(cuda):
