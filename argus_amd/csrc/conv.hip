@@ -709,8 +709,14 @@ __global__ __launch_bounds__(256, ARGUS_WGRAD_OCC) void wgrad_kernel(const WgPar
   }
   const T* ap_col = AP ? reinterpret_cast<const T*>(p.ap_y) + mt * BM + ca * E : nullptr;
 
+  // load() only issues the global loads of a k-step; everything that consumes the loaded registers (the
+  // apply, the BN prologue, zeroing rows past the split's range) runs in store(), after the previous
+  // k-step's MFMAs: a transform in load() made the wave wait for its loads there (s_waitcnt vmcnt(0)
+  // ahead of every MFMA of the k-step), so no load latency overlapped the MFMAs
   struct Stage {
     u32x4 a[PA], b[PB];
+    u32x4 y[AP ? PA : 1];  // the apply's y rows beside the dm rows
+    bool oka[PA], okb[PB];
   };
 
   auto load = [&](int p0, Stage& S) {
@@ -719,15 +725,8 @@ __global__ __launch_bounds__(256, ARGUS_WGRAD_OCC) void wgrad_kernel(const WgPar
       const int pix = p0 + ra0 + RPA * i;
       const bool ok = pix < pend;
       S.a[i] = ld16(a_col + (size_t)(ok ? pix : pbeg) * p.M);  // pbeg < P: a safe clamp
-      if constexpr (AP) {  // dy = ca*dm + cb*y + cc (argus_bn_bwd_apply's formula, fp32, rounded to T)
-        float d[E], yv[E];
-        unpack(S.a[i], d);
-        unpack(ld16(ap_col + (size_t)(ok ? pix : pbeg) * p.M), yv);
-#pragma unroll
-        for (int j = 0; j < E; ++j) d[j] = fmaf(apa[j], d[j], fmaf(apb[j], yv[j], apc[j]));
-        S.a[i] = pack(d);
-      }
-      S.a[i] = sel(ok, S.a[i]);
+      if constexpr (AP) S.y[i] = ld16(ap_col + (size_t)(ok ? pix : pbeg) * p.M);
+      S.oka[i] = ok;
     }
     int n0 = 0, oh0 = 0, ow0 = 0;
     if constexpr (FAST) {  // uniform: the k-step lies inside one image
@@ -761,15 +760,16 @@ __global__ __launch_bounds__(256, ARGUS_WGRAD_OCC) void wgrad_kernel(const WgPar
           const uint2 v0 = *reinterpret_cast<const uint2*>(X + (ok0 ? rowoff + iw0 * 4 : 0));
           const uint2 v1 = *reinterpret_cast<const uint2*>(X + (ok1 ? rowoff + iw1 * 4 : 0));
           S.b[i] = u32x4{ok0 ? v0.x : 0u, ok0 ? v0.y : 0u, ok1 ? v1.x : 0u, ok1 ? v1.y : 0u};
+          S.okb[i] = true;
         } else {
           const bool ok = hok && (unsigned)iw0 < (unsigned)p.W;
-          S.b[i] = sel(ok, ld16(X + (ok ? rowoff + iw0 * 4 : 0)));
+          S.b[i] = ld16(X + (ok ? rowoff + iw0 * 4 : 0));
+          S.okb[i] = ok;
         }
       } else {
         const bool ok = hok && (unsigned)iw0 < (unsigned)p.W;
-        u32x4 v = ld16(X + (ok ? rowoff + iw0 * p.lda + ci : 0));
-        if constexpr (PRO) v = pc.apply(v);
-        S.b[i] = sel(ok, v);
+        S.b[i] = ld16(X + (ok ? rowoff + iw0 * p.lda + ci : 0));
+        S.okb[i] = ok;
       }
     }
   };
@@ -779,14 +779,25 @@ __global__ __launch_bounds__(256, ARGUS_WGRAD_OCC) void wgrad_kernel(const WgPar
       const int row = ra0 + RPA * i;
       int c = ca;
       if constexpr (BF) c = (((ca >> 1) ^ swz32(row)) << 1) | (ca & 1);
-      lds[buf][row * RSA + c] = S.a[i];
+      u32x4 v = S.a[i];
+      if constexpr (AP) {  // dy = ca*dm + cb*y + cc (argus_bn_bwd_apply's formula, fp32, rounded to T)
+        float d[E], yv[E];
+        unpack(v, d);
+        unpack(S.y[i], yv);
+#pragma unroll
+        for (int j = 0; j < E; ++j) d[j] = fmaf(apa[j], d[j], fmaf(apb[j], yv[j], apc[j]));
+        v = pack(d);
+      }
+      lds[buf][row * RSA + c] = sel(S.oka[i], v);
     }
 #pragma unroll
     for (int i = 0; i < PB; ++i) {
       const int row = rb0 + RPB * i;
       int c = cb;
       if constexpr (BF) c = (((cb >> 1) ^ swz32(row)) << 1) | (cb & 1);
-      lds[buf][BKP * RSA + row * RSB + c] = S.b[i];
+      u32x4 v = S.b[i];
+      if constexpr (PRO && !STEM) v = pc.apply(v);
+      lds[buf][BKP * RSA + row * RSB + c] = sel(S.okb[i], v);
     }
   };
 
