@@ -245,11 +245,7 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
         if constexpr (F8) S.a2[i] = ld16(A + (ok ? a_off[i] + tap + E : ch));
         if constexpr (AP) S.y[i] = ld16(reinterpret_cast<const T*>(p.ap.y) + (ok ? a_off[i] + tap : ch));
         if constexpr (AP && F8) S.y2[i] = ld16(reinterpret_cast<const T*>(p.ap.y) + (ok ? a_off[i] + tap + E : ch));
-        if constexpr (!PRO && !AP) {
-          S.a[i] = sel(ok, S.a[i]);
-          if constexpr (F8) S.a2[i] = sel(ok, S.a2[i]);
-        }
-        S.ok[i] = ok;
+        S.ok[i] = ok;  // rows outside the image are zeroed in store(): load() only issues loads
       }
 #pragma unroll
       for (int i = 0; i < BR; ++i) {
@@ -267,6 +263,13 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
 
   auto store = [&](int buf, Stage& S) {
     u32x4* L = lds + buf * (BM + BN) * 8;
+    if constexpr (!PRO && !AP && !STEM) {
+#pragma unroll
+      for (int i = 0; i < AR; ++i) {
+        S.a[i] = sel(S.ok[i], S.a[i]);
+        if constexpr (F8) S.a2[i] = sel(S.ok[i], S.a2[i]);
+      }
+    }
     if constexpr (PRO && !STEM) {
       ProCoef<T> pc;
       if (pro_in_lds) pc.load_lds(pro_lds, S.ch);
@@ -376,7 +379,21 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
   // Main loop: LDS double buffer + 2-deep register prefetch ring (S0/S1). At the MFMAs of step kt,
   // the global loads of steps kt+1 and kt+2 are in flight.
   const int nk = ph.K / BKE;
-  if constexpr (NBUF == 1) {
+  // one LDS buffer: the next k-step's loads are issued into the same staging registers once this step's
+  // are in LDS, and land under its MFMAs - except for the apply-prologue variants built for 4 workgroups
+  // per CU, where the live staging registers (dm and y rows) across the MFMAs would spill
+  constexpr bool PREF = !(AP && OCC >= 4);
+  if constexpr (NBUF == 1 && PREF) {
+    Stage S0;
+    if (nk > 0) load(0, S0);
+    for (int kt = 0; kt < nk; ++kt) {
+      store(0, S0);
+      __syncthreads();
+      if (kt + 1 < nk) load(kt + 1, S0);
+      compute(0);
+      __syncthreads();
+    }
+  } else if constexpr (NBUF == 1) {
     for (int kt = 0; kt < nk; ++kt) {
       Stage S0;
       load(kt, S0);

@@ -1601,7 +1601,10 @@ def test_conv_fwd_apply_out_matches_apply_then_conv(cuda):
             assert torch.equal(a, a_ref), (n, h, w, c, k)
             y_ref = torch.empty(n, h, w, k, device=cuda, dtype=torch.bfloat16) if store_y else None
             st_ref = torch.empty_like(st)
-            L.conv_fwd(C.byref(d), BF16, ptr(a_ref), ptr(wf), ptr(y_ref), None, None, ptr(st_ref), stream())
+            # (the statistics-only reference on the igemm too: key 44 would send it to the persistent
+            # kernel, whose partial rows group differently)
+            L.conv_fwd(C.byref(d.with_tuning({44: 0})), BF16, ptr(a_ref), ptr(wf), ptr(y_ref), None, None, ptr(st_ref),
+                       stream())
             assert torch.equal(st, st_ref), (n, h, w, c, k, store_y)
             if store_y:
                 assert torch.equal(y, y_ref)
@@ -1738,7 +1741,8 @@ def test_glds_two_stage_ring_matches_three(cuda):
                                             (512, 2048, 5, False), (256, 1024, 7, True)])
 def test_conv_fwd_bn_out_matches_conv_and_apply(cuda, cin, cout, hw, ds):
     """argus_conv_fwd_bn_out (the bottleneck tail: conv3's C tile -> bn3 + residual (+ the downsample
-    BN) + ReLU, mask bits) and the statistics-only forward (argus_conv_fwd with y = NULL) against
+    BN) + ReLU, mask bits) and the register-staged statistics-only forward (argus_conv_fwd with y = NULL,
+    policy key 44 = 0) against
     argus_conv_fwd + argus_bn_apply: every output bit-identical (y, out, mask bits, BN partials);
     ragged row tiles (hw = 5, 7) included."""
     torch.manual_seed(77)
@@ -1753,7 +1757,9 @@ def test_conv_fwd_bn_out_matches_conv_and_apply(cuda, cin, cout, hw, ds):
     st_new = torch.full((rows * cout * 2,), float("nan"), device=cuda)
     y_ref = torch.empty(n, hw, hw, cout, dtype=torch.bfloat16, device=cuda)
     L.conv_fwd(C.byref(d), BF16, ptr(x), ptr(wf), ptr(y_ref), None, None, ptr(st_ref), stream())
-    L.conv_fwd(C.byref(d), BF16, ptr(x), ptr(wf), None, None, None, ptr(st_new), stream())
+    # (the register-staged statistics-only pass: key 44 = 0; the persistent one writes another partial
+    # layout, test_stats_only_forward_persistent_kernel)
+    L.conv_fwd(C.byref(d.with_tuning({44: 0})), BF16, ptr(x), ptr(wf), None, None, None, ptr(st_new), stream())
     assert torch.equal(st_ref, st_new)
     sc, sh = torch.rand(cout, device=cuda) + 0.5, torch.randn(cout, device=cuda)
     res = torch.randn(n, hw, hw, cout, device=cuda).to(torch.bfloat16)
