@@ -177,11 +177,11 @@ class ResNetEngine:
         self.x8 = True
         # training forward with the fused tail: conv3's statistics pass applies bn2 to y2 while staging its
         # operand and stores a2 itself (argus_conv_fwd_apply_out, bit-identical to the bn_apply pass it
-        # replaces: one pass over y2 and one launch fewer per block). Measured slower (round 5, B=64
-        # interleaved x3: 14.06-14.09 vs 13.99-14.02 ms, profiles/r05o_ab_a2_in_stats.txt): the register-
-        # staged statistics pass applies bn2 once per column tile and its stores lengthen the short,
-        # latency-bound workgroups more than the apply pass costs
-        self.a2_in_stats = False
+        # replaces: one pass over y2 and one launch fewer per block). First measured 0.5 % slower (round 5,
+        # profiles/r05o_ab_a2_in_stats.txt); after the register-staged kernels stopped waiting for their
+        # loads inside load() (the next k-step's loads now land under the MFMAs), 0.4 % faster: B=64
+        # interleaved x4 13.79-13.81 vs 13.84-13.85 ms (profiles/r05u_ab_a2_in_stats.txt)
+        self.a2_in_stats = True
         # (the schedule switches above are attributes, not environment variables: tools/engine_ab.py
         # A/B-measures them; test_gpu_train.py runs the overlap / tail placements against each other)
 
