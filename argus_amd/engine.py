@@ -179,9 +179,10 @@ class ResNetEngine:
         # operand and stores a2 itself (argus_conv_fwd_apply_out, bit-identical to the bn_apply pass it
         # replaces: one pass over y2 and one launch fewer per block). First measured 0.5 % slower (round 5,
         # profiles/r05o_ab_a2_in_stats.txt); after the register-staged kernels stopped waiting for their
-        # loads inside load() (the next k-step's loads now land under the MFMAs), 0.4 % faster: B=64
-        # interleaved x4 13.79-13.81 vs 13.84-13.85 ms (profiles/r05u_ab_a2_in_stats.txt)
-        self.a2_in_stats = True
+        # loads inside load(), 0.4 % faster at B=64 (13.79-13.81 vs 13.84-13.85 ms, r05u_ab_a2_in_stats.txt)
+        # but 1.5 % slower at B=256 (47.2-47.8 vs 46.7-46.9 ms) and 0.9 % at 376x672 (91.5-92.5 vs
+        # 90.6-91.5 ms, r05aa_ab_a2_in_stats_*.txt): off
+        self.a2_in_stats = False
         # (the schedule switches above are attributes, not environment variables: tools/engine_ab.py
         # A/B-measures them; test_gpu_train.py runs the overlap / tail placements against each other)
 
