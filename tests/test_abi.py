@@ -62,6 +62,15 @@ def test_bad_arguments_are_reported():
     s2 = ConvDesc(8, 16, 16, 256, 256, 3, 3, 2, 1, 8, 8, 0).with_tuning({13: 1})
     c64 = ConvDesc(8, 16, 16, 64, 64, 3, 3, 1, 1, 16, 16, 0).with_tuning({13: 1})
     assert [L.dll.argus_conv_x8_ok(C.byref(d_), ps) for d_ in (s2, c64) for ps in (0, 1)] == [0, 0, 0, 0]
+    # the statistics-only forward's partial layout (host-only): the persistent kernel's ragged rows (one per
+    # row split, negative tile) for bf16 1x1 stride-1 convs under key 44, the igemm layout otherwise
+    so = ConvDesc(64, 64, 64, 64, 256, 1, 1, 1, 0, 64, 64, 0)
+    rows, tile = L.dll.argus_conv_fwd_stats_only_rows(C.byref(so), 1), L.dll.argus_conv_fwd_stats_only_tile(C.byref(so), 1)
+    assert tile < 0 and 0 < rows <= 1024 and rows * -tile >= 64 * 64 * 64
+    so0 = so.with_tuning({44: 0})
+    assert (L.dll.argus_conv_fwd_stats_only_rows(C.byref(so0), 1), L.dll.argus_conv_fwd_stats_only_tile(C.byref(so0), 1)) == \
+        (L.dll.argus_conv_fwd_stat_rows(C.byref(so0), 1), L.dll.argus_conv_fwd_stat_tile(C.byref(so0), 1))
+    assert L.dll.argus_conv_fwd_stats_only_tile(C.byref(good), 1) == L.dll.argus_conv_fwd_stat_tile(C.byref(good), 1)
     unknown = good.with_tuning({30: 1})  # removed key (the 64-channel halo variant is a constant)
     with pytest.raises(ArgusHipError, match="unknown tuning key 30"):
         L.conv_fwd(C.byref(unknown), 1, 16, 16, 16, None, None, None, None)
