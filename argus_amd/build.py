@@ -18,7 +18,7 @@ CSRC = HERE / "csrc"
 OUT = HERE / "libargus_hip.so"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
-SOURCES = ["capi.cpp", "ktimer.cpp", "conv.hip", "conv_glds.hip", "conv_halo.hip", "conv_dgw.hip", "conv_p1x1.hip", "reduce.hip", "stem.hip", "bn.hip", "head.hip", "loss.hip", "optim.hip", "augment.hip"]
+SOURCES = ["capi.cpp", "ktimer.cpp", "conv.hip", "conv_glds.hip", "conv_halo.hip", "conv_dgw.hip", "conv_p1x1.hip", "conv_wgdma.hip", "reduce.hip", "stem.hip", "bn.hip", "head.hip", "loss.hip", "optim.hip", "augment.hip"]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
          "-Wno-unused-variable", "-Wno-unused-but-set-variable"]
 

@@ -1298,6 +1298,9 @@ static const Policy kDefaultPolicy = [] {
   // 43: the bottleneck conv1 data gradients (1x1, apply prologue, mask-bits BN epilogue with the folded
   //     finalize) on the persistent kernel of conv_p1x1.hip (1) or the register-staged igemm (0)
   p.v[kP1x1Dgrad] = 1;
+  // 45: 1x1 bf16 weight gradients on the LDS-DMA ring kernel of conv_wgdma.hip with 128 x 128 tiles (1),
+  //     128 x 256 tiles where Cin % 256 == 0 (2), or the register-staged wgrad_kernel (0)
+  p.v[kWgradDma] = 2;
   return p;
 }();
 
@@ -1934,6 +1937,9 @@ static int conv_wgrad_impl(const argus_conv_desc& d, int dtype, const void* x, c
   int splits = pl.splits;
   if (d.stem && pol[kStemLdsWgrad] && stem_wgrad_launch(d, dtype, x, dy, ap, ws, ws_bytes, &splits, st)) {
     if (int e = check_launch("stem_wgrad_kernel")) return e;
+  } else if (!sc && wgrad_dma_ok(d, dtype, pl.bm, pl.bn, pol[kWgradDma])) {  // 1x1: LDS-DMA ring
+    wgrad_dma_launch(d, p, pol[kWgradDma], pl.splits, st);
+    if (int e = check_launch("wgrad_dma_kernel")) return e;
   } else if (ap) {  // the register-staged kernel stages the apply; no halo / glds variant does
     if (dtype == ARGUS_BF16) dispatch_wg<bf16>(p, pl, st);
     else dispatch_wg<float>(p, pl, st);

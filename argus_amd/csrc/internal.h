@@ -56,7 +56,8 @@ enum TuneKey : int {
   kBwdSmallKOcc = 42,     // workgroups per CU the small-K BN-epilogue / apply-prologue dgrads are built for (4 or 3)
   kP1x1Dgrad = 43,        // the persistent 1x1 dgrad (apply prologue + mask-bits BN epilogue) for conv1 (1 on)
   kP1x1FwdStats = 44,     // statistics-only 1x1 forwards on the persistent kernel (conv_p1x1.hip; 1 on)
-  kNumTuneKeys = 45
+  kWgradDma = 45,         // 1x1 bf16 weight gradients on the LDS-DMA ring kernel (conv_wgdma.hip)
+  kNumTuneKeys = 46
 };
 struct Policy {
   int v[kNumTuneKeys];

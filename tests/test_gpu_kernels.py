@@ -1210,6 +1210,64 @@ def test_unstored_apply_and_wgrad_apply(cuda, dt):
     assert staged >= 3
 
 
+def test_wgrad_dma_kernel_bitwise(cuda):
+    """1x1 stride-1 bf16 weight gradients on the LDS-DMA ring kernel (policy key 45, conv_wgdma.hip:
+    1 = 128 x 128 tiles, 2 = 128 x 256 where Cin % 256 == 0) vs the register-staged wgrad_kernel
+    (key 45 = 0), plain and with the BN-backward apply staged
+    from dm (argus_conv_wgrad_apply): dW bit-identical (same apply formula, same MFMA order over
+    32-pixel blocks, same splits). Pixel counts that end mid k-step (ragged last split: zero-page
+    rows), split targets from one split per tile to many short ones (ring prologue with fewer
+    k-steps than stages), and dW against a float64 torch reference."""
+    from argus_amd._lib import BnBwdPrologue
+    from argus_amd.profiling import KernelTimer
+
+    torch.manual_seed(45)
+    L = lib()
+    ran = 0
+    for cin, cout, hh, ww, n in [(128, 128, 8, 8, 1), (256, 128, 7, 9, 2), (128, 512, 14, 14, 2),
+                                 (512, 256, 5, 3, 1), (256, 256, 56, 56, 2), (1024, 256, 13, 11, 3)]:
+        for target in (None, 4, 2048):
+            tune = {} if target is None else {6: target}
+            x = torch.randn(n, hh, ww, cin, device=cuda).to(torch.bfloat16)
+            dm = torch.randn(n, hh, ww, cout, device=cuda).to(torch.bfloat16)
+            yb = torch.randn(n, hh, ww, cout, device=cuda).to(torch.bfloat16)
+            ca, cb, cc = (torch.randn(cout, device=cuda) * 0.3 for _ in range(3))
+            for apply in (False, True):
+                outs = []
+                for key in (2, 1, 0):
+                    d, _ = _desc(n, hh, ww, cin, cout, 1, 1)
+                    d = d.with_tuning({**tune, 45: key})
+                    wsb = L.dll.argus_conv_wgrad_workspace_bytes(C.byref(d), BF16)
+                    ws = torch.empty(wsb, dtype=torch.uint8, device=cuda)
+                    dw = torch.empty(cout, 1, 1, cin, device=cuda)
+                    with KernelTimer("argus::wgrad_dma_kernel<%s" % ("true" if apply else "false")) as t:
+                        if apply:
+                            ap = BnBwdPrologue(ptr(yb), ptr(ca), ptr(cb), ptr(cc), None)
+                            rc = L.conv_wgrad_apply(C.byref(d), BF16, ptr(x), ptr(dm), C.byref(ap), ptr(dw), ptr(ws),
+                                                    wsb, stream())
+                        else:
+                            rc = L.conv_wgrad(C.byref(d), BF16, ptr(x), None, None, ptr(dm), ptr(dw), ptr(ws), wsb,
+                                              stream())
+                    assert rc in (0, None), L.dll.argus_last_error()
+                    torch.cuda.synchronize()
+                    ks = list(t.summary())
+                    want = 0 if not key else (256 if key == 2 and cin % 256 == 0 else 128)
+                    assert len(ks) == (1 if key else 0) and (not key or ks[0].endswith(", %d>" % want)), \
+                        ("dma kernel use", cin, cout, hh, ww, n, key, ks)
+                    outs.append(dw.cpu())
+                assert torch.equal(outs[0], outs[2]) and torch.equal(outs[1], outs[2]), \
+                    (cin, cout, hh, ww, n, target, apply)
+                dy = dm.double()
+                if apply:
+                    dy = (ca.double() * dm.double() + (cb.double() * yb.double() + cc.double()))
+                    dy = dy.float().to(torch.bfloat16).double()
+                ref = torch.einsum("pk,pc->kc", dy.reshape(-1, cout), x.double().reshape(-1, cin)).cpu()
+                tol = 1e-3 if apply else 1e-4  # fp32 accumulation of exact bf16 products (+ the bf16 dy rounding)
+                assert _rel(outs[0].reshape(cout, cin), ref) < tol, (cin, cout, apply)
+                ran += 1
+    assert ran == 36
+
+
 @pytest.mark.parametrize("dt", ["fp32", "bf16"])
 def test_stem_backward_fusions(cuda, dt):
     """argus_maxpool_bwd_bn (maxpool backward + the stem BN's backward reduction) against
