@@ -1299,7 +1299,9 @@ static const Policy kDefaultPolicy = [] {
   //     finalize) on the persistent kernel of conv_p1x1.hip (1) or the register-staged igemm (0)
   p.v[kP1x1Dgrad] = 1;
   // 45: 1x1 bf16 weight gradients on the LDS-DMA ring kernel of conv_wgdma.hip with 128 x 128 tiles (1),
-  //     128 x 256 tiles where Cin % 256 == 0 (2), or the register-staged wgrad_kernel (0)
+  //     128 x 256 tiles where Cin % 256 == 0 for the apply variant (2) or both (3), or the
+  //     register-staged wgrad_kernel (0): engine A/B 2 vs 0: B=256 46.05-46.21 vs 46.54-46.57 ms,
+  //     376x672 89.6-89.9 vs 90.6-91.2 ms, B=64 within drift (profiles/r05ai_ab_key45_*.txt)
   p.v[kWgradDma] = 2;
   return p;
 }();

@@ -243,21 +243,24 @@ __global__ __launch_bounds__(2 * BN, BN == 256 ? 1 : 2) void wgrad_dma_kernel(co
     }
 }
 
-// the column-tile width wgrad_dma_launch uses for d under key 45 (0: not served)
-static int wgrad_dma_bn(const argus_conv_desc& d, int dtype, int bm, int bn, int key) {
+// the column-tile width wgrad_dma_launch uses for d under key 45 (0: not served): 256 with the apply
+// (key 2) or always (key 3) where Cin % 256 == 0. Measured alone (tools/wgbench.py, B=64, the 12
+// 1x1 stride-1 shapes): apply 785 / 815 us (256 / 128 wide), plain 592 / 562 us: the plain kernel
+// at one workgroup per CU stalls at its per-k-step barrier with no second workgroup to fill it
+static int wgrad_dma_bn(const argus_conv_desc& d, int dtype, int bm, int bn, int key, bool ap) {
   if (!key || dtype != ARGUS_BF16 || d.stem || d.r != 1 || d.s != 1 || d.stride != 1 || d.pad != 0 ||
       d.h != d.ho || d.w != d.wo || bm != 128 || bn != 128 || d.k % 128 || d.c % 128)
     return 0;
-  return key >= 2 && d.c % 256 == 0 ? 256 : 128;
+  return ((key == 2 && ap) || key >= 3) && d.c % 256 == 0 ? 256 : 128;
 }
 
 bool wgrad_dma_ok(const argus_conv_desc& d, int dtype, int bm, int bn, int enabled) {
-  return wgrad_dma_bn(d, dtype, bm, bn, enabled) != 0;
+  return wgrad_dma_bn(d, dtype, bm, bn, enabled, false) != 0;
 }
 
 // grid: the 128 x 128 tiles x splits of the plan; 256-wide tiles take two of its column tiles
 void wgrad_dma_launch(const argus_conv_desc& d, const WgParams& p, int key, int splits, hipStream_t st) {
-  const int bn = wgrad_dma_bn(d, ARGUS_BF16, 128, 128, key);
+  const int bn = wgrad_dma_bn(d, ARGUS_BF16, 128, 128, key, p.ap_y != nullptr);
   const int grid = (p.M / 128) * (p.N / bn) * splits;
   if (bn == 256) {
     if (p.ap_y)

@@ -1212,7 +1212,8 @@ def test_unstored_apply_and_wgrad_apply(cuda, dt):
 
 def test_wgrad_dma_kernel_bitwise(cuda):
     """1x1 stride-1 bf16 weight gradients on the LDS-DMA ring kernel (policy key 45, conv_wgdma.hip:
-    1 = 128 x 128 tiles, 2 = 128 x 256 where Cin % 256 == 0) vs the register-staged wgrad_kernel
+    1 = 128 x 128 tiles, 2 / 3 = 128 x 256 where Cin % 256 == 0 with the apply / always) vs the
+    register-staged wgrad_kernel
     (key 45 = 0), plain and with the BN-backward apply staged
     from dm (argus_conv_wgrad_apply): dW bit-identical (same apply formula, same MFMA order over
     32-pixel blocks, same splits). Pixel counts that end mid k-step (ragged last split: zero-page
@@ -1234,7 +1235,7 @@ def test_wgrad_dma_kernel_bitwise(cuda):
             ca, cb, cc = (torch.randn(cout, device=cuda) * 0.3 for _ in range(3))
             for apply in (False, True):
                 outs = []
-                for key in (2, 1, 0):
+                for key in (3, 2, 1, 0):
                     d, _ = _desc(n, hh, ww, cin, cout, 1, 1)
                     d = d.with_tuning({**tune, 45: key})
                     wsb = L.dll.argus_conv_wgrad_workspace_bytes(C.byref(d), BF16)
@@ -1251,11 +1252,12 @@ def test_wgrad_dma_kernel_bitwise(cuda):
                     assert rc in (0, None), L.dll.argus_last_error()
                     torch.cuda.synchronize()
                     ks = list(t.summary())
-                    want = 0 if not key else (256 if key == 2 and cin % 256 == 0 else 128)
+                    wide = key == 3 or (key == 2 and apply)
+                    want = 0 if not key else (256 if wide and cin % 256 == 0 else 128)
                     assert len(ks) == (1 if key else 0) and (not key or ks[0].endswith(", %d>" % want)), \
                         ("dma kernel use", cin, cout, hh, ww, n, key, ks)
                     outs.append(dw.cpu())
-                assert torch.equal(outs[0], outs[2]) and torch.equal(outs[1], outs[2]), \
+                assert all(torch.equal(o, outs[-1]) for o in outs[:-1]), \
                     (cin, cout, hh, ww, n, target, apply)
                 dy = dm.double()
                 if apply:
