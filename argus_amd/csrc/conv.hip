@@ -1812,7 +1812,8 @@ struct WgPlan {
   int N;
 };
 
-static WgPlan wgrad_plan(const argus_conv_desc& d, int dtype) {
+// ap: the BN-backward-apply form (argus_conv_wgrad_apply), which may pick another DMA tile width
+static WgPlan wgrad_plan(const argus_conv_desc& d, int dtype, bool ap = false) {
   const Policy pol = policy_of(d);
   WgPlan pl;
   pl.N = d.stem ? 256 : d.r * d.s * d.c;
@@ -1823,7 +1824,10 @@ static WgPlan wgrad_plan(const argus_conv_desc& d, int dtype) {
   pl.nt = pl.N / pl.bn;
   pl.kstep = dtype == ARGUS_BF16 ? 64 : 32;
   const long P = (long)d.n * d.ho * d.wo;
-  const long tiles = (long)pl.mt * pl.nt;
+  // the plain 128 x 256 DMA kernel runs two workgroups per CU: the target counts its wider tiles (the
+  // apply form's runs one per CU, so the 128 x 128 count, i.e. half the grid, is its target)
+  const bool wide2 = !ap && wgrad_dma_width(d, dtype, pl.bm, pl.bn, pol[kWgradDma], false) == 256;
+  const long tiles = (long)pl.mt * (wide2 ? pl.nt / 2 : pl.nt);
   // measured (tools/tilesweep.py, MI355X): 1x1 convs peak near 512 workgroups, 3x3 near 1024
   // (2048 when Cout = 64: one row tile, 9 column tiles)
   long target = pol[kWgradTarget];
@@ -1844,8 +1848,8 @@ static WgPlan wgrad_plan(const argus_conv_desc& d, int dtype) {
 
 size_t conv_wgrad_ws(const argus_conv_desc& d, int dtype) {
   if (check_desc(d)) return 0;
-  const WgPlan pl = wgrad_plan(d, dtype);
-  size_t b = (size_t)pl.splits * d.k * pl.N * sizeof(float);
+  const WgPlan pl = wgrad_plan(d, dtype), pla = wgrad_plan(d, dtype, true);
+  size_t b = (size_t)(pl.splits > pla.splits ? pl.splits : pla.splits) * d.k * pl.N * sizeof(float);
   int hs, htps;
   if (stem_wgrad_plan(d, dtype, &hs, &htps)) {
     const size_t sb = (size_t)hs * 64 * 256 * sizeof(float);
@@ -1912,7 +1916,7 @@ static int conv_wgrad_impl(const argus_conv_desc& d, int dtype, const void* x, c
   if (int e = check_desc(d)) return e;
   const Policy pol = policy_of(d);
   g_launch_work = 2.0 * d.n * d.ho * d.wo * d.k * d.r * d.s * d.c;  // algorithmic flops / bytes (ktimer)
-  const WgPlan pl = wgrad_plan(d, dtype);
+  const WgPlan pl = wgrad_plan(d, dtype, ap != nullptr);
   // algorithmic bytes: x + dy read once, the fp32 dW written once (the split partials and their
   // reduction are this implementation's overhead, visible in the PMC traffic, not algorithmic work)
   g_launch_bytes = (double)(dtype == ARGUS_BF16 ? 2 : 4) *

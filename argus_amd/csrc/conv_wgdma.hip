@@ -73,11 +73,11 @@ template <int K, int D> ARGUS_DEV void wg_wait_after(int after) {
 constexpr int kWgdBK = 32;  // pixels per k-step
 
 // Tiles of 128 rows (output channels) x BN columns (input channels): BN = 128 with 256 threads, two
-// workgroups per CU; BN = 256 with 512 threads, one per CU (the wider tile reads the A side, dm and
+// workgroups per CU; BN = 256 with 512 threads, one per CU with the apply, two without (the wider tile reads the A side, dm and
 // y, once for 256 columns: 16 instead of 24 KB per 128 x 128 x 32 block with the apply, 12 instead of
 // 16 without). Per stage: images A (dm / dy) [, Y] of 32 rows x 256 B and B (x) of 32 rows x 2 BN B.
 template <bool AP, int BN>
-__global__ __launch_bounds__(2 * BN, BN == 256 ? 1 : 2) void wgrad_dma_kernel(const WgParams p) {
+__global__ __launch_bounds__(2 * BN, BN == 256 && AP ? 1 : 2) void wgrad_dma_kernel(const WgParams p) {
   constexpr int NT = 2 * BN, NW = NT / 64;
   constexpr int AIMG = kWgdBK * 256, BIMG = kWgdBK * BN * 2;
   constexpr int BOFF = AP ? 2 * AIMG : AIMG;   // B image offset in a stage
@@ -86,8 +86,8 @@ __global__ __launch_bounds__(2 * BN, BN == 256 ? 1 : 2) void wgrad_dma_kernel(co
   constexpr int BPW = 2;                       // 1 KB B pieces per wave
   constexpr int LPR = BN / 8;                  // lanes per B row (16-byte chunks)
   constexpr int D = APW * (AP ? 2 : 1) + BPW;  // DMAs per wave per stage
-  // ring stages: 72 / 64 KB (two workgroups per CU) at BN = 128, 128 / 144 KB at BN = 256
-  constexpr int NS = BN == 256 ? (AP ? 4 : 6) : (AP ? 3 : 4);
+  // ring stages: 72 / 64 KB (two workgroups per CU) at BN = 128; 128 KB (one) / 72 KB (two) at BN = 256
+  constexpr int NS = BN == 256 ? (AP ? 4 : 3) : (AP ? 3 : 4);
   static_assert(NS >= 3 && BPW * NW * 1024 == BIMG && APW * NW * 1024 == AIMG, "wgrad_dma geometry");
   __shared__ __attribute__((aligned(1024))) u32x4 lds[NS * STAGE / 16];
   const uint32_t lds0 = (uint32_t)(uintptr_t)lds;
@@ -245,9 +245,10 @@ __global__ __launch_bounds__(2 * BN, BN == 256 ? 1 : 2) void wgrad_dma_kernel(co
 
 // the column-tile width wgrad_dma_launch uses for d under key 45 (0: not served): 256 with the apply
 // (key 2) or always (key 3) where Cin % 256 == 0. Measured alone (tools/wgbench.py, B=64, the 12
-// 1x1 stride-1 shapes): apply 785 / 815 us (256 / 128 wide), plain 592 / 562 us: the plain kernel
-// at one workgroup per CU stalls at its per-k-step barrier with no second workgroup to fill it
-static int wgrad_dma_bn(const argus_conv_desc& d, int dtype, int bm, int bn, int key, bool ap) {
+// 1x1 stride-1 shapes): apply 785 / 815 us (256 / 128 wide), plain 592 / 562 us with the plain
+// 256-wide kernel at one workgroup per CU (stalled at its per-k-step barrier with no second workgroup
+// to fill it); now two per CU (128 VGPRs, 3 stages) over a grid planned for its tile count
+int wgrad_dma_width(const argus_conv_desc& d, int dtype, int bm, int bn, int key, bool ap) {
   if (!key || dtype != ARGUS_BF16 || d.stem || d.r != 1 || d.s != 1 || d.stride != 1 || d.pad != 0 ||
       d.h != d.ho || d.w != d.wo || bm != 128 || bn != 128 || d.k % 128 || d.c % 128)
     return 0;
@@ -255,12 +256,12 @@ static int wgrad_dma_bn(const argus_conv_desc& d, int dtype, int bm, int bn, int
 }
 
 bool wgrad_dma_ok(const argus_conv_desc& d, int dtype, int bm, int bn, int enabled) {
-  return wgrad_dma_bn(d, dtype, bm, bn, enabled, false) != 0;
+  return wgrad_dma_width(d, dtype, bm, bn, enabled, false) != 0;
 }
 
 // grid: the 128 x 128 tiles x splits of the plan; 256-wide tiles take two of its column tiles
 void wgrad_dma_launch(const argus_conv_desc& d, const WgParams& p, int key, int splits, hipStream_t st) {
-  const int bn = wgrad_dma_bn(d, ARGUS_BF16, 128, 128, key, p.ap_y != nullptr);
+  const int bn = wgrad_dma_width(d, ARGUS_BF16, 128, 128, key, p.ap_y != nullptr);
   const int grid = (p.M / 128) * (p.N / bn) * splits;
   if (bn == 256) {
     if (p.ap_y)

@@ -1,6 +1,7 @@
 """1x1 weight-gradient microbenchmark (dev tool, GPU): every distinct 1x1 stride-1 ResNet-50 conv at a
 given batch, plain (argus_conv_wgrad) and with the BN-backward apply staged (argus_conv_wgrad_apply),
-under policy key 45 = 2 / 1 (LDS-DMA ring kernel, 256- / 128-wide tiles) and 0 (register-staged wgrad_kernel), timed in
+under policy key 45 = 3 / 2 / 1 (LDS-DMA ring kernel; 3: 256-wide tiles for both forms, 2: for the
+apply form, 1: 128-wide) and 0 (register-staged wgrad_kernel), timed in
 isolation with HIP events. python tools/wgbench.py [--batch 64] [--hw 256 256]"""
 import argparse
 import ctypes as C
@@ -39,7 +40,7 @@ def main():
         dw = torch.empty(d0.k * d0.c, device=dev)
         cols = []
         for apply in (False, True):
-            for k45 in (2, 1, 0):
+            for k45 in (3, 2, 1, 0):
                 d = d0.with_tuning({45: k45})
                 wsb = L.dll.argus_conv_wgrad_workspace_bytes(C.byref(d), BF16)
                 ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
