@@ -1257,7 +1257,10 @@ def test_wgrad_dma_kernel_bitwise(cuda):
                     assert len(ks) == (1 if key else 0) and (not key or ks[0].endswith(", %d>" % want)), \
                         ("dma kernel use", cin, cout, hh, ww, n, key, ks)
                     outs.append(dw.cpu())
-                assert all(torch.equal(o, outs[-1]) for o in outs[:-1]), \
+                # key 3 plain on 256-wide tiles plans its splits for two workgroups per CU over half the
+                # tiles: another split grouping, so another fp32 summation order (checked against fp64)
+                resplit = not apply and cin % 256 == 0
+                assert all(torch.equal(o, outs[-1]) for o in outs[1 if resplit else 0:-1]), \
                     (cin, cout, hh, ww, n, target, apply)
                 dy = dm.double()
                 if apply:
@@ -1265,7 +1268,8 @@ def test_wgrad_dma_kernel_bitwise(cuda):
                     dy = dy.float().to(torch.bfloat16).double()
                 ref = torch.einsum("pk,pc->kc", dy.reshape(-1, cout), x.double().reshape(-1, cin)).cpu()
                 tol = 1e-3 if apply else 1e-4  # fp32 accumulation of exact bf16 products (+ the bf16 dy rounding)
-                assert _rel(outs[0].reshape(cout, cin), ref) < tol, (cin, cout, apply)
+                for o in (outs[0], outs[-1]):
+                    assert _rel(o.reshape(cout, cin), ref) < tol, (cin, cout, apply)
                 ran += 1
     assert ran == 36
 

@@ -1,6 +1,6 @@
 """Build-time ISA check of the inline-asm transposed LDS reads (CPU: hipcc cross-compiles gfx950).
 
-conv_halo.hip's weight-gradient kernel issues its ds_read_b64_tr_b16 reads as inline asm (the builtin
+conv_halo.hip's and conv_wgdma.hip's weight-gradient kernels issue their ds_read_b64_tr_b16 reads as inline asm (the builtin
 made the compiler drain the global->LDS ring before every k-step) and waits for their
 data with a separate ``s_waitcnt lgkmcnt(0)`` asm statement. The compiler's waitcnt pass does not see
 those reads, so nothing but register allocation keeps an instruction from touching a destination
@@ -19,7 +19,7 @@ import pytest
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 
-ASM_SOURCES = ["conv_halo.hip"]  # the sources with inline-asm LDS reads
+ASM_SOURCES = ["conv_halo.hip", "conv_wgdma.hip"]  # the sources with inline-asm LDS reads
 
 
 def _vregs(text):
