@@ -207,8 +207,11 @@ static EwGeom ew_geom(int C, int E, int64_t pixels, int target_blocks) {
 
 // Every elementwise kernel below walks its pixels U at a time: the U iterations' loads are issued
 // before any of their arithmetic or stores, so each thread keeps U x (tensors read) 16-byte loads in
-// flight (the memory-level parallelism an HBM stream needs at 4-8 waves per SIMD).
-constexpr int kEwU = 4;
+// flight (the memory-level parallelism an HBM stream needs at 4-8 waves per SIMD). U = 8 over 4:
+// B=64 13.62-13.66 vs 13.67-13.75 ms in three interleaved rounds, B=256 level (no spills; the bf16
+// BN-backward apply at 226 VGPRs, two workgroups per CU as the grid targets; profiles/r05an_*).
+// A grid target of 1024 instead of 512 blocks was slower (13.70-13.77 ms, B=256 +0.7 %).
+constexpr int kEwU = 8;
 
 // MX-fp8 copy of a stored bf16 chunk (element offset off of a [P][C] tensor): 8 e4m3 bytes at out8 + off
 // and, by the first of the 4 lanes of each 32-channel block (chunk cc % 4 == 0), its E8M0 scale at
