@@ -1303,6 +1303,11 @@ static const Policy kDefaultPolicy = [] {
   //     register-staged wgrad_kernel (0): engine A/B 2 vs 0: B=256 46.05-46.21 vs 46.54-46.57 ms,
   //     376x672 89.6-89.9 vs 90.6-91.2 ms, B=64 within drift (profiles/r05ai_ab_key45_*.txt)
   p.v[kWgradDma] = 2;
+  // 46: 1x1 weight gradients over at most this many pixels take half the split target (256): engine
+  //     A/B at B=64 (layers 2-4) 13.69-13.74 vs 13.79-13.85 ms, B=256 (layers 3-4) 46.95-47.01 vs
+  //     47.02-47.07, 376x672 (layer 4) within drift; 262144 no better; a global target of 256 gains
+  //     at B=64 but costs 376x672 0.7 % (profiles/r05ap_*, r05ar_*)
+  p.v[kWgradSmallP] = 65536;
   return p;
 }();
 
@@ -1832,6 +1837,9 @@ static WgPlan wgrad_plan(const argus_conv_desc& d, int dtype, bool ap = false) {
   // (2048 when Cout = 64: one row tile, 9 column tiles)
   long target = pol[kWgradTarget];
   if (target == 512 && d.r == 3) target = d.k <= 64 ? 2048 : pol[kWgradTarget3x3];
+  // key 46: 1x1 weight gradients over few pixels take half the split target: the side stream then
+  // holds fewer CUs beside the main stream's chain, and writes half the split partials
+  if (target == 512 && d.r == 1 && P <= pol[kWgradSmallP]) target = 256;
   // the grid (tiles x splits) stays within the target: a grid just past it (e.g. 36 tiles x 15 splits
   // = 540 for 512 two-per-CU slots) runs a second, nearly empty round of workgroups
   long splits = target / tiles;

@@ -57,7 +57,8 @@ enum TuneKey : int {
   kP1x1Dgrad = 43,        // the persistent 1x1 dgrad (apply prologue + mask-bits BN epilogue) for conv1 (1 on)
   kP1x1FwdStats = 44,     // statistics-only 1x1 forwards on the persistent kernel (conv_p1x1.hip; 1 on)
   kWgradDma = 45,         // 1x1 bf16 weight gradients on the LDS-DMA ring kernel (conv_wgdma.hip)
-  kNumTuneKeys = 46
+  kWgradSmallP = 46,      // 1x1 weight gradients over at most this many pixels: half the split target
+  kNumTuneKeys = 47
 };
 struct Policy {
   int v[kNumTuneKeys];
