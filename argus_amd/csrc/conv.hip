@@ -1308,6 +1308,8 @@ static const Policy kDefaultPolicy = [] {
   //     47.02-47.07, 376x672 (layer 4) within drift; 262144 no better; a global target of 256 gains
   //     at B=64 but costs 376x672 0.7 % (profiles/r05ap_*, r05ar_*)
   p.v[kWgradSmallP] = 65536;
+  // 47: the stride-2 plain weight gradients (1x1 downsample, 3x3 conv2) on the gathering DMA kernel
+  p.v[kWgradDmaGather] = 0;
   return p;
 }();
 
@@ -1831,7 +1833,7 @@ static WgPlan wgrad_plan(const argus_conv_desc& d, int dtype, bool ap = false) {
   const long P = (long)d.n * d.ho * d.wo;
   // the plain 128 x 256 DMA kernel runs two workgroups per CU: the target counts its wider tiles (the
   // apply form's runs one per CU, so the 128 x 128 count, i.e. half the grid, is its target)
-  const bool wide2 = !ap && wgrad_dma_width(d, dtype, pl.bm, pl.bn, pol[kWgradDma], false) == 256;
+  const bool wide2 = !ap && wgrad_dma_width(d, dtype, pl.bm, pl.bn, pol[kWgradDma], false, pol[kWgradDmaGather]) == 256;
   const long tiles = (long)pl.mt * (wide2 ? pl.nt / 2 : pl.nt);
   // measured (tools/tilesweep.py, MI355X): 1x1 convs peak near 512 workgroups, 3x3 near 1024
   // (2048 when Cout = 64: one row tile, 9 column tiles)
@@ -1951,8 +1953,8 @@ static int conv_wgrad_impl(const argus_conv_desc& d, int dtype, const void* x, c
   int splits = pl.splits;
   if (d.stem && pol[kStemLdsWgrad] && stem_wgrad_launch(d, dtype, x, dy, ap, ws, ws_bytes, &splits, st)) {
     if (int e = check_launch("stem_wgrad_kernel")) return e;
-  } else if (!sc && wgrad_dma_ok(d, dtype, pl.bm, pl.bn, pol[kWgradDma])) {  // 1x1: LDS-DMA ring
-    wgrad_dma_launch(d, p, pol[kWgradDma], pl.splits, st);
+  } else if (!sc && wgrad_dma_ok(d, dtype, pl.bm, pl.bn, pol[kWgradDma], ap != nullptr, pol[kWgradDmaGather])) {
+    wgrad_dma_launch(d, p, pol[kWgradDma], pol[kWgradDmaGather], pl.splits, st);  // LDS-DMA ring
     if (int e = check_launch("wgrad_dma_kernel")) return e;
   } else if (ap) {  // the register-staged kernel stages the apply; no halo / glds variant does
     if (dtype == ARGUS_BF16) dispatch_wg<bf16>(p, pl, st);

@@ -76,8 +76,13 @@ constexpr int kWgdBK = 32;  // pixels per k-step
 // workgroups per CU; BN = 256 with 512 threads, one per CU with the apply, two without (the wider tile reads the A side, dm and
 // y, once for 256 columns: 16 instead of 24 KB per 128 x 128 x 32 block with the apply, 12 instead of
 // 16 without). Per stage: images A (dm / dy) [, Y] of 32 rows x 256 B and B (x) of 32 rows x 2 BN B.
-template <bool AP, int BN>
+//
+// G (gather, plain form, BN = 128): the x rows of a k-step are gathered per pixel for strided or 3x3
+// filters (N = taps x Cin, Cin % 128 == 0: a column tile lies in one tap); rows outside the image
+// read the zero page, as the register-staged kernel zeroes them.
+template <bool AP, int BN, bool G = false>
 __global__ __launch_bounds__(2 * BN, BN == 256 && AP ? 1 : 2) void wgrad_dma_kernel(const WgParams p) {
+  static_assert(!G || (!AP && BN == 128), "gather: plain 128-wide tiles");
   constexpr int NT = 2 * BN, NW = NT / 64;
   constexpr int AIMG = kWgdBK * 256, BIMG = kWgdBK * BN * 2;
   constexpr int BOFF = AP ? 2 * AIMG : AIMG;   // B image offset in a stage
@@ -131,6 +136,15 @@ __global__ __launch_bounds__(2 * BN, BN == 256 && AP ? 1 : 2) void wgrad_dma_ker
   const char* zero = reinterpret_cast<const char*>(wgdma_zero_page);
   const long dz = reinterpret_cast<const char*>(DY) - zero, yz = reinterpret_cast<const char*>(Y) - zero,
              xz = reinterpret_cast<const char*>(X) - zero;
+  // G: this column tile's tap and first channel
+  int tap_r = 0, tap_s = 0, ci0 = nt * BN;
+  if constexpr (G) {
+    const int t = (nt * BN) / p.Cin;
+    ci0 = nt * BN - t * p.Cin;
+    tap_r = t / p.S;
+    tap_s = t - tap_r * p.S;
+  }
+  const int HWo = p.Ho * p.Wo;
   auto issue = [&](int kt) {
     const uint32_t sb = lds0 + (kt % NS) * STAGE;
     const int pk = pbeg + kt * kWgdBK;
@@ -146,8 +160,20 @@ __global__ __launch_bounds__(2 * BN, BN == 256 && AP ? 1 : 2) void wgrad_dma_ker
 #pragma unroll
     for (int j = 0; j < BPW; ++j) {
       const int pix = pk + brow[j];
-      const bool ok = pix < pend;
-      const long x_off = 2 * ((long)pix * p.lda + nt * BN + bch[j]);
+      bool ok = pix < pend;
+      long x_off;
+      if constexpr (G) {
+        const int pp = ok ? pix : pbeg;
+        const int nimg = fdiv(pp, p.fd_hw);
+        const int rem = pp - nimg * HWo;
+        const int oh = fdiv(rem, p.fd_w);
+        const int ow = rem - oh * p.Wo;
+        const int ih = oh * p.stride - p.pad + tap_r, iw = ow * p.stride - p.pad + tap_s;
+        ok = ok && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+        x_off = 2 * ((long)((nimg * p.H + ih) * p.W + iw) * p.lda + ci0 + bch[j]);
+      } else {
+        x_off = 2 * ((long)pix * p.lda + ci0 + bch[j]);
+      }
       wg_gl16(zero + (ok ? xz + x_off : 0), sb + BOFF + (BPW * wave + j) * 1024);
     }
   };
@@ -248,22 +274,33 @@ __global__ __launch_bounds__(2 * BN, BN == 256 && AP ? 1 : 2) void wgrad_dma_ker
 // 1x1 stride-1 shapes): apply 785 / 815 us (256 / 128 wide), plain 592 / 562 us with the plain
 // 256-wide kernel at one workgroup per CU (stalled at its per-k-step barrier with no second workgroup
 // to fill it); now two per CU (128 VGPRs, 3 stages) over a grid planned for its tile count
-int wgrad_dma_width(const argus_conv_desc& d, int dtype, int bm, int bn, int key, bool ap) {
-  if (!key || dtype != ARGUS_BF16 || d.stem || d.r != 1 || d.s != 1 || d.stride != 1 || d.pad != 0 ||
-      d.h != d.ho || d.w != d.wo || bm != 128 || bn != 128 || d.k % 128 || d.c % 128)
-    return 0;
+// the strided (1x1 / 3x3 stride 2) weight gradients in the plain form gather their x rows (key 47)
+static bool wgrad_dma_gather(const argus_conv_desc& d) { return d.stride != 1 || d.r != 1; }
+
+int wgrad_dma_width(const argus_conv_desc& d, int dtype, int bm, int bn, int key, bool ap, int gather_key) {
+  if (!key || dtype != ARGUS_BF16 || d.stem || bm != 128 || bn != 128 || d.k % 128 || d.c % 128) return 0;
+  if (wgrad_dma_gather(d)) {  // 3x3 stride 1 stays on the halo / register-staged kernels
+    const bool g = gather_key && !ap && d.stride == 2 && d.r == d.s && (d.r == 1 || d.r == 3) &&
+                   d.pad == (d.r - 1) / 2;
+    return g ? 128 : 0;
+  }
+  if (d.pad != 0 || d.h != d.ho || d.w != d.wo) return 0;
   return ((key == 2 && ap) || key >= 3) && d.c % 256 == 0 ? 256 : 128;
 }
 
-bool wgrad_dma_ok(const argus_conv_desc& d, int dtype, int bm, int bn, int enabled) {
-  return wgrad_dma_width(d, dtype, bm, bn, enabled, false) != 0;
+bool wgrad_dma_ok(const argus_conv_desc& d, int dtype, int bm, int bn, int enabled, bool ap, int gather_key) {
+  return wgrad_dma_width(d, dtype, bm, bn, enabled, ap, gather_key) != 0;
 }
 
 // grid: the 128 x 128 tiles x splits of the plan; 256-wide tiles take two of its column tiles
-void wgrad_dma_launch(const argus_conv_desc& d, const WgParams& p, int key, int splits, hipStream_t st) {
-  const int bn = wgrad_dma_width(d, ARGUS_BF16, 128, 128, key, p.ap_y != nullptr);
+void wgrad_dma_launch(const argus_conv_desc& d, const WgParams& p, int key, int gather_key, int splits,
+                      hipStream_t st) {
+  const int bn = wgrad_dma_width(d, ARGUS_BF16, 128, 128, key, p.ap_y != nullptr, gather_key);
   const int grid = (p.M / 128) * (p.N / bn) * splits;
-  if (bn == 256) {
+  if (wgrad_dma_gather(d)) {
+    timed_launch("argus::wgrad_dma_kernel<false, 128, gather>", wgrad_dma_kernel<false, 128, true>, dim3(grid),
+                 dim3(256), st, p);
+  } else if (bn == 256) {
     if (p.ap_y)
       timed_launch("argus::wgrad_dma_kernel<true, 256>", wgrad_dma_kernel<true, 256>, dim3(grid), dim3(512), st, p);
     else

@@ -244,7 +244,8 @@ int argus_conv_dgrad_bn_x8(const argus_conv_desc* d, const void* dy8, const void
  * statistics-only 1x1 forwards on the persistent kernel (1) or the igemm (0), key 45 the 1x1 bf16
  * weight gradients on the LDS-DMA ring kernel with 128 x 128 tiles (1), 128 x 256 tiles where
  * Cin % 256 == 0 for the BN-backward-apply form (2) or both forms (3), or the register-staged one (0);
- * key 46 the pixel count up to which 1x1 weight gradients take half the split target (key 6).
+ * key 46 the pixel count up to which 1x1 weight gradients take half the split target (key 6); key 47
+ * the stride-2 plain bf16 weight gradients (1x1, 3x3) on the DMA kernel with gathered x rows (1) or not (0).
  * (Keys scaled with the batch keep a smaller batch's kernel selection that of the larger one:
  * tests/test_gpu_parity.py stage-checks the benched configurations' kernels that way.) */
 int argus_conv_policy_default(int key);

@@ -50,7 +50,7 @@ def test_bad_arguments_are_reported():
     assert L.dll.argus_conv_policy_default(99) == -1 and L.dll.argus_conv_policy_default(20) == -1
     assert L.dll.argus_conv_policy_default(35) == 16384 and L.dll.argus_conv_policy_default(7) == 1024
     assert 0 <= L.dll.argus_conv_policy_default(37) <= 15
-    assert L.dll.argus_conv_policy_default(45) in (0, 1, 2, 3) and L.dll.argus_conv_policy_default(47) == -1
+    assert L.dll.argus_conv_policy_default(45) in (0, 1, 2, 3) and L.dll.argus_conv_policy_default(48) == -1
     forced = good.with_tuning({1: 128, 4: 64})  # dgrad row / column tiles
     assert L.dll.argus_conv_launch_info(C.byref(forced), 1, 1, None) % 1000000 == 128 * 1000 + 64
     assert L.dll.argus_conv_launch_info(C.byref(good), 1, 1, None) % 1000000 == 64 * 1000 + 64

@@ -1274,6 +1274,43 @@ def test_wgrad_dma_kernel_bitwise(cuda):
     assert ran == 36
 
 
+def test_wgrad_dma_gather_stride2_bitwise(cuda):
+    """Stride-2 bf16 weight gradients (1x1 downsample, 3x3 pad 1) on the gathering LDS-DMA kernel
+    (policy key 47) vs the register-staged wgrad_kernel (key 47 = 0): dW bit-identical (same MFMA
+    order, same splits; rows outside the image read the zero page where the register-staged kernel
+    zeroes them). Odd and ragged frames, split targets 4 / default / 2048, and dW against a float64
+    torch reference."""
+    from argus_amd.profiling import KernelTimer
+
+    torch.manual_seed(47)
+    L = lib()
+    ran = 0
+    for cin, cout, k, hh, ww, n in [(128, 128, 3, 16, 16, 2), (256, 512, 1, 15, 9, 2), (128, 256, 3, 13, 7, 3),
+                                    (512, 128, 3, 8, 8, 1), (1024, 256, 1, 12, 21, 1)]:
+        for target in (None, 4, 2048):
+            tune = {} if target is None else {6: target}
+            d0, _ = _desc(n, hh, ww, cin, cout, k, 2)
+            x = torch.randn(n, hh, ww, cin, device=cuda).to(torch.bfloat16)
+            dy = torch.randn(n, d0.ho, d0.wo, cout, device=cuda).to(torch.bfloat16)
+            outs = []
+            for key in (1, 0):
+                d = d0.with_tuning({**tune, 47: key})
+                wsb = L.dll.argus_conv_wgrad_workspace_bytes(C.byref(d), BF16)
+                ws = torch.empty(wsb, dtype=torch.uint8, device=cuda)
+                dw = torch.empty(cout, k, k, cin, device=cuda)
+                with KernelTimer("argus::wgrad_dma_kernel<false, 128, gather>") as t:
+                    L.conv_wgrad(C.byref(d), BF16, ptr(x), None, None, ptr(dy), ptr(dw), ptr(ws), wsb, stream())
+                torch.cuda.synchronize()
+                assert len(t.summary()) == key, ("gather kernel use", cin, cout, k, hh, ww, n, key)
+                outs.append(dw.cpu())
+            assert torch.equal(outs[0], outs[1]), (cin, cout, k, hh, ww, n, target)
+            ref = torch.nn.grad.conv2d_weight(x.permute(0, 3, 1, 2).double().cpu(), (cout, cin, k, k),
+                                              dy.permute(0, 3, 1, 2).double().cpu(), stride=2, padding=(k - 1) // 2)
+            assert _rel(outs[0].permute(0, 3, 1, 2), ref) < 1e-4, (cin, cout, k, hh, ww, n)
+            ran += 1
+    assert ran == 15
+
+
 @pytest.mark.parametrize("dt", ["fp32", "bf16"])
 def test_stem_backward_fusions(cuda, dt):
     """argus_maxpool_bwd_bn (maxpool backward + the stem BN's backward reduction) against
