@@ -1308,8 +1308,9 @@ static const Policy kDefaultPolicy = [] {
   //     47.02-47.07, 376x672 (layer 4) within drift; 262144 no better; a global target of 256 gains
   //     at B=64 but costs 376x672 0.7 % (profiles/r05ap_*, r05ar_*)
   p.v[kWgradSmallP] = 65536;
-  // 47: the stride-2 plain weight gradients (1x1 downsample, 3x3 conv2) on the gathering DMA kernel
-  p.v[kWgradDmaGather] = 0;
+  // 47: the stride-2 plain weight gradients (1x1 downsample, 3x3 conv2) on the gathering DMA kernel:
+  //     engine A/B B=64 13.42-13.46 vs 13.51-13.57 ms, 376x672 within drift (profiles/r05as_*)
+  p.v[kWgradDmaGather] = 1;
   return p;
 }();
 
