@@ -18,7 +18,7 @@ import torch  # noqa: F401  (must precede the CDLL, see module docstring)
 LIB_PATH = Path(os.environ.get("ARGUS_HIP_LIB", Path(__file__).resolve().parent / "libargus_hip.so"))
 
 F32, BF16, FP8 = 0, 1, 2
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 
 class Tuning(C.Structure):
@@ -90,6 +90,7 @@ SIGNATURES = {
     "argus_conv_x8_ok": (_I, [_DESC, _I]),
     "argus_conv_fwd_stats_only_rows": (_I, [_DESC, _I]),
     "argus_conv_fwd_stats_only_tile": (_I, [_DESC, _I]),
+    "argus_conv_fwd_stat_part_bytes": (_SZ, [_DESC, _I, _I]),
     "argus_conv_fwd_apply_out": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "argus_conv_fwd_x8": (_I, [_DESC, _P, _P, _P, _P, _P]),
     "argus_conv_dgrad_bn_x8": (_I, [_DESC, _P, _P, _P, C.POINTER(BnBwdEpilogue), _P]),

@@ -27,7 +27,7 @@ using namespace argus;
 
 extern "C" {
 
-int argus_abi_version(void) { return 16; }
+int argus_abi_version(void) { return 17; }
 
 const char* argus_last_error(void) { return g_last_error.c_str(); }
 
@@ -94,6 +94,14 @@ int argus_conv_fwd_stats_only_rows(const argus_conv_desc* d, int dtype) {
 }
 int argus_conv_fwd_stats_only_tile(const argus_conv_desc* d, int dtype) {
   return d ? conv_fwd_stats_only_tile(*d, dtype) : 0;
+}
+size_t argus_conv_fwd_stat_part_bytes(const argus_conv_desc* d, int dtype, int stats_only) {
+  if (!d || conv_check_desc(*d)) return 0;
+  const int rows = stats_only ? conv_fwd_stats_only_rows(*d, dtype) : conv_fwd_stat_rows(*d, dtype);
+  const int tile = stats_only ? conv_fwd_stats_only_tile(*d, dtype) : conv_fwd_stat_tile(*d, dtype);
+  if (rows <= 0) return 0;
+  // float2 {sum, M2} [rows][k], then int32 pixel counts [rows] when the tiling is ragged (tile < 0)
+  return (size_t)rows * d->k * 2 * sizeof(float) + (tile < 0 ? (size_t)rows * sizeof(int32_t) : 0);
 }
 
 int argus_conv_policy_default(int key) { return policy_default(key); }

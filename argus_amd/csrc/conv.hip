@@ -1308,9 +1308,15 @@ static const Policy kDefaultPolicy = [] {
   //     47.02-47.07, 376x672 (layer 4) within drift; 262144 no better; a global target of 256 gains
   //     at B=64 but costs 376x672 0.7 % (profiles/r05ap_*, r05ar_*)
   p.v[kWgradSmallP] = 65536;
-  // 47: the stride-2 plain weight gradients (1x1 downsample, 3x3 conv2) on the gathering DMA kernel:
-  //     engine A/B B=64 13.42-13.46 vs 13.51-13.57 ms, 376x672 within drift (profiles/r05as_*)
-  p.v[kWgradDmaGather] = 1;
+  // 47: the stride-2 plain weight gradients (1x1 downsample, 3x3 conv2) on the gathering DMA kernel
+  //     (0 off, 1 every size, > 1 up to that many output pixels): engine A/B with every size on, B=64
+  //     13.42-13.46 vs 13.51-13.57 ms, 376x672 within drift (profiles/r05as_*), but B=256 46.56-46.86 vs
+  //     46.43-46.60 ms (r05at_*: its 524,288-pixel layer-2 launches lose); served up to 131,072 pixels:
+  //     B=64 every layer, B=256 layers 3-4, 376x672 B=128 layer 4
+  p.v[kWgradDmaGather] = 131072;
+  // 48: LDS ring stages of the 128 x 256 apply weight gradient (32 KB each; 4 = 128 KB, one workgroup
+  //     per CU; 5 = all 160 KB, one more stage in flight; 2 / 3 leave room for main-stream workgroups)
+  p.v[kWgradDmaStages] = 4;
   return p;
 }();
 
@@ -1955,7 +1961,7 @@ static int conv_wgrad_impl(const argus_conv_desc& d, int dtype, const void* x, c
   if (d.stem && pol[kStemLdsWgrad] && stem_wgrad_launch(d, dtype, x, dy, ap, ws, ws_bytes, &splits, st)) {
     if (int e = check_launch("stem_wgrad_kernel")) return e;
   } else if (!sc && wgrad_dma_ok(d, dtype, pl.bm, pl.bn, pol[kWgradDma], ap != nullptr, pol[kWgradDmaGather])) {
-    wgrad_dma_launch(d, p, pol[kWgradDma], pol[kWgradDmaGather], pl.splits, st);  // LDS-DMA ring
+    wgrad_dma_launch(d, p, pol[kWgradDma], pol[kWgradDmaGather], pl.splits, pol[kWgradDmaStages], st);  // LDS-DMA ring
     if (int e = check_launch("wgrad_dma_kernel")) return e;
   } else if (ap) {  // the register-staged kernel stages the apply; no halo / glds variant does
     if (dtype == ARGUS_BF16) dispatch_wg<bf16>(p, pl, st);

@@ -360,7 +360,7 @@ int conv_dgw(const argus_conv_desc& d, int dtype, const void* dm, const void* wd
     g_launch_work = (yr ? 3.0 : 2.0) * 2.0 * p.P * kKo * kCi;
     g_launch_bytes = 2.0 * ((double)p.P * ((yr ? 1 : 2) * kKo + (addend ? 3 : 2) * kCi)) + 4.0 * kKo * kCi;
     if (yr) timed_launch("argus::dgw1x1_kernel<false, true>", dgw1x1_kernel<false, true>, dim3(G), dim3(256), st, p);
-    else timed_launch("argus::dgw1x1_kernel<false>", dgw1x1_kernel<false, false>, dim3(G), dim3(256), st, p);
+    else timed_launch("argus::dgw1x1_kernel<false, false>", dgw1x1_kernel<false, false>, dim3(G), dim3(256), st, p);
     if (int e = check_launch("dgw1x1_kernel")) return e;
     return wgrad_reduce_launch(reinterpret_cast<const float*>(ws), G, kKo, kCi, 0, dw, st);
   }
@@ -386,7 +386,7 @@ int conv_dgw(const argus_conv_desc& d, int dtype, const void* dm, const void* wd
   g_launch_work = (yr ? 3.0 : 2.0) * 2.0 * p.P * kKo * kCi;
   g_launch_bytes = 2.0 * ((double)p.P * ((yr ? 1 : 2) * kKo + 3 * kCi)) + 4.0 * kKo * kCi;
   if (yr) timed_launch("argus::dgw1x1_kernel<true, true>", dgw1x1_kernel<true, true>, dim3(G), dim3(256), st, p);
-  else timed_launch("argus::dgw1x1_kernel<true>", dgw1x1_kernel<true, false>, dim3(G), dim3(256), st, p);
+  else timed_launch("argus::dgw1x1_kernel<true, false>", dgw1x1_kernel<true, false>, dim3(G), dim3(256), st, p);
   if (int e = check_launch("dgw1x1_kernel")) return e;
   return wgrad_reduce_launch(reinterpret_cast<const float*>(ws), G, kKo, kCi, 0, dw, st);
 }

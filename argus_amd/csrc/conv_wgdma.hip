@@ -80,7 +80,7 @@ constexpr int kWgdBK = 32;  // pixels per k-step
 // G (gather, plain form, BN = 128): the x rows of a k-step are gathered per pixel for strided or 3x3
 // filters (N = taps x Cin, Cin % 128 == 0: a column tile lies in one tap); rows outside the image
 // read the zero page, as the register-staged kernel zeroes them.
-template <bool AP, int BN, bool G = false>
+template <bool AP, int BN, bool G = false, int NSX = 0>
 __global__ __launch_bounds__(2 * BN, BN == 256 && AP ? 1 : 2) void wgrad_dma_kernel(const WgParams p) {
   static_assert(!G || (!AP && BN == 128), "gather: plain 128-wide tiles");
   constexpr int NT = 2 * BN, NW = NT / 64;
@@ -92,8 +92,9 @@ __global__ __launch_bounds__(2 * BN, BN == 256 && AP ? 1 : 2) void wgrad_dma_ker
   constexpr int LPR = BN / 8;                  // lanes per B row (16-byte chunks)
   constexpr int D = APW * (AP ? 2 : 1) + BPW;  // DMAs per wave per stage
   // ring stages: 72 / 64 KB (two workgroups per CU) at BN = 128; 128 KB (one) / 72 KB (two) at BN = 256
-  constexpr int NS = BN == 256 ? (AP ? 4 : 3) : (AP ? 3 : 4);
-  static_assert(NS >= 3 && BPW * NW * 1024 == BIMG && APW * NW * 1024 == AIMG, "wgrad_dma geometry");
+  // NSX: the ring depth of the apply / 256-wide form (policy key 48; 5 stages = all 160 KB of LDS)
+  constexpr int NS = NSX ? NSX : BN == 256 ? (AP ? 4 : 3) : (AP ? 3 : 4);
+  static_assert(NS >= 2 && BPW * NW * 1024 == BIMG && APW * NW * 1024 == AIMG, "wgrad_dma geometry");
   __shared__ __attribute__((aligned(1024))) u32x4 lds[NS * STAGE / 16];
   const uint32_t lds0 = (uint32_t)(uintptr_t)lds;
 
@@ -170,7 +171,7 @@ __global__ __launch_bounds__(2 * BN, BN == 256 && AP ? 1 : 2) void wgrad_dma_ker
         const int ow = rem - oh * p.Wo;
         const int ih = oh * p.stride - p.pad + tap_r, iw = ow * p.stride - p.pad + tap_s;
         ok = ok && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-        x_off = 2 * ((long)((nimg * p.H + ih) * p.W + iw) * p.lda + ci0 + bch[j]);
+        x_off = 2 * ((((long)nimg * p.H + ih) * p.W + iw) * p.lda + ci0 + bch[j]);  // 64-bit pixel index
       } else {
         x_off = 2 * ((long)pix * p.lda + ci0 + bch[j]);
       }
@@ -280,8 +281,9 @@ static bool wgrad_dma_gather(const argus_conv_desc& d) { return d.stride != 1 ||
 int wgrad_dma_width(const argus_conv_desc& d, int dtype, int bm, int bn, int key, bool ap, int gather_key) {
   if (!key || dtype != ARGUS_BF16 || d.stem || bm != 128 || bn != 128 || d.k % 128 || d.c % 128) return 0;
   if (wgrad_dma_gather(d)) {  // 3x3 stride 1 stays on the halo / register-staged kernels
+    // key 47: 0 off, 1 every size, > 1 at most that many output pixels
     const bool g = gather_key && !ap && d.stride == 2 && d.r == d.s && (d.r == 1 || d.r == 3) &&
-                   d.pad == (d.r - 1) / 2;
+                   d.pad == (d.r - 1) / 2 && (gather_key == 1 || (long)d.n * d.ho * d.wo <= gather_key);
     return g ? 128 : 0;
   }
   if (d.pad != 0 || d.h != d.ho || d.w != d.wo) return 0;
@@ -293,23 +295,32 @@ bool wgrad_dma_ok(const argus_conv_desc& d, int dtype, int bm, int bn, int enabl
 }
 
 // grid: the 128 x 128 tiles x splits of the plan; 256-wide tiles take two of its column tiles
-void wgrad_dma_launch(const argus_conv_desc& d, const WgParams& p, int key, int gather_key, int splits,
+void wgrad_dma_launch(const argus_conv_desc& d, const WgParams& p, int key, int gather_key, int splits, int ns,
                       hipStream_t st) {
   const int bn = wgrad_dma_width(d, ARGUS_BF16, 128, 128, key, p.ap_y != nullptr, gather_key);
   const int grid = (p.M / 128) * (p.N / bn) * splits;
   if (wgrad_dma_gather(d)) {
-    timed_launch("argus::wgrad_dma_kernel<false, 128, gather>", wgrad_dma_kernel<false, 128, true>, dim3(grid),
+    timed_launch("argus::wgrad_dma_kernel<false, 128, true, 0>", wgrad_dma_kernel<false, 128, true>, dim3(grid),
                  dim3(256), st, p);
   } else if (bn == 256) {
-    if (p.ap_y)
-      timed_launch("argus::wgrad_dma_kernel<true, 256>", wgrad_dma_kernel<true, 256>, dim3(grid), dim3(512), st, p);
-    else
-      timed_launch("argus::wgrad_dma_kernel<false, 256>", wgrad_dma_kernel<false, 256>, dim3(grid), dim3(512), st, p);
+    if (p.ap_y) {
+      switch (ns) {
+        case 2: timed_launch("argus::wgrad_dma_kernel<true, 256, false, 2>", wgrad_dma_kernel<true, 256, false, 2>,
+                             dim3(grid), dim3(512), st, p); break;
+        case 3: timed_launch("argus::wgrad_dma_kernel<true, 256, false, 3>", wgrad_dma_kernel<true, 256, false, 3>,
+                             dim3(grid), dim3(512), st, p); break;
+        case 5: timed_launch("argus::wgrad_dma_kernel<true, 256, false, 5>", wgrad_dma_kernel<true, 256, false, 5>,
+                             dim3(grid), dim3(512), st, p); break;
+        default: timed_launch("argus::wgrad_dma_kernel<true, 256, false, 0>", wgrad_dma_kernel<true, 256>, dim3(grid),
+                              dim3(512), st, p);
+      }
+    } else
+      timed_launch("argus::wgrad_dma_kernel<false, 256, false, 0>", wgrad_dma_kernel<false, 256>, dim3(grid), dim3(512), st, p);
   } else {
     if (p.ap_y)
-      timed_launch("argus::wgrad_dma_kernel<true, 128>", wgrad_dma_kernel<true, 128>, dim3(grid), dim3(256), st, p);
+      timed_launch("argus::wgrad_dma_kernel<true, 128, false, 0>", wgrad_dma_kernel<true, 128>, dim3(grid), dim3(256), st, p);
     else
-      timed_launch("argus::wgrad_dma_kernel<false, 128>", wgrad_dma_kernel<false, 128>, dim3(grid), dim3(256), st, p);
+      timed_launch("argus::wgrad_dma_kernel<false, 128, false, 0>", wgrad_dma_kernel<false, 128>, dim3(grid), dim3(256), st, p);
   }
 }
 

@@ -316,7 +316,7 @@ int p1x1_fwd_stats_launch(const argus_conv_desc& d, const void* x, const void* w
 bool wgrad_dma_ok(const argus_conv_desc& d, int dtype, int bm, int bn, int enabled, bool ap, int gather_key);
 // its column-tile width (128 / 256) for the plain (ap false) or the apply form; 0 = not served
 int wgrad_dma_width(const argus_conv_desc& d, int dtype, int bm, int bn, int key, bool ap, int gather_key);
-void wgrad_dma_launch(const argus_conv_desc& d, const WgParams& p, int key, int gather_key, int splits,
+void wgrad_dma_launch(const argus_conv_desc& d, const WgParams& p, int key, int gather_key, int splits, int ns,
                       hipStream_t st);
 int p1x1_rows(const argus_conv_desc& d);
 int p1x1_launch(const argus_conv_desc& d, const void* dm, const void* wd, void* out, const void* addend,

@@ -58,8 +58,9 @@ enum TuneKey : int {
   kP1x1FwdStats = 44,     // statistics-only 1x1 forwards on the persistent kernel (conv_p1x1.hip; 1 on)
   kWgradDma = 45,         // 1x1 bf16 weight gradients on the LDS-DMA ring kernel (conv_wgdma.hip)
   kWgradSmallP = 46,      // 1x1 weight gradients over at most this many pixels: half the split target
-  kWgradDmaGather = 47,   // ... and the stride-2 (1x1 / 3x3) plain ones, x rows gathered (1 on)
-  kNumTuneKeys = 48
+  kWgradDmaGather = 47,   // ... and the stride-2 (1x1 / 3x3) plain ones, x rows gathered (1 on, >1 pixel cap)
+  kWgradDmaStages = 48,   // LDS ring stages of the 128 x 256 apply DMA weight gradient (2..5)
+  kNumTuneKeys = 49
 };
 struct Policy {
   int v[kNumTuneKeys];

@@ -65,6 +65,7 @@ class _Conv:
     flops: int  # algorithmic flops of one pass
     so_rows: int  # BN partial rows / tile of a statistics-only forward (y not stored: the fused tail)
     so_tile: int
+    part_bytes: int = 0  # stat_part bytes either forward form needs (argus_conv_fwd_stat_part_bytes)
 
 
 class ResNetEngine:
@@ -218,7 +219,10 @@ class ResNetEngine:
             tags = tuple(L.dll.argus_conv_launch_info(C.byref(d), dt, ps, C.byref(fl)) for ps in range(3))
             so = (L.dll.argus_conv_fwd_stats_only_rows(C.byref(d), BF16),
                   L.dll.argus_conv_fwd_stats_only_tile(C.byref(d), BF16))
-            convs[name] = _Conv(name, d, wf, wd, rows, tile, tags, fl.value, *so)
+            pb = max(L.dll.argus_conv_fwd_stat_part_bytes(C.byref(d), self.cdt, 0),
+                     L.dll.argus_conv_fwd_stat_part_bytes(C.byref(d), dt, 0),
+                     L.dll.argus_conv_fwd_stat_part_bytes(C.byref(d), BF16, 1))
+            convs[name] = _Conv(name, d, wf, wd, rows, tile, tags, fl.value, *so, part_bytes=pb)
             return d.ho, d.wo
 
         H1, W1 = add("resnet.conv1", N, H, W, 3, 64, 7, 2, 3, stem=True)
@@ -288,14 +292,13 @@ class ResNetEngine:
         self.bn_state = {n: self._f(4, c) for n, c in chans.items()}
         self.bn_coef = {n: self._f(3, c) for n, c in chans.items()}
 
-        max_stat = max(max(cv.stat_rows, cv.so_rows) * cv.desc.k for cv in convs.values())
-        # + int32 row counts after the partials of a ragged producer (negative stat tile: the stem, the
-        # persistent statistics-only forward)
-        self.stat_part = self._f(max_stat * 2 + max(max(cv.stat_rows, cv.so_rows) for cv in convs.values()))
+        # sized by the library (argus_conv_fwd_stat_part_bytes): the float2 partials plus the int32 row counts
+        # of a ragged producer (negative stat tile: the stem, the persistent statistics-only forward)
+        self.stat_part = self._f((max(cv.part_bytes for cv in convs.values()) + 3) // 4)
         self.bn_ws = torch.zeros(L.dll.argus_bn_workspace_bytes(2048), dtype=torch.uint8, device=self.device)
         # the downsample branch's own statistics workspaces (it runs on the side stream in forward)
-        ds_stat = max([cv.stat_rows * cv.desc.k for n, cv in convs.items() if ".downsample." in n] or [1])
-        self.stat_part_ds = self._f(ds_stat * 2)
+        self.stat_part_ds = self._f((max([cv.part_bytes for n, cv in convs.items() if ".downsample." in n] or [8])
+                                     + 3) // 4)
         self.bn_ws_ds = torch.zeros(L.dll.argus_bn_workspace_bytes(2048), dtype=torch.uint8, device=self.device)
         max_bwd = 0
         for b, a in zip(self.blocks, act):

@@ -75,36 +75,38 @@ def _config_name(B: int, H: int, W: int, world: int) -> str:
     return f"custom ({H}x{W}, batch {B} per rank)"
 
 
-def pmc_traffic(kernel: str, B: int, H: int, W: int, dtype: str):
-    """HBM bytes per launch of ``kernel`` from the committed PMC summary of this exact workload
-    (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from separate FETCH_SIZE and
-    WRITE_SIZE rocprofv3 passes of this bench command). None when no summary matches."""
-    prof = sorted(Path(__file__).resolve().parent.glob("profiles/*_pmc_traffic.json"))
-    for p in reversed(prof):
+def _newest_summary(pattern: str, B: int, H: int, W: int, dtype: str):
+    """The newest committed PMC summary (profiles/<pattern>) of this exact workload, or None. Only the
+    newest one (by name: rNN<tag>_..., later rounds and tags sort later) is consulted: an older summary
+    is of older code, so a kernel missing from the newest reads None, not an older profile's figure."""
+    for p in sorted(Path(__file__).resolve().parent.glob(f"profiles/{pattern}"), key=lambda p: p.name)[::-1]:
         d = json.loads(p.read_text())
-        if d.get("meta", {}).get("workload") != [B, H, W, dtype]:
-            continue
-        for name, v in d["kernels"].items():
-            if name.startswith(kernel):
-                return round(v["traffic_bytes_per_launch"])
-    return None
+        if d.get("meta", {}).get("workload") == [B, H, W, dtype]:
+            return p, d
+    return None, None
+
+
+def pmc_traffic(kernel: str, B: int, H: int, W: int, dtype: str):
+    """HBM bytes per launch of ``kernel`` (its exact demangled name, which the kernel timer's labels use)
+    from the newest committed PMC summary of this exact workload (profiles/*_pmc_traffic.json, written
+    by tools/pmc_traffic.py from separate FETCH_SIZE and WRITE_SIZE rocprofv3 passes of this bench
+    command). None when that summary lacks the kernel."""
+    _, d = _newest_summary("*_pmc_traffic.json", B, H, W, dtype)
+    v = (d or {}).get("kernels", {}).get(kernel)
+    return round(v["traffic_bytes_per_launch"]) if v else None
 
 
 def pmc_mfma(kernel: str, B: int, H: int, W: int, dtype: str):
     """MFMA-pipe busy fraction of ``kernel`` (SQ_VALU_MFMA_BUSY_CYCLES over 4 SIMD x 256 CU x kernel
     cycles) and its wave-state split, from the newest committed PMC summary of this workload
-    (profiles/*_pmc_mfma_summary.json, tools/prof_pmc.sh). None when no summary matches."""
-    prof = sorted(Path(__file__).resolve().parent.glob("profiles/*_pmc_mfma_summary.json"))
-    for p in reversed(prof):
-        d = json.loads(p.read_text())
-        if d.get("meta", {}).get("workload") != [B, H, W, dtype]:
-            continue
-        for name, v in d["kernels"].items():
-            if name == kernel and "mfma_busy" in v:
-                return {"mfma_busy": round(v["mfma_busy"], 4), "wait_frac": round(v.get("wait_frac", 0), 3),
-                        "issue_stall_frac": round(v.get("issue_stall_frac", 0), 3),
-                        "active_frac": round(v.get("active_frac", 0), 3), "source": p.name}
-    return None
+    (profiles/*_pmc_mfma_summary.json, tools/prof_pmc.sh). None when that summary lacks the kernel."""
+    p, d = _newest_summary("*_pmc_mfma_summary.json", B, H, W, dtype)
+    v = (d or {}).get("kernels", {}).get(kernel)
+    if not v or "mfma_busy" not in v:
+        return None
+    return {"mfma_busy": round(v["mfma_busy"], 4), "wait_frac": round(v.get("wait_frac", 0), 3),
+            "issue_stall_frac": round(v.get("issue_stall_frac", 0), 3),
+            "active_frac": round(v.get("active_frac", 0), 3), "source": p.name}
 
 
 def cpu_model() -> str:
@@ -121,9 +123,9 @@ def cpu_model() -> str:
 def oracle_validation(model, vimg: torch.Tensor, vtgt: torch.Tensor) -> dict:
     """The validation pass of argus/train.py:327-348 (eval mode, running BN statistics, mean SE(3) loss)
     on the held-out batch, by the CPU oracle carrying this model's trained weights and buffers: fp32
-    (the reference's numbers for the same weights) and under the reference's own reduced-precision
-    mode, autocast (train.py:334-337; bf16 on the CPU, the dtype of our path): the distance of the
-    latter from fp32 is the yardstick for ours."""
+    (the reference's numbers for the same weights), under the reference's real --amp mode (fp16 autocast,
+    argus/train.py:298-299,334-335) and under bf16 autocast (the dtype of our path; a yardstick this
+    project chose, not a mode the reference runs)."""
     from oracle import se3
     from oracle.ncamera import build_reference_model
 
@@ -133,8 +135,8 @@ def oracle_validation(model, vimg: torch.Tensor, vtgt: torch.Tensor) -> dict:
     out = {}
     with torch.no_grad():
         x = vimg.cpu().float()
-        for mode in ("fp32", "bf16_autocast"):
-            with torch.autocast("cpu", dtype=torch.bfloat16, enabled=mode != "fp32"):
+        for mode, dt in (("fp32", None), ("fp16_autocast", torch.float16), ("bf16_autocast", torch.bfloat16)):
+            with torch.autocast("cpu", dtype=dt or torch.bfloat16, enabled=dt is not None):
                 pred = ref(x)
             pred = pred.float()
             out[mode] = {"pred": pred, "loss": se3.geometric_loss(pred.double(), vtgt.cpu().double())}
@@ -143,11 +145,26 @@ def oracle_validation(model, vimg: torch.Tensor, vtgt: torch.Tensor) -> dict:
 
 # the stated eval-mode tolerances of the val_vs_oracle check: fp32 within north_star's
 # 1e-4; the reduced-precision paths within 2x (bf16) / 4x (fp8: e4m3 keeps 3 mantissa bits to bf16's 7)
-# the distance of the reference's own bf16 autocast from fp32 (the same bars as
-# tests/test_gpu_parity.py::test_lowp_eval_predictions_at_trained_point), both on max |pred diff| and
-# on max |per-sample loss diff|
+# the distance of the reference model under CPU bf16 autocast from fp32 - a yardstick chosen by this
+# project for a bf16 path (the same bars as tests/test_gpu_parity.py::test_lowp_eval_predictions_at_trained_point),
+# both on max |pred diff| and on max |per-sample loss diff|. The reference's own --amp mode is fp16
+# autocast (argus/train.py:298-299): its distance is reported beside it, with our ratio to it, and an
+# absolute bound VAL_LOWP_ABS caps the relative bar so it cannot only loosen
 VAL_FP32_TOL = 1e-4
 VAL_LOWP_FACTOR = {"bf16": 2.0, "fp8": 4.0}
+VAL_LOWP_ABS = {"bf16": {"pred": 0.25, "per_sample_loss": 0.5}, "fp8": {"pred": 0.5, "per_sample_loss": 1.0}}
+
+
+def cpu_share() -> int:
+    """Threads for the CPU legs: the host's CPU share for one GPU, not the whole machine. The GPU box
+    runs one job per GPU on a shared many-core host (os.cpu_count() reports all of its cores, e.g. 64 on
+    an EPYC 9575F, shared by 8 GPUs' jobs) and exports OMP_NUM_THREADS=16 as this job's share; more
+    threads than the share would time CPU cores other jobs hold."""
+    try:
+        share = int(os.environ.get("OMP_NUM_THREADS", "16"))
+    except ValueError:
+        share = 16
+    return max(1, min(share, 16, os.cpu_count() or 1))
 
 
 def cpu_baseline(batch: int, H: int, W: int, budget_s: float = 15.0) -> dict:
@@ -155,7 +172,7 @@ def cpu_baseline(batch: int, H: int, W: int, budget_s: float = 15.0) -> dict:
     from oracle import se3
     from oracle.ncamera import build_reference_model
 
-    threads = min(16, os.cpu_count() or 1)
+    threads = cpu_share()
     torch.set_num_threads(threads)
     model = build_reference_model(42)
     model.train()
@@ -178,7 +195,9 @@ def cpu_baseline(batch: int, H: int, W: int, budget_s: float = 15.0) -> dict:
         n += 1
     dt = time.perf_counter() - t0
     return {"value": round(2 * batch * n / dt, 3), "unit": "images/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model(),
+            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+            "cores_note": "the job's CPU share for one GPU (OMP_NUM_THREADS, 16 on the GPU box), not the "
+                          "whole host: the other cores belong to the other GPUs' jobs",
             "sample": f"oracle (reference torch.nn ops on CPU) fp32 train step, batch {batch} samples "
                       f"({2 * batch} images) of {H}x{W}, {n} timed steps after 1 warm-up, {dt:.1f} s"}
 
@@ -376,37 +395,46 @@ def main() -> None:
     val_oracle = None
     if rank == 0 and not args.no_val_oracle:
         nv = min(B, args.val_oracle_batch)
-        torch.set_num_threads(min(16, os.cpu_count() or 1))
+        torch.set_num_threads(cpu_share())
         o = oracle_validation(model, vimg[:nv], vtgt[:nv])
-        o32, o16 = o["fp32"], o["bf16_autocast"]
+        o32, o16, oh = o["fp32"], o["bf16_autocast"], o["fp16_autocast"]
         ours = geometric_loss_fn(vpred[:nv], vtgt[:nv]).double().cpu()
         d_pred = (vpred[:nv].float().cpu() - o32["pred"]).abs().max().item()
         d_loss = (ours - o32["loss"]).abs().max().item()
         r_pred = (o16["pred"] - o32["pred"]).abs().max().item()
         r_loss = (o16["loss"] - o32["loss"]).abs().max().item()
+        h_pred = (oh["pred"] - o32["pred"]).abs().max().item()
+        h_loss = (oh["loss"] - o32["loss"]).abs().max().item()
         if args.dtype == "fp32":
             bar_pred = bar_loss = VAL_FP32_TOL
             bar = f"fp32: |pred diff| and |per-sample loss diff| <= {VAL_FP32_TOL:g} (north_star)"
         else:
-            fac = VAL_LOWP_FACTOR[args.dtype]
-            bar_pred, bar_loss = fac * r_pred, fac * r_loss
-            bar = (f"{args.dtype}: <= {fac:g}x the distance of the reference's own bf16 autocast "
-                   f"(argus/train.py:334-337) from fp32, on the same weights and samples")
+            fac, cap = VAL_LOWP_FACTOR[args.dtype], VAL_LOWP_ABS[args.dtype]
+            bar_pred, bar_loss = min(fac * r_pred, cap["pred"]), min(fac * r_loss, cap["per_sample_loss"])
+            bar = (f"{args.dtype}: <= {fac:g}x the distance of the reference model under CPU bf16 autocast from "
+                   f"fp32 (a yardstick chosen by this project for a bf16 path; the reference's own --amp is fp16 "
+                   f"autocast, argus/train.py:298-299, reported beside it), capped at {cap['pred']:g} (pred) / "
+                   f"{cap['per_sample_loss']:g} (per-sample loss), on the same weights and samples")
         val_oracle = {
             "samples": nv,
             "val_loss_gpu": round(ours.mean().item(), 6),
             "val_loss_oracle_fp32": round(o32["loss"].mean().item(), 6),
+            "val_loss_oracle_fp16_autocast": round(oh["loss"].mean().item(), 6),
             "val_loss_oracle_bf16_autocast": round(o16["loss"].mean().item(), 6),
             "val_loss_abs_diff": float(f"{abs(ours.mean().item() - o32['loss'].mean().item()):.3e}"),
             "pred_max_abs_diff": float(f"{d_pred:.3e}"),
             "per_sample_loss_max_abs_diff": float(f"{d_loss:.3e}"),
-            "ref_autocast_pred_max_abs_diff": float(f"{r_pred:.3e}"),
-            "ref_autocast_per_sample_loss_max_abs_diff": float(f"{r_loss:.3e}"),
+            "ref_fp16_autocast_pred_max_abs_diff": float(f"{h_pred:.3e}"),
+            "ref_fp16_autocast_per_sample_loss_max_abs_diff": float(f"{h_loss:.3e}"),
+            "ratio_to_ref_fp16_autocast": {"pred": float(f"{d_pred / max(h_pred, 1e-30):.3g}"),
+                                           "per_sample_loss": float(f"{d_loss / max(h_loss, 1e-30):.3g}")},
+            "ref_bf16_autocast_pred_max_abs_diff": float(f"{r_pred:.3e}"),
+            "ref_bf16_autocast_per_sample_loss_max_abs_diff": float(f"{r_loss:.3e}"),
             "tolerance": {"pred": float(f"{bar_pred:.3e}"), "per_sample_loss": float(f"{bar_loss:.3e}"), "rule": bar},
             "within_tolerance": bool(d_pred <= bar_pred and d_loss <= bar_loss),
             "note": f"eval-mode validation (argus/train.py:327-348) of the trained weights on the first {nv} "
-                    f"held-out samples: {args.dtype} HIP path and the reference under CPU bf16 autocast, each vs "
-                    f"the CPU fp32 oracle with the same weights",
+                    f"held-out samples: the {args.dtype} HIP path, and the reference model under CPU fp16 autocast "
+                    f"(its --amp mode) and bf16 autocast, each vs the CPU fp32 oracle with the same weights",
         }
 
     # the dominant kernel's own MFMA roof: MX-fp8 igemm variants (template flag 32) and the fp8 halo

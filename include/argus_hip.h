@@ -129,6 +129,11 @@ int argus_conv_fwd_stat_tile(const argus_conv_desc* d, int dtype);
  * (negative tile: ragged rows); other convs as argus_conv_fwd_stat_rows / _stat_tile. */
 int argus_conv_fwd_stats_only_rows(const argus_conv_desc* d, int dtype);
 int argus_conv_fwd_stats_only_tile(const argus_conv_desc* d, int dtype);
+/* Bytes a stat_part buffer needs for argus_conv_fwd of d (stats_only = 0) or for its statistics-only
+ * form (y == NULL, stats_only = 1): 2*rows*k floats plus, for a ragged tiling (negative tile), int32
+ * counts[rows] after them (ABI 17). Size every statistics workspace with it; rows*k*2 floats alone is
+ * too small for the ragged stem and the persistent statistics-only forward. 0 for a bad descriptor. */
+size_t argus_conv_fwd_stat_part_bytes(const argus_conv_desc* d, int dtype, int stats_only);
 /* dx = dgrad(dy, w_dgrad) [+ addend]: when addend != NULL (same NHWC layout as dx; may be dx itself
  * for in-place accumulation) it is added, element-wise masked by addend_mask when that is non-NULL
  * (the bn_apply ReLU mask: the residual path of a bottleneck, dx += relu'(out) * dout). */

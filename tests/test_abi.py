@@ -50,7 +50,8 @@ def test_bad_arguments_are_reported():
     assert L.dll.argus_conv_policy_default(99) == -1 and L.dll.argus_conv_policy_default(20) == -1
     assert L.dll.argus_conv_policy_default(35) == 16384 and L.dll.argus_conv_policy_default(7) == 1024
     assert 0 <= L.dll.argus_conv_policy_default(37) <= 15
-    assert L.dll.argus_conv_policy_default(45) in (0, 1, 2, 3) and L.dll.argus_conv_policy_default(48) == -1
+    assert L.dll.argus_conv_policy_default(45) in (0, 1, 2, 3) and L.dll.argus_conv_policy_default(49) == -1
+    assert L.dll.argus_conv_policy_default(48) == 4 and L.dll.argus_conv_policy_default(47) == 131072
     forced = good.with_tuning({1: 128, 4: 64})  # dgrad row / column tiles
     assert L.dll.argus_conv_launch_info(C.byref(forced), 1, 1, None) % 1000000 == 128 * 1000 + 64
     assert L.dll.argus_conv_launch_info(C.byref(good), 1, 1, None) % 1000000 == 64 * 1000 + 64
@@ -72,6 +73,16 @@ def test_bad_arguments_are_reported():
     assert (L.dll.argus_conv_fwd_stats_only_rows(C.byref(so0), 1), L.dll.argus_conv_fwd_stats_only_tile(C.byref(so0), 1)) == \
         (L.dll.argus_conv_fwd_stat_rows(C.byref(so0), 1), L.dll.argus_conv_fwd_stat_tile(C.byref(so0), 1))
     assert L.dll.argus_conv_fwd_stats_only_tile(C.byref(good), 1) == L.dll.argus_conv_fwd_stat_tile(C.byref(good), 1)
+    # stat_part sizing (ABI 17): the ragged layouts need the int32 counts after the float2 partials, so
+    # rows*k*2 floats alone is too small for the persistent statistics-only forward and the ragged stem
+    nb = L.dll.argus_conv_fwd_stat_part_bytes
+    assert nb(C.byref(so), 1, 1) == rows * 256 * 8 + rows * 4
+    r0 = L.dll.argus_conv_fwd_stat_rows(C.byref(so), 1)
+    assert L.dll.argus_conv_fwd_stat_tile(C.byref(so), 1) > 0 and nb(C.byref(so), 1, 0) == r0 * 256 * 8
+    stem = ConvDesc(8, 376, 672, 3, 64, 7, 7, 2, 3, 188, 336, 1)  # 188 x 336 output: ragged 8 x 32 tiles
+    sr, st = L.dll.argus_conv_fwd_stat_rows(C.byref(stem), 1), L.dll.argus_conv_fwd_stat_tile(C.byref(stem), 1)
+    assert st < 0 and nb(C.byref(stem), 1, 0) == sr * 64 * 8 + sr * 4 > sr * 64 * 8
+    assert nb(C.byref(bad), 1, 0) == 0
     unknown = good.with_tuning({30: 1})  # removed key (the 64-channel halo variant is a constant)
     with pytest.raises(ArgusHipError, match="unknown tuning key 30"):
         L.conv_fwd(C.byref(unknown), 1, 16, 16, 16, None, None, None, None)

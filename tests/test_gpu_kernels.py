@@ -1235,9 +1235,10 @@ def test_wgrad_dma_kernel_bitwise(cuda):
             ca, cb, cc = (torch.randn(cout, device=cuda) * 0.3 for _ in range(3))
             for apply in (False, True):
                 outs = []
-                for key in (3, 2, 1, 0):
+                # key 48: the ring depth of the 128 x 256 apply form (2..5 stages; same arithmetic)
+                for key, extra in ((3, {}), (2, {}), (2, {48: 5}), (2, {48: 3}), (2, {48: 2}), (1, {}), (0, {})):
                     d, _ = _desc(n, hh, ww, cin, cout, 1, 1)
-                    d = d.with_tuning({**tune, 45: key})
+                    d = d.with_tuning({**tune, 45: key, **extra})
                     wsb = L.dll.argus_conv_wgrad_workspace_bytes(C.byref(d), BF16)
                     ws = torch.empty(wsb, dtype=torch.uint8, device=cuda)
                     dw = torch.empty(cout, 1, 1, cin, device=cuda)
@@ -1254,7 +1255,9 @@ def test_wgrad_dma_kernel_bitwise(cuda):
                     ks = list(t.summary())
                     wide = key == 3 or (key == 2 and apply)
                     want = 0 if not key else (256 if wide and cin % 256 == 0 else 128)
-                    assert len(ks) == (1 if key else 0) and (not key or ks[0].endswith(", %d>" % want)), \
+                    nsx = extra.get(48, 0) if want == 256 and apply else 0
+                    assert len(ks) == (1 if key else 0) and (not key or ks[0] == "argus::wgrad_dma_kernel<%s, %d, false, %d>"
+                                                             % ("true" if apply else "false", want, nsx)), \
                         ("dma kernel use", cin, cout, hh, ww, n, key, ks)
                     outs.append(dw.cpu())
                 # key 3 plain on 256-wide tiles plans its splits for two workgroups per CU over half the
@@ -1298,7 +1301,7 @@ def test_wgrad_dma_gather_stride2_bitwise(cuda):
                 wsb = L.dll.argus_conv_wgrad_workspace_bytes(C.byref(d), BF16)
                 ws = torch.empty(wsb, dtype=torch.uint8, device=cuda)
                 dw = torch.empty(cout, k, k, cin, device=cuda)
-                with KernelTimer("argus::wgrad_dma_kernel<false, 128, gather>") as t:
+                with KernelTimer("argus::wgrad_dma_kernel<false, 128, true, 0>") as t:
                     L.conv_wgrad(C.byref(d), BF16, ptr(x), None, None, ptr(dy), ptr(dw), ptr(ws), wsb, stream())
                 torch.cuda.synchronize()
                 assert len(t.summary()) == key, ("gather kernel use", cin, cout, k, hh, ww, n, key)
@@ -1309,6 +1312,23 @@ def test_wgrad_dma_gather_stride2_bitwise(cuda):
             assert _rel(outs[0].permute(0, 3, 1, 2), ref) < 1e-4, (cin, cout, k, hh, ww, n)
             ran += 1
     assert ran == 15
+    # the default (key 47 = 131072) serves up to that many output pixels; a cap below the launch's pixel
+    # count sends it to the register-staged kernel, with the same bits
+    d0, _ = _desc(2, 16, 16, 128, 128, 3, 2)
+    x = torch.randn(2, 16, 16, 128, device=cuda).to(torch.bfloat16)
+    dy = torch.randn(2, d0.ho, d0.wo, 128, device=cuda).to(torch.bfloat16)
+    outs = []
+    for tune, used in (({}, 1), ({47: 2 * d0.ho * d0.wo - 1}, 0), ({47: 2 * d0.ho * d0.wo}, 1)):
+        d = d0.with_tuning(tune)
+        wsb = L.dll.argus_conv_wgrad_workspace_bytes(C.byref(d), BF16)
+        ws = torch.empty(wsb, dtype=torch.uint8, device=cuda)
+        dw = torch.empty(128, 3, 3, 128, device=cuda)
+        with KernelTimer("argus::wgrad_dma_kernel<false, 128, true, 0>") as t:
+            L.conv_wgrad(C.byref(d), BF16, ptr(x), None, None, ptr(dy), ptr(dw), ptr(ws), wsb, stream())
+        torch.cuda.synchronize()
+        assert len(t.summary()) == used, (tune, used)
+        outs.append(dw.cpu())
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
 
 
 @pytest.mark.parametrize("dt", ["fp32", "bf16"])
