@@ -1317,6 +1317,9 @@ static const Policy kDefaultPolicy = [] {
   // 48: LDS ring stages of the 128 x 256 apply weight gradient (32 KB each; 4 = 128 KB, one workgroup
   //     per CU; 5 = all 160 KB, one more stage in flight; 2 / 3 leave room for main-stream workgroups)
   p.v[kWgradDmaStages] = 4;
+  // 49: 1x1 BN-backward-apply prologues are staged by the dgrad only up to this many 128-column tiles
+  //     (0: always): beyond it the redundant per-tile apply (VALU) costs more than materialising dy
+  p.v[kDgradApMaxCols] = 0;
   return p;
 }();
 
@@ -1646,7 +1649,12 @@ static bool dgrad_stages_prologue(const argus_conv_desc& d, int dtype, IgParams&
     maxK = p.ph[i].K > maxK ? p.ph[i].K : maxK;
   }
   if ((*p.pol)[kDgradApStaged]) return true;  // the glds kernel is not used: no dy to materialise
-  return !(dtype == ARGUS_BF16 && (conv3x3_halo_ok(p) || igemm_glds_ok(p, maxM, maxK)));
+  if (dtype == ARGUS_BF16 && (conv3x3_halo_ok(p) || igemm_glds_ok(p, maxM, maxK))) return false;
+  // key 49: every 128-column tile of the dgrad (d.c / 128 of them) redoes the apply of the same A rows
+  // (the register-staged igemm and the persistent conv1 kernel alike); past that many tiles the apply
+  // kernel materialises dy once instead (0: no limit)
+  const int maxcols = (*p.pol)[kDgradApMaxCols];
+  return !(dtype == ARGUS_BF16 && maxcols > 0 && d.c / 128 > maxcols);
 }
 
 int conv_dgrad_stages_prologue(const argus_conv_desc& d, int dtype) {

@@ -60,7 +60,8 @@ enum TuneKey : int {
   kWgradSmallP = 46,      // 1x1 weight gradients over at most this many pixels: half the split target
   kWgradDmaGather = 47,   // ... and the stride-2 (1x1 / 3x3) plain ones, x rows gathered (1 on, >1 pixel cap)
   kWgradDmaStages = 48,   // LDS ring stages of the 128 x 256 apply DMA weight gradient (2..5)
-  kNumTuneKeys = 49
+  kDgradApMaxCols = 49,   // 1x1 dgrads stage the apply prologue up to this many 128-column tiles (0: any)
+  kNumTuneKeys = 50
 };
 struct Policy {
   int v[kNumTuneKeys];
