@@ -1320,6 +1320,10 @@ static const Policy kDefaultPolicy = [] {
   // 49: 1x1 BN-backward-apply prologues are staged by the dgrad only up to this many 128-column tiles
   //     (0: always): beyond it the redundant per-tile apply (VALU) costs more than materialising dy
   p.v[kDgradApMaxCols] = 0;
+  // 50: the LDS-DMA weight gradients sum their split partials inside the launch (reducing workgroups
+  //     after the compute grid, conv_wgdma.hip) instead of a wgrad_reduce launch; the caller's workspace
+  //     must end in kWgFoldCtrBytes of zeros (argus_conv_wgrad_workspace_bytes includes them)
+  p.v[kWgradFold] = 0;
   return p;
 }();
 
@@ -1884,7 +1888,8 @@ size_t conv_wgrad_ws(const argus_conv_desc& d, int dtype) {
     const size_t hb = (size_t)hs * d.k * 9 * d.c * sizeof(float);
     b = hb > b ? hb : b;
   }
-  return b;
+  // + the folded reduction's counters (key 50): the last kWgFoldCtrBytes, past every kernel's partials
+  return b + kWgFoldCtrBytes;
 }
 
 template <typename T, int BM, int BN, bool STEM, bool PRO, bool FAST, bool AP>
@@ -1969,8 +1974,20 @@ static int conv_wgrad_impl(const argus_conv_desc& d, int dtype, const void* x, c
   if (d.stem && pol[kStemLdsWgrad] && stem_wgrad_launch(d, dtype, x, dy, ap, ws, ws_bytes, &splits, st)) {
     if (int e = check_launch("stem_wgrad_kernel")) return e;
   } else if (!sc && wgrad_dma_ok(d, dtype, pl.bm, pl.bn, pol[kWgradDma], ap != nullptr, pol[kWgradDmaGather])) {
+    // key 50: the split sum folded into the launch (its last kWgFoldCtrBytes of ws hold the counters,
+    // zero before the first launch; every launch leaves them zero)
+    const int ft = wgrad_dma_fold_tiles(d, pol[kWgradDma], pol[kWgradDmaGather], ap != nullptr);
+    const size_t need = (size_t)pl.splits * d.k * pl.N * sizeof(float);
+    const bool fold = pol[kWgradFold] && ft > 0 && (2 * ft + 1) * 4 <= (int)kWgFoldCtrBytes &&
+                      ws_bytes >= need + kWgFoldCtrBytes;
+    if (fold) {
+      p.fold.cnt = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(ws) + ((ws_bytes - kWgFoldCtrBytes) & ~(size_t)255));
+      p.fold.dw = dw;
+      p.fold.sl = wgrad_reduce_lanes(d.k, pl.N);
+    }
     wgrad_dma_launch(d, p, pol[kWgradDma], pol[kWgradDmaGather], pl.splits, pol[kWgradDmaStages], st);  // LDS-DMA ring
     if (int e = check_launch("wgrad_dma_kernel")) return e;
+    if (fold) return ARGUS_OK;
   } else if (ap) {  // the register-staged kernel stages the apply; no halo / glds variant does
     if (dtype == ARGUS_BF16) dispatch_wg<bf16>(p, pl, st);
     else dispatch_wg<float>(p, pl, st);

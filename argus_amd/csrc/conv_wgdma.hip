@@ -68,7 +68,78 @@ template <int K, int D> ARGUS_DEV void wg_wait_after(int after) {
     else wg_wait_after<K - 1, D>(after);
   }
 }
+typedef __attribute__((address_space(1))) unsigned wg_gu32;
+// 16-byte write-through (sc1) store: the slab leaves the writer's L2 for the reducing workgroup
+ARGUS_DEV void wg_st16_wt(f32x4* p, f32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
 }  // namespace
+
+// A tile's split slabs summed by the reducing workgroups of a folded launch (policy key 50). Workgroup
+// r (after the compute grid) takes tile r % nwg and part r / nwg of its 128 x BN / 4 float4 fragments;
+// it waits for the tile's nsplit arrivals, then sums every fragment over the splits in the order of
+// wgrad_reduce_kernel (reduce.hip) for this M x N: lane l of SL sums splits l, l + SL, ... from 0, and
+// the SL lane sums are added in lane order - the same fp32 additions, so dW is bit-identical to the
+// unfolded launch + wgrad_reduce. The last reducing workgroup of the tile resets its two counters.
+template <int NT, int MI, int NI, bool AP, int BN>
+ARGUS_DEV void wg_fold_reduce(const WgParams& p, int nwg, int nsplit, int r, f32x4* red) {
+  const int tile = r % nwg, part = r / nwg;
+  const int ntiles = p.N / BN, mt = tile / ntiles, nt = tile - mt * ntiles;
+  constexpr int FR = 128 * BN / 4;  // float4 fragments per tile
+  const int SL = p.fold.sl, rpt = p.fold.rpt;
+  const int fbeg = (int)((long)FR * part / rpt), fend = (int)((long)FR * (part + 1) / rpt);
+  if (threadIdx.x == 0) {
+    // poll the tile's arrivals with an atomic read-modify-write (performed at the memory side: a plain
+    // or sc1 load may keep returning the XCD's L2 copy); bounded, so a launch can never hang
+    wg_gu32* c = (wg_gu32*)(p.fold.cnt + tile);
+    int it = 0;
+    while (__hip_atomic_fetch_add(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)nsplit) {
+      if (++it > (1 << 16)) break;
+      __builtin_amdgcn_s_sleep(32);
+    }
+    if (it > (1 << 16)) __hip_atomic_store((wg_gu32*)(p.fold.cnt + 2 * nwg), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  const f32x4* slab0 = reinterpret_cast<const f32x4*>(p.part) + (size_t)tile * nsplit * FR;
+  const int t = threadIdx.x, l = t % SL, per = NT / SL;
+  for (int f0 = fbeg; f0 < fend; f0 += per) {
+    const int f = f0 + t / SL;
+    const bool valid = f < fend;
+    const int fc = valid ? f : fbeg;
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    for (int kb = l; kb < nsplit; kb += SL * kLoadBatch) {
+      f32x4 v[kLoadBatch];  // in flight together; clamped, masked below (as wgrad_reduce_kernel)
+#pragma unroll
+      for (int u = 0; u < kLoadBatch; ++u) v[u] = slab0[(size_t)min(kb + u * SL, nsplit - 1) * FR + fc];
+#pragma unroll
+      for (int u = 0; u < kLoadBatch; ++u) s += kb + u * SL < nsplit ? v[u] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    red[t] = s;
+    __syncthreads();
+    if (l == 0 && valid) {
+      for (int j = 1; j < SL; ++j) s += red[t + j];
+      // fragment f -> (wave, mi, ni, lane) -> rows m .. m + 3 of column n (the compute epilogue's map)
+      const int lane = f & 63, q = f >> 6, ni = q % NI, mi = (q / NI) % MI, wave = q / (NI * MI);
+      const int rbase = AP ? 16 * MI * wave : 64 * (wave / (BN / 64));
+      const int cbase = AP ? 0 : 64 * (wave % (BN / 64));
+      const int n = nt * BN + cbase + 16 * ni + (lane & 15);
+      const int m = mt * 128 + rbase + 16 * mi + 4 * (lane >> 4);
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) p.fold.dw[(size_t)(m + rr) * p.N + n] = s[rr];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    wg_gu32* c = (wg_gu32*)(p.fold.cnt + tile);
+    wg_gu32* dn = (wg_gu32*)(p.fold.cnt + nwg + tile);
+    if (__hip_atomic_fetch_add(dn, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)rpt - 1) {
+      __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(dn, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
 
 constexpr int kWgdBK = 32;  // pixels per k-step
 
@@ -100,8 +171,16 @@ __global__ __launch_bounds__(2 * BN, BN == 256 && AP ? 1 : 2) void wgrad_dma_ker
 
   const int mtiles = p.M / 128, ntiles = p.N / BN;
   const int nwg = mtiles * ntiles;
+  const int nsplit = (p.P + p.pps - 1) / p.pps;
+  // folded split reduction (p.fold.cnt set, policy key 50): the workgroups past the compute grid sum
+  // the split slabs of one tile each (wg_fold_reduce), so no separate wgrad_reduce launch runs
+  if (p.fold.cnt && (int)blockIdx.x >= nwg * nsplit) {
+    wg_fold_reduce<NT, AP ? 8 / NW : 4, AP ? BN / 16 : 4, AP, BN>(p, nwg, nsplit, (int)blockIdx.x - nwg * nsplit,
+                                                                  reinterpret_cast<f32x4*>(lds));
+    return;
+  }
   int bid, split;
-  split_tile(nwg, (p.P + p.pps - 1) / p.pps, p.group != 0, bid, split);
+  split_tile(nwg, nsplit, p.group != 0, bid, split);
   const int mt = bid / ntiles, nt = bid - mt * ntiles;
   const int pbeg = split * p.pps;
   const int pend = min(p.P, pbeg + p.pps);
@@ -256,6 +335,20 @@ __global__ __launch_bounds__(2 * BN, BN == 256 && AP ? 1 : 2) void wgrad_dma_ker
   }
   wg_waitvm<0>();
 
+  if (p.fold.cnt) {
+    // the tile's slab for this split in fragment order (one 16-byte write-through store per fragment),
+    // then one arrival on the tile's counter after every wave's stores drained (MI355X_MICROARCH.md
+    // hand-off table, row 1: sc1 stores, drained, one agent-scope add per workgroup)
+    f32x4* slab = reinterpret_cast<f32x4*>(p.part) + ((size_t)bid * nsplit + split) * (128 * BN / 4);
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) wg_st16_wt(slab + ((wave * MI + mi) * NI + ni) * 64 + lane, acc[mi][ni]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add((wg_gu32*)(p.fold.cnt + bid), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
   float* out = p.part + (size_t)split * p.M * p.N;
 #pragma unroll
   for (int mi = 0; mi < MI; ++mi)
@@ -295,10 +388,29 @@ bool wgrad_dma_ok(const argus_conv_desc& d, int dtype, int bm, int bn, int enabl
 }
 
 // grid: the 128 x 128 tiles x splits of the plan; 256-wide tiles take two of its column tiles
-void wgrad_dma_launch(const argus_conv_desc& d, const WgParams& p, int key, int gather_key, int splits, int ns,
+// the reducing workgroups of a folded launch: about 128 in all, at least one pass of NT / SL fragments each
+static int wgrad_dma_fold_rpt(int nwg, int bn, int sl) {
+  const int frag = 128 * bn / 4, per = 2 * bn / sl;
+  int rpt = (128 + nwg - 1) / nwg;
+  return rpt < 1 ? 1 : (rpt > frag / per ? frag / per : rpt);
+}
+
+int wgrad_dma_fold_tiles(const argus_conv_desc& d, int key, int gather_key, bool ap) {
+  const int bn = wgrad_dma_width(d, ARGUS_BF16, 128, 128, key, ap, gather_key);
+  const int N = d.r * d.s * d.c;
+  return bn ? (d.k / 128) * (N / bn) : 0;
+}
+
+void wgrad_dma_launch(const argus_conv_desc& d, const WgParams& p_in, int key, int gather_key, int splits, int ns,
                       hipStream_t st) {
+  WgParams p = p_in;
   const int bn = wgrad_dma_width(d, ARGUS_BF16, 128, 128, key, p.ap_y != nullptr, gather_key);
-  const int grid = (p.M / 128) * (p.N / bn) * splits;
+  const int nwg = (p.M / 128) * (p.N / bn);
+  int grid = nwg * splits;
+  if (p.fold.cnt) {
+    p.fold.rpt = wgrad_dma_fold_rpt(nwg, bn, p.fold.sl);
+    grid += nwg * p.fold.rpt;
+  }
   if (wgrad_dma_gather(d)) {
     timed_launch("argus::wgrad_dma_kernel<false, 128, true, 0>", wgrad_dma_kernel<false, 128, true>, dim3(grid),
                  dim3(256), st, p);

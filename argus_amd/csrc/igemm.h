@@ -113,6 +113,14 @@ struct WgParams {
   const float *ap_ca, *ap_cb, *ap_cc;
   FastDiv fd_hw, fd_w;  // Ho*Wo and Wo (pixel -> (image, row, column) without integer division)
   int group;            // split_tile: a split's tiles on one XCD (1x1 filters; 3x3 with tuning key 31)
+  // folded split reduction of the LDS-DMA kernel (policy key 50; cnt == nullptr: off): arrival / done
+  // counters [2 * tiles + 1] (zero before the launch, zero again after it), dW [M][N], the lane count of
+  // wgrad_reduce_kernel's order for this M x N and the reducing workgroups per tile
+  struct {
+    unsigned* cnt;
+    float* dw;
+    int sl, rpt;
+  } fold;
 };
 
 template <typename T> struct Mma;
@@ -318,6 +326,10 @@ bool wgrad_dma_ok(const argus_conv_desc& d, int dtype, int bm, int bn, int enabl
 int wgrad_dma_width(const argus_conv_desc& d, int dtype, int bm, int bn, int key, bool ap, int gather_key);
 void wgrad_dma_launch(const argus_conv_desc& d, const WgParams& p, int key, int gather_key, int splits, int ns,
                       hipStream_t st);
+// output tiles of the LDS-DMA weight gradient of d (its folded reduction's counters: 2 per tile + 1)
+int wgrad_dma_fold_tiles(const argus_conv_desc& d, int key, int gather_key, bool ap);
+// the lane count of wgrad_reduce_kernel's summation order for an M x N dW (reduce.hip)
+int wgrad_reduce_lanes(int M, int N);
 int p1x1_rows(const argus_conv_desc& d);
 int p1x1_launch(const argus_conv_desc& d, const void* dm, const void* wd, void* out, const void* addend,
                 const argus_bn_bwd_epilogue* bn, const argus_bn_bwd_prologue* pro, hipStream_t st);

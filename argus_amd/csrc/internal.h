@@ -24,6 +24,8 @@ int conv_dgrad_bn_x8(const argus_conv_desc& d, const void* dy8, const void* wt, 
 int conv_x8_ok(const argus_conv_desc& d, int pass);
 // BN workspace layout (bn.hip): [0, kBnCounterBytes) ticket counters, then double2 group results
 constexpr size_t kBnCounterBytes = 16384;
+// the folded weight-gradient reduction's counters at the end of a wgrad workspace (policy key 50)
+constexpr size_t kWgFoldCtrBytes = 16384;
 int conv_fwd_stat_tile(const argus_conv_desc& d, int dtype);
 // the partial-row layout of a statistics-only forward (argus_conv_fwd with y == NULL)
 int conv_fwd_stats_only_rows(const argus_conv_desc& d, int dtype);
@@ -61,7 +63,8 @@ enum TuneKey : int {
   kWgradDmaGather = 47,   // ... and the stride-2 (1x1 / 3x3) plain ones, x rows gathered (1 on, >1 pixel cap)
   kWgradDmaStages = 48,   // LDS ring stages of the 128 x 256 apply DMA weight gradient (2..5)
   kDgradApMaxCols = 49,   // 1x1 dgrads stage the apply prologue up to this many 128-column tiles (0: any)
-  kNumTuneKeys = 50
+  kWgradFold = 50,        // DMA weight gradients reduce their split partials in-launch (1 on)
+  kNumTuneKeys = 51
 };
 struct Policy {
   int v[kNumTuneKeys];

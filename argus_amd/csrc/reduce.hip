@@ -45,10 +45,20 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   }
 }
 
+// float4 columns per block: aim for >= 512 blocks, more split lanes when few columns
+static int reduce_cw(int M, int N) {
+  const size_t total4 = (size_t)M * N / 4;
+  int cw = 64;
+  while (cw > 4 && (total4 + cw - 1) / cw < 512) cw >>= 1;
+  return cw;
+}
+
+// split lanes per float4 column (the summation order a folded reduction must repeat: conv_wgdma.hip)
+int wgrad_reduce_lanes(int M, int N) { return 256 / reduce_cw(M, N); }
+
 int wgrad_reduce_launch(const float* part, int splits, int M, int N, int stem, float* dw, hipStream_t st) {
   const size_t total4 = (size_t)M * N / 4;
-  int cw = 64;  // float4 columns per block: aim for >= 512 blocks, more split lanes when few columns
-  while (cw > 4 && (total4 + cw - 1) / cw < 512) cw >>= 1;
+  const int cw = reduce_cw(M, N);
   const int blocks = (int)((total4 + cw - 1) / cw);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, part, splits, M, N, stem, cw, dw);
   return check_launch("wgrad_reduce_kernel");

@@ -329,7 +329,8 @@ class ResNetEngine:
         self.bwd_part = self._f(max_bwd * 2)
         self.bwd_part2 = self._f(max_bwd * 2)  # second branch (downsample BN) of a dual reduce
         ws = max(L.dll.argus_conv_wgrad_workspace_bytes(C.byref(cv.desc), dt) for cv in convs.values())
-        self.wg_ws = torch.empty(ws, dtype=torch.uint8, device=self.device)
+        # zeroed: a folded DMA weight gradient (policy key 50) keeps its counters in the last bytes
+        self.wg_ws = torch.zeros(ws, dtype=torch.uint8, device=self.device)
         self.wg_ws_bytes = ws
         wss = L.dll.argus_conv_wgrad_workspace_bytes(C.byref(convs["resnet.conv1"].desc), dt)
         # the stem weight gradient's workspace; also the first block's downsample weight gradient's, which
@@ -337,7 +338,7 @@ class ResNetEngine:
         ds0 = self.blocks[0].prefix + ".downsample.0"
         if ds0 in convs:
             wss = max(wss, L.dll.argus_conv_wgrad_workspace_bytes(C.byref(convs[ds0].desc), dt))
-        self.wg_ws_stem = torch.empty(wss, dtype=torch.uint8, device=self.device)
+        self.wg_ws_stem = torch.zeros(wss, dtype=torch.uint8, device=self.device)
         self.stages_pro = {n: bool(L.dll.argus_conv_dgrad_stages_prologue(C.byref(cv.desc), self.cdt))
                            for n, cv in convs.items() if not cv.desc.stem}
         self.gbuf = [self._t(max_elems) for _ in range(3)]  # avgpool dh; dza / dzb (the dz of bn2 / bn1)

@@ -1235,12 +1235,14 @@ def test_wgrad_dma_kernel_bitwise(cuda):
             ca, cb, cc = (torch.randn(cout, device=cuda) * 0.3 for _ in range(3))
             for apply in (False, True):
                 outs = []
-                # key 48: the ring depth of the 128 x 256 apply form (2..5 stages; same arithmetic)
-                for key, extra in ((3, {}), (2, {}), (2, {48: 5}), (2, {48: 3}), (2, {48: 2}), (1, {}), (0, {})):
+                # key 48: the ring depth of the 128 x 256 apply form (2..5 stages; same arithmetic); key 50:
+                # the split sum folded into the launch (zeroed workspace; run twice: the counters reset)
+                for key, extra in ((3, {}), (2, {}), (2, {48: 5}), (2, {48: 3}), (2, {48: 2}), (3, {50: 1}),
+                                   (2, {50: 1}), (2, {50: 1, 48: 5}), (1, {50: 1}), (1, {}), (0, {})):
                     d, _ = _desc(n, hh, ww, cin, cout, 1, 1)
                     d = d.with_tuning({**tune, 45: key, **extra})
                     wsb = L.dll.argus_conv_wgrad_workspace_bytes(C.byref(d), BF16)
-                    ws = torch.empty(wsb, dtype=torch.uint8, device=cuda)
+                    ws = torch.zeros(wsb, dtype=torch.uint8, device=cuda)
                     dw = torch.empty(cout, 1, 1, cin, device=cuda)
                     with KernelTimer("argus::wgrad_dma_kernel<%s" % ("true" if apply else "false")) as t:
                         if apply:
@@ -1252,6 +1254,19 @@ def test_wgrad_dma_kernel_bitwise(cuda):
                                               stream())
                     assert rc in (0, None), L.dll.argus_last_error()
                     torch.cuda.synchronize()
+                    if extra.get(50):
+                        # the counters (last 16 KB) are zero again, no spin timed out; a second launch on the
+                        # same workspace gives the same bits
+                        assert int(ws[-16384:].count_nonzero()) == 0
+                        first = dw.clone()
+                        dw.zero_()
+                        if apply:
+                            L.conv_wgrad_apply(C.byref(d), BF16, ptr(x), ptr(dm), C.byref(ap), ptr(dw), ptr(ws), wsb,
+                                               stream())
+                        else:
+                            L.conv_wgrad(C.byref(d), BF16, ptr(x), None, None, ptr(dm), ptr(dw), ptr(ws), wsb, stream())
+                        torch.cuda.synchronize()
+                        assert torch.equal(dw, first) and int(ws[-16384:].count_nonzero()) == 0
                     ks = list(t.summary())
                     wide = key == 3 or (key == 2 and apply)
                     want = 0 if not key else (256 if wide and cin % 256 == 0 else 128)
@@ -1263,8 +1278,12 @@ def test_wgrad_dma_kernel_bitwise(cuda):
                 # key 3 plain on 256-wide tiles plans its splits for two workgroups per CU over half the
                 # tiles: another split grouping, so another fp32 summation order (checked against fp64)
                 resplit = not apply and cin % 256 == 0
-                assert all(torch.equal(o, outs[-1]) for o in outs[1 if resplit else 0:-1]), \
-                    (cin, cout, hh, ww, n, target, apply)
+                keys = [k for k, _ in ((3, {}), (2, {}), (2, {48: 5}), (2, {48: 3}), (2, {48: 2}), (3, {50: 1}),
+                                       (2, {50: 1}), (2, {50: 1, 48: 5}), (1, {50: 1}), (1, {}), (0, {}))]
+                same = [o for o, k in zip(outs, keys) if not (resplit and k == 3)]
+                assert all(torch.equal(o, outs[-1]) for o in same), (cin, cout, hh, ww, n, target, apply)
+                if resplit:  # the key-3 plan, folded or not: one summation order
+                    assert torch.equal(outs[0], outs[5]), (cin, cout, hh, ww, n, target)
                 dy = dm.double()
                 if apply:
                     dy = (ca.double() * dm.double() + (cb.double() * yb.double() + cc.double()))
@@ -1296,17 +1315,18 @@ def test_wgrad_dma_gather_stride2_bitwise(cuda):
             x = torch.randn(n, hh, ww, cin, device=cuda).to(torch.bfloat16)
             dy = torch.randn(n, d0.ho, d0.wo, cout, device=cuda).to(torch.bfloat16)
             outs = []
-            for key in (1, 0):
-                d = d0.with_tuning({**tune, 47: key})
+            for key, fold in ((1, 0), (1, 1), (0, 0)):  # + the split sum folded into the launch (key 50)
+                d = d0.with_tuning({**tune, 47: key, 50: fold})
                 wsb = L.dll.argus_conv_wgrad_workspace_bytes(C.byref(d), BF16)
-                ws = torch.empty(wsb, dtype=torch.uint8, device=cuda)
+                ws = torch.zeros(wsb, dtype=torch.uint8, device=cuda)
                 dw = torch.empty(cout, k, k, cin, device=cuda)
                 with KernelTimer("argus::wgrad_dma_kernel<false, 128, true, 0>") as t:
                     L.conv_wgrad(C.byref(d), BF16, ptr(x), None, None, ptr(dy), ptr(dw), ptr(ws), wsb, stream())
                 torch.cuda.synchronize()
                 assert len(t.summary()) == key, ("gather kernel use", cin, cout, k, hh, ww, n, key)
+                assert int(ws[-16384:].count_nonzero()) == 0  # folded: the counters reset, no spin timed out
                 outs.append(dw.cpu())
-            assert torch.equal(outs[0], outs[1]), (cin, cout, k, hh, ww, n, target)
+            assert torch.equal(outs[0], outs[2]) and torch.equal(outs[1], outs[2]), (cin, cout, k, hh, ww, n, target)
             ref = torch.nn.grad.conv2d_weight(x.permute(0, 3, 1, 2).double().cpu(), (cout, cin, k, k),
                                               dy.permute(0, 3, 1, 2).double().cpu(), stride=2, padding=(k - 1) // 2)
             assert _rel(outs[0].permute(0, 3, 1, 2), ref) < 1e-4, (cin, cout, k, hh, ww, n)
