@@ -184,11 +184,17 @@ SELECTION_CASES = [
 def _scaled_policy(r):
     """Kernel-selection overrides that keep a batch r x smaller on the larger batch's kernels: the
     thresholds that compare a GEMM row count or a grid size (both linear in the batch) scaled by r
-    (policy keys 35: 128-row forward tiles, 36 / 9: glds rows / workgroups, 13: halo workgroups)."""
+    (policy keys 35: 128-row forward tiles, 36 / 9: glds rows / workgroups, 13: halo workgroups, 46: the
+    1x1 weight gradients' half split target, 47: the pixel cap of the gathering DMA weight gradient -
+    kept > 1, since 1 means no cap)."""
     from argus_amd._lib import lib
 
     L = lib()
-    return {k: max(1, round(L.dll.argus_conv_policy_default(k) * r)) for k in (35, 36, 9, 13)}
+    pol = {k: max(1, round(L.dll.argus_conv_policy_default(k) * r)) for k in (35, 36, 9, 13, 46)}
+    cap = L.dll.argus_conv_policy_default(47)
+    if cap > 1:
+        pol[47] = max(2, round(cap * r))
+    return pol
 
 
 @pytest.mark.parametrize("case", SELECTION_CASES, ids=[c[0] for c in SELECTION_CASES])
