@@ -1,7 +1,9 @@
-"""BN-fused 1x1 dgrad microbenchmark (dev tool, GPU): for every bottleneck block at a given batch, time the
+"""BN-fused dgrad microbenchmark (dev tool, GPU): for every bottleneck block at a given batch, time the
 conv1 dgrad (mask-bit epilogue of the previous bn3 + residual addend, apply prologue of bn1, folded
-finalize: the benched schedule) and its stripped variants, through the C ABI.
-python tools/dgradbench.py [--batch 64] [--filter layer3] [--tune k=v ...]"""
+finalize: the benched schedule), the conv3 dgrad, and with --convs conv2 the 3x3 one (bn1's recomputed-
+mask epilogue; its apply prologue is the materialising apply pass), and their stripped variants,
+through the C ABI.
+python tools/dgradbench.py [--batch 64] [--filter layer3] [--convs conv1,conv3,conv2] [--tune k=v ...]"""
 import argparse
 import ctypes as C
 import sys
@@ -32,6 +34,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--filter", default="")
     ap.add_argument("--tune", nargs="*", default=[])
+    ap.add_argument("--convs", default="conv1,conv3")
     a = ap.parse_args()
     L = lib()
     tuning = {int(k): int(v) for k, v in (kv.split("=") for kv in a.tune)}
@@ -43,7 +46,7 @@ def main():
     tot = {}
     seen = set()
     for idx, b in enumerate(eng.blocks):
-        for which in ("conv1", "conv3"):
+        for which in a.convs.split(","):
             name = f"{b.prefix}.{which}"
             if a.filter and a.filter not in name:
                 continue
@@ -67,7 +70,7 @@ def main():
             cout = {k: ck(d.c) for k in ("mean", "invstd", "sc", "sh", "gamma", "dg", "db", "ca", "cb", "cc")}
             rows = L.dll.argus_conv_dgrad_bn_rows(C.byref(d), 1)
             part = torch.empty(rows * d.c * 2, device=dev)
-            mode = 2 if which == "conv3" else 3
+            mode = 3 if which == "conv1" else 2
 
             def epi(fin):
                 e = BnBwdEpilogue()
