@@ -1318,8 +1318,11 @@ static const Policy kDefaultPolicy = [] {
   //     per CU; 5 = all 160 KB, one more stage in flight; 2 / 3 leave room for main-stream workgroups)
   p.v[kWgradDmaStages] = 4;
   // 49: 1x1 BN-backward-apply prologues are staged by the dgrad only up to this many 128-column tiles
-  //     (0: always): beyond it the redundant per-tile apply (VALU) costs more than materialising dy
-  p.v[kDgradApMaxCols] = 0;
+  //     (0: always): beyond it the redundant per-tile apply (VALU) costs more than materialising dy.
+  //     4 (the conv1 dgrads of layers 3-4 materialise dy1): engine A/B, best of 3-4 interleaved rounds,
+  //     B=64 13.65 vs 13.68-13.72 ms, B=256 46.21 vs 47.03-47.13 ms, 376x672 B=128 90.23 vs 90.71-91.56 ms;
+  //     8 level, 2 slower (14.6 ms at B=64): profiles/r06a_ab_keys.txt, r06b_ab_*_key49*.txt
+  p.v[kDgradApMaxCols] = 4;
   // 50: the LDS-DMA weight gradients sum their split partials inside the launch (reducing workgroups
   //     after the compute grid, conv_wgdma.hip) instead of a wgrad_reduce launch; the caller's workspace
   //     must end in kWgFoldCtrBytes of zeros (argus_conv_wgrad_workspace_bytes includes them)

@@ -53,6 +53,7 @@ def test_bad_arguments_are_reported():
     assert L.dll.argus_conv_policy_default(45) in (0, 1, 2, 3) and L.dll.argus_conv_policy_default(51) == -1
     assert L.dll.argus_conv_policy_default(48) == 4 and L.dll.argus_conv_policy_default(47) == 131072
     # key 49: a 1x1 dgrad stages its apply prologue only up to that many 128-column tiles (host-only query)
+    assert L.dll.argus_conv_policy_default(49) == 4 and L.dll.argus_conv_policy_default(50) == 0
     c1 = ConvDesc(2, 8, 8, 2048, 512, 1, 1, 1, 0, 8, 8, 0)
     assert [L.dll.argus_conv_dgrad_stages_prologue(C.byref(c1.with_tuning({49: v})), 1) for v in (0, 16, 8)] == [1, 1, 0]
     forced = good.with_tuning({1: 128, 4: 64})  # dgrad row / column tiles

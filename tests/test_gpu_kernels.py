@@ -2081,7 +2081,7 @@ def test_persistent_conv1_dgrad_matches_igemm(cuda, n4w, w, hw, dual):
     rows = L.dll.argus_conv_dgrad_bn_rows(C.byref(d), BF16)
     outs = []
     for key in (0, 1):
-        dk = d.with_tuning({43: key})
+        dk = d.with_tuning({43: key, 49: 0})  # 49 = 0: the prologue staged at every width (4w up to 1024)
         out = torch.empty(P, n4w, dtype=torch.bfloat16, device=cuda)
         part = torch.zeros(rows, n4w, 2, device=cuda)
         part2 = torch.zeros(rows, n4w, 2, device=cuda)
