@@ -1327,6 +1327,9 @@ static const Policy kDefaultPolicy = [] {
   //     after the compute grid, conv_wgdma.hip) instead of a wgrad_reduce launch; the caller's workspace
   //     must end in kWgFoldCtrBytes of zeros (argus_conv_wgrad_workspace_bytes includes them)
   p.v[kWgradFold] = 0;
+  // 51: the 3x3 halo forward / data gradient (128-column tiles) with a four-stage weight ring on
+  //     384-position halo images where the tile's halo fits (the 32- and 16-wide layers at 256 x 256)
+  p.v[kHaloDeepRing] = 0;
   return p;
 }();
 

@@ -48,6 +48,11 @@ constexpr int kHaloPos1 = 416;  // single-buffer variant: 2 x (416 x 128 B + 3 x
 // F8 variant: 400 positions per halo image (the fp8 shapes: 340 / 324 / 400 at W = 32 / 16x16 / 8x8),
 // so two images, their scales and three weight stages fit one CU
 constexpr int kHaloPosF8 = 400;
+// DEEP variant (policy key 51): 384-position halo images (the 256 x 256 frame's 32- and 16-wide layers
+// need 340 / 324) free LDS for a fourth weight stage: 2 x 48 KB + 4 x 16 KB = 160 KB, so three weight
+// taps are in flight under each tap's MFMAs instead of two (the loop waits on L2 -> LDS weight latency:
+// a 16 KB stage per ~0.4 us tap at one workgroup per CU)
+constexpr int kHaloPosDeep = 384;
 
 // HB = halo image buffers: 2 (double-buffered over 64-channel chunks) or 1 (Cin = 64: a single chunk,
 // nothing to prefetch; the 64-column tile then fits two workgroups per CU in LDS)
@@ -60,13 +65,23 @@ constexpr int kHaloPosF8 = 400;
 // (not 448: the fp8 shapes need no more), which leaves room for the scale images and three weight
 // stages; a wave whose last halo DMA would cover positions past 400 sends it to a 1 KB dummy slot (every
 // wave issues the same DMAs, so the counted waits hold).
-template <int BN, int BW, int HB, bool F8 = false>
+template <int N> ARGUS_DEV void waitvm_le(int n) {  // vmcnt(n) for a runtime n <= N (the next lower count)
+  if constexpr (N == 0) {
+    waitvm<0>();
+  } else {
+    if (n >= N) waitvm<N>();
+    else waitvm_le<N - 1>(n);
+  }
+}
+
+template <int BN, int BW, int HB, bool F8 = false, bool DEEP = false>
 __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_halo_kernel(const IgParams p) {
+  static_assert(!DEEP || (!F8 && HB == 2 && BN == 128), "deep weight ring: the bf16 128-column double-halo form");
   constexpr int WN = BN / 64, NW = 4 * WN, NT = NW * 64;
-  constexpr int HPOS = F8 ? kHaloPosF8 : (HB == 1 ? kHaloPos1 : kHaloPos);  // halo positions per image buffer
+  constexpr int HPOS = F8 ? kHaloPosF8 : (HB == 1 ? kHaloPos1 : (DEEP ? kHaloPosDeep : kHaloPos));  // per image buffer
   constexpr int HALO = HPOS * 128;              // bytes per halo image
   constexpr int BST = BN * 128;                 // bytes per weight stage
-  constexpr int NBS = 3;
+  constexpr int NBS = DEEP ? 4 : 3;             // weight ring stages
   constexpr int CH = F8 ? 128 : 64;             // channels per chunk (128 bytes per halo position either way)
   constexpr int ES = F8 ? 1 : 2;                // bytes per element
   constexpr int HSI = F8 ? (HPOS + 64 * NW - 1) / (64 * NW) : 0;  // halo scale DMAs per wave per chunk
@@ -87,6 +102,7 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_h
   static_assert((F8 || HG * 8 * NW == HPOS) && HPOS % 8 == 0 && BG * NT == BN * 8, "halo / tile partition");
   constexpr int HGC = HG + HSI, BGC = BG + (F8 ? 1 : 0);  // DMAs per wave: one chunk's halo, one tap's weights
   static_assert(!F8 || (BN / NW == 16 && LDS_BYTES <= 163840 && BW != 3 && BW != 4), "fp8 halo: 16 weight rows per wave");
+  static_assert(LDS_BYTES <= 163840, "halo LDS");
   __shared__ __attribute__((aligned(1024))) u32x4 lds[LDS_BYTES / 16];
 
   const IgPhase& ph = p.ph[0];
@@ -253,7 +269,7 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_h
   };
 
   // ---- main loop over k-steps kt = chunk*9 + tap ----
-  // issue order: H(0) B(0) B(1) | per step j: [H(chunk(j)+1) if tap(j)==0] [B(j+2)]
+  // issue order: H(0) B(0) .. B(NBS-2) | per step j: [H(chunk(j)+1) if tap(j)==0] [B(j+NBS-1)]
   // BN-backward epilogue operands (y, mask bits, y2) of this thread's output rows, loaded at the start
   // of the last channel chunk (step kpre) so they arrive under its nine taps instead of after the loop
   // (one workgroup per CU: nothing else would hide that latency). NLD = the loads that certainly
@@ -267,20 +283,32 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_h
   issue_halo(0);
   issue_b(0);
   if (nk > 1) issue_b(1);
+  if (NBS > 3 && nk > 2) issue_b(2);
   for (int kt = 0; kt < nk; ++kt) {
     const int t = kt % 9, cc = kt / 9;
     // loads allowed to stay in flight: everything issued after B(kt)
-    bool halo_after = false;
-    if (kt >= 1) {
-      const int j = kt - 1;
-      halo_after = (j % 9 == 0) && (j / 9 + 1 < nch);
+    if constexpr (NBS == 3) {
+      bool halo_after = false;
+      if (kt >= 1) {
+        const int j = kt - 1;
+        halo_after = (j % 9 == 0) && (j / 9 + 1 < nch);
+      }
+      const bool b_after = kt + 1 < nk;
+      const bool after_pre = PRE && kt == kpre + 1;  // the prefetch went out after B(kt)
+      if (halo_after && b_after) waitvm<HGC + BGC>();
+      else if (halo_after) waitvm<HGC>();
+      else if (b_after) { if (after_pre) waitvm<BGC + NLD>(); else waitvm<BGC>(); }
+      else waitvm<0>();
+    } else {
+      // after B(kt): B(kt+1) .. B(kt+NBS-2) and the halos steps kt-NBS+2 .. kt-1 issued (at most one: a
+      // halo goes out at tap 0 of a chunk), and the epilogue prefetch of step kpre
+      const int nb = min(NBS - 2, nk - 1 - kt);
+      int nh = 0;
+#pragma unroll
+      for (int j = kt - (NBS - 2); j < kt; ++j) nh += (j >= 0 && j % 9 == 0 && j / 9 + 1 < nch) ? 1 : 0;
+      const int npre = (PRE && kpre >= 0 && kt > kpre && kt <= kpre + NBS - 2) ? NLD : 0;
+      waitvm_le<(NBS - 2) * BGC + HGC + NLD>(nb * BGC + nh * HGC + npre);
     }
-    const bool b_after = kt + 1 < nk;
-    const bool after_pre = PRE && kt == kpre + 1;  // the prefetch went out after B(kt)
-    if (halo_after && b_after) waitvm<HGC + BGC>();
-    else if (halo_after) waitvm<HGC>();
-    else if (b_after) { if (after_pre) waitvm<BGC + NLD>(); else waitvm<BGC>(); }
-    else waitvm<0>();
     sbar();
     if constexpr (PRE) {
       if (kt == kpre) {
@@ -293,7 +321,7 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_h
       }
     }
     if (t == 0 && cc + 1 < nch) issue_halo(cc + 1);
-    if (kt + 2 < nk) issue_b(kt + 2);
+    if (kt + NBS - 1 < nk) issue_b(kt + NBS - 1);
     compute(kt);
   }
   waitvm<0>();
@@ -388,24 +416,26 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_h
   }
 }
 
-template <int BN, int BW, int HB, bool F8>
+// the demangled instantiation name (as rocprofv3 reports it: the kernel timer's labels join the PMC summaries)
+template <int BN, int BW, int HB, bool F8, bool DEEP>
 static const char* halo_name() {
   static const std::string s = std::string("argus::conv3x3_halo_kernel<") + std::to_string(BN) + ", " +
-                               std::to_string(BW) + ", " + std::to_string(HB) + (F8 ? ", true>" : ">");
+                               std::to_string(BW) + ", " + std::to_string(HB) + (F8 ? ", true" : ", false") +
+                               (DEEP ? ", true>" : ", false>");
   return s.c_str();
 }
 
 // The BN-backward epilogue operands of the halo dgrad are prefetched under its last channel chunk on
 // the single-buffer 64-column variant (layer 1: 172 -> 163 us); on the 128-column one it measured
 // 83 -> 100 us (the step within noise), so that variant loads them after the loop.
-template <int BN, int BW, int HB, bool F8 = false>
+template <int BN, int BW, int HB, bool F8 = false, bool DEEP = false>
 static void launch_halo2(const IgParams& p0, hipStream_t st) {
   IgParams p = p0;
   p.epi_pre = HB == 1;
   plan_fin(p, 256);
   dim3 grid(conv3x3_halo_tiles(p) * (p.N / BN));
-  timed_launch(halo_name<BN, BW, HB, F8>(), conv3x3_halo_kernel<BN, BW, HB, F8>, grid, dim3(4 * (BN / 64) * 64),
-               st, p);
+  timed_launch(halo_name<BN, BW, HB, F8, DEEP>(), conv3x3_halo_kernel<BN, BW, HB, F8, DEEP>, grid,
+               dim3(4 * (BN / 64) * 64), st, p);
 }
 
 template <int BN, int BW>
@@ -416,11 +446,16 @@ static void launch_halo1(const IgParams& p, hipStream_t st) {
       return;
     }
   }
+  const int HWi = p.H * p.W;
+  const int npos = HWi >= 256 ? (256 / p.W + 2) * (p.W + 2) : (256 / HWi) * (p.H + 2) * (p.W + 2);
   if constexpr (BN == 64) {
-    const int HWi = p.H * p.W;
-    const int npos = HWi >= 256 ? (256 / p.W + 2) * (p.W + 2) : (256 / HWi) * (p.H + 2) * (p.W + 2);
     if (p.Cin == 64 && npos <= kHaloPos1) {  // one channel chunk: one halo buffer, two workgroups per CU
       launch_halo2<BN, BW, 1>(p, st);
+      return;
+    }
+  } else {
+    if ((*p.pol)[kHaloDeepRing] && npos <= kHaloPosDeep) {  // key 51: the four-stage weight ring
+      launch_halo2<BN, BW, 2, false, true>(p, st);
       return;
     }
   }

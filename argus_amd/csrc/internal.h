@@ -64,7 +64,8 @@ enum TuneKey : int {
   kWgradDmaStages = 48,   // LDS ring stages of the 128 x 256 apply DMA weight gradient (2..5)
   kDgradApMaxCols = 49,   // 1x1 dgrads stage the apply prologue up to this many 128-column tiles (0: any)
   kWgradFold = 50,        // DMA weight gradients reduce their split partials in-launch (1 on)
-  kNumTuneKeys = 51
+  kHaloDeepRing = 51,     // 3x3 halo fwd / dgrad (128 columns, <= 384 halo positions): four weight stages (1 on)
+  kNumTuneKeys = 52
 };
 struct Policy {
   int v[kNumTuneKeys];

@@ -438,10 +438,10 @@ def main() -> None:
         }
 
     # the dominant kernel's own MFMA roof: MX-fp8 igemm variants (template flag 32) and the fp8 halo
-    # kernel (its last template argument true) run at the dense fp8 rate; in an "fp8" run the weight
+    # kernel (its fourth template argument, F8, true) run at the dense fp8 rate; in an "fp8" run the weight
     # gradients and the 64-channel convs stay bf16
     f8_kernel = ((dom.startswith("argus::igemm_kernel<") and int(dom.rstrip(">").split(",")[-1]) >= 32) or
-                 (dom.startswith("argus::conv3x3_halo_kernel<") and dom.endswith(", true>")))
+                 (dom.startswith("argus::conv3x3_halo_kernel<") and dom.rstrip(">").split(", ")[3] == "true"))
     peak_flops = (FP8_DENSE_PEAK_TFLOPS if f8_kernel else
                   BF16_DENSE_PEAK_TFLOPS if args.dtype in ("bf16", "fp8") else F32_MFMA_PEAK_TFLOPS)
     tflops = ks["flops_per_launch"] / (ks["avg_us"] * 1e-6) / 1e12

@@ -50,7 +50,7 @@ def test_bad_arguments_are_reported():
     assert L.dll.argus_conv_policy_default(99) == -1 and L.dll.argus_conv_policy_default(20) == -1
     assert L.dll.argus_conv_policy_default(35) == 16384 and L.dll.argus_conv_policy_default(7) == 1024
     assert 0 <= L.dll.argus_conv_policy_default(37) <= 15
-    assert L.dll.argus_conv_policy_default(45) in (0, 1, 2, 3) and L.dll.argus_conv_policy_default(51) == -1
+    assert L.dll.argus_conv_policy_default(45) in (0, 1, 2, 3) and L.dll.argus_conv_policy_default(52) == -1
     assert L.dll.argus_conv_policy_default(48) == 4 and L.dll.argus_conv_policy_default(47) == 131072
     # key 49: a 1x1 dgrad stages its apply prologue only up to that many 128-column tiles (host-only query)
     assert L.dll.argus_conv_policy_default(49) == 4 and L.dll.argus_conv_policy_default(50) == 0

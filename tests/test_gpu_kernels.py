@@ -706,16 +706,65 @@ HALO_SHAPES = [  # (cin, cout, hw, n): 256-pixel tiles = 4 rows / 8 rows / 1 ima
 ]
 
 
-def test_conv3x3_halo_kernel_parity(cuda):
+@pytest.mark.parametrize("deep", [0, 1])
+def test_conv3x3_halo_kernel_parity(cuda, deep):
     """3x3 stride-1 LDS-halo kernel vs torch (bf16): forward with BN partials at 64- and 128-row tiles,
     dgrad with in-place and masked addends; the kernel timer confirms the halo kernel served every
     call, and a forward with a BN+ReLU prologue (bf16 inputs are materialised by the benched schedule)
-    is served by the register-staged kernel instead."""
+    is served by the register-staged kernel instead. deep = policy key 51 (the four-stage weight ring on
+    384-position halo images where the halo fits)."""
     from argus_amd.profiling import KernelTimer
 
     torch.manual_seed(13)
     L = lib()
-    _halo_cases(L, cuda, {13: 1})  # force the halo kernel on every eligible shape
+    _halo_cases(L, cuda, {13: 1, 51: deep})  # force the halo kernel on every eligible shape
+
+
+def test_halo_deep_ring_bit_identical(cuda):
+    """Policy key 51 (conv_halo.hip: 384-position halo images, four weight stages in the ring) changes
+    only how far ahead the weight taps are fetched: the forward's y and BN partials, and the data
+    gradient's dm, BN-backward partials and folded finalize outputs are bit-identical to the
+    three-stage kernel's, and the deep instantiation ran where the halo fits (<= 384 positions)."""
+    from argus_amd._lib import BnBwdEpilogue
+    from argus_amd.profiling import KernelTimer
+
+    torch.manual_seed(51)
+    L = lib()
+    for cin, cout, hw, n in [(128, 128, 32, 2), (256, 256, 16, 2), (64, 128, 16, 2), (256, 128, 16, 3)]:
+        d0, _ = _desc(n, hw, hw, cin, cout, 3, 1)
+        w = torch.randn(cout, 3, 3, cin) * (2.0 / (9 * cin)) ** 0.5
+        x = (torch.randn(n, hw, hw, cin) * 1.5 + 0.2).to(cuda, torch.bfloat16)
+        dy = torch.randn(n, hw, hw, cout).to(cuda, torch.bfloat16)
+        yb = torch.randn(n, hw, hw, cin).to(cuda, torch.bfloat16)
+        mean, invstd = torch.randn(cin, device=cuda) * 0.1, torch.rand(cin, device=cuda) + 0.5
+        sc, sh = torch.randn(cin, device=cuda), torch.randn(cin, device=cuda)
+        gamma = torch.rand(cin, device=cuda) + 0.5
+        outs = []
+        for key in (0, 1):
+            d = d0.with_tuning({13: 1, 51: key})
+            wf, wt = _prep(d, "bf16", w.to(cuda), cuda)
+            rows = L.dll.argus_conv_fwd_stat_rows(C.byref(d), BF16)
+            stats = torch.zeros(rows, cout, 2, device=cuda)
+            y = torch.empty(n, hw, hw, cout, dtype=torch.bfloat16, device=cuda)
+            brows = L.dll.argus_conv_dgrad_bn_rows(C.byref(d), BF16)
+            part = torch.zeros(brows, cin, 2, device=cuda)
+            ws = torch.zeros(L.dll.argus_bn_workspace_bytes(cin), dtype=torch.uint8, device=cuda)
+            fin = torch.full((5, cin), float("nan"), device=cuda)
+            dm = torch.empty(n, hw, hw, cin, dtype=torch.bfloat16, device=cuda)
+            e = BnBwdEpilogue()
+            e.y, e.mean, e.invstd, e.mask_mode, e.scale, e.shift, e.part = ptr(yb), ptr(mean), ptr(invstd), 2, \
+                ptr(sc), ptr(sh), ptr(part)
+            e.workspace, e.gamma = ptr(ws), ptr(gamma)
+            e.dgamma, e.dbeta, e.ca, e.cb, e.cc = (ptr(fin[i]) for i in range(5))
+            with KernelTimer("argus::conv3x3_halo_kernel") as t:
+                L.conv_fwd(C.byref(d), BF16, ptr(x), ptr(wf), ptr(y), None, None, ptr(stats), stream())
+                L.conv_dgrad_bn(C.byref(d), BF16, ptr(dy), ptr(wt), ptr(dm), None, C.byref(e), None, stream())
+            torch.cuda.synchronize()
+            names = list(t.summary())
+            assert len(names) == 2 and all(nm.endswith(", true>" if key else ", false>") for nm in names), names
+            outs.append((y.view(torch.int16).cpu(), stats.cpu(), dm.view(torch.int16).cpu(), part.cpu(), fin.cpu()))
+        for a, b in zip(*outs):
+            assert torch.equal(a, b), (cin, cout, hw, n)
 
 
 def test_layer1_3x3_on_single_buffer_halo_kernel(cuda):
@@ -738,7 +787,7 @@ def test_layer1_3x3_on_single_buffer_halo_kernel(cuda):
     ref_y = F.conv2d(xr, wr, padding=1).permute(0, 2, 3, 1)
     ref_dx = torch.nn.grad.conv2d_input(xr.shape, wr, _q(dy, "bf16").permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
     outs = {}
-    for key10, kname in ((1, "conv3x3_halo_kernel<64, 0, 1>"), (0, "igemm_kernel")):
+    for key10, kname in ((1, "conv3x3_halo_kernel<64, 0, 1,"), (0, "igemm_kernel")):
         dk = d.with_tuning({10: key10})
         rows = L.dll.argus_conv_fwd_stat_rows(C.byref(dk), BF16)
         stats = torch.empty(rows, c, 2, device=cuda)
@@ -751,7 +800,7 @@ def test_layer1_3x3_on_single_buffer_halo_kernel(cuda):
         names = list(t.summary())
         assert any(kname in nm for nm in names), (key10, names)
         if key10:
-            assert any("conv3x3_halo_kernel<64, 0, 1>" in nm for nm in names) and len(names) == 1, names
+            assert any("conv3x3_halo_kernel<64, 0, 1," in nm for nm in names) and len(names) == 1, names
         assert _rel(y, ref_y) < TOL["bf16"] and _rel(dx, ref_dx) < TOL["bf16"], key10
         outs[key10] = (y.float(), dx.float())
     assert _rel(outs[1][0], outs[0][0]) < 1e-2 and _rel(outs[1][1], outs[0][1]) < 1e-2
