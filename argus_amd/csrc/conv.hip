@@ -1325,10 +1325,16 @@ static const Policy kDefaultPolicy = [] {
   p.v[kDgradApMaxCols] = 4;
   // 50: the LDS-DMA weight gradients sum their split partials inside the launch (reducing workgroups
   //     after the compute grid, conv_wgdma.hip) instead of a wgrad_reduce launch; the caller's workspace
-  //     must end in kWgFoldCtrBytes of zeros (argus_conv_wgrad_workspace_bytes includes them)
+  //     must end in kWgFoldCtrBytes of zeros (argus_conv_wgrad_workspace_bytes includes them). Engine
+  //     A/B at B=64: 14.50 vs 13.78-13.85 ms (profiles/r06a_ab_keys.txt): the reducing workgroups wait
+  //     for their tile's last split while holding a CU's LDS, and the write-through partials leave L2:
+  //     off (dW bit-identical either way)
   p.v[kWgradFold] = 0;
   // 51: the 3x3 halo forward / data gradient (128-column tiles) with a four-stage weight ring on
-  //     384-position halo images where the tile's halo fits (the 32- and 16-wide layers at 256 x 256)
+  //     384-position halo images where the tile's halo fits (the 32- and 16-wide layers at 256 x 256):
+  //     alone (tools/dgradbench.py --convs conv2, B=64) layer 2 51.5 / 68.5 vs 51.6 / 68.9 us (plain /
+  //     BN epilogue + fold), layer 3 43.4 vs 43.9 us; engine A/B level at B=64 and B=256
+  //     (profiles/r06d_*): off. The halo loop is not waiting on weight stages in flight
   p.v[kHaloDeepRing] = 0;
   return p;
 }();

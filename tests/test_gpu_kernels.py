@@ -1711,7 +1711,7 @@ def test_conv_x8_halo_fwd_dgrad(cuda):
             if name == "x8":
                 with KernelTimer("argus::conv3x3_halo_kernel") as t:
                     L.conv_dgrad_bn_x8(C.byref(d), ptr(dy8), ptr(wd), ptr(dm), C.byref(e_), stream())
-                assert any(nm.endswith(", 2, 2, true>") for nm in t.summary()), list(t.summary())
+                assert any(nm.endswith(", 2, 2, true, false>") for nm in t.summary()), list(t.summary())
             else:
                 L.conv_dgrad_bn(C.byref(d), FP8, ptr(dy), ptr(wd), ptr(dm), None, C.byref(e_), None, stream())
             outs[name] = (dm, coef)
