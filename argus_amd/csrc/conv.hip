@@ -1301,8 +1301,10 @@ static const Policy kDefaultPolicy = [] {
   // 45: 1x1 bf16 weight gradients on the LDS-DMA ring kernel of conv_wgdma.hip with 128 x 128 tiles (1),
   //     128 x 256 tiles where Cin % 256 == 0 for the apply variant (2) or both (3), or the
   //     register-staged wgrad_kernel (0): engine A/B 2 vs 0: B=256 46.05-46.21 vs 46.54-46.57 ms,
-  //     376x672 89.6-89.9 vs 90.6-91.2 ms, B=64 within drift (profiles/r05ai_ab_key45_*.txt)
-  p.v[kWgradDma] = 2;
+  //     376x672 89.6-89.9 vs 90.6-91.2 ms, B=64 within drift (profiles/r05ai_ab_key45_*.txt). Round 6: 3
+  //     (key 49 = 4 sends layer 3-4 conv1 weight gradients to the plain form): B=64 13.34-13.36 vs
+  //     13.39-13.40 ms best of 4, B=256 and 376x672 level (profiles/r06e_*, r06f_*)
+  p.v[kWgradDma] = 3;
   // 46: 1x1 weight gradients over at most this many pixels take half the split target (256): engine
   //     A/B at B=64 (layers 2-4) 13.69-13.74 vs 13.79-13.85 ms, B=256 (layers 3-4) 46.95-47.01 vs
   //     47.02-47.07, 376x672 (layer 4) within drift; 262144 no better; a global target of 256 gains
