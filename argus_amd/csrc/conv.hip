@@ -1259,7 +1259,11 @@ static const Policy kDefaultPolicy = [] {
   p.v[kGldsMinGrid] = 256;
   p.v[kHaloEnable] = 1;
   p.v[kWgHaloEnable] = 1;
-  p.v[kWgHaloTarget] = 256;
+  // 12: split target of the 3x3 halo weight gradient: 128 (round 6; 256 before): engine A/B, best of 3
+  //     interleaved rounds, B=64 13.24 vs 13.48-13.54 ms, B=256 45.49 vs 45.63-45.66 ms, 376x672 88.27 vs
+  //     88.06-88.39 ms; 64 slower, 192 between (profiles/r06h_*, r06i_*). Half the workgroups hold the CUs
+  //     beside the main stream's chain for longer, and write half the fp32 split partials
+  p.v[kWgHaloTarget] = 128;
   p.v[kHaloMinGrid] = 256;
   // 14: the halo weight gradient for 3x3 convs of up to 64 (64 x 64) channel tiles, i.e. every layer
   //     (round 4; 4 = layers 1-2 only before): engine A/B 13.86-14.05 vs 14.07-14.20 ms (B=64),
