@@ -18,7 +18,7 @@ import torch  # noqa: F401  (must precede the CDLL, see module docstring)
 LIB_PATH = Path(os.environ.get("ARGUS_HIP_LIB", Path(__file__).resolve().parent / "libargus_hip.so"))
 
 F32, BF16, FP8 = 0, 1, 2
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 
 class Tuning(C.Structure):
@@ -60,6 +60,15 @@ class BnBwdEpilogue(C.Structure):
                 ("y_k", C.c_int32), ("reserved2", C.c_int32)]
 
 
+class BnFwdFin(C.Structure):
+    """argus_bn_fwd_fin (include/argus_hip.h): the train-mode BN finalize of argus_conv_fwd_fin."""
+
+    _fields_ = [("workspace", C.c_void_p), ("gamma", C.c_void_p), ("beta", C.c_void_p), ("eps", C.c_float),
+                ("momentum", C.c_float), ("running_mean", C.c_void_p), ("running_var", C.c_void_p),
+                ("num_batches_tracked", C.c_void_p), ("mean", C.c_void_p), ("invstd", C.c_void_p),
+                ("scale", C.c_void_p), ("shift", C.c_void_p)]
+
+
 class BnBwdPrologue(C.Structure):
     """argus_bn_bwd_prologue (include/argus_hip.h)."""
 
@@ -91,6 +100,7 @@ SIGNATURES = {
     "argus_conv_fwd_stats_only_rows": (_I, [_DESC, _I]),
     "argus_conv_fwd_stats_only_tile": (_I, [_DESC, _I]),
     "argus_conv_fwd_stat_part_bytes": (_SZ, [_DESC, _I, _I]),
+    "argus_conv_fwd_fin": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P, C.POINTER(BnFwdFin), _P]),
     "argus_conv_fwd_apply_out": (_I, [_DESC, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "argus_conv_fwd_x8": (_I, [_DESC, _P, _P, _P, _P, _P]),
     "argus_conv_dgrad_bn_x8": (_I, [_DESC, _P, _P, _P, C.POINTER(BnBwdEpilogue), _P]),

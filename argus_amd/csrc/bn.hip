@@ -782,7 +782,10 @@ int argus_bn_finalize(int C, int rows, int tile_rows, const float* part, int64_t
   a.red = reinterpret_cast<double2*>(reinterpret_cast<char*>(ws) + kBnCounterBytes);
   a.gamma = gamma; a.beta = beta; a.eps = eps; a.momentum = momentum; a.running_mean = rm; a.running_var = rv;
   a.nbt = nbt; a.mean_o = mean; a.invstd_o = invstd; a.scale_o = scale; a.shift_o = shift;
-  hipLaunchKernelGGL(stats_finalize_kernel, dim3((C + 63) / 64, a.G), dim3(64 * kFinLanes), 0, st, a);
+  g_launch_work = 0.0;  // algorithmic bytes: the {sum, M2} partials read
+  g_launch_bytes = 8.0 * rows * C;
+  timed_launch("argus::stats_finalize_kernel", stats_finalize_kernel, dim3((C + 63) / 64, a.G), dim3(64 * kFinLanes),
+               st, a);
   return check_launch("stats_finalize_kernel");
 }
 

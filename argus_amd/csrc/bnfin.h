@@ -179,6 +179,176 @@ ARGUS_DEV void bn_fin_arrive(const BnFin& f, int t, int nt, double2* scratch, in
   }
 }
 
+// ---- the forward statistics finalize folded into the producing conv (argus_conv_fwd_fin) ----------
+// Producer partial rows float2{sum, M2 about the row's own mean}, row r of n_r pixels (tile_rows, the
+// last row the remainder; tile_rows < 0: int32 counts[rows] after the partials). The merge repeats
+// stats_finalize_kernel (bn.hip) operation for operation, so mean / invstd / scale / shift and the running
+// statistics are bit-identical to argus_bn_finalize's: its G = reduce_groups(rows) groups of rpg rows
+// (here gt = rpg / rpw producer tiles a group; planned on the host only where rpg % rpw == 0), and in a
+// group and over the groups 4 row lanes (lane l: rows / groups l, l + 4, ... in order; lanes added in
+// order), every row's contribution S += sum, Q += M2 + sum^2 / n_r in fp64.
+struct BnFwdFin {
+  int mode;          // 0 off, 1 on
+  int T, rpw;        // producer row tiles, partial rows per tile (row of tile t, k = t * rpw + k)
+  int rows, C;       // partial rows, channels
+  int gt, ng, G;     // tiles per group, groups with rows, stats_finalize_kernel's group count (>= ng)
+  int tile_rows;     // pixels per full row (< 0: counts after the partials)
+  long long count;   // pixels per channel
+  unsigned* cnt;     // [C / 64][ng + 1] tickets (argus_bn_workspace_bytes workspace, zero between calls)
+  double2* red;      // [ng][C]
+  const float2* part;
+  const float *gamma, *beta;
+  float eps, momentum;
+  float *running_mean, *running_var;
+  long long* nbt;
+  float *mean_o, *invstd_o, *scale_o, *shift_o;
+};
+
+ARGUS_DEV void fin_forward(const BnFwdFin& f, int c, double2 tot) {
+  const double count = (double)f.count;
+  const double mean = tot.x / count;
+  double m2 = tot.y - tot.x * mean;
+  if (m2 < 0.0) m2 = 0.0;
+  const double var = m2 / count;
+  const float invstd = (float)(1.0 / sqrt(var + (double)f.eps));
+  const float sc = f.gamma[c] * invstd;
+  if (f.mean_o) f.mean_o[c] = (float)mean;
+  if (f.invstd_o) f.invstd_o[c] = invstd;
+  if (f.scale_o) f.scale_o[c] = sc;
+  if (f.shift_o) f.shift_o[c] = f.beta[c] - (float)mean * sc;
+  if (f.running_mean) f.running_mean[c] = (1.f - f.momentum) * f.running_mean[c] + f.momentum * (float)mean;
+  if (f.running_var) {
+    const double unbiased = count > 1.0 ? m2 / (count - 1.0) : var;
+    f.running_var[c] = (1.f - f.momentum) * f.running_var[c] + f.momentum * (float)unbiased;
+  }
+}
+
+// Called by every thread of a producer workgroup (NT threads) after its partial rows are stored
+// write-through (store_part): tile t, column tile nt of width COLS. scratch: LDS of >= 4 * COLS * 16
+// bytes (reused; the caller is done with it) and an int flag. 4 * COLS threads take part in the merges.
+template <int NT, int COLS>
+ARGUS_DEV void bn_fwd_fin_arrive(const BnFwdFin& f, int t, int nt, double2* scratch, int* flag) {
+  constexpr int CPT = 4 * COLS / NT < 1 ? 1 : 4 * COLS / NT;  // channels per thread (adjacent)
+  constexpr int TC = COLS / CPT;                               // threads per row lane
+  static_assert(CPT == 1 || CPT == 2, "one or two channels a thread");
+  static_assert(TC * 4 <= NT, "four row lanes per channel");
+  const int g = t / f.gt;
+  const int gsz = min(f.gt, f.T - g * f.gt);
+  unsigned* cnt = f.cnt + (size_t)nt * (f.ng + 1);
+  if (!fin_ticket(cnt + g, (unsigned)gsz, flag)) return;
+  const int cl = threadIdx.x % TC, lr = threadIdx.x / TC;  // lr < 4: the row lanes
+  const int c = nt * COLS + cl * CPT;
+  const bool act = lr < 4 && c < f.C;
+  const int tr = f.tile_rows < 0 ? -f.tile_rows : f.tile_rows;
+  const double inv_full = 1.0 / (double)tr;
+  const int* counts = f.tile_rows < 0 ? reinterpret_cast<const int*>(f.part + (size_t)f.rows * f.C) : nullptr;
+  // level 1: the group's rows [r0, r1)
+  const int r0 = g * f.gt * f.rpw, r1 = min(f.rows, (g * f.gt + gsz) * f.rpw);
+  double S[CPT], Q[CPT];
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) { S[k] = 0.0; Q[k] = 0.0; }
+  if (act)
+    for (int rb = r0 + lr; rb < r1; rb += 4 * kLoadBatch) {
+      float2 v[kLoadBatch][CPT];
+      int nr[kLoadBatch];
+#pragma unroll
+      for (int u = 0; u < kLoadBatch; ++u) {
+        const float2* src = f.part + (size_t)min(rb + 4 * u, r1 - 1) * f.C + c;
+        if constexpr (CPT == 2) {
+          const f32x4 q4 = *reinterpret_cast<const f32x4*>(src);
+          v[u][0] = make_float2(q4.x, q4.y);
+          v[u][CPT - 1] = make_float2(q4.z, q4.w);
+        } else {
+          v[u][0] = *src;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kLoadBatch; ++u) nr[u] = counts ? counts[min(rb + 4 * u, r1 - 1)] : tr;
+#pragma unroll
+      for (int u = 0; u < kLoadBatch; ++u) {
+        const int r = rb + 4 * u;
+        const long long left = f.count - (long long)r * tr;
+        const double inv = counts ? (nr[u] > 0 ? 1.0 / (double)nr[u] : 0.0)
+                                  : (left >= tr ? inv_full : 1.0 / (double)left);
+        const bool ok = r < r1;  // selects, not branches (common.h kLoadBatch)
+#pragma unroll
+        for (int k = 0; k < CPT; ++k) {
+          S[k] += ok ? (double)v[u][k].x : 0.0;
+          Q[k] += ok ? (double)v[u][k].y + (double)v[u][k].x * (double)v[u][k].x * inv : 0.0;
+        }
+      }
+    }
+#pragma unroll
+  for (int k = 0; k < CPT; ++k)
+    if (lr < 4) scratch[lr * COLS + cl * CPT + k] = make_double2(S[k], Q[k]);
+  __syncthreads();
+  if (lr == 0 && act) {
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+      double2 a = scratch[cl * CPT + k];
+      for (int i = 1; i < 4; ++i) { a.x += scratch[i * COLS + cl * CPT + k].x; a.y += scratch[i * COLS + cl * CPT + k].y; }
+      store_wt2(f.red + (size_t)g * f.C + c + k, a);
+    }
+  }
+  __syncthreads();
+  // level 2: the G group slots in order (those past the ng groups with rows hold zeros in
+  // stats_finalize_kernel: the masked +0.0 here)
+  if (!fin_ticket(cnt + f.ng, (unsigned)f.ng, flag)) return;
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) { S[k] = 0.0; Q[k] = 0.0; }
+  if (act)
+    for (int gb = lr; gb < f.G; gb += 4 * kLoadBatch) {
+      double2 v[kLoadBatch][CPT];
+#pragma unroll
+      for (int u = 0; u < kLoadBatch; ++u)
+#pragma unroll
+        for (int k = 0; k < CPT; ++k) v[u][k] = f.red[(size_t)min(gb + 4 * u, f.ng - 1) * f.C + c + k];
+#pragma unroll
+      for (int u = 0; u < kLoadBatch; ++u) {
+        const bool ok = gb + 4 * u < f.ng;
+#pragma unroll
+        for (int k = 0; k < CPT; ++k) {
+          S[k] += ok ? v[u][k].x : 0.0;
+          Q[k] += ok ? v[u][k].y : 0.0;
+        }
+      }
+    }
+#pragma unroll
+  for (int k = 0; k < CPT; ++k)
+    if (lr < 4) scratch[lr * COLS + cl * CPT + k] = make_double2(S[k], Q[k]);
+  __syncthreads();
+  if (nt == 0 && threadIdx.x == 0 && f.nbt) f.nbt[0] += 1;
+  if (lr == 0 && act) {
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+      double2 a = scratch[cl * CPT + k];
+      for (int i = 1; i < 4; ++i) { a.x += scratch[i * COLS + cl * CPT + k].x; a.y += scratch[i * COLS + cl * CPT + k].y; }
+      fin_forward(f, c + k, a);
+    }
+  }
+}
+
+// a ragged producer's int32 row count, stored write-through (the fold reads it from another CU)
+ARGUS_DEV void store_count(int* p, int n) {
+  __hip_atomic_store((__attribute__((address_space(1))) int*)p, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// host: the fold's groups for a producer of T row tiles with rpw partial rows each (rows = its partial
+// rows): stats_finalize_kernel's grouping, false where a group boundary would split a producer tile
+// (the caller then launches argus_bn_finalize instead)
+inline bool bn_fwd_fin_plan(BnFwdFin& f, int T, int rpw, int rows) {
+  const int G = rows < 64 ? 1 : (rows < 512 ? 8 : (rows < 4096 ? 32 : 64));  // bn.hip reduce_groups
+  const int rpg = (rows + G - 1) / G;
+  if (rpg % rpw || (long long)T * rpw < rows) return false;
+  f.T = T;
+  f.rpw = rpw;
+  f.rows = rows;
+  f.G = G;
+  f.gt = rpg / rpw;
+  f.ng = (T + f.gt - 1) / f.gt;
+  return f.ng <= G;
+}
+
 // host: plan the groups of a producer with T row tiles of rpw partial rows each
 inline void bn_fin_plan(BnFin& f, int T, int rpw) {
   f.T = T;

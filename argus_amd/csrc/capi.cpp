@@ -27,7 +27,7 @@ using namespace argus;
 
 extern "C" {
 
-int argus_abi_version(void) { return 17; }
+int argus_abi_version(void) { return 18; }
 
 const char* argus_last_error(void) { return g_last_error.c_str(); }
 
@@ -67,6 +67,24 @@ int argus_conv_fwd(const argus_conv_desc* d, int dtype, const void* x, const voi
     return ARGUS_ERR_ARG;
   }
   return conv_fwd(*d, dtype, x, w, y, sc, sh, stats, (hipStream_t)stream);
+}
+
+int argus_conv_fwd_fin(const argus_conv_desc* d, int dtype, const void* x, const void* w, void* y, const float* sc,
+                       const float* sh, float* stats, const argus_bn_fwd_fin* fin, argus_stream_t stream) {
+  if (!d || !x || !w || !stats || !fin || !fin->workspace || !fin->gamma || !fin->beta ||
+      (sc == nullptr) != (sh == nullptr)) {
+    set_error("conv_fwd_fin: bad arguments");
+    return ARGUS_ERR_ARG;
+  }
+  if (int e = conv_fwd(*d, dtype, x, w, y, sc, sh, stats, (hipStream_t)stream, nullptr, fin)) return e;
+  if (g_ffin_folded) return ARGUS_OK;
+  // not folded (the producer's tiles do not align with the merge groups): the separate finalize
+  const bool so = y == nullptr && sc == nullptr;
+  const int rows = so ? conv_fwd_stats_only_rows(*d, dtype) : conv_fwd_stat_rows(*d, dtype);
+  const int tile = so ? conv_fwd_stats_only_tile(*d, dtype) : conv_fwd_stat_tile(*d, dtype == ARGUS_FP8 ? ARGUS_BF16 : dtype);
+  return argus_bn_finalize(d->k, rows, tile, stats, (int64_t)d->n * d->ho * d->wo, fin->gamma, fin->beta, fin->eps,
+                           fin->momentum, fin->running_mean, fin->running_var, fin->num_batches_tracked, fin->mean,
+                           fin->invstd, fin->scale, fin->shift, fin->workspace, stream);
 }
 
 int argus_conv_fwd_apply_out(const argus_conv_desc* d, int dtype, const void* x, const void* w, void* y,

@@ -473,6 +473,10 @@ __global__ __launch_bounds__(256, OCC) void igemm_kernel(const IgParams p) {
       store_part(p.stats + (size_t)mt * p.N + nt * BN + tid, make_float2(a0.x + a1.x, m2));
     }
     __syncthreads();
+    if (p.ffin.mode) {  // the statistics finalize folded in (bnfin.h): one partial row per row tile
+      bn_fwd_fin_arrive<256, BN>(p.ffin, mt, nt, reinterpret_cast<double2*>(lds), &fin_flag);
+      __syncthreads();
+    }
   }
   if constexpr (BW == 0 && !OUT) {
     if (!p.c) return;  // statistics-only forward (argus_conv_fwd with y == NULL)
@@ -1186,6 +1190,7 @@ template <typename T, int BM, int BN, bool STEM, bool PRO, int OCC, int BW = 0>
 static void launch_ig(const IgParams& p0, int maxM, hipStream_t st) {
   IgParams p = p0;
   plan_fin(p, BM);
+  plan_ffin(p, BM);
   const int ntiles = p.N / BN;
   dim3 grid(cdiv(maxM, BM) * ntiles, 1, p.nphase);
   timed_launch(ig_name<T, BM, BN, STEM, PRO, OCC, BW>(), igemm_kernel<T, BM, BN, STEM, PRO, OCC, BW>, grid,
@@ -1509,8 +1514,11 @@ static void fwd_params(const argus_conv_desc& d, const Policy& pol, IgParams& p)
   }
 }
 
+thread_local int g_ffin_folded = 0;
+
 int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, void* y,
-             const float* sc, const float* sh, float* stats, hipStream_t st, void* pro_out) {
+             const float* sc, const float* sh, float* stats, hipStream_t st, void* pro_out,
+             const argus_bn_fwd_fin* fin) {
   if (int e = check_desc(d)) return e;
   if (pro_out && (!sc || d.stem || d.r != 1 || d.s != 1 || d.stride != 1 || d.pad != 0 || pro_out == x ||
                   dtype == ARGUS_FP8)) {
@@ -1537,12 +1545,28 @@ int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, 
     wp_f8_layouts(d, f8f, f8d);
     if (f8f) { set_error("conv_fwd: an fp8 forward takes no BN+ReLU prologue"); return ARGUS_ERR_ARG; }
   }
-  if (stem_lds_fwd(d, dtype, pol) && stem_fwd_launch(d, dtype, x, w, y, stats, st))  // stem.hip (bf16)
+  // argus_conv_fwd_fin: the statistics finalize, folded into the launch where its planner allows
+  g_ffin_folded = 0;
+  BnFwdFin ff{};
+  if (fin && stats) {
+    ff.mode = 1;
+    ff.C = d.k;
+    ff.count = (long long)d.n * d.ho * d.wo;
+    ff.cnt = reinterpret_cast<unsigned*>(fin->workspace);
+    ff.red = reinterpret_cast<double2*>(reinterpret_cast<char*>(fin->workspace) + kBnCounterBytes);
+    ff.gamma = fin->gamma; ff.beta = fin->beta; ff.eps = fin->eps; ff.momentum = fin->momentum;
+    ff.running_mean = fin->running_mean; ff.running_var = fin->running_var;
+    ff.nbt = reinterpret_cast<long long*>(fin->num_batches_tracked);
+    ff.mean_o = fin->mean; ff.invstd_o = fin->invstd; ff.scale_o = fin->scale; ff.shift_o = fin->shift;
+  }
+  const BnFwdFin* ffp = ff.mode ? &ff : nullptr;
+  if (stem_lds_fwd(d, dtype, pol) && stem_fwd_launch(d, dtype, x, w, y, stats, st, ffp))  // stem.hip (bf16)
     return check_launch("stem_fwd_kernel");
   if (!y && !sc && p1x1_fwd_stats_ok(d, dtype, pol[kP1x1FwdStats]))  // statistics only: conv_p1x1.hip
-    return p1x1_fwd_stats_launch(d, x, w, stats, st);
+    return p1x1_fwd_stats_launch(d, x, w, stats, st, ffp);
   IgParams p;
   fwd_params(d, pol, p);
+  p.ffin = ff;
   p.a = x; p.b = w; p.c = y; p.pro_scale = sc; p.pro_shift = sh; p.pro_out = pro_out;
   p.stats = reinterpret_cast<float2*>(stats);
   const int bm = fwd_bm(d, pol), bn = d.stem ? 64 : pick_bn(pol, 0, d.k);

@@ -240,6 +240,10 @@ __global__ __launch_bounds__((BM / 64) * (BN / 64) * 64, 1) void igemm_glds_kern
       store_part(p.stats + (size_t)(mt * HALVES + h) * p.N + nt * BN + col, make_float2(a0.x + a1.x, m2));
     }
     __syncthreads();
+    if (p.ffin.mode) {  // the statistics finalize folded in (bnfin.h): BM / stat_tile partial rows a tile
+      bn_fwd_fin_arrive<NT, BN>(p.ffin, mt, nt, reinterpret_cast<double2*>(lds), &fin_flag);
+      __syncthreads();
+    }
   }
 
   // ---- epilogue: stage the C tile in LDS, then 16-byte coalesced (+addend) stores ----
@@ -317,6 +321,7 @@ template <int BM, int BN, int BW, int NS>
 static void launch_glds1(const IgParams& p0, int maxM, hipStream_t st) {
   IgParams p = p0;
   plan_fin(p, BM);
+  plan_ffin(p, BM);
   dim3 grid(cdiv(maxM, BM) * (p.N / BN), 1, p.nphase);
   timed_launch(glds_name<BM, BN, BW, NS>(), igemm_glds_kernel<BM, BN, BW, NS>, grid,
                dim3((BM / 64) * (BN / 64) * 64), st, p);

@@ -368,6 +368,11 @@ __global__ __launch_bounds__(4 * (BN / 64) * 64, HB == 1 ? 2 : 1) void conv3x3_h
       }
     }
     __syncthreads();
+    if (p.ffin.mode) {  // the statistics finalize folded in (bnfin.h): 256 / stat_tile partial rows a tile
+      bn_fwd_fin_arrive<NT, BN>(p.ffin, mt, nt, reinterpret_cast<double2*>(lds),
+                                reinterpret_cast<int*>(reinterpret_cast<char*>(lds) + NT * 32));
+      __syncthreads();
+    }
   }
 
   // ---- epilogue: LDS-staged C tile, 16-byte coalesced (+addend) stores; output pixels are contiguous ----
@@ -433,6 +438,7 @@ static void launch_halo2(const IgParams& p0, hipStream_t st) {
   IgParams p = p0;
   p.epi_pre = HB == 1;
   plan_fin(p, 256);
+  plan_ffin(p, 256);
   dim3 grid(conv3x3_halo_tiles(p) * (p.N / BN));
   timed_launch(halo_name<BN, BW, HB, F8, DEEP>(), conv3x3_halo_kernel<BN, BW, HB, F8, DEEP>, grid,
                dim3(4 * (BN / 64) * 64), st, p);

@@ -280,6 +280,7 @@ struct P1FParams {
   float2* part;    // [G][N] {sum, M2}
   int* counts;     // [G] pixels per partial row (after the partials)
   int P, N, G, NB, tiles;
+  BnFwdFin ffin;   // the statistics finalize folded in (argus_conv_fwd_fin; ffin.mode != 0)
 };
 
 template <int K, int BNC>
@@ -438,7 +439,12 @@ __global__ __launch_bounds__(256) void p1x1_fwd_stats_kernel(const P1FParams p) 
       m2 = qa + qb + d * d * (na * nb_ / n);
     }
     store_part(p.part + (size_t)g0 * p.N + nb * BNC + tid, make_float2(sum, m2));
-    if (nb == 0 && tid == 0) p.counts[g0] = (int)n;
+    if (nb == 0 && tid == 0) store_count(p.counts + g0, (int)n);  // write-through (the folded finalize)
+  }
+  if (p.ffin.mode) {  // the statistics finalize folded in (bnfin.h): one partial row per row split
+    __shared__ int fin_flag;
+    __syncthreads();
+    bn_fwd_fin_arrive<256, BNC>(p.ffin, g0, nb, reinterpret_cast<double2*>(Al), &fin_flag);
   }
 }
 
@@ -474,7 +480,8 @@ int p1x1_fwd_stats_tile(const argus_conv_desc& d) {
   return ((tiles + G - 1) / G) * kP1BM;
 }
 
-int p1x1_fwd_stats_launch(const argus_conv_desc& d, const void* x, const void* w, float* stats, hipStream_t st) {
+int p1x1_fwd_stats_launch(const argus_conv_desc& d, const void* x, const void* w, float* stats, hipStream_t st,
+                          const BnFwdFin* ffin) {
   P1FParams p{};
   p.x = reinterpret_cast<const bf16*>(x);
   p.w = reinterpret_cast<const bf16*>(w);
@@ -485,6 +492,16 @@ int p1x1_fwd_stats_launch(const argus_conv_desc& d, const void* x, const void* w
   p.G = p1x1_fwd_stats_rows(d);
   p.part = reinterpret_cast<float2*>(stats);
   p.counts = reinterpret_cast<int*>(stats + (size_t)2 * p.G * p.N);
+  if (ffin) {  // the folded finalize: one ragged partial row per row split (argus_conv_fwd_fin)
+    p.ffin = *ffin;
+    if (bn_fwd_fin_plan(p.ffin, p.G, 1, p.G)) {
+      p.ffin.tile_rows = -p1x1_fwd_stats_tile(d);
+      p.ffin.part = p.part;
+      g_ffin_folded = 1;
+    } else {
+      p.ffin.mode = 0;
+    }
+  }
   const dim3 grid(p.G * p.NB);
   switch (d.c) {
     case 64: timed_launch("argus::p1x1_fwd_stats_kernel<64, 128>", p1x1_fwd_stats_kernel<64, 128>, grid, dim3(256), st, p); break;

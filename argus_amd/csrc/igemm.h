@@ -77,6 +77,7 @@ struct IgParams {
   IgPhase ph[4];
   BnBwdEpi bb;    // dgrad only
   BnFin fin;      // BN finalize folded into this launch (fin.mode != 0)
+  BnFwdFin ffin;  // forward: the statistics finalize folded into this launch (ffin.mode != 0, argus_conv_fwd_fin)
   BnApplyPro ap;  // dgrad only: the A operand is dm (ap.y != nullptr)
   BnOutEpi oe;    // forward only (kOutBit): the block output from the C tile
   int f8;         // ARGUS_FP8: MX-fp8 operands where the shape allows (host dispatch only)
@@ -283,6 +284,22 @@ inline void plan_fin(IgParams& p, int) {
   p.fin.rows = p.fin.T;
 }
 
+// host: plan the folded forward statistics finalize (p.ffin) of a producer with BM-row tiles, each
+// BM / p.stat_tile partial rows; mode 0 (argus_conv_fwd_fin then launches argus_bn_finalize) where the
+// fold's groups cannot repeat argus_bn_finalize's (bnfin.h bn_fwd_fin_plan)
+inline void plan_ffin(IgParams& p, int BM) {
+  if (!p.ffin.mode) return;
+  const int M = p.ph[0].M;
+  if (!p.stats || p.nphase != 1 || p.stat_tile <= 0 || BM % p.stat_tile ||
+      !bn_fwd_fin_plan(p.ffin, (M + BM - 1) / BM, BM / p.stat_tile, (M + p.stat_tile - 1) / p.stat_tile)) {
+    p.ffin.mode = 0;
+    return;
+  }
+  p.ffin.tile_rows = p.stat_tile;
+  p.ffin.part = p.stats;
+  g_ffin_folded = 1;
+}
+
 // host: the epilogue variant of a BnBwdEpi (0 when off)
 inline int bwd_variant(const BnBwdEpi& b) { return b.mode == 0 ? 0 : (b.mode == 2 ? 2 : (b.y2 ? 4 : 3)); }
 
@@ -319,7 +336,8 @@ bool p1x1_ok(const argus_conv_desc& d, int dtype);
 bool p1x1_fwd_stats_ok(const argus_conv_desc& d, int dtype, int enabled);
 int p1x1_fwd_stats_rows(const argus_conv_desc& d);
 int p1x1_fwd_stats_tile(const argus_conv_desc& d);
-int p1x1_fwd_stats_launch(const argus_conv_desc& d, const void* x, const void* w, float* stats, hipStream_t st);
+int p1x1_fwd_stats_launch(const argus_conv_desc& d, const void* x, const void* w, float* stats, hipStream_t st,
+                          const BnFwdFin* ffin = nullptr);
 // conv_wgdma.hip: 1x1 stride-1 bf16 weight gradients (optionally with the BN-backward apply) by LDS-DMA
 bool wgrad_dma_ok(const argus_conv_desc& d, int dtype, int bm, int bn, int enabled, bool ap, int gather_key);
 // its column-tile width (128 / 256) for the plain (ap false) or the apply form; 0 = not served
@@ -349,7 +367,7 @@ bool stem_fwd_ok(const argus_conv_desc& d, int dtype);
 int stem_stat_rows(const argus_conv_desc& d);
 bool stem_ragged(const argus_conv_desc& d);
 bool stem_fwd_launch(const argus_conv_desc& d, int dtype, const void* x, const void* w, void* y, float* stats,
-                     hipStream_t st);
+                     hipStream_t st, const BnFwdFin* ffin = nullptr);
 // stem weight gradient on the LDS patch + dy tile (stem.hip): split plan and launch of the fp32
 // partials [splits][64][256]; ap = the fused BN-backward apply (dy = ca*dm + cb*y + cc) or null
 bool stem_wgrad_plan(const argus_conv_desc& d, int dtype, int* splits, int* tiles_per_split);

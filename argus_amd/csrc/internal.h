@@ -16,7 +16,10 @@ int conv_fwd_bn_out(const argus_conv_desc& d, int dtype, const void* x, const vo
                     const float* sh, const void* res, const float* rsc, const float* rsh, void* out, uint8_t* bits,
                     void* y, hipStream_t st);
 int conv_fwd(const argus_conv_desc& d, int dtype, const void* x, const void* w, void* y,
-             const float* sc, const float* sh, float* stats, hipStream_t st, void* pro_out = nullptr);
+             const float* sc, const float* sh, float* stats, hipStream_t st, void* pro_out = nullptr,
+             const argus_bn_fwd_fin* fin = nullptr);
+// set by a forward launch that folded its statistics finalize (argus_conv_fwd_fin; conv.hip)
+extern thread_local int g_ffin_folded;
 int conv_fwd_stat_rows(const argus_conv_desc& d, int dtype);
 int conv_fwd_x8(const argus_conv_desc& d, const void* x8, const void* w, void* y, float* stats, hipStream_t st);
 int conv_dgrad_bn_x8(const argus_conv_desc& d, const void* dy8, const void* wt, void* dm, const argus_bn_bwd_epilogue* bn,

@@ -53,6 +53,7 @@ struct StemParams {
   float2* stats;   // {sum, M2} per 128 output pixels x 64 channels, or null
   int* counts;     // ragged tilings: pixels per partial row (after the partials), else null
   int n, H, W, Ho, Wo;
+  BnFwdFin ffin;   // the statistics finalize folded in (argus_conv_fwd_fin; ffin.mode != 0)
 };
 
 ARGUS_HOST_DEV inline int stem_tpr(int wo) { return (wo + kTW - 1) / kTW; }
@@ -186,10 +187,15 @@ __global__ __launch_bounds__(256, 3) void stem_fwd_kernel(const StemParams p) {
       store_part(p.stats + (tile_lin * 2 + h) * 64 + col, o);
       if (p.counts && col == 0) {
         const int n = full ? 128 : (min(max(vr - 4 * h, 0), 4) * vc);
-        p.counts[tile_lin * 2 + h] = n;
+        store_count(p.counts + tile_lin * 2 + h, n);  // write-through (the folded finalize)
       }
     }
     __syncthreads();
+    if (p.ffin.mode) {  // the statistics finalize folded in (bnfin.h): two partial rows a tile
+      __shared__ int fin_flag;
+      bn_fwd_fin_arrive<256, 64>(p.ffin, tile_lin, 0, reinterpret_cast<double2*>(lds), &fin_flag);
+      __syncthreads();
+    }
   }
 
   // ---- epilogue: C tile through LDS, 16-byte coalesced non-temporal stores ----
@@ -412,9 +418,21 @@ bool stem_fwd_ok(const argus_conv_desc& d, int dtype) { return stem_shape_ok(d, 
 // The partial-row layout this kernel writes is argus_conv_fwd_stat_rows / _stat_tile: stem_stat_rows
 // rows of 128 pixels (-128 when ragged: int32 pixel counts per row follow the float2[rows][64] partials)
 bool stem_fwd_launch(const argus_conv_desc& d, int dtype, const void* x, const void* w, void* y, float* stats,
-                     hipStream_t st) {
+                     hipStream_t st, const BnFwdFin* ffin) {
   if (!stem_fwd_ok(d, dtype)) return false;
   StemParams p;
+  p.ffin = BnFwdFin{};
+  if (ffin && stats) {  // the folded finalize: two partial rows a tile (argus_conv_fwd_fin)
+    p.ffin = *ffin;
+    const int T = d.n * stem_tpi(d.ho, d.wo);
+    if (bn_fwd_fin_plan(p.ffin, T, 2, stem_stat_rows(d))) {
+      p.ffin.tile_rows = stem_ragged(d) ? -128 : 128;
+      p.ffin.part = reinterpret_cast<const float2*>(stats);
+      g_ffin_folded = 1;
+    } else {
+      p.ffin.mode = 0;
+    }
+  }
   p.x = reinterpret_cast<const bf16*>(x);
   p.w = reinterpret_cast<const bf16*>(w);
   p.y = reinterpret_cast<bf16*>(y);

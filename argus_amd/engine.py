@@ -27,7 +27,7 @@ from dataclasses import dataclass
 
 import torch
 
-from argus_amd._lib import BF16, F32, FP8, BnBwdEpilogue, BnBwdPrologue, ConvDesc, lib, ptr, stream
+from argus_amd._lib import BnFwdFin, BF16, F32, FP8, BnBwdEpilogue, BnBwdPrologue, ConvDesc, lib, ptr, stream
 
 
 @dataclass(frozen=True)
@@ -117,6 +117,9 @@ class ResNetEngine:
         # the separate bwd_finalize kernels. The forward statistics keep their own
         # finalize launch (folding it into the conv measured neutral).
         self.fold_fin = True
+        # the forward BN statistics finalize folded into the producing conv's last workgroups
+        # (argus_conv_fwd_fin: bit-identical to argus_conv_fwd + argus_bn_finalize; round 6)
+        self.fold_fwd_fin = True
         # ... and the stem BN's finalize into the maxpool backward pass (argus_maxpool_bwd_bn_fin)
         self.fold_stem_fin = True
         self._side: torch.cuda.Stream | None = None
@@ -384,6 +387,17 @@ class ResNetEngine:
                               ptr(Bf[name + ".running_mean"]), ptr(Bf[name + ".running_var"]),
                               C.c_float(Bf.get(name + ".eps", 1e-5)), ptr(st[2]), ptr(st[3]), stream())
 
+    def _fwd_fin(self, P, Bf, name, ws):
+        """argus_bn_fwd_fin of BN ``name`` (the arguments _bn_train passes to argus_bn_finalize)."""
+        st = self.bn_state[name]
+        f = BnFwdFin()
+        f.workspace, f.gamma, f.beta = ptr(ws), ptr(P[name + ".weight"]), ptr(P[name + ".bias"])
+        f.eps, f.momentum = Bf.get(name + ".eps", 1e-5), Bf.get(name + ".momentum", 0.1)
+        f.running_mean, f.running_var = ptr(Bf[name + ".running_mean"]), ptr(Bf[name + ".running_var"])
+        f.num_batches_tracked = ptr(Bf[name + ".num_batches_tracked"])
+        f.mean, f.invstd, f.scale, f.shift = ptr(st[0]), ptr(st[1]), ptr(st[2]), ptr(st[3])
+        return f
+
     def _conv_bn(self, P, Bf, conv, bn, x, y, pro, training, part=None, ws=None, x8=None, x_out=None):
         """conv (+ BN statistics and finalize when training); ``x8``: the input's MX-fp8 copy
         (argus_conv_fwd_x8 instead of argus_conv_fwd); ``x_out``: where the prologue's applied input is
@@ -405,6 +419,11 @@ class ResNetEngine:
         elif x8 is not None:
             self._launch(cv, 0, lambda: self.L.conv_fwd_x8(C.byref(cv.desc), ptr(x8), ptr(cv.wf), ptr(y),
                                                             ptr(part) if training else None, stream()))
+        elif training and self.fold_fwd_fin:
+            fin = self._fwd_fin(P, Bf, bn, ws)
+            self._launch(cv, 0, lambda: self.L.conv_fwd_fin(C.byref(cv.desc), cdt, ptr(x), ptr(cv.wf), ptr(y),
+                                                             ptr(sc), ptr(sh), ptr(part), C.byref(fin), stream()))
+            return
         else:
             self._launch(cv, 0, lambda: self.L.conv_fwd(C.byref(cv.desc), cdt, ptr(x), ptr(cv.wf), ptr(y), ptr(sc),
                                                          ptr(sh), ptr(part) if training else None, stream()))

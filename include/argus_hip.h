@@ -129,6 +129,32 @@ int argus_conv_fwd_stat_tile(const argus_conv_desc* d, int dtype);
  * (negative tile: ragged rows); other convs as argus_conv_fwd_stat_rows / _stat_tile. */
 int argus_conv_fwd_stats_only_rows(const argus_conv_desc* d, int dtype);
 int argus_conv_fwd_stats_only_tile(const argus_conv_desc* d, int dtype);
+/* The BatchNorm train-mode finalize of a forward conv's statistics (argus_bn_finalize's arguments
+ * past its partial layout), for argus_conv_fwd_fin. workspace: argus_bn_workspace_bytes(k), zeroed once
+ * (every call leaves it zeroed); running_mean / running_var / num_batches_tracked may be NULL. */
+typedef struct argus_bn_fwd_fin {
+  void* workspace;
+  const float* gamma;
+  const float* beta;
+  float eps;
+  float momentum;
+  float* running_mean;
+  float* running_var;
+  int64_t* num_batches_tracked;
+  float* mean;
+  float* invstd;
+  float* scale;
+  float* shift;
+} argus_bn_fwd_fin;
+/* argus_conv_fwd (stat_part required) followed by argus_bn_finalize of its partials (the layout
+ * argus_conv_fwd_stat_rows / _tile, or _stats_only_rows / _tile when y == NULL), with the finalize
+ * folded into the conv's last-arriving workgroups where the producing kernel's row tiles align with
+ * argus_bn_finalize's merge groups (otherwise it is launched after the conv): mean, invstd, scale, shift
+ * and the running statistics are bit-identical to the two calls either way (ABI 18). Replaces the
+ * BatchNorm2d train forward's statistics pass of torchvision's Bottleneck (argus/models.py:43). */
+int argus_conv_fwd_fin(const argus_conv_desc* d, int dtype, const void* x, const void* w_fwd, void* y,
+                       const float* pro_scale, const float* pro_shift, float* stat_part,
+                       const argus_bn_fwd_fin* fin, argus_stream_t stream);
 /* Bytes a stat_part buffer needs for argus_conv_fwd of d (stats_only = 0) or for its statistics-only
  * form (y == NULL, stats_only = 1): 2*rows*k floats plus, for a ragged tiling (negative tile), int32
  * counts[rows] after them (ABI 17). Size every statistics workspace with it; rows*k*2 floats alone is

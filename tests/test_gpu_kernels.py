@@ -2159,3 +2159,108 @@ def test_persistent_conv1_dgrad_matches_igemm(cuda, n4w, w, hw, dual):
             continue
         assert torch.isfinite(b).all(), i
         assert _rel(b, a) < 1e-5, (i, _rel(b, a))
+
+
+# (cin, cout, k, stride, hw, n, dtype, tuning, prologue, store y): one forward producer each —
+# igemm 1x1 / strided / 3x3 (fp32 + bf16, with and without the BN+ReLU prologue), glds (key 8),
+# halo (key 13, plain and deep ring), the persistent statistics-only 1x1 (y NULL), MX-fp8
+FWD_FIN_CASES = [
+    (64, 256, 1, 1, 12, 3, "fp32", None, False, True), (64, 256, 1, 1, 12, 3, "bf16", None, True, True),
+    (256, 512, 1, 2, 13, 2, "bf16", None, False, True), (128, 128, 3, 2, 12, 2, "bf16", None, False, True),
+    (128, 128, 3, 1, 9, 3, "fp32", None, True, True),
+    (128, 256, 1, 1, 24, 4, "bf16", {8: 64, 9: 1}, False, True), (256, 256, 3, 2, 20, 4, "bf16", {8: 64, 9: 1}, False, True),
+    (64, 64, 3, 1, 64, 1, "bf16", {13: 1}, False, True), (128, 128, 3, 1, 16, 3, "bf16", {13: 1, 51: 1}, False, True),
+    (64, 256, 1, 1, 16, 4, "bf16", None, False, False), (128, 512, 1, 1, 9, 3, "bf16", None, False, False),
+    (256, 1024, 1, 1, 30, 8, "bf16", None, False, False),
+    (128, 128, 3, 1, 16, 4, "fp8", {37: 7}, False, True), (256, 512, 1, 1, 12, 4, "fp8", {37: 7}, False, True),
+]
+
+
+def _fwd_fin_run(L, d, dt, x, wf, y, sc, sh, rows, tile, count, cout, folded, cuda):
+    """one training forward + finalize: argus_conv_fwd_fin (folded) or argus_conv_fwd + argus_bn_finalize;
+    returns every output, the kernel names launched and the workspace counters."""
+    from argus_amd._lib import BnFwdFin
+    from argus_amd.profiling import KernelTimer
+
+    ws = torch.zeros(L.dll.argus_bn_workspace_bytes(2048), dtype=torch.uint8, device=cuda)
+    st = torch.full((rows * cout * 2 + rows,), float("nan"), device=cuda)
+    g = torch.linspace(0.5, 1.5, cout, device=cuda)
+    b = torch.linspace(-0.2, 0.3, cout, device=cuda)
+    rm, rv = torch.linspace(-1, 1, cout, device=cuda), torch.linspace(0.5, 2, cout, device=cuda)
+    nbt = torch.full((1,), 7, dtype=torch.int64, device=cuda)
+    outs = torch.full((4, cout), float("nan"), device=cuda)
+    with KernelTimer() as t:
+        if folded:
+            f = BnFwdFin()
+            f.workspace, f.gamma, f.beta, f.eps, f.momentum = ptr(ws), ptr(g), ptr(b), 1e-5, 0.1
+            f.running_mean, f.running_var, f.num_batches_tracked = ptr(rm), ptr(rv), ptr(nbt)
+            f.mean, f.invstd, f.scale, f.shift = ptr(outs[0]), ptr(outs[1]), ptr(outs[2]), ptr(outs[3])
+            L.conv_fwd_fin(C.byref(d), DT[dt], ptr(x), ptr(wf), ptr(y), ptr(sc), ptr(sh), ptr(st), C.byref(f), stream())
+        else:
+            L.conv_fwd(C.byref(d), DT[dt], ptr(x), ptr(wf), ptr(y), ptr(sc), ptr(sh), ptr(st), stream())
+            L.bn_finalize(cout, rows, tile, ptr(st), count, ptr(g), ptr(b), C.c_float(1e-5), C.c_float(0.1), ptr(rm),
+                          ptr(rv), ptr(nbt), ptr(outs[0]), ptr(outs[1]), ptr(outs[2]), ptr(outs[3]), ptr(ws), stream())
+        names = set(t.summary())
+    torch.cuda.synchronize()
+    ctr = int(ws[:16384].view(torch.int32).abs().sum())
+    return [v.cpu() for v in ((y if y is not None else st[:0]), st, outs, rm, rv, nbt)], names, ctr
+
+
+def test_forward_bn_finalize_folded_bit_identical(cuda):
+    """argus_conv_fwd_fin (ABI 18): the forward BN statistics finalize folded into the producing conv's
+    last-arriving workgroups (bnfin.h: row lanes merge each workgroup's tiles, one group slot per
+    argus_bn_finalize group, the last group's arrival finishes the channel) gives BIT-IDENTICAL y,
+    partials, mean / invstd / scale / shift, running mean / var and num_batches_tracked to argus_conv_fwd
+    + argus_bn_finalize on the same inputs, launches no stats_finalize_kernel where the producer's tiles
+    align with the finalize's groups (igemm, persistent statistics-only, stem) and leaves its ticket
+    counters at zero; igemm / glds / halo (plain, deep ring) / statistics-only / MX-fp8 producers, with
+    and without a BN+ReLU prologue, ragged M; the stem at 376x672 (ragged int32 row counts)."""
+    torch.manual_seed(41)
+    L = lib()
+    unfolded = []
+    for cin, cout, k, s, hw, n, dt, tune, pro, store in FWD_FIN_CASES:
+        d, _ = _desc(n, hw, hw, cin, cout, k, s)
+        if tune:
+            d = d.with_tuning(tune)
+        wdt = "bf16" if dt == "fp8" else dt  # argus_conv_fwd_stat_tile of an MX-fp8 forward: the bf16 tile
+        x = (torch.randn(n, hw, hw, cin, device=cuda) * 1.3 + 0.1).to(TDT[dt])
+        wf, _ = _prep(d, dt, (torch.randn(cout, k, k, cin) * (2.0 / (k * k * cin)) ** 0.5).to(cuda), cuda)
+        sc = (torch.rand(cin, device=cuda) + 0.5) if pro else None
+        sh = (torch.randn(cin, device=cuda) * 0.3) if pro else None
+        so = not store and not pro
+        rows = (L.dll.argus_conv_fwd_stats_only_rows if so else L.dll.argus_conv_fwd_stat_rows)(C.byref(d), DT[dt])
+        tile = (L.dll.argus_conv_fwd_stats_only_tile if so else L.dll.argus_conv_fwd_stat_tile)(C.byref(d), DT[wdt])
+        count = n * d.ho * d.wo
+        res = []
+        for folded in (False, True):
+            y = torch.empty(n, d.ho, d.wo, cout, dtype=TDT[dt], device=cuda) if store else None
+            res.append(_fwd_fin_run(L, d, dt, x, wf, y, sc, sh, rows, tile, count, cout, folded, cuda))
+        case = (cin, cout, k, s, hw, n, dt, tune, pro, store)
+        for a, b in zip(res[0][0], res[1][0]):
+            assert torch.equal(a.view(torch.uint8) if a.is_floating_point() else a,
+                               b.view(torch.uint8) if b.is_floating_point() else b), case
+        assert int(res[1][0][5]) == 8 and res[0][2] == 0 and res[1][2] == 0, case
+        assert "argus::stats_finalize_kernel" in res[0][1], case
+        if "argus::stats_finalize_kernel" in res[1][1]:
+            unfolded.append((case, sorted(res[1][1])))
+    # the register-staged igemm (one partial row per tile) and the statistics-only kernel always fold
+    assert not [c for c in unfolded if any(k.startswith(("argus::igemm_kernel", "argus::p1x1_fwd_stats"))
+                                           for k in c[1])], unfolded
+    # the stem: ragged 376x672 (int32 row counts after the partials) and a small odd image
+    for n, H, W in [(1, 376, 672), (3, 38, 30)]:
+        for dt in ("fp32", "bf16"):
+            d, _ = _desc(n, H, W, 3, 64, 7, 2, stem=True)
+            x4 = torch.zeros(n, H, W, 4, device=cuda)
+            x4[..., :3] = torch.rand(n, H, W, 3, device=cuda)
+            x4 = x4.to(TDT[dt])
+            wm = (torch.randn(64, 3, 7, 7) * 0.1).to(cuda)
+            wf = torch.empty(64, 256, dtype=TDT[dt], device=cuda)
+            L.conv_weight_prep(C.byref(d), DT[dt], ptr(wm), (C.c_int64 * 4)(*wm.stride()), ptr(wf), None, stream())
+            rows = L.dll.argus_conv_fwd_stat_rows(C.byref(d), DT[dt])
+            tile = L.dll.argus_conv_fwd_stat_tile(C.byref(d), DT[dt])
+            res = [_fwd_fin_run(L, d, dt, x4, wf, torch.empty(n, d.ho, d.wo, 64, dtype=TDT[dt], device=cuda), None,
+                                None, rows, tile, n * d.ho * d.wo, 64, folded, cuda) for folded in (False, True)]
+            for a, b in zip(res[0][0], res[1][0]):
+                assert torch.equal(a.view(torch.uint8) if a.is_floating_point() else a,
+                                   b.view(torch.uint8) if b.is_floating_point() else b), ("stem", n, H, W, dt)
+            assert "argus::stats_finalize_kernel" not in res[1][1] and res[1][2] == 0, ("stem", n, H, W, dt, res[1][1])
