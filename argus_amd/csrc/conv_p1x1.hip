@@ -439,7 +439,10 @@ __global__ __launch_bounds__(256) void p1x1_fwd_stats_kernel(const P1FParams p) 
       m2 = qa + qb + d * d * (na * nb_ / n);
     }
     store_part(p.part + (size_t)g0 * p.N + nb * BNC + tid, make_float2(sum, m2));
-    if (nb == 0 && tid == 0) store_count(p.counts + g0, (int)n);  // write-through (the folded finalize)
+    // the row count, write-through: with the finalize folded in, every column block's workgroup writes it
+    // (the same value), since the last arriver of column block nb reads the counts of its own group's
+    // row splits, which only that column block's workgroups are ordered before
+    if (tid == 0 && (nb == 0 || p.ffin.mode)) store_count(p.counts + g0, (int)n);
   }
   if (p.ffin.mode) {  // the statistics finalize folded in (bnfin.h): one partial row per row split
     __shared__ int fin_flag;

@@ -118,8 +118,10 @@ class ResNetEngine:
         # finalize launch (folding it into the conv measured neutral).
         self.fold_fin = True
         # the forward BN statistics finalize folded into the producing conv's last workgroups
-        # (argus_conv_fwd_fin: bit-identical to argus_conv_fwd + argus_bn_finalize; round 6)
-        self.fold_fwd_fin = True
+        # (argus_conv_fwd_fin: bit-identical to argus_conv_fwd + argus_bn_finalize; round 6). Off: the
+        # last arrivers' fp64 merges serialise at each producer's tail for about as long as the separate
+        # launch, and measured 13.27-13.42 vs 13.12-13.19 ms at B=64 (profiles/r06j_ab_b64_fold_fwd_fin.txt)
+        self.fold_fwd_fin = False
         # ... and the stem BN's finalize into the maxpool backward pass (argus_maxpool_bwd_bn_fin)
         self.fold_stem_fin = True
         self._side: torch.cuda.Stream | None = None

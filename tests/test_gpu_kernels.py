@@ -2171,7 +2171,7 @@ FWD_FIN_CASES = [
     (128, 256, 1, 1, 24, 4, "bf16", {8: 64, 9: 1}, False, True), (256, 256, 3, 2, 20, 4, "bf16", {8: 64, 9: 1}, False, True),
     (64, 64, 3, 1, 64, 1, "bf16", {13: 1}, False, True), (128, 128, 3, 1, 16, 3, "bf16", {13: 1, 51: 1}, False, True),
     (64, 256, 1, 1, 16, 4, "bf16", None, False, False), (128, 512, 1, 1, 9, 3, "bf16", None, False, False),
-    (256, 1024, 1, 1, 30, 8, "bf16", None, False, False),
+    (256, 1024, 1, 1, 30, 8, "bf16", None, False, False), (256, 1024, 1, 1, 16, 128, "bf16", None, False, False),
     (128, 128, 3, 1, 16, 4, "fp8", {37: 7}, False, True), (256, 512, 1, 1, 12, 4, "fp8", {37: 7}, False, True),
 ]
 
@@ -2246,8 +2246,10 @@ def test_forward_bn_finalize_folded_bit_identical(cuda):
     # the register-staged igemm (one partial row per tile) and the statistics-only kernel always fold
     assert not [c for c in unfolded if any(k.startswith(("argus::igemm_kernel", "argus::p1x1_fwd_stats"))
                                            for k in c[1])], unfolded
-    # the stem: ragged 376x672 (int32 row counts after the partials) and a small odd image
-    for n, H, W in [(1, 376, 672), (3, 38, 30)]:
+    # the stem: ragged 376x672 (int32 row counts after the partials) and a small odd image; n = 1 at
+    # 376x672 gives 528 partial rows in 32 finalize groups of 17 rows, which splits a two-row stem tile,
+    # so that case takes the separate finalize (still bit-identical); n = 4 (66-row groups) folds
+    for n, H, W, folds in [(1, 376, 672, False), (4, 376, 672, True), (3, 38, 30, True)]:
         for dt in ("fp32", "bf16"):
             d, _ = _desc(n, H, W, 3, 64, 7, 2, stem=True)
             x4 = torch.zeros(n, H, W, 4, device=cuda)
@@ -2263,4 +2265,6 @@ def test_forward_bn_finalize_folded_bit_identical(cuda):
             for a, b in zip(res[0][0], res[1][0]):
                 assert torch.equal(a.view(torch.uint8) if a.is_floating_point() else a,
                                    b.view(torch.uint8) if b.is_floating_point() else b), ("stem", n, H, W, dt)
-            assert "argus::stats_finalize_kernel" not in res[1][1] and res[1][2] == 0, ("stem", n, H, W, dt, res[1][1])
+            assert res[1][2] == 0, ("stem", n, H, W, dt)
+            if folds or dt == "fp32":  # fp32: the register-staged STEM igemm (one partial row a tile)
+                assert "argus::stats_finalize_kernel" not in res[1][1], ("stem", n, H, W, dt, res[1][1])

@@ -147,7 +147,8 @@ def test_side_stream_overlap_is_bit_identical(cuda):
     bn_apply), the 3x3 data gradients run alone (engine.gate3x3) and bn3's input recomputed from a2 in
     the BN-backward epilogue rather than read (engine.yrec_epi) or never stored at all for the layer-1
     blocks (engine.y3_free: the fused conv3 data + weight gradient recomputes it too), bn2's apply
-    outside conv3's statistics pass (engine.a2_in_stats off: the separate bn_apply pass); eval-mode
+    outside conv3's statistics pass (engine.a2_in_stats off: the separate bn_apply pass), the forward
+    statistics finalize folded into the producing convs (engine.fold_fwd_fin, argus_conv_fwd_fin); eval-mode
     predictions after the steps too."""
     from argus_amd.models import NCameraCNN
     from argus_amd.step import FusedTrainer
@@ -163,7 +164,7 @@ def test_side_stream_overlap_is_bit_identical(cuda):
     # (its pass stays on the igemm, with the bn2 prologue) and fuse_out are compared against a second
     # baseline under key 44 = 0.
     group_a = ({}, {"tail_main": False}, {"wgrad_overlap": False}, {"gate3x3": True}, {"yrec_epi": True},
-               {"yrec_epi": True, "y3_free": True})
+               {"yrec_epi": True, "y3_free": True}, {"fold_fwd_fin": True})
     group_b = ({"_tune": {44: 0}}, {"a2_in_stats": True}, {"_tune": {44: 0}, "fuse_out": False})
     for attrs in group_a + group_b:
         torch.manual_seed(42)
