@@ -50,6 +50,14 @@ def main():
         ran out of memory at 376x672 B=128). Returns (ms/step, peak device GiB of this configuration)."""
         tune, attrs = parse(cfg)
         dtype = attrs.pop("dtype", a.dtype)  # a per-configuration compute dtype (e.g. fp8 vs bf16)
+        # main_priority=-1: the whole step (the engine's main chain) on a high-priority stream, the side
+        # stream at its own side_priority
+        mp = int(attrs.pop("main_priority", 0))
+        ms_ = torch.cuda.Stream(device=dev, priority=mp) if mp else torch.cuda.current_stream(dev)
+        with torch.cuda.stream(ms_):
+            return run_on(tune, attrs, dtype)
+
+    def run_on(tune, attrs, dtype):
         torch.cuda.empty_cache()
         torch.cuda.reset_peak_memory_stats(dev)
         torch.manual_seed(42)
