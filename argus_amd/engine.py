@@ -159,6 +159,9 @@ class ResNetEngine:
         # otherwise hold the CUs' LDS and registers beside it (the block's own deferred weight gradients
         # are issued after it, at the block's end, as usual)
         self.gate3x3 = False
+        # ... only for the blocks of at most this width (64: layer 1, whose halo data gradients run at 76 KB of
+        # LDS a workgroup and lose CUs to the side stream's 128-148 KB weight-gradient workgroups); 0 = off
+        self.gate3x3_width = 0
         # the bottleneck tail on the bf16 schedule: conv3's forward only reduces bn3's statistics (nothing
         # stored), then one pass recomputes its C tile and applies bn3 + the residual + ReLU there
         # (argus_conv_fwd_bn_out): the bn_apply pass no longer reads y3 back (bit-identical outputs)
@@ -723,7 +726,7 @@ class ResNetEngine:
             # conv2 -> bn1 (dm1 goes to a ring buffer when the side stream's conv1 wgrad reads it)
             if wg1_apply:
                 dzb = self._next_dy()
-            if self.gate3x3:
+            if self.gate3x3 or b.width <= self.gate3x3_width:
                 self._drain_side()
             r1 = self._dgrad_bn(pf + ".conv2", dza if pro2 else dy2, dzb, None, pf + ".bn1", a["y1"], 2, P=P, G=G,
                                 pro=pro2, x8=self.x8buf if x8d else None)
