@@ -133,6 +133,9 @@ class ResNetEngine:
         # ring buffers it reuses was measured too (-2.5 %: it waits earlier than the per-buffer guards).
         # False issues every weight gradient as soon as its dy is ready.
         self.side_batch = True
+        # a block's deferred weight gradients issued in reverse order (conv1 first; they write separate
+        # dW buffers and share one workspace in stream order, so the results are identical)
+        self.side_reverse = False
         self._deferred: list = []  # (cv, fn, buffer data_ptrs)
         self._side_seq = 0
         self._waited_seq = 0
@@ -1020,7 +1023,7 @@ class ResNetEngine:
         items, self._deferred = self._deferred, []
 
         def run():
-            for cv, fn, _ in items:
+            for cv, fn, _ in (items[::-1] if self.side_reverse else items):
                 self._launch(cv, 2, fn)
 
         done = self._on_side(run)
