@@ -18,7 +18,7 @@ import torch  # noqa: F401  (must precede the CDLL, see module docstring)
 LIB_PATH = Path(os.environ.get("ARGUS_HIP_LIB", Path(__file__).resolve().parent / "libargus_hip.so"))
 
 F32, BF16, FP8 = 0, 1, 2
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 
 class Tuning(C.Structure):
@@ -120,6 +120,10 @@ SIGNATURES = {
     "argus_conv_dgrad_wgrad_bn_rows": (_I, [_DESC, _I]),
     "argus_conv_dgrad_wgrad_bn": (_I, [_DESC, _I, _P, _P, _P, _P, _P, C.POINTER(BnBwdEpilogue),
                                        C.POINTER(BnBwdPrologue), _P, _P, _SZ, _P]),
+    "argus_event_create": (_I, [C.POINTER(C.c_void_p)]),
+    "argus_event_record": (_I, [_P, _P]),
+    "argus_stream_wait_event": (_I, [_P, _P]),
+    "argus_event_destroy": (_I, [_P]),
     "argus_ktimer_enable": (_I, [C.c_char_p]),
     "argus_ktimer_enable_on": (_I, [C.c_char_p, _P]),
     "argus_ktimer_disable": (_I, []),
@@ -212,3 +216,28 @@ def ptr(t) -> int | None:
 
 def stream() -> int:
     return torch.cuda.current_stream().cuda_stream
+
+
+class DeviceEvent:
+    """argus_event_t: orders two streams of this device with a device-scope release / acquire
+    (hipEventDisableSystemFence), without the system-scope cache writeback a torch.cuda.Event record
+    carries. ``record(stream)`` and ``wait(stream)`` take torch streams (None: the current stream)."""
+
+    __slots__ = ("h",)
+
+    def __init__(self) -> None:
+        h = C.c_void_p()
+        lib().event_create(C.byref(h))
+        self.h = h.value
+
+    def record(self, s=None) -> "DeviceEvent":
+        lib().event_record(self.h, (s or torch.cuda.current_stream()).cuda_stream)
+        return self
+
+    def wait(self, s=None) -> None:
+        lib().stream_wait_event((s or torch.cuda.current_stream()).cuda_stream, self.h)
+
+    def __del__(self) -> None:
+        if self.h and _LIB is not None:
+            _LIB.dll.argus_event_destroy(self.h)
+            self.h = None

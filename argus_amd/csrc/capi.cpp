@@ -27,9 +27,47 @@ using namespace argus;
 
 extern "C" {
 
-int argus_abi_version(void) { return 18; }
+int argus_abi_version(void) { return 19; }
 
 const char* argus_last_error(void) { return g_last_error.c_str(); }
+
+// cross-stream events: device-scope release / acquire only (hipEventDisableSystemFence)
+int argus_event_create(argus_event_t* event) {
+  if (!event) { set_error("event_create: null out pointer"); return ARGUS_ERR_ARG; }
+  hipEvent_t e = nullptr;
+  if (hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) {
+    set_error("event_create: hipEventCreateWithFlags failed");
+    return ARGUS_ERR_HIP;
+  }
+  *event = e;
+  return ARGUS_OK;
+}
+
+int argus_event_record(argus_event_t event, argus_stream_t stream) {
+  if (!event) { set_error("event_record: null event"); return ARGUS_ERR_ARG; }
+  if (hipEventRecord((hipEvent_t)event, (hipStream_t)stream) != hipSuccess) {
+    set_error("event_record: hipEventRecord failed");
+    return ARGUS_ERR_HIP;
+  }
+  return ARGUS_OK;
+}
+
+int argus_stream_wait_event(argus_stream_t stream, argus_event_t event) {
+  if (!event) { set_error("stream_wait_event: null event"); return ARGUS_ERR_ARG; }
+  if (hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)event, 0) != hipSuccess) {
+    set_error("stream_wait_event: hipStreamWaitEvent failed");
+    return ARGUS_ERR_HIP;
+  }
+  return ARGUS_OK;
+}
+
+int argus_event_destroy(argus_event_t event) {
+  if (event && hipEventDestroy((hipEvent_t)event) != hipSuccess) {
+    set_error("event_destroy: hipEventDestroy failed");
+    return ARGUS_ERR_HIP;
+  }
+  return ARGUS_OK;
+}
 
 int argus_images_to_nhwc4(int dtype, int64_t nimg, int h, int w, const float* x, void* out, argus_stream_t stream) {
   if (nimg <= 0 || h <= 0 || w <= 0 || !x || !out) { set_error("images_to_nhwc4: bad arguments"); return ARGUS_ERR_ARG; }

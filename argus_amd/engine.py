@@ -22,12 +22,14 @@ Eval mode uses running statistics (bn_eval_coeffs) and skips all statistics / ru
 from __future__ import annotations
 
 import ctypes as C
+import collections
 import contextlib
 from dataclasses import dataclass
 
 import torch
 
-from argus_amd._lib import BnFwdFin, BF16, F32, FP8, BnBwdEpilogue, BnBwdPrologue, ConvDesc, lib, ptr, stream
+from argus_amd._lib import (BnFwdFin, BF16, F32, FP8, BnBwdEpilogue, BnBwdPrologue, ConvDesc, DeviceEvent, lib, ptr,
+                             stream)
 
 
 @dataclass(frozen=True)
@@ -136,6 +138,12 @@ class ResNetEngine:
         # a block's deferred weight gradients issued in reverse order (conv1 first; they write separate
         # dW buffers and share one workspace in stream order, so the results are identical)
         self.side_reverse = False
+        # cross-stream events with a device-scope release / acquire (argus_event_*, hipEventDisableSystemFence)
+        # instead of torch.cuda.Event; the collectives' stream hand-off (_comm) keeps torch's events either
+        # way. Off: measured 13.34-13.43 vs 13.28-13.34 ms at B=64 (profiles/r06j_ab_b64_light_events.txt);
+        # the ~6 us main-stream gap at each cross-stream event is not the system-scope fence
+        self.light_events = False
+        self._ev_keep: collections.deque = collections.deque(maxlen=512)  # recent events, destroyed late
         self._deferred: list = []  # (cv, fn, buffer data_ptrs)
         self._side_seq = 0
         self._waited_seq = 0
@@ -546,7 +554,7 @@ class ResNetEngine:
                 if ds_done is None:
                     self._conv_bn(P, Bf, pf + ".downsample.0", pf + ".downsample.1", h, a["yd"], None, training)
                 else:
-                    torch.cuda.current_stream().wait_event(ds_done)
+                    ds_done.wait(torch.cuda.current_stream())
                 sd = self.bn_state[pf + ".downsample.1"]
                 res, rsc, rsh = a["yd"], sd[2], sd[3]
             else:
@@ -1032,18 +1040,24 @@ class ResNetEngine:
             self._pending[bp] = (self._side_seq, done)
         self._last_side = done
 
+    def _event(self):
+        """A cross-stream event (record(stream) / wait(stream)): device-scope (light_events) or torch's."""
+        ev = DeviceEvent() if self.light_events else torch.cuda.Event()
+        self._ev_keep.append(ev)
+        return ev
+
     def _on_side(self, fn):
         """Run ``fn``'s launches on the side stream after the main stream's work so far; returns the
         side-stream event that marks their completion."""
         main = torch.cuda.current_stream()
         if self._side is None:
             self._side = torch.cuda.Stream(device=self.device, priority=self.side_priority)
-        ready = torch.cuda.Event()
+        ready = self._event()
         ready.record(main)
-        self._side.wait_event(ready)
+        ready.wait(self._side)
         with torch.cuda.stream(self._side):
             fn()
-        done = torch.cuda.Event()
+        done = self._event()
         done.record(self._side)
         return done
 
@@ -1061,7 +1075,7 @@ class ResNetEngine:
             self._flush_side()
         ev = self._pending.pop(bp, None)
         if ev is not None and ev[0] > self._waited_seq:
-            torch.cuda.current_stream().wait_event(ev[1])
+            ev[1].wait(torch.cuda.current_stream())
             self._waited_seq = ev[0]
 
     @contextlib.contextmanager
@@ -1083,7 +1097,7 @@ class ResNetEngine:
         """Main stream waits for the weight gradients issued on the side stream so far (the deferred ones
         stay deferred): nothing of the side stream is resident during the next main-stream launch."""
         if self._last_side is not None and self._waited_seq < self._side_seq:
-            torch.cuda.current_stream().wait_event(self._last_side)
+            self._last_side.wait(torch.cuda.current_stream())
             self._pending.clear()
             self._waited_seq = self._side_seq
 
@@ -1091,7 +1105,7 @@ class ResNetEngine:
         """Main stream waits for every weight gradient issued so far."""
         self._flush_side()
         if self._last_side is not None:
-            torch.cuda.current_stream().wait_event(self._last_side)
+            self._last_side.wait(torch.cuda.current_stream())
             self._pending.clear()
             self._last_side = None
             self._waited_seq = self._side_seq

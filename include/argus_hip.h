@@ -333,6 +333,19 @@ int argus_ktimer_count(void);
 int argus_ktimer_get(int index, char* name, int name_len, int64_t* launches, double* total_ms,
                      double* work, double* bytes);
 
+/* ---- cross-stream ordering (ABI 19) ------------------------------------------------------------
+ * Events for ordering two streams of one device: created with hipEventDisableTiming |
+ * hipEventDisableSystemFence, so recording one performs a device-scope release and waiting on it a
+ * device-scope acquire, without the system-scope cache writeback / invalidation a default event carries.
+ * Work on this device only (the weight-gradient side stream and the main stream of one process); the
+ * host and other devices need a default event. Replaces the torch.cuda.Event record / wait_event pairs
+ * the DDP-free training step of argus/train.py:298-321 would use between two streams (it uses one). */
+typedef void* argus_event_t; /* hipEvent_t */
+int argus_event_create(argus_event_t* event);
+int argus_event_record(argus_event_t event, argus_stream_t stream);
+int argus_stream_wait_event(argus_stream_t stream, argus_event_t event);
+int argus_event_destroy(argus_event_t event);
+
 /* ---- BatchNorm2d (train: batch stats, eps, momentum; eval: running stats) --------------------- */
 /* Workspace of argus_bn_finalize / argus_bn_bwd_finalize / the folded finalize of argus_conv_dgrad_bn
  * for up to `channels` channels. Its first 16 KiB hold inter-workgroup ticket counters: zero-fill the workspace ONCE when it is allocated;

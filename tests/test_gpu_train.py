@@ -165,7 +165,7 @@ def test_side_stream_overlap_is_bit_identical(cuda):
     # baseline under key 44 = 0.
     group_a = ({}, {"tail_main": False}, {"wgrad_overlap": False}, {"gate3x3": True}, {"yrec_epi": True},
                {"yrec_epi": True, "y3_free": True}, {"fold_fwd_fin": True},
-               {"side_reverse": True, "gate3x3_width": 64})
+               {"side_reverse": True, "gate3x3_width": 64}, {"light_events": True})
     group_b = ({"_tune": {44: 0}}, {"a2_in_stats": True}, {"_tune": {44: 0}, "fuse_out": False})
     for attrs in group_a + group_b:
         torch.manual_seed(42)
